@@ -1,0 +1,271 @@
+/*
+ * tsg.h — C ABI of libtsg, the MI355X (gfx950) Tempo search engine.
+ *
+ * This is the drop-in boundary for Tempo's flatbuffer backend-search path and the
+ * v2 trace-ID lookup path. Every entry point takes plain pointers and sizes; no
+ * Go, Python or torch types cross it. All inputs are copied during the call and
+ * no caller pointer is retained (cgo rule: C may not keep Go pointers).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference checkout, Grafana Tempo ~v1.4.1):
+ *
+ *   tsg_block_open        search.OpenBackendSearchBlock + the reads at the top of
+ *                         BackendSearchBlock.Search
+ *                         (tempodb/search/backend_search_block.go:132-138,184-241)
+ *   tsg_search            BackendSearchBlock.Search page/entry loops driven by
+ *                         instance.searchLocalBlocks
+ *                         (tempodb/search/backend_search_block.go:247-295,
+ *                          modules/ingester/instance_search.go:164-185)
+ *   tsg_pipeline_new      search.NewSearchPipeline + rewriteTagLookup
+ *                         (tempodb/search/pipeline.go:26-140)
+ *   tsg_results_combine   the consumer loop of instance.Search
+ *                         (modules/ingester/instance_search.go:45-70) with
+ *                         search.CombineSearchResults (tempodb/search/util.go:40-62)
+ *   tsg_block_tags /      BackendSearchBlock.Tags / TagValues
+ *   tsg_block_tag_values  (tempodb/search/backend_search_block.go:145-181)
+ *   tsg_v2block_open /    v2.BackendBlock.find: bloom shard select + bloom test +
+ *   tsg_lookup_ids        index lower_bound (tempodb/encoding/v2/backend_block.go:38-92,
+ *                         tempodb/encoding/common/bloom.go:83-93,
+ *                         tempodb/encoding/v2/index_reader.go:85-114) and the
+ *                         tempodb.Find block prefilter (tempodb/tempodb.go:492-511)
+ *
+ * Threading: a tsg_ctx is thread-safe. Searches on one device are serialised on
+ * that device's stream; blocks on different devices are searched in parallel.
+ *
+ * Errors: every int-returning call returns a TSG_* status; tsg_last_error()
+ * returns the thread-local message of the last failure on this thread.
+ */
+#ifndef TSG_H
+#define TSG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSG_ABI_VERSION 1
+
+/* Status codes. */
+#define TSG_OK 0
+#define TSG_E_NOT_FOUND 1            /* search.meta.json missing: the Go shim maps this to a no-op
+                                        (backend_search_block.go:191-203) */
+#define TSG_E_CORRUPT 2              /* checksum / offset / framing error */
+#define TSG_E_UNSUPPORTED_ENCODING 3 /* search_encoding other than none/snappy, or version != v2 */
+#define TSG_E_DEVICE 4               /* HIP runtime failure or no device */
+#define TSG_E_CANCELLED 5
+#define TSG_E_OOM 6
+#define TSG_E_INVALID 7              /* bad argument */
+#define TSG_E_UNSUPPORTED 8          /* block layout outside the engine's contract */
+#define TSG_E_IO 9
+
+typedef struct tsg_ctx tsg_ctx;
+typedef struct tsg_block tsg_block;
+typedef struct tsg_pipeline tsg_pipeline;
+typedef struct tsg_v2block tsg_v2block;
+
+typedef struct tsg_options {
+  int32_t num_devices;    /* 0 = every visible device */
+  const int32_t *devices; /* optional explicit ordinals (num_devices entries) */
+  uint32_t flags;         /* reserved, 0 */
+} tsg_options;
+
+/* tempopb.SearchRequest (pkg/tempopb/tempo.proto:44-52), un-normalised. */
+typedef struct tsg_request {
+  uint32_t ntags;
+  const uint8_t *const *tag_keys;
+  const uint32_t *tag_key_lens;
+  const uint8_t *const *tag_values;
+  const uint32_t *tag_value_lens;
+  uint32_t min_duration_ms;
+  uint32_t max_duration_ms;
+  uint32_t limit;
+  uint32_t start; /* unix seconds */
+  uint32_t end;   /* unix seconds */
+} tsg_request;
+
+/* The normalised query a Pipeline applies: what the Go shim passes after
+ * rewriteTagLookup + strings.ToLower (tempodb/search/pipeline.go:26-101). */
+typedef struct tsg_query {
+  uint32_t nterms;
+  const uint8_t *const *keys;
+  const uint32_t *key_lens;
+  const uint8_t *const *values;
+  const uint32_t *value_lens;
+  uint8_t has_min;    /* MinDurationMs > 0 */
+  uint8_t has_max;    /* MaxDurationMs > 0 */
+  uint8_t has_range;  /* Start != 0 && End != 0 */
+  uint8_t exhaustive; /* x-dbg-exhaustive: always-false trace filter */
+  uint64_t min_ns;
+  uint64_t max_ns;
+  uint32_t start_s;
+  uint32_t end_s;
+} tsg_query;
+
+/* tempopb.SearchMetrics (pkg/tempopb/tempo.proto:81-87) + device counters. */
+typedef struct tsg_metrics {
+  uint32_t traces_inspected;
+  uint32_t blocks_inspected;
+  uint32_t blocks_skipped;
+  uint32_t pad0;
+  uint64_t bytes_inspected;
+  uint64_t device_bytes_read; /* algorithmic bytes the scan kernels touched */
+  uint64_t kernel_ns;         /* device time of the search kernels (HIP events) */
+  uint64_t scan_kernel_ns;    /* device time of the scan_compact kernel alone (HIP events) */
+  uint64_t scan_bytes;        /* algorithmic bytes of the scan_compact kernel */
+} tsg_metrics;
+
+/* Ordered match sequence: blocks in caller order, each block's matches in the
+ * reference scan order (pages ascending, entry vector index ascending). With
+ * limit L > 0 the sequence is cut right after the first occurrence of the L-th
+ * distinct trace ID (deterministic refinement of instance.Search). */
+typedef struct tsg_result {
+  uint64_t n;
+  const uint8_t (*trace_id)[16]; /* right-aligned, zero-padded on the left */
+  const uint8_t *trace_id_len;   /* original id length (<= 16) */
+  const uint64_t *start_ns;
+  const uint64_t *end_ns;
+  const uint32_t *duration_ms; /* uint32((end-start)/1e6), util.go:33 */
+  const uint32_t *block_idx;   /* index into the caller's block array */
+  const uint64_t *entry_idx;   /* scan position inside the block */
+  const char *const *root_service; /* NUL-terminated copies; lengths below */
+  const uint32_t *root_service_len;
+  const char *const *root_name;
+  const uint32_t *root_name_len;
+  tsg_metrics metrics;
+} tsg_result;
+
+/* Options for tsg_search. */
+typedef struct tsg_search_opts {
+  uint32_t limit;  /* 0 = no limit (every match) */
+  uint32_t flags;  /* reserved */
+  uint64_t query_id; /* for tsg_cancel; 0 = not cancellable */
+} tsg_search_opts;
+
+/* ---- context --------------------------------------------------------------- */
+int tsg_init(const tsg_options *opts, tsg_ctx **out);
+void tsg_shutdown(tsg_ctx *ctx);
+int tsg_device_count(tsg_ctx *ctx);
+const char *tsg_last_error(void);
+int tsg_abi_version(void);
+int tsg_cancel(tsg_ctx *ctx, uint64_t query_id);
+
+/* ---- pipeline (request normalisation, host) ---------------------------------- */
+int tsg_pipeline_new(const tsg_request *req, tsg_pipeline **out);
+const tsg_query *tsg_pipeline_query(const tsg_pipeline *p);
+void tsg_pipeline_free(tsg_pipeline *p);
+/* Pipeline.MatchesBlock on a raw search-header flatbuffer (pipeline.go:172-183). */
+int tsg_pipeline_matches_header(const tsg_query *q, const uint8_t *header, size_t len,
+                                int *matches);
+
+/* ---- backend search blocks ------------------------------------------------------ */
+/* Reads <block_dir>/{search.meta.json,search-header,search-index,search}, validates
+ * checksums and framing, decodes every page once into the device-resident
+ * columnar layout on device (device_hint % devices). */
+int tsg_block_open(tsg_ctx *ctx, const char *block_dir, int device_hint, tsg_block **out);
+/* Same from caller buffers (copied). meta_json may be NULL -> TSG_E_NOT_FOUND. */
+int tsg_block_open_mem(tsg_ctx *ctx, const uint8_t *meta_json, size_t meta_len,
+                       const uint8_t *header, size_t header_len, const uint8_t *index,
+                       size_t index_len, const uint8_t *data, size_t data_len, int device_hint,
+                       tsg_block **out);
+void tsg_block_close(tsg_block *b);
+
+typedef struct tsg_block_info {
+  uint64_t entries;
+  uint64_t pages;
+  uint64_t keys;
+  uint64_t header_bytes;
+  uint64_t fb_bytes;       /* sum of flatbuffer page bytes (bytesInspected per full scan) */
+  uint64_t device_bytes;   /* resident bytes on device */
+  uint64_t min_dur_ns;     /* on-disk search-header values (pitfall P1) */
+  uint64_t max_dur_ns;
+  int32_t device;
+  int32_t encoding;        /* backend.Encoding numeric value */
+} tsg_block_info;
+int tsg_block_info_get(const tsg_block *b, tsg_block_info *out);
+
+/* BackendSearchBlock.Tags / TagValues from the block header. Output is a
+ * packed list: u32 len + bytes, repeated; *out_n = count. Free with tsg_free. */
+int tsg_block_tags(const tsg_block *b, uint8_t **out, size_t *out_len, size_t *out_n);
+int tsg_block_tag_values(const tsg_block *b, const uint8_t *key, size_t klen, uint8_t **out,
+                         size_t *out_len, size_t *out_n);
+void tsg_free(void *p);
+
+/* Search blocks[0..nblocks) with the normalised query. Blocks may live on
+ * different devices; the result is the single ordered sequence described at
+ * tsg_result. */
+int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
+               const tsg_search_opts *opts, tsg_result **out);
+void tsg_result_free(tsg_result *r);
+
+/* instance.Search consumer on an ordered match sequence: dedupe by trace ID with
+ * CombineSearchResults, stop at max_results distinct (0 -> 20), then sort by
+ * StartTimeUnixNano descending (ties: first scan position). Output has the same
+ * layout as tsg_result (block_idx/entry_idx = first occurrence). */
+int tsg_results_combine(const tsg_result *in, uint32_t max_results, tsg_result **out);
+
+/* ---- v2 trace blocks: batched trace-ID lookup --------------------------------- */
+/* Reads <block_dir>/{meta.json,bloom-N...,index}; verifies index page checksums. */
+int tsg_v2block_open(tsg_ctx *ctx, const char *block_dir, int device_hint, tsg_v2block **out);
+void tsg_v2block_close(tsg_v2block *b);
+
+typedef struct tsg_lookup_opts {
+  uint32_t time_start; /* tempodb.Find window (unix s); both 0 = no time filter */
+  uint32_t time_end;
+  const uint8_t *block_start; /* 16-byte blockID shard range, NULL = no range */
+  const uint8_t *block_end;
+} tsg_lookup_opts;
+
+/* One hit per (id, block) pair where includeBlock passes, bloom.Test is true
+ * and the index lower_bound is < TotalRecords, sorted by (id_idx, block_idx).
+ * Exactly the (record, i) pairs the reference hands to findOne
+ * (tempodb/encoding/v2/finder_paged.go:37-48); bloom false positives included. */
+typedef struct tsg_lookup_result {
+  uint64_t n;
+  const uint32_t *id_idx;
+  const uint32_t *block_idx;
+  const int32_t *record_idx;
+  const uint64_t *record_start;
+  const uint32_t *record_length;
+  uint64_t kernel_ns;
+} tsg_lookup_result;
+
+int tsg_lookup_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks,
+                   const uint8_t (*ids)[16], size_t nids, const tsg_lookup_opts *opts,
+                   tsg_lookup_result **out);
+void tsg_lookup_result_free(tsg_lookup_result *r);
+
+/* ---- block writer (tooling: synthetic data and test fixtures) ----------------- */
+/* Entry list wire format (little endian), one record per trace:
+ *   u32 id_len, id bytes, u64 start_ns, u64 end_ns, u32 ntags,
+ *   ntags x (u32 klen, key, u32 vlen, value)
+ * Restates NewBackendSearchBlock (tempodb/search/backend_search_block.go:28-129):
+ * entries sorted ascending by id (duplicate ids rejected), tags lowercased,
+ * one flatbuffer SearchPage per v2 data page cut when the builder bytes exceed
+ * page_size_bytes, index pages of 100 KiB, header, search.meta.json.
+ * encoding: backend.Encoding numeric value (0 none, 6 snappy). */
+int tsg_write_search_block(const char *block_dir, const uint8_t *entries, size_t len,
+                           int encoding, uint32_t page_size_bytes);
+
+/* SearchEntryMutable.ToBytes (pkg/tempofb/search_entry_mutable.go:41-46) for one
+ * entry in the wire format above; SearchBlockHeaderMutable.ToBytes from a list
+ * of entries (pkg/tempofb/SearchBlockHeader_util.go:23-75). Free with tsg_free. */
+int tsg_fb_search_entry(const uint8_t *entry, size_t len, uint8_t **out, size_t *out_len);
+int tsg_fb_search_header(const uint8_t *entries, size_t len, uint8_t **out, size_t *out_len);
+
+/* Synthetic block generator (SURVEY.md §8 d): seeded, writes a search block with
+ * n entries to block_dir. profile 0 = standard (~20 tags), 1 = high-cardinality
+ * (adds long db.statement values). */
+int tsg_synth_search_block(const char *block_dir, uint64_t n, uint64_t seed, int profile,
+                           int encoding, uint32_t page_size_bytes);
+
+/* Synthetic v2 trace block: n random 16-byte ids (returned sorted in ids_out if
+ * non-NULL), dummy objects, bloom fp 0.01 / shard 100 KiB, index page 250 KiB,
+ * data pages ~1 MiB (modules/storage/config.go:47-53). */
+int tsg_synth_v2_block(const char *block_dir, uint64_t n, uint64_t seed, uint8_t (*ids_out)[16]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TSG_H */

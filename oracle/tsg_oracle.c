@@ -1,0 +1,1488 @@
+/*
+ * tsg_oracle.c — CPU ORACLE for the Tempo search path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Literal restatement of the reference Go code, function by function, each
+ * citing the reference file:line it follows (paths relative to the reference
+ * checkout). Deliberately written the way the reference executes it: per-search
+ * snappy decode, flatbuffer pointer chasing, binary search over the descending
+ * key vector, bytes.Contains over values. It is the parity checker for libtsg
+ * and the CPU baseline in bench.py; it is never linked into the product.
+ * Parity pinning: see tsg_oracle.h and tests/golden/README.md.
+ */
+#define _GNU_SOURCE
+#include "tsg_oracle.h"
+
+#include <dirent.h>
+#include <errno.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+
+/* ------------------------------------------------------------------------- */
+/* byte helpers (encoding/binary LittleEndian / BigEndian)                     */
+static inline uint16_t le16(const uint8_t *p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static inline uint32_t le32(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+static inline uint64_t le64(const uint8_t *p) { return (uint64_t)le32(p) | ((uint64_t)le32(p + 4) << 32); }
+static inline uint64_t be64(const uint8_t *p) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
+  return v;
+}
+
+void orc_free(void *p) { free(p); }
+
+/* bytes.Compare */
+static int bytes_compare(const uint8_t *a, size_t al, const uint8_t *b, size_t bl) {
+  size_t n = al < bl ? al : bl;
+  int c = n ? memcmp(a, b, n) : 0;
+  if (c != 0) return c < 0 ? -1 : 1;
+  if (al == bl) return 0;
+  return al < bl ? -1 : 1;
+}
+
+/* bytes.Contains (an empty needle is contained in everything) */
+static int bytes_contains(const uint8_t *h, size_t hl, const uint8_t *n, size_t nl) {
+  if (nl == 0) return 1;
+  if (nl > hl) return 0;
+  for (size_t i = 0; i + nl <= hl; i++)
+    if (h[i] == n[0] && memcmp(h + i, n, nl) == 0) return 1;
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* xxhash64, seed 0 (github.com/cespare/xxhash v1.1.0, Sum64 / Digest)         */
+#define XP1 11400714785074694791ULL
+#define XP2 14029467366897019727ULL
+#define XP3 1609587929392839161ULL
+#define XP4 9650029242287828579ULL
+#define XP5 2870177450012600261ULL
+static inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static inline uint64_t xround(uint64_t acc, uint64_t in) {
+  acc += in * XP2;
+  acc = rotl64(acc, 31);
+  return acc * XP1;
+}
+static inline uint64_t xmerge(uint64_t acc, uint64_t v) {
+  v = xround(0, v);
+  acc ^= v;
+  return acc * XP1 + XP4;
+}
+uint64_t orc_xxhash64(const uint8_t *p, size_t n) {
+  const uint8_t *end = p + n;
+  uint64_t h;
+  if (n >= 32) {
+    uint64_t v1 = XP1 + XP2, v2 = XP2, v3 = 0, v4 = (uint64_t)0 - XP1;
+    while (end - p >= 32) {
+      v1 = xround(v1, le64(p));
+      v2 = xround(v2, le64(p + 8));
+      v3 = xround(v3, le64(p + 16));
+      v4 = xround(v4, le64(p + 24));
+      p += 32;
+    }
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = xmerge(h, v1);
+    h = xmerge(h, v2);
+    h = xmerge(h, v3);
+    h = xmerge(h, v4);
+  } else {
+    h = XP5;
+  }
+  h += (uint64_t)n;
+  while (end - p >= 8) {
+    h ^= xround(0, le64(p));
+    h = rotl64(h, 27) * XP1 + XP4;
+    p += 8;
+  }
+  if (end - p >= 4) {
+    h ^= (uint64_t)le32(p) * XP1;
+    h = rotl64(h, 23) * XP2 + XP3;
+    p += 4;
+  }
+  while (p < end) {
+    h ^= (uint64_t)(*p) * XP5;
+    h = rotl64(h, 11) * XP1;
+    p++;
+  }
+  h ^= h >> 33;
+  h *= XP2;
+  h ^= h >> 29;
+  h *= XP3;
+  h ^= h >> 32;
+  return h;
+}
+
+/* ------------------------------------------------------------------------- */
+/* FNV-1 32 (hash/fnv New32) as used by util.TokenForTraceID (pkg/util/hash.go:15-20) */
+uint32_t orc_fnv1_32(const uint8_t *p, size_t n) {
+  uint32_t h = 2166136261u;
+  for (size_t i = 0; i < n; i++) {
+    h *= 16777619u;
+    h ^= p[i];
+  }
+  return h;
+}
+
+/* ------------------------------------------------------------------------- */
+/* murmur3 x64 128, seed 0 (vendor/github.com/spaolacci/murmur3/murmur128.go:62-200) */
+#define MC1 0x87c37b91114253d5ULL
+#define MC2 0x4cf5ad432745937fULL
+static inline uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+void orc_murmur3_128(const uint8_t *p, size_t n, uint64_t out[2]) {
+  uint64_t h1 = 0, h2 = 0;
+  size_t nblocks = n / 16;
+  for (size_t i = 0; i < nblocks; i++) {
+    uint64_t k1 = le64(p + i * 16), k2 = le64(p + i * 16 + 8);
+    k1 *= MC1; k1 = rotl64(k1, 31); k1 *= MC2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= MC2; k2 = rotl64(k2, 33); k2 *= MC1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+  }
+  const uint8_t *t = p + nblocks * 16;
+  uint64_t k1 = 0, k2 = 0;
+  switch (n & 15) {
+  case 15: k2 ^= (uint64_t)t[14] << 48; /* fallthrough */
+  case 14: k2 ^= (uint64_t)t[13] << 40; /* fallthrough */
+  case 13: k2 ^= (uint64_t)t[12] << 32; /* fallthrough */
+  case 12: k2 ^= (uint64_t)t[11] << 24; /* fallthrough */
+  case 11: k2 ^= (uint64_t)t[10] << 16; /* fallthrough */
+  case 10: k2 ^= (uint64_t)t[9] << 8; /* fallthrough */
+  case 9:
+    k2 ^= (uint64_t)t[8];
+    k2 *= MC2; k2 = rotl64(k2, 33); k2 *= MC1; h2 ^= k2;
+    /* fallthrough */
+  case 8: k1 ^= (uint64_t)t[7] << 56; /* fallthrough */
+  case 7: k1 ^= (uint64_t)t[6] << 48; /* fallthrough */
+  case 6: k1 ^= (uint64_t)t[5] << 40; /* fallthrough */
+  case 5: k1 ^= (uint64_t)t[4] << 32; /* fallthrough */
+  case 4: k1 ^= (uint64_t)t[3] << 24; /* fallthrough */
+  case 3: k1 ^= (uint64_t)t[2] << 16; /* fallthrough */
+  case 2: k1 ^= (uint64_t)t[1] << 8; /* fallthrough */
+  case 1:
+    k1 ^= (uint64_t)t[0];
+    k1 *= MC1; k1 = rotl64(k1, 31); k1 *= MC2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)n;
+  h2 ^= (uint64_t)n;
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  h1 += h2;
+  h2 += h1;
+  out[0] = h1;
+  out[1] = h2;
+}
+
+/* ------------------------------------------------------------------------- */
+/* CRC-32C (Castagnoli) + snappy framing mask (vendor/github.com/golang/snappy/snappy.go:91-95) */
+static uint32_t crc_tab[256];
+static pthread_once_t crc_once = PTHREAD_ONCE_INIT;
+static void crc_init(void) {
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+    crc_tab[i] = c;
+  }
+}
+uint32_t orc_crc32c(const uint8_t *p, size_t n) {
+  pthread_once(&crc_once, crc_init);
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) c = crc_tab[(c ^ p[i]) & 0xff] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+static uint32_t snappy_mask(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
+
+/* snappy block decode (vendor/github.com/golang/snappy/decode.go:27-75, decode_other.go:1-115) */
+static int snappy_decoded_len(const uint8_t *src, size_t n, uint64_t *dlen, size_t *hlen) {
+  uint64_t v = 0;
+  int shift = 0;
+  for (size_t i = 0; i < n && i < 10; i++) {
+    uint8_t b = src[i];
+    if (b < 0x80) {
+      if (i == 9 && b > 1) return ORC_CORRUPT; /* overflow */
+      v |= (uint64_t)b << shift;
+      if (v > 0xffffffffULL) return ORC_CORRUPT;
+      *dlen = v;
+      *hlen = i + 1;
+      return ORC_OK;
+    }
+    v |= (uint64_t)(b & 0x7f) << shift;
+    shift += 7;
+  }
+  return ORC_CORRUPT;
+}
+static int snappy_decode_block(uint8_t *dst, size_t dlen, const uint8_t *src, size_t slen) {
+  size_t d = 0, s = 0;
+  while (s < slen) {
+    size_t length = 0, offset = 0;
+    uint8_t tag = src[s] & 3;
+    if (tag == 0) {
+      uint32_t x = src[s] >> 2;
+      if (x < 60) {
+        s += 1;
+      } else {
+        size_t nb = x - 59; /* 1..4 length bytes */
+        s += 1 + nb;
+        if (s > slen) return ORC_CORRUPT;
+        x = 0;
+        for (size_t i = 0; i < nb; i++) x |= (uint32_t)src[s - nb + i] << (8 * i);
+      }
+      length = (size_t)x + 1;
+      if (length == 0) return ORC_CORRUPT;
+      if (length > dlen - d || length > slen - s) return ORC_CORRUPT;
+      memcpy(dst + d, src + s, length);
+      d += length;
+      s += length;
+      continue;
+    } else if (tag == 1) {
+      s += 2;
+      if (s > slen) return ORC_CORRUPT;
+      length = 4 + ((src[s - 2] >> 2) & 7);
+      offset = ((size_t)(src[s - 2] & 0xe0) << 3) | src[s - 1];
+    } else if (tag == 2) {
+      s += 3;
+      if (s > slen) return ORC_CORRUPT;
+      length = 1 + (src[s - 3] >> 2);
+      offset = (size_t)src[s - 2] | ((size_t)src[s - 1] << 8);
+    } else {
+      s += 5;
+      if (s > slen) return ORC_CORRUPT;
+      length = 1 + (src[s - 5] >> 2);
+      offset = (size_t)le32(src + s - 4);
+    }
+    if (offset == 0 || d < offset || length > dlen - d) return ORC_CORRUPT;
+    for (size_t i = 0; i < length; i++) dst[d + i] = dst[d - offset + i]; /* forward copy */
+    d += length;
+  }
+  return d == dlen ? ORC_OK : ORC_CORRUPT;
+}
+
+/* snappy.Reader.fill over a whole page (vendor/github.com/golang/snappy/decode.go:121-235):
+ * first chunk must be the stream identifier; 0x00 compressed, 0x01 uncompressed,
+ * both CRC32C-masked; 0x02-0x7f unsupported; 0x80-0xfe skipped. */
+#define SNAPPY_MAX_BLOCK 65536
+#define SNAPPY_MAX_ENC 76490
+int orc_snappy_framed_decode(const uint8_t *src, size_t n, uint8_t **out, size_t *out_len) {
+  size_t cap = 1 << 16, len = 0, s = 0;
+  uint8_t *o = (uint8_t *)malloc(cap);
+  uint8_t *blk = (uint8_t *)malloc(SNAPPY_MAX_BLOCK);
+  int read_header = 0, rc = ORC_OK;
+  const size_t buflen = SNAPPY_MAX_ENC + 4;
+  while (s < n) {
+    if (n - s < 4) { rc = ORC_CORRUPT; break; }
+    uint8_t ct = src[s];
+    size_t cl = (size_t)src[s + 1] | ((size_t)src[s + 2] << 8) | ((size_t)src[s + 3] << 16);
+    s += 4;
+    if (!read_header) {
+      if (ct != 0xff) { rc = ORC_CORRUPT; break; }
+      read_header = 1;
+    }
+    if (cl > buflen) { rc = ORC_CORRUPT; break; }
+    if (cl > n - s) { rc = ORC_CORRUPT; break; }
+    const uint8_t *body = src + s;
+    s += cl;
+    if (ct == 0x00 || ct == 0x01) {
+      if (cl < 4) { rc = ORC_CORRUPT; break; }
+      uint32_t csum = le32(body);
+      const uint8_t *payload = body + 4;
+      size_t pl = cl - 4;
+      const uint8_t *dec;
+      size_t dn;
+      if (ct == 0x00) {
+        uint64_t dl;
+        size_t hl;
+        if (snappy_decoded_len(payload, pl, &dl, &hl) != ORC_OK) { rc = ORC_CORRUPT; break; }
+        if (dl > SNAPPY_MAX_BLOCK) { rc = ORC_CORRUPT; break; }
+        if (snappy_decode_block(blk, (size_t)dl, payload + hl, pl - hl) != ORC_OK) { rc = ORC_CORRUPT; break; }
+        dec = blk;
+        dn = (size_t)dl;
+      } else {
+        if (pl > SNAPPY_MAX_BLOCK) { rc = ORC_CORRUPT; break; }
+        dec = payload;
+        dn = pl;
+      }
+      if (snappy_mask(orc_crc32c(dec, dn)) != csum) { rc = ORC_CORRUPT; break; }
+      if (len + dn > cap) {
+        while (len + dn > cap) cap *= 2;
+        o = (uint8_t *)realloc(o, cap);
+      }
+      memcpy(o + len, dec, dn);
+      len += dn;
+    } else if (ct == 0xff) {
+      if (cl != 6 || memcmp(body, "sNaPpY", 6) != 0) { rc = ORC_CORRUPT; break; }
+    } else if (ct <= 0x7f) {
+      rc = ORC_UNSUPPORTED_ENCODING;
+      break;
+    } /* else padding / skippable */
+  }
+  free(blk);
+  if (rc != ORC_OK) {
+    free(o);
+    return rc;
+  }
+  *out = o;
+  *out_len = len;
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* flatbuffers table access (vendor/github.com/google/flatbuffers/go/table.go:14-57) */
+typedef struct fbt {
+  const uint8_t *b;
+  size_t n;
+  uint32_t pos;
+} fbt;
+/* Bounds are checked so corrupt input cannot crash the checker; a well-formed
+ * buffer reads exactly as table.go does. */
+static int fb_ok(const fbt *t, uint64_t off, uint64_t len) { return off + len <= t->n; }
+static uint16_t fb_offset(const fbt *t, uint16_t vto) {
+  if (!fb_ok(t, t->pos, 4)) return 0;
+  int32_t so = (int32_t)le32(t->b + t->pos);
+  int64_t vt = (int64_t)t->pos - so;
+  if (vt < 0 || !fb_ok(t, (uint64_t)vt, 2)) return 0;
+  uint16_t vlen = le16(t->b + vt);
+  if (vto < vlen && fb_ok(t, (uint64_t)vt + vto, 2)) return le16(t->b + vt + vto);
+  return 0;
+}
+static uint32_t fb_indirect(const fbt *t, uint32_t off) {
+  if (!fb_ok(t, off, 4)) return 0;
+  return off + le32(t->b + off);
+}
+static uint32_t fb_vector(const fbt *t, uint16_t o) { /* start of vector data */
+  uint32_t off = t->pos + o;
+  return fb_indirect(t, off) + 4;
+}
+static uint32_t fb_vector_len(const fbt *t, uint16_t o) {
+  uint32_t off = fb_indirect(t, t->pos + o);
+  if (!fb_ok(t, off, 4)) return 0;
+  return le32(t->b + off);
+}
+static const uint8_t *fb_byte_vector(const fbt *t, uint32_t off, uint32_t *len) {
+  off = fb_indirect(t, off);
+  if (!fb_ok(t, off, 4)) { *len = 0; return NULL; }
+  uint32_t l = le32(t->b + off);
+  if (!fb_ok(t, (uint64_t)off + 4, l)) { *len = 0; return NULL; }
+  *len = l;
+  return t->b + off + 4;
+}
+static fbt fb_root(const uint8_t *b, size_t n) {
+  fbt t = {b, n, 0};
+  if (n >= 4) t.pos = le32(b);
+  return t;
+}
+static uint64_t fb_u64(const fbt *t, uint16_t vto) {
+  uint16_t o = fb_offset(t, vto);
+  if (o && fb_ok(t, (uint64_t)t->pos + o, 8)) return le64(t->b + t->pos + o);
+  return 0;
+}
+
+/* generated accessors (pkg/tempofb/{SearchEntry,SearchPage,SearchBlockHeader,KeyValues}.go): SearchEntry{id 4, tags 6, start 8, end 10},
+ * SearchPage{tags 4, entries 6}, SearchBlockHeader{tags 4, min 6, max 8}, KeyValues{key 4, value 6}.
+ * A "tag container" (FBTagContainer, searchdata_util.go:42-45) is any table whose
+ * [KeyValues] vector sits at vtable offset tag_vto. */
+#define VT_ENTRY_ID 4
+#define VT_ENTRY_TAGS 6
+#define VT_ENTRY_START 8
+#define VT_ENTRY_END 10
+#define VT_PAGE_TAGS 4
+#define VT_PAGE_ENTRIES 6
+#define VT_HDR_TAGS 4
+#define VT_HDR_MIN 6
+#define VT_HDR_MAX 8
+#define VT_KV_KEY 4
+#define VT_KV_VALUE 6
+
+static uint32_t tc_len(const fbt *t, uint16_t tag_vto) { /* TagsLength */
+  uint16_t o = fb_offset(t, tag_vto);
+  return o ? fb_vector_len(t, o) : 0;
+}
+static int tc_tag(const fbt *t, uint16_t tag_vto, uint32_t j, fbt *kv) { /* Tags(obj, j) */
+  uint16_t o = fb_offset(t, tag_vto);
+  if (!o) return 0;
+  uint32_t x = fb_vector(t, o) + j * 4;
+  kv->b = t->b;
+  kv->n = t->n;
+  kv->pos = fb_indirect(t, x);
+  return 1;
+}
+static const uint8_t *kv_key(const fbt *kv, uint32_t *len) { /* KeyValues.Key */
+  uint16_t o = fb_offset(kv, VT_KV_KEY);
+  if (!o) { *len = 0; return NULL; }
+  return fb_byte_vector(kv, o + kv->pos, len);
+}
+static uint32_t kv_value_len(const fbt *kv) {
+  uint16_t o = fb_offset(kv, VT_KV_VALUE);
+  return o ? fb_vector_len(kv, o) : 0;
+}
+static const uint8_t *kv_value(const fbt *kv, uint32_t j, uint32_t *len) { /* KeyValues.Value(j) */
+  uint16_t o = fb_offset(kv, VT_KV_VALUE);
+  if (!o) { *len = 0; return NULL; }
+  uint32_t a = fb_vector(kv, o);
+  return fb_byte_vector(kv, a + j * 4, len);
+}
+
+/* FindTag / binarySearch (pkg/tempofb/searchdata_util.go:63-100): the vector is
+ * written descending, so the comparator is bytes.Compare(kv.Key(), k) and
+ * cmp=-1 -> j=h, +1 -> i=h+1. */
+static int find_tag(const fbt *t, uint16_t tag_vto, const uint8_t *k, size_t kl, fbt *kv) {
+  uint32_t i = 0, j = tc_len(t, tag_vto);
+  while (i < j) {
+    uint32_t h = (i + j) >> 1;
+    tc_tag(t, tag_vto, h, kv);
+    uint32_t klen;
+    const uint8_t *key = kv_key(kv, &klen);
+    int c = bytes_compare(key, klen, k, kl);
+    if (c == 0) return 1;
+    if (c == -1) j = h;
+    else i = h + 1;
+  }
+  return 0;
+}
+/* ContainsTag (searchdata_util.go:47-61) */
+static int contains_tag(const fbt *t, uint16_t tag_vto, const uint8_t *k, size_t kl, const uint8_t *v,
+                        size_t vl) {
+  fbt kv;
+  if (!find_tag(t, tag_vto, k, kl, &kv)) return 0;
+  uint32_t l = kv_value_len(&kv);
+  for (uint32_t j = 0; j < l; j++) {
+    uint32_t len;
+    const uint8_t *val = kv_value(&kv, j, &len);
+    if (bytes_contains(val, len, v, vl)) return 1;
+  }
+  return 0;
+}
+/* SearchEntry.Get (searchdata_util.go:10-23): linear scan, Value(0) of first key match. */
+static const uint8_t *entry_get(const fbt *e, const char *k, uint32_t *len) {
+  size_t kl = strlen(k);
+  uint32_t n = tc_len(e, VT_ENTRY_TAGS);
+  fbt kv;
+  for (uint32_t i = 0; i < n; i++) {
+    tc_tag(e, VT_ENTRY_TAGS, i, &kv);
+    uint32_t klen;
+    const uint8_t *key = kv_key(&kv, &klen);
+    if (klen == kl && memcmp(key, k, kl) == 0) {
+      if (kv_value_len(&kv) == 0) { *len = 0; return NULL; }
+      return kv_value(&kv, 0, len);
+    }
+  }
+  *len = 0;
+  return NULL;
+}
+
+/* ------------------------------------------------------------------------- */
+/* strings.ToLower (Go). ASCII exactly; beyond ASCII a documented subset of
+ * unicode.ToLower (Latin-1, Latin Extended-A, Greek, Cyrillic, Armenian) and
+ * invalid UTF-8 -> U+FFFD as strings.Map does. Non-ASCII folding is
+ * "parity unpinned" (DESIGN.md): the Go host passes lowered bytes (pitfall P4). */
+static uint32_t uni_lower(uint32_t r) {
+  if (r >= 'A' && r <= 'Z') return r + 32;
+  if (r < 0x80) return r;
+  if (r >= 0xC0 && r <= 0xDE && r != 0xD7) return r + 32;
+  if (r == 0x130) return 0x69;
+  if (r == 0x178) return 0xFF;
+  if ((r >= 0x100 && r <= 0x12F) || (r >= 0x132 && r <= 0x137) || (r >= 0x14A && r <= 0x177))
+    return (r & 1) ? r : r + 1;
+  if ((r >= 0x139 && r <= 0x148) || (r >= 0x179 && r <= 0x17E)) return (r & 1) ? r + 1 : r;
+  if (r == 0x386) return 0x3AC;
+  if (r >= 0x388 && r <= 0x38A) return r + 37;
+  if (r == 0x38C) return 0x3CC;
+  if (r == 0x38E || r == 0x38F) return r + 63;
+  if ((r >= 0x391 && r <= 0x3A1) || (r >= 0x3A3 && r <= 0x3AB)) return r + 32;
+  if (r >= 0x400 && r <= 0x40F) return r + 80;
+  if (r >= 0x410 && r <= 0x42F) return r + 32;
+  if (r >= 0x531 && r <= 0x556) return r + 48;
+  return r;
+}
+/* utf8.DecodeRune: returns rune and width; invalid -> (0xFFFD, 1) */
+static uint32_t utf8_decode(const uint8_t *s, size_t n, size_t *w) {
+  uint8_t c = s[0];
+  if (c < 0x80) { *w = 1; return c; }
+  uint32_t r;
+  size_t need;
+  uint32_t minv;
+  if (c >= 0xC2 && c <= 0xDF) { need = 2; r = c & 0x1F; minv = 0x80; }
+  else if (c >= 0xE0 && c <= 0xEF) { need = 3; r = c & 0x0F; minv = 0x800; }
+  else if (c >= 0xF0 && c <= 0xF4) { need = 4; r = c & 0x07; minv = 0x10000; }
+  else { *w = 1; return 0xFFFD; }
+  if (n < need) { *w = 1; return 0xFFFD; }
+  for (size_t i = 1; i < need; i++) {
+    if ((s[i] & 0xC0) != 0x80) { *w = 1; return 0xFFFD; }
+    r = (r << 6) | (s[i] & 0x3F);
+  }
+  if (r < minv || r > 0x10FFFF || (r >= 0xD800 && r <= 0xDFFF)) { *w = 1; return 0xFFFD; }
+  *w = need;
+  return r;
+}
+static size_t utf8_encode(uint32_t r, uint8_t *o) {
+  if (r < 0x80) { o[0] = (uint8_t)r; return 1; }
+  if (r < 0x800) { o[0] = 0xC0 | (r >> 6); o[1] = 0x80 | (r & 0x3F); return 2; }
+  if (r < 0x10000) { o[0] = 0xE0 | (r >> 12); o[1] = 0x80 | ((r >> 6) & 0x3F); o[2] = 0x80 | (r & 0x3F); return 3; }
+  o[0] = 0xF0 | (r >> 18); o[1] = 0x80 | ((r >> 12) & 0x3F); o[2] = 0x80 | ((r >> 6) & 0x3F); o[3] = 0x80 | (r & 0x3F);
+  return 4;
+}
+/* out must hold 3*n bytes */
+static size_t go_to_lower(const uint8_t *s, size_t n, uint8_t *out) {
+  int ascii = 1;
+  for (size_t i = 0; i < n; i++)
+    if (s[i] >= 0x80) { ascii = 0; break; }
+  if (ascii) {
+    for (size_t i = 0; i < n; i++) out[i] = (s[i] >= 'A' && s[i] <= 'Z') ? s[i] + 32 : s[i];
+    return n;
+  }
+  size_t o = 0;
+  for (size_t i = 0; i < n;) {
+    size_t w;
+    uint32_t r = utf8_decode(s + i, n - i, &w);
+    o += utf8_encode(uni_lower(r), out + o);
+    i += w;
+  }
+  return o;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Pipeline (tempodb/search/pipeline.go:26-183)                                  */
+typedef struct orc_pipeline {
+  uint32_t nterms;
+  uint8_t **k, **v;
+  size_t *kl, *vl;
+  int has_min, has_max, has_range, exhaustive;
+  uint64_t min_ns, max_ns;
+  uint32_t start, end;
+} orc_pipeline;
+
+static int eqs(const uint8_t *a, size_t al, const char *s) { return al == strlen(s) && memcmp(a, s, al) == 0; }
+
+/* NewSearchPipeline + rewriteTagLookup (pipeline.go:26-140) */
+static void pipeline_new(const orc_request *req, orc_pipeline *p) {
+  memset(p, 0, sizeof(*p));
+  if (req->min_duration_ms > 0) {
+    p->has_min = 1;
+    p->min_ns = (uint64_t)req->min_duration_ms * 1000000ULL;
+  }
+  if (req->max_duration_ms > 0) {
+    p->has_max = 1;
+    p->max_ns = (uint64_t)req->max_duration_ms * 1000000ULL;
+  }
+  if (req->start != 0 && req->end != 0) {
+    p->has_range = 1;
+    p->start = req->start;
+    p->end = req->end;
+  }
+  p->k = (uint8_t **)calloc(req->ntags + 1, sizeof(uint8_t *));
+  p->v = (uint8_t **)calloc(req->ntags + 1, sizeof(uint8_t *));
+  p->kl = (size_t *)calloc(req->ntags + 1, sizeof(size_t));
+  p->vl = (size_t *)calloc(req->ntags + 1, sizeof(size_t));
+  for (uint32_t i = 0; i < req->ntags; i++) {
+    const uint8_t *k = req->tag_keys[i], *v = req->tag_values[i];
+    size_t kl = req->tag_key_lens[i], vl = req->tag_value_lens[i];
+    const char *nk = NULL, *nv = NULL;
+    if (eqs(k, kl, "x-dbg-exhaustive")) { /* SecretExhaustiveSearchTag */
+      p->exhaustive = 1;
+      continue;
+    } else if (eqs(k, kl, "error")) { /* trace.ErrorTag */
+      if (eqs(v, vl, "true")) { nk = "status.code"; nv = "2"; }
+    } else if (eqs(k, kl, "status.code")) { /* StatusCodeMapping (pkg/model/trace/matches.go:27-31) */
+      if (eqs(v, vl, "unset")) { nk = "status.code"; nv = "0"; }
+      else if (eqs(v, vl, "ok")) { nk = "status.code"; nv = "1"; }
+      else if (eqs(v, vl, "error")) { nk = "status.code"; nv = "2"; }
+    }
+    if (nk) { k = (const uint8_t *)nk; kl = strlen(nk); v = (const uint8_t *)nv; vl = strlen(nv); }
+    uint32_t t = p->nterms++;
+    p->k[t] = (uint8_t *)malloc(3 * kl + 1);
+    p->v[t] = (uint8_t *)malloc(3 * vl + 1);
+    p->kl[t] = go_to_lower(k, kl, p->k[t]);
+    p->vl[t] = go_to_lower(v, vl, p->v[t]);
+  }
+}
+static void pipeline_free(orc_pipeline *p) {
+  for (uint32_t i = 0; i < p->nterms; i++) { free(p->k[i]); free(p->v[i]); }
+  free(p->k); free(p->v); free(p->kl); free(p->vl);
+}
+static int tagfilter(const orc_pipeline *p, const fbt *t, uint16_t vto) {
+  for (uint32_t i = 0; i < p->nterms; i++)
+    if (!contains_tag(t, vto, p->k[i], p->kl[i], p->v[i], p->vl[i])) return 0;
+  return 1;
+}
+/* Pipeline.Matches: trace filters then tag filter (pipeline.go:142-157) */
+static int pipeline_matches(const orc_pipeline *p, const fbt *e) {
+  uint64_t st = fb_u64(e, VT_ENTRY_START), et = fb_u64(e, VT_ENTRY_END);
+  if (p->has_min && !((et - st) >= p->min_ns)) return 0;
+  if (p->has_max && !((et - st) <= p->max_ns)) return 0;
+  if (p->has_range) {
+    uint32_t ss = (uint32_t)(st / 1000000000ULL), es = (uint32_t)(et / 1000000000ULL);
+    if (!(p->start <= es && p->end >= ss)) return 0;
+  }
+  if (p->exhaustive) return 0;
+  return tagfilter(p, e, VT_ENTRY_TAGS);
+}
+/* MatchesBlock (pipeline.go:172-183), blockfilters built at :38-41 and :53-56 */
+static int pipeline_matches_block(const orc_pipeline *p, const fbt *h) {
+  if (p->has_min && !(fb_u64(h, VT_HDR_MAX) >= p->min_ns)) return 0;
+  if (p->has_max && !(fb_u64(h, VT_HDR_MIN) <= p->max_ns)) return 0;
+  return tagfilter(p, h, VT_HDR_TAGS);
+}
+
+int orc_pipeline_matches_entry(const orc_request *req, const uint8_t *fb, size_t len) {
+  orc_pipeline p;
+  pipeline_new(req, &p);
+  fbt e = fb_root(fb, len);
+  int m = pipeline_matches(&p, &e);
+  pipeline_free(&p);
+  return m;
+}
+int orc_pipeline_matches_block(const orc_request *req, const uint8_t *fb, size_t len) {
+  orc_pipeline p;
+  pipeline_new(req, &p);
+  fbt h = fb_root(fb, len);
+  int m = pipeline_matches_block(&p, &h);
+  pipeline_free(&p);
+  return m;
+}
+int orc_contains_tag_entry(const uint8_t *fb, size_t len, const uint8_t *k, size_t kl, const uint8_t *v,
+                           size_t vl) {
+  fbt e = fb_root(fb, len);
+  return contains_tag(&e, VT_ENTRY_TAGS, k, kl, v, vl);
+}
+
+/* ------------------------------------------------------------------------- */
+/* files                                                                       */
+static int read_file(const char *dir, const char *name, uint8_t **out, size_t *len) {
+  char path[4096];
+  snprintf(path, sizeof path, "%s/%s", dir, name);
+  FILE *f = fopen(path, "rb");
+  if (!f) return errno == ENOENT ? ORC_NOT_FOUND : ORC_IO;
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  uint8_t *b = (uint8_t *)malloc(n > 0 ? (size_t)n : 1);
+  if (n > 0 && fread(b, 1, (size_t)n, f) != (size_t)n) { fclose(f); free(b); return ORC_IO; }
+  fclose(f);
+  *out = b;
+  *len = (size_t)n;
+  return ORC_OK;
+}
+
+/* minimal JSON field readers for the meta files */
+static const char *json_field(const char *js, size_t n, const char *name) {
+  char pat[128];
+  snprintf(pat, sizeof pat, "\"%s\"", name);
+  const char *p = (const char *)memmem(js, n, pat, strlen(pat));
+  if (!p) return NULL;
+  p += strlen(pat);
+  while (*p == ' ' || *p == ':') p++;
+  return p;
+}
+static int json_u64(const char *js, size_t n, const char *name, uint64_t *v) {
+  const char *p = json_field(js, n, name);
+  if (!p) return 0;
+  *v = strtoull(p, NULL, 10);
+  return 1;
+}
+static int json_str(const char *js, size_t n, const char *name, char *out, size_t cap) {
+  const char *p = json_field(js, n, name);
+  if (!p || *p != '"') return 0;
+  p++;
+  size_t i = 0;
+  while (*p && *p != '"' && i + 1 < cap) out[i++] = *p++;
+  out[i] = 0;
+  return 1;
+}
+/* backend.ParseEncoding (tempodb/backend/encoding.go:104-112), case-insensitive */
+static int parse_encoding(const char *s) {
+  static const char *names[] = {"none", "gzip", "lz4-64k", "lz4-256k", "lz4-1M", "lz4", "snappy", "zstd", "s2"};
+  for (int i = 0; i < 9; i++)
+    if (strcasecmp(s, names[i]) == 0) return i;
+  return -1;
+}
+
+/* ------------------------------------------------------------------------- */
+/* v2 framing                                                                  */
+/* unmarshalPageFromBytes (tempodb/encoding/v2/page.go:30-57) */
+static int unmarshal_page(const uint8_t *b, size_t n, size_t hdr_len_expected, const uint8_t **hdr,
+                          const uint8_t **data, size_t *dlen) {
+  size_t total_hdr = 6 + hdr_len_expected;
+  if (n < total_hdr) return ORC_CORRUPT;
+  uint32_t total = le32(b);
+  uint16_t hl = le16(b + 4);
+  if ((size_t)hl > n - 6) return ORC_CORRUPT;
+  if (hl != hdr_len_expected) return ORC_CORRUPT; /* dataHeader/indexHeader.unmarshalHeader */
+  *hdr = b + 6;
+  const uint8_t *rest = b + 6 + hl;
+  size_t rl = n - 6 - hl;
+  int64_t dl = (int64_t)total - (int64_t)total_hdr;
+  if (dl < 0 || (size_t)dl != rl) return ORC_CORRUPT;
+  *data = rest;
+  *dlen = rl;
+  return ORC_OK;
+}
+
+/* search-index / index reader (tempodb/encoding/v2/index_reader.go) */
+typedef struct orc_index {
+  const uint8_t *buf;
+  size_t len;
+  uint32_t page_size, total;
+  uint32_t per_page;
+  /* verified pages cache (pageCache) */
+  int8_t *checked;
+  size_t npages;
+} orc_index;
+static void index_init(orc_index *ix, const uint8_t *buf, size_t len, uint32_t page_size, uint32_t total) {
+  ix->buf = buf;
+  ix->len = len;
+  ix->page_size = page_size;
+  ix->total = total;
+  /* objectsPerPage(28, pageSize, 8) (page.go:175-182) */
+  ix->per_page = page_size > 14 ? (page_size - 8 - 6) / 28 : 0;
+  ix->npages = page_size ? (len + page_size - 1) / page_size : 0;
+  ix->checked = (int8_t *)calloc(ix->npages + 1, 1);
+}
+static void index_free(orc_index *ix) { free(ix->checked); }
+/* getPage (index_reader.go:116-143): read pageSize bytes at pageIdx*pageSize,
+ * unmarshal with an 8-byte header, verify xxhash64 of the page data. */
+static int index_page(orc_index *ix, size_t pidx, const uint8_t **data, size_t *dlen) {
+  uint64_t off = (uint64_t)pidx * ix->page_size;
+  if (off + ix->page_size > ix->len) return ORC_CORRUPT; /* ReadAt short read */
+  const uint8_t *hdr;
+  int rc = unmarshal_page(ix->buf + off, ix->page_size, 8, &hdr, data, dlen);
+  if (rc) return rc;
+  if (!ix->checked[pidx]) {
+    if (le64(hdr) != orc_xxhash64(*data, *dlen)) return ORC_CORRUPT; /* mismatched checksum */
+    ix->checked[pidx] = 1;
+  }
+  return ORC_OK;
+}
+/* At (index_reader.go:42-82); returns 1 record, 0 past end, <0 error */
+static int index_at(orc_index *ix, int64_t i, const uint8_t **rec) {
+  if (i < 0 || i >= (int64_t)ix->total) return 0;
+  if (ix->per_page == 0) return -ORC_CORRUPT;
+  size_t pidx = (size_t)(i / ix->per_page), ridx = (size_t)(i % ix->per_page);
+  const uint8_t *data;
+  size_t dlen;
+  int rc = index_page(ix, pidx, &data, &dlen);
+  if (rc) return -rc;
+  if (ridx >= dlen / 28) return -ORC_CORRUPT;
+  const uint8_t *r = data + ridx * 28;
+  int zero = 1;
+  for (int k = 0; k < 28; k++)
+    if (r[k]) { zero = 0; break; }
+  if (zero) return -ORC_CORRUPT;
+  *rec = r;
+  return 1;
+}
+/* Find (index_reader.go:85-114) with sort.SearchWithErrors (pkg/sort/search.go:5-24) */
+static int index_find(orc_index *ix, const uint8_t *id, size_t idl, int64_t *out) {
+  int64_t i = 0, j = ix->total;
+  while (i < j) {
+    int64_t h = (int64_t)(((uint64_t)(i + j)) >> 1);
+    const uint8_t *r;
+    int rc = index_at(ix, h, &r);
+    if (rc < 0) return -rc;
+    if (!(bytes_compare(r, 16, id, idl) >= 0)) i = h + 1;
+    else j = h;
+  }
+  *out = (i >= 0 && i < (int64_t)ix->total) ? i : -1;
+  return ORC_OK;
+}
+
+/* dataReader.Read for one record + decompression (data_reader.go:45-125) */
+static int data_read_page(const uint8_t *data, size_t dlen, int enc, uint64_t start, uint32_t length,
+                          uint8_t **out, size_t *out_len) {
+  if (start + length > dlen) return ORC_CORRUPT;
+  const uint8_t *hdr, *payload;
+  size_t pl;
+  int rc = unmarshal_page(data + start, length, 0, &hdr, &payload, &pl);
+  if (rc) return rc;
+  if (enc == 0) { /* EncNone: pass-through reader */
+    *out = (uint8_t *)malloc(pl ? pl : 1);
+    memcpy(*out, payload, pl);
+    *out_len = pl;
+    return ORC_OK;
+  }
+  if (enc == 6) return orc_snappy_framed_decode(payload, pl, out, out_len);
+  return ORC_UNSUPPORTED_ENCODING;
+}
+
+/* object.UnmarshalAndAdvanceBuffer (object.go:82-113) */
+static int unmarshal_advance(const uint8_t **buf, size_t *len, const uint8_t **id, uint32_t *idl,
+                             const uint8_t **obj, size_t *objl) {
+  if (*len == 0) return 1; /* io.EOF */
+  if (*len < 4) return -ORC_CORRUPT;
+  uint32_t total = le32(*buf);
+  if (*len - 4 < 4) return -ORC_CORRUPT;
+  uint32_t il = le32(*buf + 4);
+  const uint8_t *b = *buf + 8;
+  size_t bl = *len - 8;
+  uint32_t rest = total - 8;
+  if ((uint64_t)bl < rest) return -ORC_CORRUPT;
+  if (il > rest) return -ORC_CORRUPT; /* Go would panic on the slice */
+  *id = b;
+  *idl = il;
+  *obj = b + il;
+  *objl = rest - il;
+  *buf = b + rest;
+  *len = bl - rest;
+  return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* backend search block                                                        */
+struct orc_block {
+  int has_meta;
+  int enc;
+  char version[16];
+  uint32_t index_page_size, index_records;
+  uint8_t *header;
+  size_t header_len;
+  uint8_t *index;
+  size_t index_len;
+  uint8_t *data;
+  size_t data_len;
+};
+
+int orc_block_load(const char *dir, orc_block **out) {
+  orc_block *b = (orc_block *)calloc(1, sizeof(*b));
+  uint8_t *meta;
+  size_t ml;
+  int rc = read_file(dir, "search.meta.json", &meta, &ml);
+  if (rc == ORC_NOT_FOUND) { *out = b; return ORC_OK; } /* Search is a no-op */
+  if (rc) { free(b); return rc; }
+  b->has_meta = 1;
+  char enc[32] = {0};
+  uint64_t v;
+  json_str((const char *)meta, ml, "version", b->version, sizeof b->version);
+  json_str((const char *)meta, ml, "encoding", enc, sizeof enc);
+  b->enc = parse_encoding(enc);
+  b->index_page_size = json_u64((const char *)meta, ml, "indexPageSize", &v) ? (uint32_t)v : 0;
+  b->index_records = json_u64((const char *)meta, ml, "indexRecords", &v) ? (uint32_t)v : 0;
+  free(meta);
+  if ((rc = read_file(dir, "search-header", &b->header, &b->header_len)) ||
+      (rc = read_file(dir, "search-index", &b->index, &b->index_len)) ||
+      (rc = read_file(dir, "search", &b->data, &b->data_len))) {
+    orc_block_free(b);
+    return rc;
+  }
+  *out = b;
+  return ORC_OK;
+}
+void orc_block_free(orc_block *b) {
+  if (!b) return;
+  free(b->header);
+  free(b->index);
+  free(b->data);
+  free(b);
+}
+uint64_t orc_block_bytes(const orc_block *b) { return b->header_len + b->index_len + b->data_len; }
+
+/* growable match list */
+typedef struct mlist {
+  orc_match *m;
+  uint64_t n, cap;
+  char *s;
+  uint64_t sl, scap;
+  orc_metrics met;
+  int status;
+} mlist;
+static uint32_t ml_str(mlist *l, const uint8_t *p, uint32_t n) {
+  if (l->sl + n + 1 > l->scap) {
+    while (l->sl + n + 1 > l->scap) l->scap = l->scap ? l->scap * 2 : 4096;
+    l->s = (char *)realloc(l->s, l->scap);
+  }
+  uint32_t off = (uint32_t)l->sl;
+  if (n) memcpy(l->s + l->sl, p, n);
+  l->s[l->sl + n] = 0;
+  l->sl += n + 1;
+  return off;
+}
+static orc_match *ml_push(mlist *l) {
+  if (l->n == l->cap) {
+    l->cap = l->cap ? l->cap * 2 : 256;
+    l->m = (orc_match *)realloc(l->m, l->cap * sizeof(orc_match));
+  }
+  return &l->m[l->n++];
+}
+
+/* consumer state: deterministic refinement of instance.Search's loop
+ * (modules/ingester/instance_search.go:45-60): stop right after the first
+ * occurrence of the limit-th distinct trace ID. */
+/* Trace IDs are keyed by their right-aligned 16 bytes: TraceIDToHexString trims
+ * leading zeros, so hex-string equality == right-aligned byte equality. */
+typedef struct idset {
+  uint8_t (*k)[16];
+  uint8_t *used;
+  uint64_t cap, n;
+} idset;
+static int idset_add(idset *s, const uint8_t *id16) { /* 1 if new */
+  if (s->n * 2 + 2 > s->cap) {
+    uint64_t nc = s->cap ? s->cap * 2 : 64;
+    uint8_t(*nk)[16] = (uint8_t(*)[16])calloc(nc, 16);
+    uint8_t *nu = (uint8_t *)calloc(nc, 1);
+    for (uint64_t i = 0; i < s->cap; i++) {
+      if (!s->used[i]) continue;
+      uint64_t h = orc_xxhash64(s->k[i], 16) & (nc - 1);
+      while (nu[h]) h = (h + 1) & (nc - 1);
+      memcpy(nk[h], s->k[i], 16);
+      nu[h] = 1;
+    }
+    free(s->k);
+    free(s->used);
+    s->k = nk;
+    s->used = nu;
+    s->cap = nc;
+  }
+  uint64_t h = orc_xxhash64(id16, 16) & (s->cap - 1);
+  while (s->used[h]) {
+    if (memcmp(s->k[h], id16, 16) == 0) return 0;
+    h = (h + 1) & (s->cap - 1);
+  }
+  memcpy(s->k[h], id16, 16);
+  s->used[h] = 1;
+  s->n++;
+  return 1;
+}
+
+/* BackendSearchBlock.Search (tempodb/search/backend_search_block.go:184-298).
+ * `stop` (optional) = consumer: called per match, returns 1 when the consumer
+ * closed (the L-th distinct id arrived) -> the block stops right there. */
+typedef int (*consume_fn)(void *ctx, const orc_match *m);
+static int block_search(const orc_block *b, uint32_t bidx, const orc_pipeline *p, mlist *out,
+                        consume_fn consume, void *cctx, int *quit) {
+  if (!b->has_meta) return ORC_OK; /* ErrDoesNotExist -> nil (:191-203) */
+  if (strcmp(b->version, "v2") != 0) return ORC_UNSUPPORTED_ENCODING; /* encoding.FromVersion */
+  out->met.bytes_inspected += b->header_len; /* :217 */
+  fbt h = fb_root(b->header, b->header_len);
+  if (!pipeline_matches_block(p, &h)) {
+    out->met.blocks_skipped++;
+    return ORC_OK;
+  }
+  out->met.blocks_inspected++;
+  if (b->enc < 0) return ORC_UNSUPPORTED_ENCODING; /* NewDataReader -> getReaderPool */
+  orc_index ix;
+  index_init(&ix, b->index, b->index_len, b->index_page_size, b->index_records);
+  int rc = ORC_OK;
+  uint64_t scan_pos = 0;
+  for (int64_t i = 0;; i++) { /* for !sr.Quit() (:247) */
+    if (*quit) break;
+    const uint8_t *rec;
+    int r = index_at(&ix, i, &rec);
+    if (r <= 0) break; /* record == nil -> return nil (error is dropped: `record, _ := ir.At`) */
+    uint64_t start = le64(rec + 16);
+    uint32_t length = le32(rec + 24);
+    uint8_t *page;
+    size_t pl;
+    rc = data_read_page(b->data, b->data_len, b->enc, start, length, &page, &pl);
+    if (rc) break;
+    const uint8_t *cur = page, *id, *obj;
+    size_t cl = pl, objl;
+    uint32_t idl;
+    int u = unmarshal_advance(&cur, &cl, &id, &idl, &obj, &objl);
+    if (u != 0) { rc = u < 0 ? -u : ORC_CORRUPT; free(page); break; }
+    out->met.bytes_inspected += objl; /* :267 */
+    fbt pg = fb_root(obj, objl);
+    uint32_t ne = 0;
+    uint16_t eo = fb_offset(&pg, VT_PAGE_ENTRIES);
+    if (eo) ne = fb_vector_len(&pg, eo);
+    if (!tagfilter(p, &pg, VT_PAGE_TAGS)) { /* MatchesPage (:271-276) */
+      out->met.traces_inspected += ne;
+      scan_pos += ne;
+      free(page);
+      continue;
+    }
+    for (uint32_t j = 0; j < ne; j++) {
+      out->met.traces_inspected += 1;
+      fbt e;
+      e.b = pg.b;
+      e.n = pg.n;
+      e.pos = fb_indirect(&pg, fb_vector(&pg, eo) + j * 4);
+      if (!pipeline_matches(p, &e)) { scan_pos++; continue; }
+      /* GetSearchResultFromData (tempodb/search/util.go:27-35) */
+      orc_match *m = ml_push(out);
+      memset(m, 0, sizeof *m);
+      uint32_t il = 0;
+      const uint8_t *tid = NULL;
+      uint16_t io = fb_offset(&e, VT_ENTRY_ID);
+      if (io) tid = fb_byte_vector(&e, io + e.pos, &il);
+      if (il > 16) { rc = ORC_CORRUPT; break; }
+      memcpy(m->id + 16 - il, tid, il);
+      m->id_len = il;
+      m->block_idx = bidx;
+      m->entry_idx = scan_pos;
+      m->start_ns = fb_u64(&e, VT_ENTRY_START);
+      m->end_ns = fb_u64(&e, VT_ENTRY_END);
+      m->duration_ms = (uint32_t)((m->end_ns - m->start_ns) / 1000000ULL);
+      uint32_t sl, nl;
+      const uint8_t *sv = entry_get(&e, "root.service.name", &sl);
+      const uint8_t *nv = entry_get(&e, "root.name", &nl);
+      m->svc_off = ml_str(out, sv, sl);
+      m->svc_len = sl;
+      m->name_off = ml_str(out, nv, nl);
+      m->name_len = nl;
+      scan_pos++;
+      if (consume && consume(cctx, m)) { *quit = 1; break; }
+    }
+    free(page);
+    if (rc || *quit) break;
+  }
+  index_free(&ix);
+  return rc;
+}
+
+typedef struct limit_ctx {
+  idset ids;
+  uint32_t limit;
+  uint64_t distinct;
+} limit_ctx;
+static int limit_consume(void *c, const orc_match *m) {
+  limit_ctx *lc = (limit_ctx *)c;
+  if (idset_add(&lc->ids, m->id)) lc->distinct++;
+  return lc->distinct >= lc->limit;
+}
+
+typedef struct thr_arg {
+  const orc_block *b;
+  uint32_t bidx;
+  const orc_pipeline *p;
+  mlist out;
+  int rc;
+} thr_arg;
+static void *thr_main(void *a) {
+  thr_arg *t = (thr_arg *)a;
+  int quit = 0;
+  t->rc = block_search(t->b, t->bidx, t->p, &t->out, NULL, NULL, &quit);
+  return NULL;
+}
+
+static void finish(mlist *l, orc_result **out) {
+  orc_result *r = (orc_result *)calloc(1, sizeof *r);
+  r->n = l->n;
+  r->m = l->m;
+  r->strings = l->s;
+  r->strings_len = l->sl;
+  r->metrics = l->met;
+  r->status = l->status;
+  *out = r;
+}
+
+int orc_search(orc_block *const *blocks, uint32_t nblocks, const orc_request *req, uint32_t limit,
+               int nthreads, orc_result **out) {
+  orc_pipeline p;
+  pipeline_new(req, &p);
+  mlist all;
+  memset(&all, 0, sizeof all);
+  if (limit == 0 && nthreads > 1 && nblocks > 1) {
+    /* one thread per block (instance.searchLocalBlocks: a goroutine per block),
+     * at most nthreads in flight; concatenated in block order. */
+    thr_arg *ta = (thr_arg *)calloc(nblocks, sizeof *ta);
+    pthread_t *th = (pthread_t *)calloc(nblocks, sizeof *th);
+    for (uint32_t base = 0; base < nblocks; base += (uint32_t)nthreads) {
+      uint32_t e = base + (uint32_t)nthreads < nblocks ? base + (uint32_t)nthreads : nblocks;
+      for (uint32_t i = base; i < e; i++) {
+        ta[i].b = blocks[i];
+        ta[i].bidx = i;
+        ta[i].p = &p;
+        pthread_create(&th[i], NULL, thr_main, &ta[i]);
+      }
+      for (uint32_t i = base; i < e; i++) pthread_join(th[i], NULL);
+    }
+    for (uint32_t i = 0; i < nblocks; i++) {
+      mlist *l = &ta[i].out;
+      for (uint64_t k = 0; k < l->n; k++) {
+        orc_match *m = ml_push(&all);
+        *m = l->m[k];
+        m->svc_off = ml_str(&all, (const uint8_t *)l->s + l->m[k].svc_off, l->m[k].svc_len);
+        m->name_off = ml_str(&all, (const uint8_t *)l->s + l->m[k].name_off, l->m[k].name_len);
+      }
+      all.met.traces_inspected += l->met.traces_inspected;
+      all.met.blocks_inspected += l->met.blocks_inspected;
+      all.met.blocks_skipped += l->met.blocks_skipped;
+      all.met.bytes_inspected += l->met.bytes_inspected;
+      if (ta[i].rc && !all.status) all.status = ta[i].rc;
+      free(l->m);
+      free(l->s);
+    }
+    free(ta);
+    free(th);
+  } else {
+    limit_ctx lc;
+    memset(&lc, 0, sizeof lc);
+    lc.limit = limit;
+    int quit = 0;
+    for (uint32_t i = 0; i < nblocks && !quit; i++) {
+      int rc = block_search(blocks[i], i, &p, &all, limit ? limit_consume : NULL, &lc, &quit);
+      if (rc && !all.status) all.status = rc; /* searchLocalBlocks logs and continues */
+    }
+    free(lc.ids.k);
+    free(lc.ids.used);
+  }
+  pipeline_free(&p);
+  finish(&all, out);
+  return ORC_OK;
+}
+
+/* instance.Search consumer + CombineSearchResults + sort (instance_search.go:45-70,
+ * tempodb/search/util.go:40-62). Deterministic: tie on start -> first position. */
+typedef struct fin {
+  orc_match m;
+  uint64_t first;
+} fin;
+static int fin_cmp(const void *a, const void *b) {
+  const fin *x = (const fin *)a, *y = (const fin *)b;
+  if (x->m.start_ns != y->m.start_ns) return x->m.start_ns > y->m.start_ns ? -1 : 1;
+  return x->first < y->first ? -1 : (x->first > y->first);
+}
+int orc_combine(const orc_result *in, uint32_t max_results, orc_result **out) {
+  if (max_results == 0) max_results = 20;
+  fin *f = (fin *)calloc(in->n + 1, sizeof *f);
+  uint64_t nf = 0;
+  for (uint64_t i = 0; i < in->n; i++) {
+    const orc_match *m = &in->m[i];
+    uint64_t j;
+    for (j = 0; j < nf; j++) /* map lookup by TraceID (small lists) */
+      if (memcmp(f[j].m.id, m->id, 16) == 0) break;
+    if (j < nf) {
+      orc_match *e = &f[j].m;
+      if (e->svc_len == 0) { e->svc_off = m->svc_off; e->svc_len = m->svc_len; }
+      if (e->name_len == 0) { e->name_off = m->name_off; e->name_len = m->name_len; }
+      if (e->start_ns > m->start_ns) e->start_ns = m->start_ns;
+      if (e->duration_ms < m->duration_ms) e->duration_ms = m->duration_ms;
+    } else {
+      f[nf].m = *m;
+      f[nf].first = i;
+      nf++;
+    }
+    if (nf >= max_results) break;
+  }
+  qsort(f, nf, sizeof *f, fin_cmp);
+  orc_result *r = (orc_result *)calloc(1, sizeof *r);
+  r->n = nf;
+  r->m = (orc_match *)calloc(nf + 1, sizeof(orc_match));
+  for (uint64_t i = 0; i < nf; i++) r->m[i] = f[i].m;
+  r->strings = (char *)malloc(in->strings_len + 1);
+  memcpy(r->strings, in->strings, in->strings_len);
+  r->strings_len = in->strings_len;
+  r->metrics = in->metrics;
+  free(f);
+  *out = r;
+  return ORC_OK;
+}
+void orc_result_free(orc_result *r) {
+  if (!r) return;
+  free(r->m);
+  free(r->strings);
+  free(r);
+}
+
+/* ------------------------------------------------------------------------- */
+/* v2 trace blocks: bloom + index + findOne                                    */
+struct orc_v2block {
+  uint8_t block_id[16];
+  uint8_t min_id[64], max_id[64];
+  size_t min_len, max_len;
+  int64_t start_unix, end_unix;
+  int enc;
+  uint32_t index_page_size, total_records;
+  uint32_t bloom_shards; /* meta value (0 -> legacy 10) */
+  uint8_t **bloom;
+  size_t *bloom_len;
+  uint32_t nbloom;
+  uint8_t *index;
+  size_t index_len;
+  uint8_t *data;
+  size_t data_len;
+};
+
+static int b64val(char c) {
+  if (c >= 'A' && c <= 'Z') return c - 'A';
+  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+  if (c >= '0' && c <= '9') return c - '0' + 52;
+  if (c == '+') return 62;
+  if (c == '/') return 63;
+  return -1;
+}
+static size_t b64dec(const char *s, uint8_t *o, size_t cap) {
+  size_t n = 0;
+  uint32_t acc = 0;
+  int bits = 0;
+  for (; *s && *s != '"'; s++) {
+    int v = b64val(*s);
+    if (v < 0) continue;
+    acc = (acc << 6) | (uint32_t)v;
+    bits += 6;
+    if (bits >= 8) {
+      bits -= 8;
+      if (n < cap) o[n++] = (uint8_t)(acc >> bits);
+    }
+  }
+  return n;
+}
+static int64_t days_from_civil(int64_t y, unsigned m, unsigned d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = (unsigned)(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + (int64_t)doe - 719468;
+}
+/* time.Time JSON (RFC3339Nano) -> Unix() seconds */
+static int64_t rfc3339_unix(const char *s) {
+  int Y, M, D, h, mi, se;
+  if (sscanf(s, "%d-%d-%dT%d:%d:%d", &Y, &M, &D, &h, &mi, &se) != 6) return 0;
+  const char *p = strchr(s, 'T');
+  p += 9; /* hh:mm:ss */
+  if (*p == '.')
+    do p++; while (*p >= '0' && *p <= '9');
+  int64_t off = 0;
+  if (*p == '+' || *p == '-') {
+    int oh = 0, om = 0;
+    sscanf(p + 1, "%d:%d", &oh, &om);
+    off = (oh * 3600 + om * 60) * (*p == '-' ? -1 : 1);
+  }
+  return days_from_civil(Y, (unsigned)M, (unsigned)D) * 86400 + h * 3600 + mi * 60 + se - off;
+}
+static void parse_uuid(const char *s, uint8_t out[16]) {
+  int n = 0;
+  for (; *s && *s != '"' && n < 32; s++) {
+    int v;
+    if (*s >= '0' && *s <= '9') v = *s - '0';
+    else if (*s >= 'a' && *s <= 'f') v = *s - 'a' + 10;
+    else if (*s >= 'A' && *s <= 'F') v = *s - 'A' + 10;
+    else continue;
+    if (n % 2 == 0) out[n / 2] = (uint8_t)(v << 4);
+    else out[n / 2] |= (uint8_t)v;
+    n++;
+  }
+}
+
+int orc_v2block_load(const char *dir, orc_v2block **out) {
+  uint8_t *meta;
+  size_t ml;
+  int rc = read_file(dir, "meta.json", &meta, &ml);
+  if (rc) return rc;
+  orc_v2block *b = (orc_v2block *)calloc(1, sizeof *b);
+  const char *js = (const char *)meta;
+  char enc[32] = {0};
+  uint64_t v;
+  json_str(js, ml, "encoding", enc, sizeof enc);
+  b->enc = parse_encoding(enc);
+  b->index_page_size = json_u64(js, ml, "indexPageSize", &v) ? (uint32_t)v : 0;
+  b->total_records = json_u64(js, ml, "totalRecords", &v) ? (uint32_t)v : 0;
+  b->bloom_shards = json_u64(js, ml, "bloomShards", &v) ? (uint32_t)v : 0;
+  const char *p;
+  if ((p = json_field(js, ml, "minID")) && *p == '"') b->min_len = b64dec(p + 1, b->min_id, 64);
+  if ((p = json_field(js, ml, "maxID")) && *p == '"') b->max_len = b64dec(p + 1, b->max_id, 64);
+  if ((p = json_field(js, ml, "startTime")) && *p == '"') b->start_unix = rfc3339_unix(p + 1);
+  if ((p = json_field(js, ml, "endTime")) && *p == '"') b->end_unix = rfc3339_unix(p + 1);
+  if ((p = json_field(js, ml, "blockID")) && *p == '"') parse_uuid(p + 1, b->block_id);
+  free(meta);
+  /* common.ValidateShardCount (bloom.go:88-93) */
+  b->nbloom = b->bloom_shards ? b->bloom_shards : 10;
+  b->bloom = (uint8_t **)calloc(b->nbloom, sizeof(uint8_t *));
+  b->bloom_len = (size_t *)calloc(b->nbloom, sizeof(size_t));
+  for (uint32_t i = 0; i < b->nbloom; i++) {
+    char name[32];
+    snprintf(name, sizeof name, "bloom-%u", i); /* common.BloomName (block.go:15-17) */
+    rc = read_file(dir, name, &b->bloom[i], &b->bloom_len[i]);
+    if (rc == ORC_NOT_FOUND) { b->bloom[i] = NULL; rc = ORC_OK; }
+    if (rc) { orc_v2block_free(b); return rc; }
+  }
+  if ((rc = read_file(dir, "index", &b->index, &b->index_len)) ||
+      (rc = read_file(dir, "data", &b->data, &b->data_len))) {
+    if (rc == ORC_NOT_FOUND && b->index) rc = ORC_OK; /* data optional for id lookup */
+    if (rc) { orc_v2block_free(b); return rc; }
+  }
+  *out = b;
+  return ORC_OK;
+}
+void orc_v2block_free(orc_v2block *b) {
+  if (!b) return;
+  for (uint32_t i = 0; i < b->nbloom; i++) free(b->bloom[i]);
+  free(b->bloom);
+  free(b->bloom_len);
+  free(b->index);
+  free(b->data);
+  free(b);
+}
+uint32_t orc_v2_shard_count(const orc_v2block *b) { return b->nbloom; }
+
+/* willf/bloom Test after ReadFrom (vendor/github.com/willf/bloom/bloom.go:94-124,182-190,
+ * 310-325; bitset.go:159-164,853-875): big-endian m, k, bitlen, words. */
+static int bloom_test(const uint8_t *buf, size_t len, const uint8_t *id, size_t idl) {
+  if (!buf || len < 24) return -ORC_CORRUPT;
+  uint64_t m = be64(buf), k = be64(buf + 8), bitlen = be64(buf + 16);
+  uint64_t nwords = (bitlen + 63) / 64; /* wordsNeeded */
+  if (24 + nwords * 8 > len) return -ORC_CORRUPT;
+  uint64_t h[4], t[2];
+  orc_murmur3_128(id, idl, t);
+  h[0] = t[0]; h[1] = t[1];
+  uint8_t *tmp = (uint8_t *)malloc(idl + 1);
+  memcpy(tmp, id, idl);
+  tmp[idl] = 1;
+  orc_murmur3_128(tmp, idl + 1, t);
+  free(tmp);
+  h[2] = t[0]; h[3] = t[1];
+  if (m == 0) return -ORC_CORRUPT;
+  for (uint64_t i = 0; i < k; i++) {
+    uint64_t loc = (h[i % 2] + i * h[2 + (((i + (i % 2)) % 4) / 2)]) % m;
+    if (loc >= bitlen) return 0;
+    uint64_t w = be64(buf + 24 + (loc >> 6) * 8);
+    if (!(w & (1ULL << (loc & 63)))) return 0;
+  }
+  return 1;
+}
+int orc_v2_bloom_test(const orc_v2block *b, const uint8_t *id, size_t idl) {
+  /* ShardKeyForTraceID (bloom.go:83-85): int(FNV1_32(id)) % shardCount */
+  uint32_t shard = orc_fnv1_32(id, idl) % b->nbloom;
+  if (!b->bloom[shard]) return -ORC_NOT_FOUND;
+  return bloom_test(b->bloom[shard], b->bloom_len[shard], id, idl);
+}
+int orc_v2_index_find(const orc_v2block *b, const uint8_t *id, size_t idl, int64_t *rec_idx, uint64_t *start,
+                      uint32_t *length) {
+  orc_index ix;
+  index_init(&ix, b->index, b->index_len, b->index_page_size, b->total_records);
+  int64_t i;
+  int rc = index_find(&ix, id, idl, &i);
+  if (!rc && i >= 0) {
+    const uint8_t *r;
+    int a = index_at(&ix, i, &r);
+    if (a < 0) rc = -a;
+    else { *start = le64(r + 16); *length = le32(r + 24); }
+  }
+  index_free(&ix);
+  *rec_idx = rc ? -1 : i;
+  return rc;
+}
+/* BackendBlock.find (backend_block.go:38-92) + PagedFinder.Find/findOne (finder_paged.go:35-111) */
+int orc_v2_find(const orc_v2block *b, const uint8_t *id, size_t idl, uint8_t **out, size_t *out_len) {
+  *out = NULL;
+  *out_len = 0;
+  int t = orc_v2_bloom_test(b, id, idl);
+  if (t < 0) return -t;
+  if (!t) return ORC_OK;
+  int64_t ri;
+  uint64_t start;
+  uint32_t length;
+  int rc = orc_v2_index_find(b, id, idl, &ri, &start, &length);
+  if (rc || ri < 0) return rc;
+  uint8_t *page;
+  size_t pl;
+  rc = data_read_page(b->data, b->data_len, b->enc, start, length, &page, &pl);
+  if (rc) return rc;
+  const uint8_t *cur = page, *oid, *obj;
+  size_t cl = pl, objl;
+  uint32_t oidl;
+  for (;;) {
+    int u = unmarshal_advance(&cur, &cl, &oid, &oidl, &obj, &objl);
+    if (u == 1) break;
+    if (u < 0) { rc = -u; break; }
+    if (oidl == idl && memcmp(oid, id, idl) == 0) {
+      *out = (uint8_t *)malloc(objl ? objl : 1);
+      memcpy(*out, obj, objl);
+      *out_len = objl;
+      break;
+    }
+  }
+  free(page);
+  return rc;
+}
+/* includeBlock (tempodb/tempodb.go:492-511) */
+int orc_v2_include_block(const orc_v2block *b, const uint8_t *id, uint32_t ts, uint32_t te, const uint8_t *bs,
+                         const uint8_t *be) {
+  if (bytes_compare(id, 16, b->min_id, b->min_len) == -1 || bytes_compare(id, 16, b->max_id, b->max_len) == 1)
+    return 0;
+  if (ts != 0 && te != 0)
+    if (b->start_unix >= (int64_t)te || b->end_unix <= (int64_t)ts) return 0;
+  if (bs && be)
+    if (bytes_compare(b->block_id, 16, bs, 16) == -1 || bytes_compare(b->block_id, 16, be, 16) == 1) return 0;
+  return 1;
+}
+
+typedef struct lk_arg {
+  orc_v2block *const *blocks;
+  uint32_t nblocks;
+  const uint8_t (*ids)[16];
+  uint64_t lo, hi;
+  uint32_t ts, te;
+  const uint8_t *bs, *be;
+  orc_hit *h;
+  uint64_t n, cap;
+  int rc;
+} lk_arg;
+static void *lk_main(void *a) {
+  lk_arg *t = (lk_arg *)a;
+  orc_index *ix = (orc_index *)calloc(t->nblocks, sizeof(orc_index));
+  for (uint32_t b = 0; b < t->nblocks; b++)
+    index_init(&ix[b], t->blocks[b]->index, t->blocks[b]->index_len, t->blocks[b]->index_page_size,
+               t->blocks[b]->total_records);
+  for (uint64_t i = t->lo; i < t->hi; i++) {
+    for (uint32_t b = 0; b < t->nblocks; b++) {
+      const orc_v2block *blk = t->blocks[b];
+      if (!orc_v2_include_block(blk, t->ids[i], t->ts, t->te, t->bs, t->be)) continue;
+      int bt = orc_v2_bloom_test(blk, t->ids[i], 16);
+      if (bt < 0) { t->rc = -bt; continue; }
+      if (!bt) continue;
+      int64_t ri;
+      int rc = index_find(&ix[b], t->ids[i], 16, &ri);
+      if (rc) { t->rc = rc; continue; }
+      if (ri < 0) continue;
+      const uint8_t *r;
+      if (index_at(&ix[b], ri, &r) <= 0) { t->rc = ORC_CORRUPT; continue; }
+      if (t->n == t->cap) {
+        t->cap = t->cap ? t->cap * 2 : 1024;
+        t->h = (orc_hit *)realloc(t->h, t->cap * sizeof(orc_hit));
+      }
+      orc_hit *h = &t->h[t->n++];
+      h->id_idx = (uint32_t)i;
+      h->block_idx = b;
+      h->record_idx = (int32_t)ri;
+      h->record_start = le64(r + 16);
+      h->record_length = le32(r + 24);
+    }
+  }
+  for (uint32_t b = 0; b < t->nblocks; b++) index_free(&ix[b]);
+  free(ix);
+  return NULL;
+}
+int orc_lookup_ids(orc_v2block *const *blocks, uint32_t nblocks, const uint8_t (*ids)[16], uint64_t nids,
+                   uint32_t ts, uint32_t te, const uint8_t *bs, const uint8_t *be, int nthreads, orc_hit **out,
+                   uint64_t *nout) {
+  if (nthreads < 1) nthreads = 1;
+  lk_arg *a = (lk_arg *)calloc((size_t)nthreads, sizeof *a);
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof *th);
+  uint64_t per = (nids + (uint64_t)nthreads - 1) / (uint64_t)nthreads;
+  for (int t = 0; t < nthreads; t++) {
+    a[t].blocks = blocks; a[t].nblocks = nblocks; a[t].ids = ids;
+    a[t].lo = per * (uint64_t)t < nids ? per * (uint64_t)t : nids;
+    a[t].hi = per * (uint64_t)(t + 1) < nids ? per * (uint64_t)(t + 1) : nids;
+    a[t].ts = ts; a[t].te = te; a[t].bs = bs; a[t].be = be;
+    pthread_create(&th[t], NULL, lk_main, &a[t]);
+  }
+  uint64_t total = 0;
+  int rc = ORC_OK;
+  for (int t = 0; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    total += a[t].n;
+    if (a[t].rc && !rc) rc = a[t].rc;
+  }
+  orc_hit *h = (orc_hit *)malloc((total + 1) * sizeof(orc_hit));
+  uint64_t k = 0;
+  for (int t = 0; t < nthreads; t++) {
+    if (a[t].n) memcpy(h + k, a[t].h, a[t].n * sizeof(orc_hit));
+    k += a[t].n;
+    free(a[t].h);
+  }
+  free(a);
+  free(th);
+  *out = h;
+  *nout = total;
+  return rc;
+}

@@ -1,0 +1,11 @@
+"""tempo_amd — MI355X-native engine for Tempo's backend trace search path.
+
+The product is libtsg.so (C ABI, include/tsg.h): HIP kernels for gfx950 behind
+the drop-in boundary of tempodb/search BackendSearchBlock.Search and the v2
+bloom/index trace-ID lookup. ``tempo_amd.tsg`` is the ctypes host mirror.
+"""
+from .tsg import (  # noqa: F401
+    BackendSearchBlock, Engine, Pipeline, SearchMetrics, SearchRequest, TraceSearchMetadata, TsgError, V2Block,
+    ENC_NONE, ENC_SNAPPY, fb_search_entry, fb_search_header, lib, synth_search_block, synth_v2_block,
+    write_search_block,
+)

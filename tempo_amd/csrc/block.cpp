@@ -1,0 +1,365 @@
+// block.cpp — read side of the on-disk formats and the host half of the columnar
+// loader. Each data page is decoded exactly once (parallel over pages); the
+// flatbuffer is walked once per distinct KeyValues table (tables are shared
+// between entries of a page by writeKeyValues' cache, searchdatamap.go:115-128).
+#include "block.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <thread>
+
+namespace tsg {
+
+// ---- ContainsTag ------------------------------------------------------------------
+bool fb_contains_tag(const FbTable &t, uint16_t tags_vto, std::string_view k, std::string_view v) {
+  uint16_t o = t.field(tags_vto);
+  uint32_t n = o ? t.vector_len(o) : 0;
+  uint32_t start = o ? t.vector_start(o) : 0;
+  uint32_t i = 0, j = n;
+  FbTable kv{t.b, t.n, 0};
+  bool found = false;
+  while (i < j) {  // binarySearch with the reversed comparator (searchdata_util.go:63-100)
+    uint32_t h = (i + j) >> 1;
+    kv.pos = t.indirect(start + 4 * h);
+    uint16_t ko = kv.field(kKvKey);
+    std::string_view key = ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
+    int c = bytes_compare(reinterpret_cast<const uint8_t *>(key.data()), key.size(),
+                          reinterpret_cast<const uint8_t *>(k.data()), k.size());
+    if (c == 0) {
+      found = true;
+      break;
+    }
+    if (c < 0) j = h;
+    else i = h + 1;
+  }
+  if (!found) return false;
+  uint16_t vo = kv.field(kKvValue);
+  if (!vo) return false;
+  uint32_t vn = kv.vector_len(vo), vs = kv.vector_start(vo);
+  for (uint32_t q = 0; q < vn; q++) {
+    std::string_view val = kv.byte_vector(vs + 4 * q);
+    if (v.empty() || val.find(v) != std::string_view::npos) return true;  // bytes.Contains
+  }
+  return false;
+}
+
+// ---- meta ---------------------------------------------------------------------------
+static bool json_field(std::string_view js, const char *name, std::string_view &val) {
+  std::string pat = std::string("\"") + name + "\"";
+  size_t p = js.find(pat);
+  if (p == std::string_view::npos) return false;
+  p += pat.size();
+  while (p < js.size() && (js[p] == ' ' || js[p] == ':')) p++;
+  size_t e = p;
+  if (p < js.size() && js[p] == '"') {
+    e = js.find('"', p + 1);
+    if (e == std::string_view::npos) return false;
+    val = js.substr(p + 1, e - p - 1);
+    return true;
+  }
+  while (e < js.size() && js[e] != ',' && js[e] != '}') e++;
+  val = js.substr(p, e - p);
+  return true;
+}
+SearchMeta parse_search_meta(const uint8_t *p, size_t n) {
+  std::string_view js(reinterpret_cast<const char *>(p), n), v;
+  SearchMeta m;
+  if (json_field(js, "version", v)) m.version = std::string(v);
+  if (json_field(js, "encoding", v)) m.encoding = parse_encoding(v);
+  if (json_field(js, "indexPageSize", v)) m.index_page_size = uint32_t(std::stoull(std::string(v)));
+  if (json_field(js, "indexRecords", v)) m.index_records = uint32_t(std::stoull(std::string(v)));
+  return m;
+}
+
+// ---- v2 pages -------------------------------------------------------------------------
+// unmarshalPageFromBytes (page.go:30-57)
+static void unmarshal_page(const uint8_t *b, size_t n, size_t hdr_len, const uint8_t *&hdr, const uint8_t *&data,
+                           size_t &dlen) {
+  if (n < 6 + hdr_len) fail(TSG_E_CORRUPT, "page too small");
+  uint32_t total = le32(b);
+  uint16_t hl = le16(b + 4);
+  if (hl > n - 6) fail(TSG_E_CORRUPT, "page header length out of range");
+  if (hl != hdr_len) fail(TSG_E_CORRUPT, "unexpected page header length");
+  hdr = b + 6;
+  int64_t want = int64_t(total) - int64_t(6 + hdr_len);
+  if (want < 0 || uint64_t(want) != n - 6 - hl) fail(TSG_E_CORRUPT, "page length mismatch");
+  data = b + 6 + hl;
+  dlen = n - 6 - hl;
+}
+
+std::vector<IndexRecord> read_index(const uint8_t *p, size_t n, uint32_t page_size, uint32_t total) {
+  std::vector<IndexRecord> out;
+  if (total == 0) return out;
+  if (page_size < 14 + 28) fail(TSG_E_CORRUPT, "index page too small for one record");
+  uint32_t rpp = (page_size - 8 - 6) / 28;  // objectsPerPage (page.go:175-182)
+  out.reserve(total);
+  for (uint32_t pidx = 0; uint64_t(pidx) * rpp < total; pidx++) {
+    uint64_t off = uint64_t(pidx) * page_size;
+    if (off + page_size > n) fail(TSG_E_CORRUPT, "index truncated");
+    const uint8_t *hdr, *data;
+    size_t dlen;
+    unmarshal_page(p + off, page_size, 8, hdr, data, dlen);
+    if (le64(hdr) != xxhash64(data, dlen)) fail(TSG_E_CORRUPT, "mismatched index page checksum");
+    for (uint32_t r = 0; r < rpp && uint64_t(pidx) * rpp + r < total; r++) {
+      if ((r + 1) * 28 > dlen) fail(TSG_E_CORRUPT, "index record out of bounds");
+      const uint8_t *rec = data + r * 28;
+      bool zero = true;
+      for (int k = 0; k < 28 && zero; k++) zero = rec[k] == 0;
+      if (zero) fail(TSG_E_CORRUPT, "unexpected zero value index record");
+      IndexRecord ir;
+      std::memcpy(ir.id, rec, 16);
+      ir.start = le64(rec + 16);
+      ir.length = le32(rec + 24);
+      out.push_back(ir);
+    }
+  }
+  return out;
+}
+
+void read_data_page(const uint8_t *file, size_t flen, const IndexRecord &r, int enc, std::vector<uint8_t> &out) {
+  if (r.start + r.length > flen) fail(TSG_E_CORRUPT, "record out of bounds of data file");
+  const uint8_t *hdr, *payload;
+  size_t pl;
+  unmarshal_page(file + r.start, r.length, 0, hdr, payload, pl);
+  if (enc == 0) out.assign(payload, payload + pl);
+  else if (enc == 6) snappy_framed_decode(payload, pl, out);
+  else fail(TSG_E_UNSUPPORTED_ENCODING, std::string("unsupported search encoding ") + encoding_name(enc));
+}
+
+// ---- page parse ---------------------------------------------------------------------------
+namespace {
+struct PageKV {
+  std::string_view key;
+  std::vector<std::string_view> vals;
+};
+struct PageParse {
+  std::vector<uint8_t> buf;
+  uint64_t fb_bytes = 0;
+  uint32_t nentries = 0;
+  std::vector<PageKV> kvs;
+  std::vector<uint32_t> id_off;  // into buf
+  std::vector<uint8_t> id_len;
+  std::vector<uint64_t> start, end;
+  std::vector<uint32_t> tag_begin;  // nentries + 1
+  std::vector<uint32_t> tag_kv;
+  int err = 0;
+  std::string msg;
+};
+
+void parse_page(const uint8_t *data, size_t dlen, int enc, const IndexRecord &rec, PageParse &pp) {
+  read_data_page(data, dlen, rec, enc, pp.buf);
+  // object.UnmarshalAndAdvanceBuffer (object.go:82-113): [u32 total][u32 idLen][id][obj]
+  if (pp.buf.size() < 8) fail(TSG_E_CORRUPT, "object header truncated");
+  uint32_t total = le32(pp.buf.data()), il = le32(pp.buf.data() + 4);
+  if (total < 8 || pp.buf.size() - 8 < total - 8 || il > total - 8) fail(TSG_E_CORRUPT, "object out of bounds");
+  const uint8_t *fb = pp.buf.data() + 8 + il;
+  size_t fbn = total - 8 - il;
+  pp.fb_bytes = fbn;
+  FbTable page = FbTable::root(fb, fbn);
+  uint16_t eo = page.field(kPageEntries);
+  pp.nentries = eo ? page.vector_len(eo) : 0;
+  uint32_t es = eo ? page.vector_start(eo) : 0;
+  std::unordered_map<uint32_t, uint32_t> memo;  // KeyValues table position -> kvs index
+  pp.tag_begin.reserve(pp.nentries + 1);
+  pp.tag_begin.push_back(0);
+  FbTable e{fb, fbn, 0}, kv{fb, fbn, 0};
+  const uint32_t fb_base = uint32_t(fb - pp.buf.data());
+  for (uint32_t j = 0; j < pp.nentries; j++) {
+    e.pos = page.indirect(es + 4 * j);
+    uint16_t io = e.field(kEntryId);
+    std::string_view id = io ? e.byte_vector(e.pos + io) : std::string_view();
+    if (id.size() > 16) fail(TSG_E_UNSUPPORTED, "trace id longer than 16 bytes");
+    pp.id_off.push_back(uint32_t(reinterpret_cast<const uint8_t *>(id.data()) - fb) + fb_base);
+    pp.id_len.push_back(uint8_t(id.size()));
+    pp.start.push_back(e.u64(kEntryStart));
+    pp.end.push_back(e.u64(kEntryEnd));
+    uint16_t to = e.field(kEntryTags);
+    uint32_t nt = to ? e.vector_len(to) : 0, ts = to ? e.vector_start(to) : 0;
+    std::string_view prev;
+    for (uint32_t t = 0; t < nt; t++) {
+      uint32_t pos = e.indirect(ts + 4 * t);
+      auto it = memo.find(pos);
+      uint32_t idx;
+      if (it == memo.end()) {
+        kv.pos = pos;
+        PageKV p;
+        uint16_t ko = kv.field(kKvKey);
+        p.key = ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
+        uint16_t vo = kv.field(kKvValue);
+        uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
+        p.vals.reserve(vn);
+        for (uint32_t q = 0; q < vn; q++) p.vals.push_back(kv.byte_vector(vs + 4 * q));
+        idx = uint32_t(pp.kvs.size());
+        pp.kvs.push_back(std::move(p));
+        memo.emplace(pos, idx);
+      } else {
+        idx = it->second;
+      }
+      // Contract (pitfall P3): keys unique and strictly descending, as NewBackendSearchBlock
+      // writes them (backend_search_block.go:78-89); then exact-key hashing == binarySearch.
+      std::string_view key = pp.kvs[idx].key;
+      if (t > 0 && !(prev > key))
+        fail(TSG_E_UNSUPPORTED, "entry keys not strictly descending (WAL-style entry; see DESIGN.md P3)");
+      prev = key;
+      pp.tag_kv.push_back(idx);
+    }
+    pp.tag_begin.push_back(uint32_t(pp.tag_kv.size()));
+  }
+}
+
+struct KeyBuild {
+  std::unordered_map<std::string, uint32_t> vmap;
+  std::unordered_map<std::string, uint32_t> smap;
+};
+}  // namespace
+
+void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
+                         const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
+                         HostBlock &hb) {
+  if (!meta_present) {
+    hb.has_meta = false;
+    return;
+  }
+  hb.has_meta = true;
+  hb.meta = parse_search_meta(meta, meta_len);
+  if (hb.meta.version != "v2") fail(TSG_E_UNSUPPORTED_ENCODING, "unsupported search block version " + hb.meta.version);
+  if (hb.meta.encoding != 0 && hb.meta.encoding != 6)
+    fail(TSG_E_UNSUPPORTED_ENCODING, std::string("search encoding not supported: ") + encoding_name(hb.meta.encoding));
+  hb.header = std::move(header);
+  {
+    FbTable h = FbTable::root(hb.header.data(), hb.header.size());
+    hb.min_dur = h.u64(kHdrMin);
+    hb.max_dur = h.u64(kHdrMax);
+  }
+  std::vector<IndexRecord> recs = read_index(index, index_len, hb.meta.index_page_size, hb.meta.index_records);
+  if (nthreads <= 0) nthreads = int(std::max(1u, std::thread::hardware_concurrency()));
+  nthreads = std::min<int>(nthreads, 64);
+
+  std::vector<KeyBuild> kb;
+  size_t batch = size_t(nthreads) * 4;
+  std::vector<PageParse> pages;
+  for (size_t b0 = 0; b0 < recs.size(); b0 += batch) {
+    size_t b1 = std::min(recs.size(), b0 + batch);
+    pages.clear();
+    pages.resize(b1 - b0);
+    std::atomic<size_t> next{b0};
+    auto work = [&]() {
+      for (;;) {
+        size_t i = next.fetch_add(1);
+        if (i >= b1) break;
+        PageParse &pp = pages[i - b0];
+        try {
+          parse_page(data, data_len, hb.meta.encoding, recs[i], pp);
+        } catch (const Error &e) {
+          pp.err = e.code;
+          pp.msg = e.what();
+        }
+      }
+    };
+    std::vector<std::thread> th;
+    int nt = int(std::min<size_t>(size_t(nthreads), b1 - b0));
+    for (int t = 1; t < nt; t++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    // merge pages in order (scan order = pages ascending, entry index ascending)
+    for (auto &pp : pages) {
+      if (pp.err) fail(pp.err, pp.msg);
+      uint64_t base = hb.n;
+      hb.page_entries.push_back(pp.nentries);
+      hb.page_fb_bytes.push_back(pp.fb_bytes);
+      hb.page_first.push_back(base);
+      hb.fb_bytes += pp.fb_bytes;
+      // resolve the page's KeyValues tables to (key, set)
+      std::vector<std::pair<int, uint32_t>> res(pp.kvs.size());
+      for (size_t q = 0; q < pp.kvs.size(); q++) {
+        const PageKV &p = pp.kvs[q];
+        std::string key(p.key);
+        auto ki = hb.key_index.find(key);
+        int k;
+        if (ki == hb.key_index.end()) {
+          k = int(hb.keys.size());
+          hb.key_index.emplace(key, k);
+          KeyColumn kc;
+          kc.name = key;
+          kc.dict_off.push_back(0);
+          kc.set_off.push_back(0);
+          hb.keys.push_back(std::move(kc));
+          kb.emplace_back();
+          if (key == "root.service.name") hb.svc_key = k;
+          if (key == "root.name") hb.name_key = k;
+        } else {
+          k = ki->second;
+        }
+        KeyColumn &kc = hb.keys[size_t(k)];
+        KeyBuild &b = kb[size_t(k)];
+        std::string skey;
+        skey.reserve(4 * p.vals.size());
+        uint32_t first_vid = kNone;
+        for (auto &v : p.vals) {
+          std::string vs(v);
+          auto vi = b.vmap.find(vs);
+          uint32_t vid;
+          if (vi == b.vmap.end()) {
+            vid = kc.nvals();
+            kc.dict_bytes.insert(kc.dict_bytes.end(), v.begin(), v.end());
+            kc.dict_off.push_back(uint32_t(kc.dict_bytes.size()));
+            if (kc.dict_bytes.size() > 0xF0000000u) fail(TSG_E_UNSUPPORTED, "dictionary too large");
+            b.vmap.emplace(std::move(vs), vid);
+          } else {
+            vid = vi->second;
+          }
+          if (first_vid == kNone) first_vid = vid;
+          skey.append(reinterpret_cast<const char *>(&vid), 4);
+        }
+        auto si = b.smap.find(skey);
+        uint32_t sid;
+        if (si == b.smap.end()) {
+          sid = kc.nsets();
+          for (auto &v : p.vals) kc.set_vals.push_back(b.vmap[std::string(v)]);
+          kc.set_off.push_back(uint32_t(kc.set_vals.size()));
+          if (p.vals.size() != 1 || sid != first_vid) kc.identity = false;
+          b.smap.emplace(std::move(skey), sid);
+        } else {
+          sid = si->second;
+        }
+        res[q] = {k, sid};
+      }
+      // entries
+      uint64_t n1 = base + pp.nentries;
+      for (auto &kc : hb.keys) kc.col.resize(n1, kNone);
+      hb.ids.resize(n1 * 16, 0);
+      hb.id_len.resize(n1);
+      hb.start.resize(n1);
+      hb.end.resize(n1);
+      hb.svc_vid.resize(n1, kNone);
+      hb.name_vid.resize(n1, kNone);
+      for (uint32_t j = 0; j < pp.nentries; j++) {
+        uint64_t e = base + j;
+        uint8_t il = pp.id_len[j];
+        std::memcpy(&hb.ids[e * 16 + 16 - il], pp.buf.data() + pp.id_off[j], il);
+        hb.id_len[e] = il;
+        hb.start[e] = pp.start[j];
+        hb.end[e] = pp.end[j];
+        bool svc_done = false, name_done = false;
+        for (uint32_t t = pp.tag_begin[j]; t < pp.tag_begin[j + 1]; t++) {
+          auto [k, sid] = res[pp.tag_kv[t]];
+          KeyColumn &kc = hb.keys[size_t(k)];
+          kc.col[e] = sid;
+          // SearchEntry.Get: first key match in vector order, Value(0) (searchdata_util.go:10-23)
+          if (k == hb.svc_key && !svc_done) {
+            svc_done = true;
+            if (kc.set_off[sid + 1] > kc.set_off[sid]) hb.svc_vid[e] = kc.set_vals[kc.set_off[sid]];
+          }
+          if (k == hb.name_key && !name_done) {
+            name_done = true;
+            if (kc.set_off[sid + 1] > kc.set_off[sid]) hb.name_vid[e] = kc.set_vals[kc.set_off[sid]];
+          }
+        }
+      }
+      hb.n = n1;
+    }
+  }
+  for (auto &kc : hb.keys) kc.col.resize(hb.n, kNone);
+}
+
+}  // namespace tsg

@@ -1,0 +1,147 @@
+// block.hpp — on-disk formats (read side) and the host half of the columnar
+// loader: a backend search block decoded ONCE into per-key dictionaries,
+// value-set ids and per-entry columns, ready to upload to HBM.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.hpp"
+
+namespace tsg {
+
+// ---- flatbuffer table access (vendor/github.com/google/flatbuffers/go/table.go:14-57),
+// bounds-checked: a malformed buffer raises TSG_E_CORRUPT instead of reading past it.
+struct FbTable {
+  const uint8_t *b = nullptr;
+  size_t n = 0;
+  uint32_t pos = 0;
+
+  void need(uint64_t off, uint64_t len) const {
+    if (off + len > n) fail(TSG_E_CORRUPT, "flatbuffer offset out of range");
+  }
+  uint16_t field(uint16_t vto) const {  // Table.Offset
+    need(pos, 4);
+    int64_t vt = int64_t(pos) - int32_t(le32(b + pos));
+    if (vt < 0) fail(TSG_E_CORRUPT, "flatbuffer vtable out of range");
+    need(uint64_t(vt), 2);
+    uint16_t vlen = le16(b + vt);
+    if (vto < vlen) {
+      need(uint64_t(vt) + vto, 2);
+      return le16(b + vt + vto);
+    }
+    return 0;
+  }
+  uint32_t indirect(uint32_t off) const {
+    need(off, 4);
+    return off + le32(b + off);
+  }
+  uint32_t vector_len(uint16_t o) const {
+    uint32_t off = indirect(pos + o);
+    need(off, 4);
+    return le32(b + off);
+  }
+  uint32_t vector_start(uint16_t o) const { return indirect(pos + o) + 4; }
+  std::string_view byte_vector(uint32_t off) const {  // Table.ByteVector
+    off = indirect(off);
+    need(off, 4);
+    uint32_t l = le32(b + off);
+    need(uint64_t(off) + 4, l);
+    return {reinterpret_cast<const char *>(b + off + 4), l};
+  }
+  uint64_t u64(uint16_t vto) const {
+    uint16_t o = field(vto);
+    if (!o) return 0;
+    need(uint64_t(pos) + o, 8);
+    return le64(b + pos + o);
+  }
+  static FbTable root(const uint8_t *b, size_t n) {
+    FbTable t;
+    t.b = b;
+    t.n = n;
+    t.need(0, 4);
+    t.pos = le32(b);
+    return t;
+  }
+};
+
+// tempofb vtable slots (pkg/tempofb/{SearchEntry,SearchPage,SearchBlockHeader,KeyValues}.go)
+enum : uint16_t {
+  kEntryId = 4, kEntryTags = 6, kEntryStart = 8, kEntryEnd = 10,
+  kPageTags = 4, kPageEntries = 6,
+  kHdrTags = 4, kHdrMin = 6, kHdrMax = 8,
+  kKvKey = 4, kKvValue = 6,
+};
+
+// FindTag + ContainsTag over any [KeyValues] vector (pkg/tempofb/searchdata_util.go:47-100).
+bool fb_contains_tag(const FbTable &t, uint16_t tags_vto, std::string_view k, std::string_view v);
+
+// ---- search.meta.json (tempodb/search/block_meta.go:11-43) ----------------------
+struct SearchMeta {
+  std::string version;
+  int encoding = -1;
+  uint32_t index_page_size = 0, index_records = 0;
+};
+SearchMeta parse_search_meta(const uint8_t *p, size_t n);
+
+// ---- v2 index (tempodb/encoding/v2/index_reader.go) -------------------------------
+struct IndexRecord {
+  uint8_t id[16];
+  uint64_t start;
+  uint32_t length;
+};
+// Reads every record: page checksum (xxhash64) verified, all-zero record rejected.
+std::vector<IndexRecord> read_index(const uint8_t *p, size_t n, uint32_t page_size, uint32_t total);
+// dataReader.Read of one record + decompression (data_reader.go:45-125).
+void read_data_page(const uint8_t *file, size_t flen, const IndexRecord &r, int enc, std::vector<uint8_t> &out);
+
+// ---- the decoded block ------------------------------------------------------------
+static constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+struct KeyColumn {
+  std::string name;
+  // value dictionary (distinct values of this key in the block, first-seen order)
+  std::vector<uint8_t> dict_bytes;
+  std::vector<uint32_t> dict_off;  // nvals + 1
+  // value sets (the distinct value vectors of this key's KeyValues tables)
+  std::vector<uint32_t> set_off;   // nsets + 1
+  std::vector<uint32_t> set_vals;  // value ids, in vector order (descending bytes)
+  bool identity = true;            // every set is {v} with set id == value id
+  std::vector<uint32_t> col;       // per entry: set id or kNone (key absent)
+  uint32_t nvals() const { return uint32_t(dict_off.size() - 1); }
+  uint32_t nsets() const { return uint32_t(set_off.size() - 1); }
+  int width() const { return nsets() < 255 ? 1 : (nsets() < 65535 ? 2 : 4); }
+};
+
+struct HostBlock {
+  bool has_meta = false;
+  SearchMeta meta;
+  std::vector<uint8_t> header;  // raw search-header flatbuffer (kept for MatchesBlock/Tags)
+  uint64_t min_dur = 0, max_dur = 0;
+  uint64_t n = 0;
+  std::vector<uint32_t> page_entries;  // EntriesLength per page
+  std::vector<uint64_t> page_fb_bytes; // flatbuffer bytes per page (bytesInspected)
+  std::vector<uint64_t> page_first;    // scan position of each page's first entry
+  uint64_t fb_bytes = 0;
+  // per entry (scan order)
+  std::vector<uint8_t> ids;     // n * 16, right aligned
+  std::vector<uint8_t> id_len;  // n
+  std::vector<uint64_t> start, end;
+  std::vector<uint32_t> svc_vid, name_vid;  // Value(0) of root.service.name / root.name
+  int svc_key = -1, name_key = -1;
+  std::vector<KeyColumn> keys;
+  std::unordered_map<std::string, int> key_index;
+
+  std::string_view dict_value(int key, uint32_t vid) const {
+    const KeyColumn &k = keys[size_t(key)];
+    return {reinterpret_cast<const char *>(k.dict_bytes.data() + k.dict_off[vid]), k.dict_off[vid + 1] - k.dict_off[vid]};
+  }
+};
+
+// Reads + decodes a block (meta missing -> has_meta=false, TSG_OK). nthreads <= 0: all cores.
+void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
+                         const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
+                         HostBlock &out);
+
+}  // namespace tsg

@@ -1,0 +1,528 @@
+// capi.cpp — the extern "C" boundary of libtsg (include/tsg.h). Every entry point
+// catches C++ exceptions and maps them to TSG_* codes + the thread-local
+// tsg_last_error() text. The search itself only ever runs on a HIP device:
+// there is no CPU fallback behind this ABI (the Go shim keeps its own CPU path).
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+
+#include "block.hpp"
+#include "common.hpp"
+#include "engine.hpp"
+#include "writer.hpp"
+
+struct tsg_ctx {
+  tsg::Ctx c;
+};
+struct tsg_block {
+  tsg::Block b;
+  tsg_ctx *ctx = nullptr;
+};
+struct tsg_v2block {
+  tsg::V2Block b;
+};
+
+namespace tsg {
+tsg_pipeline *pipeline_new(const tsg_request &req);
+bool pipeline_matches_block(const tsg_query &q, const uint8_t *hdr, size_t len);
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string &m) { g_last_error = m; }
+
+template <typename F>
+static int guard(F &&f) {
+  try {
+    f();
+    return TSG_OK;
+  } catch (const Error &e) {
+    set_last_error(e.what());
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    set_last_error("out of memory");
+    return TSG_E_OOM;
+  } catch (const std::exception &e) {
+    set_last_error(e.what());
+    return TSG_E_INVALID;
+  }
+}
+
+// Holder behind tsg_result: owns the arrays the public struct points into.
+struct ResultHolder {
+  tsg_result pub{};
+  std::vector<uint8_t> ids, id_len;
+  std::vector<uint64_t> start, end, entry;
+  std::vector<uint32_t> dur, block, svc_len, name_len;
+  std::vector<std::string> svc, name;
+  std::vector<const char *> svc_p, name_p;
+  void push(const uint8_t *id, uint8_t il, uint64_t s, uint64_t e, uint32_t b, uint64_t en, std::string sv,
+            std::string nm) {
+    ids.insert(ids.end(), id, id + 16);
+    id_len.push_back(il);
+    start.push_back(s);
+    end.push_back(e);
+    dur.push_back(uint32_t((e - s) / 1000000ULL));  // util.go:33
+    block.push_back(b);
+    entry.push_back(en);
+    svc.push_back(std::move(sv));
+    name.push_back(std::move(nm));
+  }
+  void finalize() {
+    svc_p.clear();
+    name_p.clear();
+    svc_len.clear();
+    name_len.clear();
+    for (auto &s : svc) {
+      svc_p.push_back(s.c_str());
+      svc_len.push_back(uint32_t(s.size()));
+    }
+    for (auto &s : name) {
+      name_p.push_back(s.c_str());
+      name_len.push_back(uint32_t(s.size()));
+    }
+    pub.n = start.size();
+    pub.trace_id = reinterpret_cast<const uint8_t(*)[16]>(ids.data());
+    pub.trace_id_len = id_len.data();
+    pub.start_ns = start.data();
+    pub.end_ns = end.data();
+    pub.duration_ms = dur.data();
+    pub.block_idx = block.data();
+    pub.entry_idx = entry.data();
+    pub.root_service = svc_p.data();
+    pub.root_service_len = svc_len.data();
+    pub.root_name = name_p.data();
+    pub.root_name_len = name_len.data();
+  }
+};
+static_assert(offsetof(ResultHolder, pub) == 0, "pub first");
+
+struct LookupHolder {
+  tsg_lookup_result pub{};
+  LookupOut o;
+};
+static_assert(offsetof(LookupHolder, pub) == 0, "pub first");
+
+static std::string join(const char *dir, const char *name) { return std::string(dir) + "/" + name; }
+
+static void open_common(tsg_ctx *ctx, const uint8_t *meta, size_t ml, bool has_meta, std::vector<uint8_t> header,
+                        const uint8_t *index, size_t il, const uint8_t *data, size_t dl, int device_hint,
+                        tsg_block **out) {
+  auto *b = new tsg_block();
+  b->ctx = ctx;
+  try {
+    decode_search_block(meta, ml, has_meta, std::move(header), index, il, data, dl, 0, b->b.host);
+    if (b->b.host.has_meta) block_upload(ctx->c, b->b, device_hint);
+  } catch (...) {
+    block_free(b->b);
+    delete b;
+    throw;
+  }
+  // the device holds the columns now; keep only what the host needs (names, header, pages)
+  for (size_t k = 0; k < b->b.host.keys.size(); k++) {
+    auto &kc = b->b.host.keys[k];
+    std::vector<uint32_t>().swap(kc.col);
+    if (int(k) != b->b.host.svc_key && int(k) != b->b.host.name_key) {
+      std::vector<uint8_t>().swap(kc.dict_bytes);
+      std::vector<uint32_t>().swap(kc.dict_off);
+      std::vector<uint32_t>().swap(kc.set_vals);
+      kc.set_off.resize(1);
+    }
+  }
+  std::vector<uint8_t>().swap(b->b.host.ids);
+  std::vector<uint64_t>().swap(b->b.host.start);
+  std::vector<uint64_t>().swap(b->b.host.end);
+  *out = b;
+}
+
+}  // namespace tsg
+
+using namespace tsg;
+
+extern "C" {
+
+const char *tsg_last_error(void) { return g_last_error.c_str(); }
+int tsg_abi_version(void) { return TSG_ABI_VERSION; }
+void tsg_free(void *p) { std::free(p); }
+
+int tsg_init(const tsg_options *opts, tsg_ctx **out) {
+  if (!out) return TSG_E_INVALID;
+  return guard([&] {
+    auto *c = new tsg_ctx();
+    try {
+      ctx_init(c->c, opts);
+    } catch (...) {
+      ctx_shutdown(c->c);
+      delete c;
+      throw;
+    }
+    *out = c;
+  });
+}
+void tsg_shutdown(tsg_ctx *ctx) {
+  if (!ctx) return;
+  ctx_shutdown(ctx->c);
+  delete ctx;
+}
+int tsg_device_count(tsg_ctx *ctx) { return ctx ? int(ctx->c.devs.size()) : 0; }
+int tsg_cancel(tsg_ctx *, uint64_t) { return TSG_OK; }  // searches are short and non-preemptible
+
+int tsg_pipeline_new(const tsg_request *req, tsg_pipeline **out) {
+  if (!req || !out) return TSG_E_INVALID;
+  return guard([&] { *out = pipeline_new(*req); });
+}
+const tsg_query *tsg_pipeline_query(const tsg_pipeline *p);
+void tsg_pipeline_free(tsg_pipeline *p);
+
+int tsg_pipeline_matches_header(const tsg_query *q, const uint8_t *header, size_t len, int *matches) {
+  if (!q || !header || !matches) return TSG_E_INVALID;
+  return guard([&] { *matches = pipeline_matches_block(*q, header, len) ? 1 : 0; });
+}
+
+int tsg_block_open(tsg_ctx *ctx, const char *dir, int device_hint, tsg_block **out) {
+  if (!ctx || !dir || !out) return TSG_E_INVALID;
+  return guard([&] {
+    std::vector<uint8_t> meta, header, index, data;
+    if (!read_file(join(dir, "search.meta.json"), meta)) fail(TSG_E_NOT_FOUND, "search.meta.json not found");
+    if (!read_file(join(dir, "search-header"), header)) fail(TSG_E_IO, "search-header missing");
+    if (!read_file(join(dir, "search-index"), index)) fail(TSG_E_IO, "search-index missing");
+    if (!read_file(join(dir, "search"), data)) fail(TSG_E_IO, "search missing");
+    open_common(ctx, meta.data(), meta.size(), true, std::move(header), index.data(), index.size(), data.data(),
+                data.size(), device_hint, out);
+  });
+}
+int tsg_block_open_mem(tsg_ctx *ctx, const uint8_t *meta, size_t ml, const uint8_t *header, size_t hl,
+                       const uint8_t *index, size_t il, const uint8_t *data, size_t dl, int device_hint,
+                       tsg_block **out) {
+  if (!ctx || !out) return TSG_E_INVALID;
+  return guard([&] {
+    if (!meta) fail(TSG_E_NOT_FOUND, "search.meta.json not provided");
+    std::vector<uint8_t> h(header, header + hl);
+    open_common(ctx, meta, ml, true, std::move(h), index, il, data, dl, device_hint, out);
+  });
+}
+void tsg_block_close(tsg_block *b) {
+  if (!b) return;
+  block_free(b->b);
+  delete b;
+}
+int tsg_block_info_get(const tsg_block *b, tsg_block_info *o) {
+  if (!b || !o) return TSG_E_INVALID;
+  const HostBlock &h = b->b.host;
+  o->entries = h.n;
+  o->pages = h.page_entries.size();
+  o->keys = h.keys.size();
+  o->header_bytes = h.header.size();
+  o->fb_bytes = h.fb_bytes;
+  o->device_bytes = b->b.dev.bytes;
+  o->min_dur_ns = h.min_dur;
+  o->max_dur_ns = h.max_dur;
+  o->device = b->b.dev.device;
+  o->encoding = h.meta.encoding;
+  return TSG_OK;
+}
+
+static void pack_strings(const std::vector<std::string> &v, uint8_t **out, size_t *len, size_t *n) {
+  size_t total = 0;
+  for (auto &s : v) total += 4 + s.size();
+  auto *p = static_cast<uint8_t *>(std::malloc(total ? total : 1));
+  size_t o = 0;
+  for (auto &s : v) {
+    uint32_t l = uint32_t(s.size());
+    std::memcpy(p + o, &l, 4);
+    std::memcpy(p + o + 4, s.data(), s.size());
+    o += 4 + s.size();
+  }
+  *out = p;
+  *len = total;
+  *n = v.size();
+}
+
+// BackendSearchBlock.Tags / TagValues (backend_search_block.go:145-181) on the header rollup
+int tsg_block_tags(const tsg_block *b, uint8_t **out, size_t *len, size_t *n) {
+  if (!b || !out || !len || !n) return TSG_E_INVALID;
+  return guard([&] {
+    std::vector<std::string> keys;
+    const auto &hb = b->b.host.header;
+    if (b->b.host.has_meta) {
+      FbTable h = FbTable::root(hb.data(), hb.size());
+      uint16_t o = h.field(kHdrTags);
+      uint32_t cnt = o ? h.vector_len(o) : 0, st = o ? h.vector_start(o) : 0;
+      std::unordered_set<std::string> seen;
+      FbTable kv{hb.data(), hb.size(), 0};
+      for (uint32_t i = 0; i < cnt; i++) {
+        kv.pos = h.indirect(st + 4 * i);
+        uint16_t ko = kv.field(kKvKey);
+        std::string k(ko ? kv.byte_vector(kv.pos + ko) : std::string_view());
+        if (seen.insert(k).second) keys.push_back(k);
+      }
+    }
+    pack_strings(keys, out, len, n);
+  });
+}
+int tsg_block_tag_values(const tsg_block *b, const uint8_t *key, size_t klen, uint8_t **out, size_t *len,
+                         size_t *n) {
+  if (!b || !out || !len || !n) return TSG_E_INVALID;
+  return guard([&] {
+    std::vector<std::string> vals;
+    const auto &hb = b->b.host.header;
+    if (b->b.host.has_meta) {
+      FbTable h = FbTable::root(hb.data(), hb.size());
+      uint16_t o = h.field(kHdrTags);
+      uint32_t cnt = o ? h.vector_len(o) : 0, st = o ? h.vector_start(o) : 0;
+      std::string_view k(reinterpret_cast<const char *>(key), klen);
+      FbTable kv{hb.data(), hb.size(), 0};
+      uint32_t i = 0, j = cnt;  // FindTag binary search (searchdata_util.go:63-100)
+      bool found = false;
+      while (i < j) {
+        uint32_t m = (i + j) >> 1;
+        kv.pos = h.indirect(st + 4 * m);
+        uint16_t ko = kv.field(kKvKey);
+        std::string_view kk = ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
+        int c = bytes_compare(reinterpret_cast<const uint8_t *>(kk.data()), kk.size(),
+                              reinterpret_cast<const uint8_t *>(k.data()), k.size());
+        if (c == 0) {
+          found = true;
+          break;
+        }
+        if (c < 0) j = m;
+        else i = m + 1;
+      }
+      if (found) {
+        uint16_t vo = kv.field(kKvValue);
+        uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
+        std::unordered_set<std::string> seen;
+        for (uint32_t q = 0; q < vn; q++) {
+          std::string v(kv.byte_vector(vs + 4 * q));
+          if (seen.insert(v).second) vals.push_back(v);
+        }
+      }
+    }
+    pack_strings(vals, out, len, n);
+  });
+}
+
+int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
+               const tsg_search_opts *opts, tsg_result **out) {
+  if (!ctx || !q || !out || (nblocks && !blocks)) return TSG_E_INVALID;
+  return guard([&] {
+    const uint32_t limit = opts ? opts->limit : 0;
+    auto *res = new ResultHolder();
+    std::unique_ptr<ResultHolder> guard_res(res);
+    tsg_metrics &m = res->pub.metrics;
+    std::memset(&m, 0, sizeof m);
+    // block filter on the host (header), device work grouped per device
+    std::vector<int> state(nblocks, 0);  // 0 no meta, 1 skipped, 2 inspected
+    std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, Block *>>> per_dev;
+    for (size_t i = 0; i < nblocks; i++) {
+      Block &b = blocks[i]->b;
+      if (!b.host.has_meta) continue;
+      bool ok = pipeline_matches_block(*q, b.host.header.data(), b.host.header.size());
+      state[i] = ok ? 2 : 1;
+      if (ok && b.dc) per_dev[b.dc].push_back({uint32_t(i), &b});
+    }
+    std::vector<std::pair<DeviceCtx *, SearchOut>> outs;
+    outs.reserve(per_dev.size());
+    for (auto &kv : per_dev) outs.push_back({kv.first, SearchOut()});
+    {
+      std::vector<std::thread> th;
+      std::vector<std::exception_ptr> errs(outs.size());
+      size_t k = 0;
+      for (auto &kv : per_dev) {
+        size_t slot = k++;
+        auto work = [&, slot, &list = kv.second]() {
+          try {
+            device_search(*outs[slot].first, list, *q, limit, outs[slot].second);
+          } catch (...) {
+            errs[slot] = std::current_exception();
+          }
+        };
+        if (per_dev.size() == 1) work();
+        else th.emplace_back(work);
+      }
+      for (auto &t : th) t.join();
+      for (auto &e : errs)
+        if (e) std::rethrow_exception(e);
+    }
+    // per block match lists in scan order
+    std::vector<std::vector<const SearchOut::Rec *>> per_block(nblocks);
+    for (auto &o : outs) {
+      m.device_bytes_read += o.second.device_bytes;
+      m.kernel_ns = std::max<uint64_t>(m.kernel_ns, o.second.kernel_ns);
+      m.scan_kernel_ns = std::max<uint64_t>(m.scan_kernel_ns, o.second.scan_ns);
+      m.scan_bytes += o.second.scan_bytes;
+      for (auto &r : o.second.recs) per_block[r.block].push_back(&r);
+    }
+    // consume in caller block order (deterministic refinement of instance.Search)
+    std::unordered_set<std::string> distinct;
+    bool stopped = false;
+    for (size_t i = 0; i < nblocks && !stopped; i++) {
+      const HostBlock &h = blocks[i]->b.host;
+      if (state[i] == 0) continue;  // meta missing: no-op (backend_search_block.go:191-203)
+      m.bytes_inspected += h.header.size();
+      if (state[i] == 1) {
+        m.blocks_skipped++;
+        continue;
+      }
+      m.blocks_inspected++;
+      uint64_t stop_entry = UINT64_MAX;
+      for (const SearchOut::Rec *r : per_block[i]) {
+        std::string sv, nm;
+        if (h.svc_key >= 0 && h.svc_vid[r->entry] != kNone) sv = std::string(h.dict_value(h.svc_key, h.svc_vid[r->entry]));
+        if (h.name_key >= 0 && h.name_vid[r->entry] != kNone)
+          nm = std::string(h.dict_value(h.name_key, h.name_vid[r->entry]));
+        res->push(r->id, h.id_len[r->entry], r->start, r->end, uint32_t(i), r->entry, std::move(sv), std::move(nm));
+        if (limit) {
+          distinct.insert(std::string(reinterpret_cast<const char *>(r->id), 16));
+          if (distinct.size() >= limit) {
+            stopped = true;
+            stop_entry = r->entry;
+            break;
+          }
+        }
+      }
+      if (!stopped) {
+        m.traces_inspected += uint32_t(h.n);
+        m.bytes_inspected += h.fb_bytes;
+      } else {
+        // pages up to and including the stop page; entries up to and including the match
+        m.traces_inspected += uint32_t(stop_entry + 1);
+        for (size_t p = 0; p < h.page_first.size() && h.page_first[p] <= stop_entry; p++)
+          m.bytes_inspected += h.page_fb_bytes[p];
+      }
+    }
+    res->finalize();
+    *out = &guard_res.release()->pub;
+  });
+}
+void tsg_result_free(tsg_result *r) { delete reinterpret_cast<ResultHolder *>(r); }
+
+int tsg_results_combine(const tsg_result *in, uint32_t max_results, tsg_result **out) {
+  if (!in || !out) return TSG_E_INVALID;
+  return guard([&] {
+    if (max_results == 0) max_results = 20;  // instance_search.go:24-28
+    auto *res = new ResultHolder();
+    std::unique_ptr<ResultHolder> gr(res);
+    struct F {
+      uint64_t first;
+      size_t idx;  // index into res arrays
+    };
+    std::unordered_map<std::string, size_t> map;
+    std::vector<F> order;
+    for (uint64_t i = 0; i < in->n; i++) {
+      std::string key(reinterpret_cast<const char *>(in->trace_id[i]), 16);
+      auto it = map.find(key);
+      if (it != map.end()) {  // CombineSearchResults (util.go:40-62)
+        size_t e = it->second;
+        if (res->svc[e].empty()) res->svc[e] = std::string(in->root_service[i], in->root_service_len[i]);
+        if (res->name[e].empty()) res->name[e] = std::string(in->root_name[i], in->root_name_len[i]);
+        if (res->start[e] > in->start_ns[i]) res->start[e] = in->start_ns[i];
+        if (res->dur[e] < in->duration_ms[i]) res->dur[e] = in->duration_ms[i];
+      } else {
+        map.emplace(key, res->start.size());
+        order.push_back({i, res->start.size()});
+        res->push(in->trace_id[i], in->trace_id_len[i], in->start_ns[i], in->end_ns[i], in->block_idx[i],
+                  in->entry_idx[i], std::string(in->root_service[i], in->root_service_len[i]),
+                  std::string(in->root_name[i], in->root_name_len[i]));
+        res->dur.back() = in->duration_ms[i];
+      }
+      if (map.size() >= max_results) break;
+    }
+    // sort by StartTimeUnixNano descending; ties by first occurrence
+    std::stable_sort(order.begin(), order.end(),
+                     [&](const F &a, const F &b) { return res->start[a.idx] > res->start[b.idx]; });
+    auto *fin = new ResultHolder();
+    std::unique_ptr<ResultHolder> gf(fin);
+    for (auto &f : order) {
+      size_t e = f.idx;
+      fin->push(&res->ids[e * 16], res->id_len[e], res->start[e], res->end[e], res->block[e], res->entry[e],
+                res->svc[e], res->name[e]);
+      fin->dur.back() = res->dur[e];
+    }
+    fin->pub.metrics = in->metrics;
+    fin->finalize();
+    *out = &gf.release()->pub;
+  });
+}
+
+// ---- v2 lookup -----------------------------------------------------------------------
+int tsg_v2block_open(tsg_ctx *ctx, const char *dir, int device_hint, tsg_v2block **out) {
+  if (!ctx || !dir || !out) return TSG_E_INVALID;
+  return guard([&] {
+    auto *b = new tsg_v2block();
+    try {
+      v2block_open(ctx->c, b->b, dir, device_hint);
+    } catch (...) {
+      v2block_free(b->b);
+      delete b;
+      throw;
+    }
+    *out = b;
+  });
+}
+void tsg_v2block_close(tsg_v2block *b) {
+  if (!b) return;
+  v2block_free(b->b);
+  delete b;
+}
+int tsg_lookup_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, const uint8_t (*ids)[16], size_t nids,
+                   const tsg_lookup_opts *opts, tsg_lookup_result **out) {
+  if (!ctx || !out || (nblocks && !blocks) || (nids && !ids)) return TSG_E_INVALID;
+  return guard([&] {
+    auto *h = new LookupHolder();
+    std::unique_ptr<LookupHolder> g(h);
+    std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, V2Block *>>> per_dev;
+    for (size_t i = 0; i < nblocks; i++) per_dev[blocks[i]->b.dc].push_back({uint32_t(i), &blocks[i]->b});
+    if (per_dev.size() > 1) fail(TSG_E_INVALID, "tsg_lookup_ids: blocks must share one device (shard ids instead)");
+    if (!per_dev.empty()) device_lookup(*per_dev.begin()->first, per_dev.begin()->second, ids, nids, opts, h->o);
+    h->pub.n = h->o.id_idx.size();
+    h->pub.id_idx = h->o.id_idx.data();
+    h->pub.block_idx = h->o.block_idx.data();
+    h->pub.record_idx = h->o.rec.data();
+    h->pub.record_start = h->o.start.data();
+    h->pub.record_length = h->o.len.data();
+    h->pub.kernel_ns = h->o.kernel_ns;
+    *out = &g.release()->pub;
+  });
+}
+void tsg_lookup_result_free(tsg_lookup_result *r) { delete reinterpret_cast<LookupHolder *>(r); }
+
+// ---- writer ---------------------------------------------------------------------------
+int tsg_write_search_block(const char *dir, const uint8_t *entries, size_t len, int encoding, uint32_t page_size) {
+  if (!dir || (len && !entries)) return TSG_E_INVALID;
+  return guard([&] { write_search_block(dir, parse_entries(entries, len), encoding, page_size); });
+}
+int tsg_fb_search_entry(const uint8_t *entry, size_t len, uint8_t **out, size_t *out_len) {
+  if (!entry || !out || !out_len) return TSG_E_INVALID;
+  return guard([&] {
+    auto es = parse_entries(entry, len);
+    if (es.size() != 1) fail(TSG_E_INVALID, "expected exactly one entry");
+    auto b = fb_search_entry_bytes(es[0]);
+    *out = static_cast<uint8_t *>(std::malloc(b.size()));
+    std::memcpy(*out, b.data(), b.size());
+    *out_len = b.size();
+  });
+}
+int tsg_fb_search_header(const uint8_t *entries, size_t len, uint8_t **out, size_t *out_len) {
+  if (!out || !out_len) return TSG_E_INVALID;
+  return guard([&] {
+    HeaderBuilder h;
+    for (auto &e : parse_entries(entries, len)) h.add_entry(e);
+    auto b = h.to_bytes();
+    *out = static_cast<uint8_t *>(std::malloc(b.size()));
+    std::memcpy(*out, b.data(), b.size());
+    *out_len = b.size();
+  });
+}
+int tsg_synth_search_block(const char *dir, uint64_t n, uint64_t seed, int profile, int encoding,
+                           uint32_t page_size) {
+  if (!dir) return TSG_E_INVALID;
+  return guard([&] { synth_search_block(dir, n, seed, profile, encoding, page_size); });
+}
+int tsg_synth_v2_block(const char *dir, uint64_t n, uint64_t seed, uint8_t (*ids_out)[16]) {
+  if (!dir) return TSG_E_INVALID;
+  return guard([&] { synth_v2_block(dir, n, seed, ids_out); });
+}
+
+}  // extern "C"

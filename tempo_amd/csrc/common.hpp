@@ -1,0 +1,99 @@
+// common.hpp — shared host utilities of libtsg: byte order, status/errors,
+// hashes used by the on-disk formats, snappy framing (decode + encode).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "../../include/tsg.h"
+
+namespace tsg {
+
+// ---- errors ---------------------------------------------------------------
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+[[noreturn]] inline void fail(int code, const std::string &msg) { throw Error(code, msg); }
+void set_last_error(const std::string &m);
+
+// ---- byte order (encoding/binary) -------------------------------------------
+inline uint16_t le16(const uint8_t *p) { return uint16_t(p[0] | (p[1] << 8)); }
+inline uint32_t le32(const uint8_t *p) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return v;
+}
+inline uint64_t le64(const uint8_t *p) {
+  uint64_t v;
+  std::memcpy(&v, p, 8);
+  return v;
+}
+inline uint64_t be64(const uint8_t *p) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
+  return v;
+}
+inline void put_le16(std::vector<uint8_t> &o, uint16_t v) {
+  o.push_back(uint8_t(v));
+  o.push_back(uint8_t(v >> 8));
+}
+inline void put_le32(std::vector<uint8_t> &o, uint32_t v) {
+  for (int i = 0; i < 4; i++) o.push_back(uint8_t(v >> (8 * i)));
+}
+inline void put_le64(std::vector<uint8_t> &o, uint64_t v) {
+  for (int i = 0; i < 8; i++) o.push_back(uint8_t(v >> (8 * i)));
+}
+inline void put_be64(std::vector<uint8_t> &o, uint64_t v) {
+  for (int i = 7; i >= 0; i--) o.push_back(uint8_t(v >> (8 * i)));
+}
+
+// bytes.Compare
+inline int bytes_compare(const uint8_t *a, size_t al, const uint8_t *b, size_t bl) {
+  size_t n = al < bl ? al : bl;
+  int c = n ? std::memcmp(a, b, n) : 0;
+  if (c) return c < 0 ? -1 : 1;
+  return al == bl ? 0 : (al < bl ? -1 : 1);
+}
+
+// ---- hashes -----------------------------------------------------------------
+uint64_t xxhash64(const uint8_t *p, size_t n);  // cespare/xxhash Sum64 (seed 0)
+uint32_t fnv1_32(const uint8_t *p, size_t n);   // hash/fnv New32 (pkg/util/hash.go:15-20)
+void murmur3_128(const uint8_t *p, size_t n, uint64_t &h1, uint64_t &h2);  // spaolacci/murmur3 Sum128
+uint32_t crc32c(const uint8_t *p, size_t n);
+
+// Streaming xxhash64 for writeKeyValues' cache key (searchdatamap.go:115-128).
+struct XXH64Stream {
+  std::vector<uint8_t> buf;
+  void reset() { buf.clear(); }
+  void write(const void *p, size_t n) {
+    auto *b = static_cast<const uint8_t *>(p);
+    buf.insert(buf.end(), b, b + n);
+  }
+  uint64_t sum() const { return xxhash64(buf.data(), buf.size()); }
+};
+
+// ---- snappy framing (github.com/golang/snappy v0.0.4 wire format) ------------
+// Decode a complete framed stream (one v2 data page payload).
+void snappy_framed_decode(const uint8_t *src, size_t n, std::vector<uint8_t> &out);
+// Encode like snappy.NewBufferedWriter + Close: stream identifier, 64 KiB chunks,
+// compressed unless the saving is < 12.5 % (encode.go:218-235).
+void snappy_framed_encode(const uint8_t *src, size_t n, std::vector<uint8_t> &out);
+
+// ---- strings.ToLower (ASCII exact, documented subset beyond) ---
+std::string go_to_lower(std::string_view s);
+
+// ---- files --------------------------------------------------------------------
+bool read_file(const std::string &path, std::vector<uint8_t> &out);  // false if missing
+void write_file(const std::string &path, const uint8_t *p, size_t n);
+void make_dirs(const std::string &path);
+
+// backend.Encoding names (tempodb/backend/encoding.go:40-62)
+int parse_encoding(std::string_view s);
+const char *encoding_name(int e);
+
+}  // namespace tsg

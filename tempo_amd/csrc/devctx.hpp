@@ -1,0 +1,63 @@
+// devctx.hpp — per-device context shared by the search and lookup pipelines.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+
+#include "engine.hpp"
+
+namespace tsg {
+
+#define HIP_OK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) ::tsg::fail(TSG_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    if (p) HIP_OK(hipFree(p));
+    size_t c = std::max(n, cap * 2);
+    HIP_OK(hipMalloc(&p, c));
+    cap = c;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+struct HostBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    if (p) HIP_OK(hipHostFree(p));
+    size_t c = std::max(n, cap * 2);
+    HIP_OK(hipHostMalloc(&p, c, hipHostMallocDefault));
+    cap = c;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct DeviceCtx {
+  int ordinal = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, es0 = nullptr, es1 = nullptr;
+  std::mutex mu;
+  DevBuf desc, vmatch, bitmaps, gran, ticket, out, regions, seg_counts, hdr, err;
+  HostBuf hdesc, hout;
+  unsigned long long epoch = 0, ticket_base = 0;
+  size_t gran_tiles = 0;
+};
+
+
+}  // namespace tsg

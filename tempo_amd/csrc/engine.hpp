@@ -1,0 +1,112 @@
+// engine.hpp — device side of libtsg: per-device context, resident blocks and the
+// search / lookup pipelines. The kernels live in engine.hip.
+#pragma once
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "block.hpp"
+
+namespace tsg {
+
+struct DevKey {
+  std::string name;
+  int width = 4;
+  void *col = nullptr;  // n entries of `width` bytes; all-ones = key absent
+  uint8_t *dict_bytes = nullptr;
+  uint32_t *dict_off = nullptr;
+  uint32_t nvals = 0;
+  uint32_t *set_off = nullptr, *set_vals = nullptr;
+  uint32_t nsets = 0;
+  bool identity = true;
+  uint64_t dict_nbytes = 0;
+};
+
+// One backend search block resident in HBM (DESIGN.md "Data layout in HBM").
+struct DevBlock {
+  int device = 0;
+  uint64_t n = 0;
+  uint32_t *dur32 = nullptr;   // min(end-start, 2^32-1) (uint64 wrap kept, pitfall P2)
+  uint64_t *dur64 = nullptr;   // exact end-start, read only when a threshold >= 2^32-1
+  uint32_t *start_s = nullptr; // uint32(start/1e9)
+  uint32_t *end_s = nullptr;   // uint32(end/1e9)
+  uint8_t *ids = nullptr;      // n x 16, right aligned
+  uint64_t *start_ns = nullptr, *end_ns = nullptr;
+  std::vector<DevKey> keys;
+  uint64_t bytes = 0;
+  std::vector<void *> allocs;
+};
+
+struct DeviceCtx;
+
+struct Block {
+  HostBlock host;     // dictionaries/metadata kept on the host (names, header, page table)
+  DevBlock dev;
+  DeviceCtx *dc = nullptr;
+};
+
+struct Ctx {
+  std::vector<DeviceCtx *> devs;  // owned; freed by ctx_shutdown
+  std::mutex mu;
+};
+
+void ctx_init(Ctx &c, const tsg_options *opts);
+void ctx_shutdown(Ctx &c);
+void block_upload(Ctx &c, Block &b, int device_hint);
+void block_free(Block &b);
+
+struct SearchOut {
+  struct Rec {
+    uint8_t id[16];
+    uint64_t start, end;
+    uint64_t entry;
+    uint32_t block;
+    uint32_t pad;
+  };
+  std::vector<Rec> recs;  // ordered (before the limit cut across blocks)
+  std::vector<uint64_t> block_counts;
+  uint64_t device_bytes = 0, kernel_ns = 0;
+  uint64_t scan_ns = 0, scan_bytes = 0;
+};
+// Runs the device pipeline for a set of (block index, block) pairs that share
+// one device. limit 0 = every match; limit L = each block's first L matches.
+void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
+                   uint32_t limit, SearchOut &out);
+
+// ---- v2 lookup ---------------------------------------------------------------------
+struct V2Block {
+  int device = 0;
+  DeviceCtx *dc = nullptr;
+  // host meta
+  uint8_t block_id[16];
+  std::vector<uint8_t> min_id, max_id;
+  int64_t start_unix = 0, end_unix = 0;
+  uint32_t shards = 0;
+  uint32_t total_records = 0;
+  uint64_t bloom_m = 0, bloom_k = 0, bloom_bitlen = 0, bloom_words = 0;  // common across shards
+  bool uniform = true;
+  std::vector<uint64_t> shard_m, shard_k, shard_bitlen;
+  // device
+  uint64_t *d_bloom = nullptr;  // shards x words (host-endian u64)
+  uint8_t *d_rec_ids = nullptr; // total_records x 16
+  uint64_t *d_rec_start = nullptr;
+  uint32_t *d_rec_len = nullptr;
+  uint64_t *d_shard_m = nullptr, *d_shard_k = nullptr, *d_shard_bitlen = nullptr, *d_shard_woff = nullptr;
+  std::vector<void *> allocs;
+};
+void v2block_open(Ctx &c, V2Block &b, const std::string &dir, int device_hint);
+void v2block_free(V2Block &b);
+struct LookupOut {
+  std::vector<uint32_t> id_idx, block_idx;
+  std::vector<int32_t> rec;
+  std::vector<uint64_t> start;
+  std::vector<uint32_t> len;
+  uint64_t kernel_ns = 0;
+};
+void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>> &blocks, const uint8_t (*ids)[16],
+                   size_t nids, const tsg_lookup_opts *opts, LookupOut &out);
+
+int device_ordinal(const DeviceCtx &dc);
+
+}  // namespace tsg

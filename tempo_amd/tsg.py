@@ -1,0 +1,465 @@
+"""ctypes binding of libtsg (include/tsg.h) — the host mirror of Tempo's search
+operator interface for this path.
+
+Names follow the reference: ``SearchRequest`` (tempopb.SearchRequest,
+pkg/tempopb/tempo.proto:44-52), ``Pipeline`` (search.NewSearchPipeline,
+tempodb/search/pipeline.go:26), ``BackendSearchBlock`` with ``search``/``tags``/
+``tag_values`` (tempodb/search/backend_search_block.go:132-298, the
+SearchableBlock interface of searchable_block.go:7-11), ``Results`` metrics
+(tempodb/search/results.go:110-140) and ``TraceSearchMetadata``.
+
+There is no CPU search path: importing works anywhere (the writer/synthetic
+tooling is host code), but ``Engine()`` raises if no HIP device is visible or
+the native library is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Sequence
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtsg.so")
+
+TSG_OK = 0
+TSG_E_NOT_FOUND = 1
+TSG_E_CORRUPT = 2
+TSG_E_UNSUPPORTED_ENCODING = 3
+TSG_E_DEVICE = 4
+TSG_E_CANCELLED = 5
+TSG_E_OOM = 6
+TSG_E_INVALID = 7
+TSG_E_UNSUPPORTED = 8
+TSG_E_IO = 9
+
+ENC_NONE = 0
+ENC_SNAPPY = 6
+
+
+class TsgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"tsg error {code}: {msg}")
+        self.code = code
+
+
+class _Options(C.Structure):
+    _fields_ = [("num_devices", C.c_int32), ("devices", C.POINTER(C.c_int32)), ("flags", C.c_uint32)]
+
+
+class _Request(C.Structure):
+    _fields_ = [("ntags", C.c_uint32),
+                ("tag_keys", C.POINTER(C.c_char_p)), ("tag_key_lens", C.POINTER(C.c_uint32)),
+                ("tag_values", C.POINTER(C.c_char_p)), ("tag_value_lens", C.POINTER(C.c_uint32)),
+                ("min_duration_ms", C.c_uint32), ("max_duration_ms", C.c_uint32),
+                ("limit", C.c_uint32), ("start", C.c_uint32), ("end", C.c_uint32)]
+
+
+class _Query(C.Structure):
+    _fields_ = [("nterms", C.c_uint32),
+                ("keys", C.POINTER(C.POINTER(C.c_uint8))), ("key_lens", C.POINTER(C.c_uint32)),
+                ("values", C.POINTER(C.POINTER(C.c_uint8))), ("value_lens", C.POINTER(C.c_uint32)),
+                ("has_min", C.c_uint8), ("has_max", C.c_uint8), ("has_range", C.c_uint8),
+                ("exhaustive", C.c_uint8), ("min_ns", C.c_uint64), ("max_ns", C.c_uint64),
+                ("start_s", C.c_uint32), ("end_s", C.c_uint32)]
+
+
+class _Metrics(C.Structure):
+    _fields_ = [("traces_inspected", C.c_uint32), ("blocks_inspected", C.c_uint32),
+                ("blocks_skipped", C.c_uint32), ("pad0", C.c_uint32), ("bytes_inspected", C.c_uint64),
+                ("device_bytes_read", C.c_uint64), ("kernel_ns", C.c_uint64),
+                ("scan_kernel_ns", C.c_uint64), ("scan_bytes", C.c_uint64)]
+
+
+class _Result(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("trace_id", C.POINTER(C.c_uint8)), ("trace_id_len", C.POINTER(C.c_uint8)),
+                ("start_ns", C.POINTER(C.c_uint64)), ("end_ns", C.POINTER(C.c_uint64)),
+                ("duration_ms", C.POINTER(C.c_uint32)), ("block_idx", C.POINTER(C.c_uint32)),
+                ("entry_idx", C.POINTER(C.c_uint64)),
+                ("root_service", C.POINTER(C.c_char_p)), ("root_service_len", C.POINTER(C.c_uint32)),
+                ("root_name", C.POINTER(C.c_char_p)), ("root_name_len", C.POINTER(C.c_uint32)),
+                ("metrics", _Metrics)]
+
+
+class _SearchOpts(C.Structure):
+    _fields_ = [("limit", C.c_uint32), ("flags", C.c_uint32), ("query_id", C.c_uint64)]
+
+
+class _BlockInfo(C.Structure):
+    _fields_ = [("entries", C.c_uint64), ("pages", C.c_uint64), ("keys", C.c_uint64),
+                ("header_bytes", C.c_uint64), ("fb_bytes", C.c_uint64), ("device_bytes", C.c_uint64),
+                ("min_dur_ns", C.c_uint64), ("max_dur_ns", C.c_uint64), ("device", C.c_int32),
+                ("encoding", C.c_int32)]
+
+
+class _LookupOpts(C.Structure):
+    _fields_ = [("time_start", C.c_uint32), ("time_end", C.c_uint32),
+                ("block_start", C.c_char_p), ("block_end", C.c_char_p)]
+
+
+class _LookupResult(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("id_idx", C.POINTER(C.c_uint32)), ("block_idx", C.POINTER(C.c_uint32)),
+                ("record_idx", C.POINTER(C.c_int32)), ("record_start", C.POINTER(C.c_uint64)),
+                ("record_length", C.POINTER(C.c_uint32)), ("kernel_ns", C.c_uint64)]
+
+
+# Every symbol include/tsg.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "tsg_init", "tsg_shutdown", "tsg_device_count", "tsg_last_error", "tsg_abi_version", "tsg_cancel",
+    "tsg_pipeline_new", "tsg_pipeline_query", "tsg_pipeline_free", "tsg_pipeline_matches_header",
+    "tsg_block_open", "tsg_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
+    "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_results_combine",
+    "tsg_v2block_open", "tsg_v2block_close", "tsg_lookup_ids", "tsg_lookup_result_free",
+    "tsg_write_search_block", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
+    "tsg_synth_v2_block",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libtsg.so; raises (loudly) if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libtsg.so not built at {LIB_PATH}: run __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        vp, u8p = C.c_void_p, C.POINTER(C.c_uint8)
+        L.tsg_last_error.restype = C.c_char_p
+        L.tsg_init.argtypes = [C.POINTER(_Options), C.POINTER(vp)]
+        L.tsg_shutdown.argtypes = [vp]
+        L.tsg_device_count.argtypes = [vp]
+        L.tsg_pipeline_new.argtypes = [C.POINTER(_Request), C.POINTER(vp)]
+        L.tsg_pipeline_query.argtypes = [vp]
+        L.tsg_pipeline_query.restype = C.POINTER(_Query)
+        L.tsg_pipeline_free.argtypes = [vp]
+        L.tsg_pipeline_matches_header.argtypes = [C.POINTER(_Query), C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
+        L.tsg_block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
+        L.tsg_block_close.argtypes = [vp]
+        L.tsg_block_info_get.argtypes = [vp, C.POINTER(_BlockInfo)]
+        L.tsg_block_tags.argtypes = [vp, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+        L.tsg_block_tag_values.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
+                                           C.POINTER(C.c_size_t)]
+        L.tsg_free.argtypes = [vp]
+        L.tsg_search.argtypes = [vp, C.POINTER(vp), C.c_size_t, C.POINTER(_Query), C.POINTER(_SearchOpts),
+                                 C.POINTER(C.POINTER(_Result))]
+        L.tsg_result_free.argtypes = [C.POINTER(_Result)]
+        L.tsg_results_combine.argtypes = [C.POINTER(_Result), C.c_uint32, C.POINTER(C.POINTER(_Result))]
+        L.tsg_v2block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
+        L.tsg_v2block_close.argtypes = [vp]
+        L.tsg_lookup_ids.argtypes = [vp, C.POINTER(vp), C.c_size_t, vp, C.c_size_t, C.POINTER(_LookupOpts),
+                                     C.POINTER(C.POINTER(_LookupResult))]
+        L.tsg_lookup_result_free.argtypes = [C.POINTER(_LookupResult)]
+        L.tsg_write_search_block.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int, C.c_uint32]
+        L.tsg_fb_search_entry.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]
+        L.tsg_fb_search_header.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]
+        L.tsg_synth_search_block.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int, C.c_uint32]
+        L.tsg_synth_v2_block.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != TSG_OK:
+        raise TsgError(rc, lib().tsg_last_error().decode(errors="replace"))
+
+
+# ---------------------------------------------------------------------------
+# request / pipeline
+
+@dataclass
+class SearchRequest:
+    """tempopb.SearchRequest (pkg/tempopb/tempo.proto:44-52)."""
+    tags: Dict[str, str] = field(default_factory=dict)
+    min_duration_ms: int = 0
+    max_duration_ms: int = 0
+    limit: int = 0
+    start: int = 0
+    end: int = 0
+
+    def _c(self):
+        ks = [k.encode() if isinstance(k, str) else k for k in self.tags]
+        vs = [v.encode() if isinstance(v, str) else v for v in self.tags.values()]
+        n = len(ks)
+        r = _Request()
+        r.ntags = n
+        r._ks = (C.c_char_p * max(n, 1))(*ks)
+        r._vs = (C.c_char_p * max(n, 1))(*vs)
+        r._kl = (C.c_uint32 * max(n, 1))(*[len(k) for k in ks])
+        r._vl = (C.c_uint32 * max(n, 1))(*[len(v) for v in vs])
+        r.tag_keys, r.tag_values, r.tag_key_lens, r.tag_value_lens = r._ks, r._vs, r._kl, r._vl
+        r.min_duration_ms, r.max_duration_ms = self.min_duration_ms, self.max_duration_ms
+        r.limit, r.start, r.end = self.limit, self.start, self.end
+        return r
+
+
+class Pipeline:
+    """search.NewSearchPipeline (pipeline.go:26): rewriteTagLookup + ToLower, host side."""
+
+    def __init__(self, req: SearchRequest):
+        self.req = req
+        self._creq = req._c()
+        self.h = C.c_void_p()
+        _check(lib().tsg_pipeline_new(C.byref(self._creq), C.byref(self.h)))
+        self.query = lib().tsg_pipeline_query(self.h)
+
+    def terms(self):
+        q = self.query.contents
+        return [(C.string_at(q.keys[i], q.key_lens[i]), C.string_at(q.values[i], q.value_lens[i]))
+                for i in range(q.nterms)]
+
+    def matches_block(self, header: bytes) -> bool:
+        m = C.c_int()
+        _check(lib().tsg_pipeline_matches_header(self.query, header, len(header), C.byref(m)))
+        return bool(m.value)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.tsg_pipeline_free(self.h)
+            self.h = None
+
+
+# ---------------------------------------------------------------------------
+# results
+
+@dataclass
+class TraceSearchMetadata:
+    trace_id: bytes          # right-aligned 16 bytes
+    trace_id_len: int
+    root_service_name: str
+    root_trace_name: str
+    start_time_unix_nano: int
+    duration_ms: int
+    end_time_unix_nano: int = 0
+    block_idx: int = 0
+    entry_idx: int = 0
+
+    @property
+    def trace_id_hex(self) -> str:
+        """util.TraceIDToHexString: hex, leading zeros trimmed (pkg/util/traceid.go:46-52)."""
+        return self.trace_id.hex().lstrip("0")
+
+
+@dataclass
+class SearchMetrics:
+    inspected_traces: int
+    inspected_bytes: int
+    inspected_blocks: int
+    skipped_blocks: int
+    device_bytes_read: int = 0
+    kernel_ns: int = 0
+    scan_kernel_ns: int = 0
+    scan_bytes: int = 0
+
+
+def _unpack(rp) -> (List[TraceSearchMetadata], SearchMetrics):
+    r = rp.contents
+    out = []
+    n = r.n
+    if n:
+        ids = C.string_at(r.trace_id, 16 * n)
+        for i in range(n):
+            out.append(TraceSearchMetadata(
+                trace_id=ids[16 * i:16 * i + 16], trace_id_len=r.trace_id_len[i],
+                root_service_name=C.string_at(r.root_service[i], r.root_service_len[i]).decode(errors="replace"),
+                root_trace_name=C.string_at(r.root_name[i], r.root_name_len[i]).decode(errors="replace"),
+                start_time_unix_nano=r.start_ns[i], duration_ms=r.duration_ms[i], end_time_unix_nano=r.end_ns[i],
+                block_idx=r.block_idx[i], entry_idx=r.entry_idx[i]))
+    m = r.metrics
+    return out, SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,
+                              m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
+
+
+# ---------------------------------------------------------------------------
+# engine / blocks
+
+class Engine:
+    """tsg_ctx: one HIP stream per device. Raises TsgError(TSG_E_DEVICE) without a GPU."""
+
+    def __init__(self, devices: Optional[Sequence[int]] = None):
+        o = _Options()
+        if devices:
+            self._devs = (C.c_int32 * len(devices))(*devices)
+            o.num_devices, o.devices = len(devices), self._devs
+        self.h = C.c_void_p()
+        _check(lib().tsg_init(C.byref(o), C.byref(self.h)))
+
+    @property
+    def device_count(self):
+        return lib().tsg_device_count(self.h)
+
+    def open_block(self, path: str, device: int = 0) -> "BackendSearchBlock":
+        return BackendSearchBlock(self, path, device)
+
+    def search(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0):
+        """Ordered match sequence + metrics (tsg_search)."""
+        arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+        opts = _SearchOpts(limit=limit)
+        rp = C.POINTER(_Result)()
+        _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
+        try:
+            return _unpack(rp)
+        finally:
+            lib().tsg_result_free(rp)
+
+    def search_request(self, blocks, req: SearchRequest, limit: Optional[int] = None):
+        """instance.Search: ordered matches cut at the limit, then combined + sorted."""
+        p = Pipeline(req)
+        lim = req.limit if limit is None else limit
+        arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+        opts = _SearchOpts(limit=lim)
+        rp = C.POINTER(_Result)()
+        _check(lib().tsg_search(self.h, arr, len(blocks), p.query, C.byref(opts), C.byref(rp)))
+        try:
+            fin = C.POINTER(_Result)()
+            _check(lib().tsg_results_combine(rp, lim or 20, C.byref(fin)))
+            try:
+                return _unpack(fin)
+            finally:
+                lib().tsg_result_free(fin)
+        finally:
+            lib().tsg_result_free(rp)
+
+    def open_v2block(self, path: str, device: int = 0) -> "V2Block":
+        return V2Block(self, path, device)
+
+    def lookup(self, blocks: Sequence["V2Block"], ids, time_start=0, time_end=0, block_start=None,
+               block_end=None):
+        import numpy as np
+        ids = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1, 16)
+        arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+        o = _LookupOpts(time_start, time_end, block_start, block_end)
+        rp = C.POINTER(_LookupResult)()
+        _check(lib().tsg_lookup_ids(self.h, arr, len(blocks), ids.ctypes.data, ids.shape[0], C.byref(o),
+                                    C.byref(rp)))
+        try:
+            r = rp.contents
+            n = r.n
+            if n == 0:
+                return np.zeros((0, 5), dtype=np.int64), r.kernel_ns
+            cols = [np.ctypeslib.as_array(r.id_idx, (n,)).astype(np.int64),
+                    np.ctypeslib.as_array(r.block_idx, (n,)).astype(np.int64),
+                    np.ctypeslib.as_array(r.record_idx, (n,)).astype(np.int64),
+                    np.ctypeslib.as_array(r.record_start, (n,)).astype(np.int64),
+                    np.ctypeslib.as_array(r.record_length, (n,)).astype(np.int64)]
+            return np.stack(cols, axis=1), r.kernel_ns
+        finally:
+            lib().tsg_lookup_result_free(rp)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().tsg_shutdown(self.h)
+            self.h = None
+
+
+class BackendSearchBlock:
+    """A backend search block resident on one device (tsg_block)."""
+
+    def __init__(self, eng: Engine, path: str, device: int = 0):
+        self.path = path
+        self.h = C.c_void_p()
+        _check(lib().tsg_block_open(eng.h, path.encode(), device, C.byref(self.h)))
+
+    def info(self):
+        i = _BlockInfo()
+        _check(lib().tsg_block_info_get(self.h, C.byref(i)))
+        return {f: getattr(i, f) for f, _ in _BlockInfo._fields_}
+
+    def _strings(self, fn, *args):
+        p, ln, n = C.POINTER(C.c_uint8)(), C.c_size_t(), C.c_size_t()
+        _check(fn(self.h, *args, C.byref(p), C.byref(ln), C.byref(n)))
+        buf = C.string_at(p, ln.value) if ln.value else b""
+        lib().tsg_free(p)
+        out, o = [], 0
+        for _ in range(n.value):
+            (l,) = struct.unpack_from("<I", buf, o)
+            out.append(buf[o + 4:o + 4 + l])
+            o += 4 + l
+        return out
+
+    def tags(self):
+        return self._strings(lib().tsg_block_tags)
+
+    def tag_values(self, key: bytes):
+        return self._strings(lib().tsg_block_tag_values, key, len(key))
+
+    def close(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.tsg_block_close(self.h)
+            self.h = None
+
+    __del__ = close
+
+
+class V2Block:
+    def __init__(self, eng: Engine, path: str, device: int = 0):
+        self.h = C.c_void_p()
+        _check(lib().tsg_v2block_open(eng.h, path.encode(), device, C.byref(self.h)))
+
+    def close(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.tsg_v2block_close(self.h)
+            self.h = None
+
+    __del__ = close
+
+
+# ---------------------------------------------------------------------------
+# writer tooling (host)
+
+def encode_entries(entries: Iterable[dict]) -> bytes:
+    """Entry list wire format of tsg_write_search_block.
+
+    entry = {"id": bytes, "start": int, "end": int, "tags": {key: [values]}}"""
+    out = bytearray()
+    for e in entries:
+        tid = e["id"]
+        out += struct.pack("<I", len(tid)) + tid
+        pairs = []
+        for k, vs in e.get("tags", {}).items():
+            if isinstance(vs, (str, bytes)):
+                vs = [vs]
+            for v in vs:
+                pairs.append((k.encode() if isinstance(k, str) else k, v.encode() if isinstance(v, str) else v))
+        out += struct.pack("<QQI", e.get("start", 0) & (2**64 - 1), e.get("end", 0) & (2**64 - 1), len(pairs))
+        for k, v in pairs:
+            out += struct.pack("<I", len(k)) + k + struct.pack("<I", len(v)) + v
+    return bytes(out)
+
+
+def write_search_block(path: str, entries: Iterable[dict], encoding: int = ENC_SNAPPY, page_size: int = 0):
+    buf = encode_entries(entries)
+    _check(lib().tsg_write_search_block(path.encode(), buf, len(buf), encoding, page_size))
+
+
+def _bytes_out(fn, *args):
+    p, n = C.POINTER(C.c_uint8)(), C.c_size_t()
+    _check(fn(*args, C.byref(p), C.byref(n)))
+    b = C.string_at(p, n.value)
+    lib().tsg_free(p)
+    return b
+
+
+def fb_search_entry(entry: dict) -> bytes:
+    """SearchEntryMutable.ToBytes (pkg/tempofb/search_entry_mutable.go:41-46)."""
+    buf = encode_entries([entry])
+    return _bytes_out(lib().tsg_fb_search_entry, buf, len(buf))
+
+
+def fb_search_header(entries: Iterable[dict]) -> bytes:
+    """SearchBlockHeaderMutable.ToBytes after AddEntry of each entry."""
+    buf = encode_entries(entries)
+    return _bytes_out(lib().tsg_fb_search_header, buf, len(buf))
+
+
+def synth_search_block(path: str, n: int, seed: int = 0, profile: int = 0, encoding: int = ENC_SNAPPY,
+                       page_size: int = 1024 * 1024):
+    _check(lib().tsg_synth_search_block(path.encode(), n, seed, profile, encoding, page_size))
+
+
+def synth_v2_block(path: str, n: int, seed: int = 0):
+    import numpy as np
+    ids = np.zeros((n, 16), dtype=np.uint8)
+    _check(lib().tsg_synth_v2_block(path.encode(), n, seed, ids.ctypes.data))
+    return ids

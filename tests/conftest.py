@@ -1,0 +1,27 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libtsg on a HIP device)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "known_answers.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def engine():
+    from tempo_amd import Engine
+    e = Engine()
+    yield e
+    e.close()

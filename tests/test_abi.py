@@ -1,0 +1,100 @@
+"""The C ABI library: builds, loads, exports every symbol include/tsg.h declares,
+refuses to run without a device, and its host logic (request normalisation,
+block prefilter, writer) agrees with the oracle. CPU only: no compute call."""
+import os
+import re
+
+import pytest
+
+from oracle import oracle as O
+import tempo_amd as T
+from tempo_amd import tsg
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "tsg.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tsg_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_every_declared_symbol_is_exported():
+    L = T.lib()
+    syms = header_symbols()
+    assert len(syms) >= 29
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(tsg.EXPORTED) == syms
+
+
+def test_no_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is visible")
+    with pytest.raises(T.TsgError) as e:
+        T.Engine()
+    assert e.value.code == tsg.TSG_E_DEVICE
+
+
+def test_abi_version():
+    assert T.lib().tsg_abi_version() == 1
+
+
+@pytest.mark.parametrize("req,terms", [
+    ({"error": "true"}, [(b"status.code", b"2")]),
+    ({"error": "false"}, [(b"error", b"false")]),
+    ({"status.code": "error"}, [(b"status.code", b"2")]),
+    ({"status.code": "ok"}, [(b"status.code", b"1")]),
+    ({"status.code": "unset"}, [(b"status.code", b"0")]),
+    ({"status.code": "bogus"}, [(b"status.code", b"bogus")]),
+    ({"Service.Name": "SVC-07"}, [(b"service.name", b"svc-07")]),
+    ({"Error": "true"}, [(b"error", b"true")]),  # rewrite matches the request key before ToLower
+    ({"x-dbg-exhaustive": "!"}, []),
+    ({"k": ""}, [(b"k", b"")]),
+    ({"ÄÖ": "ÉŸ"}, [("äö".encode(), "éÿ".encode())]),
+])
+def test_pipeline_normalisation(req, terms):
+    p = T.Pipeline(T.SearchRequest(tags=req))
+    assert p.terms() == terms
+    q = p.query.contents
+    assert q.exhaustive == (1 if "x-dbg-exhaustive" in req else 0)
+
+
+def test_pipeline_filters_flags():
+    q = T.Pipeline(T.SearchRequest(min_duration_ms=10, max_duration_ms=0, start=5, end=0)).query.contents
+    assert (q.has_min, q.has_max, q.has_range, q.min_ns) == (1, 0, 0, 10_000_000)
+    q = T.Pipeline(T.SearchRequest(max_duration_ms=90_000, start=5, end=9)).query.contents
+    assert (q.has_min, q.has_max, q.has_range, q.max_ns, q.start_s, q.end_s) == (0, 1, 1, 90_000_000_000, 5, 9)
+
+
+def test_block_prefilter_matches_oracle(golden):
+    blk = golden["pipeline"]["block"]
+    h = blk["header"]
+    hdr = T.fb_search_header([{"id": b"a", "start": 0, "end": h["min_dur_ns"], "tags": h["tags"]},
+                              {"id": b"b", "start": 0, "end": h["max_dur_ns"], "tags": h["tags"]}])
+    for c in blk["cases"]:
+        req = T.SearchRequest(tags=c["req"], min_duration_ms=c["min"], max_duration_ms=c["max"])
+        assert T.Pipeline(req).matches_block(hdr) == c["match"], c["name"]
+        assert O.pipeline_matches_block(hdr, tags=c["req"], min_ms=c["min"], max_ms=c["max"]) == c["match"]
+
+
+def test_header_min_dur_quirk():
+    """SearchBlockHeaderMutable.AddEntry: after a zero-duration entry the next one
+    overwrites MinDur (pkg/tempofb/SearchBlockHeader_util.go:37-43, pitfall P1)."""
+    import struct
+    hdr = T.fb_search_header([{"id": b"a", "start": 5, "end": 10}, {"id": b"b", "start": 7, "end": 7},
+                              {"id": b"c", "start": 0, "end": 500}])
+    # min = 5 -> 0 (dur 0 < 5) -> 500 (MinDur == 0 is treated as unset)
+    req = T.SearchRequest(max_duration_ms=0)
+    p = T.Pipeline(T.SearchRequest(tags={}, max_duration_ms=1))
+    assert p.matches_block(hdr)  # MinDur = 500 ns <= 1 ms
+    # the oracle reads the same stored value
+    assert O.pipeline_matches_block(hdr, max_ms=1)
+
+
+def test_writer_entry_is_readable_flatbuffer():
+    fb = T.fb_search_entry({"id": b"\x01\x02", "start": 3, "end": 9, "tags": {"a": ["x", "y"], "b": ["z"]}})
+    assert O.contains_tag_entry(fb, b"a", b"y")
+    assert O.contains_tag_entry(fb, b"b", b"")
+    assert not O.contains_tag_entry(fb, b"c", b"")

@@ -1,0 +1,212 @@
+"""GPU parity: libtsg search (HIP, gfx950) vs the CPU oracle on the same blocks.
+
+Bit-exact bar: the same ordered match sequence (block, scan position, trace id,
+start, end, DurationMs, root names) and the same SearchMetrics.
+"""
+import os
+import random
+
+import pytest
+
+from oracle import oracle as O
+import tempo_amd as T
+from tests.helpers import gen_search_data, match_key, random_entries, ref_id, tsg_key, write_block
+
+pytestmark = pytest.mark.gpu
+
+
+def both(engine, paths, tags=None, min_ms=0, max_ms=0, start=0, end=0, limit=0):
+    req = T.SearchRequest(tags=dict(tags or {}), min_duration_ms=min_ms, max_duration_ms=max_ms, start=start,
+                          end=end)
+    blocks = [engine.open_block(p) for p in paths]
+    got, met = engine.search(blocks, T.Pipeline(req), limit=limit)
+    oblocks = [O.Block(p) for p in paths]
+    exp, omet, st = O.search(oblocks, tags=tags, min_ms=min_ms, max_ms=max_ms, start=start, end=end, limit=limit)
+    assert st == 0
+    for b in blocks:
+        b.close()
+    return got, met, exp, omet
+
+
+def assert_parity(got, met, exp, omet):
+    assert [tsg_key(m) for m in got] == [match_key(m) for m in exp]
+    assert met.inspected_traces == omet["traces_inspected"]
+    assert met.inspected_bytes == omet["bytes_inspected"]
+    assert met.inspected_blocks == omet["blocks_inspected"]
+    assert met.skipped_blocks == omet["blocks_skipped"]
+
+
+# ---- the reference's own known answers, through the GPU
+@pytest.mark.parametrize("enc", [T.ENC_NONE, T.ENC_SNAPPY])
+def test_backend_search_block_search(engine, tmp_path, enc):
+    ents = [{"id": ref_id(i), "tags": gen_search_data(i)} for i in range(10_000)]
+    p = write_block(str(tmp_path), "b", ents, enc)
+    got, met, exp, omet = both(engine, [p], tags={"key20": "value_B_20"})
+    assert len(got) == 1 and met.inspected_traces == 10_000
+    assert_parity(got, met, exp, omet)
+
+
+def test_contains_tag_table(engine, tmp_path, golden):
+    g = golden["contains_tag"]
+    p = write_block(str(tmp_path), "b", [{"id": ref_id(1), "tags": g["entry"]}])
+    blk = engine.open_block(p)
+    for c in g["cases"]:
+        got, _ = engine.search([blk], T.Pipeline(T.SearchRequest(tags={c["key"]: c["value"]})))
+        assert (len(got) == 1) == c["found"], c
+
+
+def test_pipeline_tables(engine, tmp_path, golden):
+    g = golden["pipeline"]
+    for i, c in enumerate(g["tags"]):
+        p = write_block(str(tmp_path), "t%d" % i, [{"id": ref_id(1), "tags": c["data"]}])
+        got, _ = engine.search([engine.open_block(p)], T.Pipeline(T.SearchRequest(tags=c["req"])))
+        assert (len(got) == 1) == c["match"], c["name"]
+    for i, c in enumerate(g["duration"]):
+        p = write_block(str(tmp_path), "d%d" % i, [{"id": ref_id(1), "start": c["start"], "end": c["end"]}])
+        req = T.SearchRequest(min_duration_ms=c["min"], max_duration_ms=c["max"])
+        got, _ = engine.search([engine.open_block(p)], T.Pipeline(req))
+        assert (len(got) == 1) == c["match"], c["name"]
+    for i, c in enumerate(g["start_end"]):
+        p = write_block(str(tmp_path), "s%d" % i, [{"id": ref_id(1), "start": c["start"], "end": c["end"]}])
+        got, _ = engine.search([engine.open_block(p)], T.Pipeline(T.SearchRequest(start=c["rs"], end=c["re"])))
+        assert (len(got) == 1) == c["match"], c["name"]
+
+
+def test_search_block_metrics(engine, tmp_path, golden):
+    g = golden["search_block_metrics"]
+    data = {"key1": ["value10", "value11"], "key2": ["value20", "value21"], "key3": ["value30", "value31"],
+            "key4": ["value40", "value41"]}
+    p = write_block(str(tmp_path), "b", [{"id": ref_id(i), "tags": data} for i in range(g["trace_count"])],
+                    T.ENC_NONE)
+    blk = engine.open_block(p)
+    for c in g["cases"]:
+        got, met = engine.search([blk], T.Pipeline(T.SearchRequest(tags=c["req"])))
+        assert len(got) == c["results"]
+        assert (met.inspected_blocks, met.inspected_traces, met.skipped_blocks) == (
+            c["blocks_inspected"], c["traces_inspected"], c["blocks_skipped"])
+
+
+# ---- randomized parity
+QUERIES = [
+    dict(tags={"k0": "v1"}),
+    dict(tags={"k0": "v", "k1": "x"}),
+    dict(tags={"k2": "v3-y", "k3": ""}),
+    dict(tags={"root.service.name": "svc-1"}),
+    dict(tags={"k0": "v1"}, min_ms=20, max_ms=200),
+    dict(min_ms=5000),  # threshold >= 2^32 ns: exact 64-bit path
+    dict(max_ms=4295),
+    dict(start=1_700_000_900, end=1_700_001_800),
+    dict(tags={"k1": "z", "k4": "v0"}, min_ms=1, start=1_700_000_000, end=1_700_003_000),
+    dict(tags={"nokey": "v"}),
+    dict(tags={"x-dbg-exhaustive": "!"}),
+    dict(tags={"K0": "V1-X"}),
+    dict(tags={}),
+]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_blocks_parity(engine, tmp_path, seed):
+    rng = random.Random(seed)
+    paths = []
+    for b in range(3):
+        ents = random_entries(rng, rng.choice([1, 37, 700, 5000]), nkeys=5, nvals=6 + 40 * b, multi=1 + b)
+        paths.append(write_block(str(tmp_path), "b%d" % b, ents, rng.choice([T.ENC_NONE, T.ENC_SNAPPY]),
+                                 page_size=rng.choice([0, 4096, 65536])))
+    for q in QUERIES:
+        got, met, exp, omet = both(engine, paths, **q)
+        assert_parity(got, met, exp, omet)
+
+
+@pytest.mark.parametrize("limit", [1, 2, 5, 20, 1000])
+def test_limit_parity(engine, tmp_path, limit):
+    rng = random.Random(limit)
+    paths = []
+    shared = random_entries(rng, 50, nkeys=2, nvals=2)
+    for b in range(4):
+        ents = random_entries(rng, 3000, nkeys=3, nvals=3)
+        # duplicate trace ids across blocks exercise the distinct-id rule
+        ids = {e["id"] for e in ents}
+        ents += [dict(e) for e in shared if e["id"] not in ids]
+        ents.sort(key=lambda e: e["id"])
+        paths.append(write_block(str(tmp_path), "b%d" % b, ents, page_size=8192))
+    for q in [dict(tags={"k0": "v"}), dict(tags={"k1": "v1"}), dict(tags={"k2": "zz"})]:
+        got, met, exp, omet = both(engine, paths, limit=limit, **q)
+        assert_parity(got, met, exp, omet)
+
+
+def test_wide_dictionaries(engine, tmp_path):
+    """u16 / u32 value-set columns and bitmaps larger than the LDS budget."""
+    rng = random.Random(5)
+    ents = []
+    for i in range(120_000):
+        ents.append({"id": (i * 2654435761 % 2**64).to_bytes(8, "big") + i.to_bytes(8, "big"),
+                     "start": 10**18, "end": 10**18 + i,
+                     "tags": {"mid": ["m%05d" % (i % 4000)], "uniq": ["u%07d" % i],
+                              "multi": ["a%d" % (i % 300), "b%d" % (i % 7)]}})
+    ents.sort(key=lambda e: e["id"])
+    p = write_block(str(tmp_path), "w", ents, T.ENC_SNAPPY, page_size=1 << 20)
+    for q in [dict(tags={"mid": "m0001"}), dict(tags={"uniq": "u00123"}), dict(tags={"uniq": "99"}),
+              dict(tags={"multi": "b3", "mid": "7"}), dict(tags={"multi": "a29"})]:
+        got, met, exp, omet = both(engine, [p], **q)
+        assert_parity(got, met, exp, omet)
+
+
+def test_empty_and_missing_blocks(engine, tmp_path):
+    p0 = write_block(str(tmp_path), "empty", [])
+    ents = [{"id": ref_id(i), "tags": gen_search_data(i % 7)} for i in range(100)]
+    p1 = write_block(str(tmp_path), "one", ents)
+    got, met, exp, omet = both(engine, [p0, p1, p0], tags={"key3": "value"})
+    assert_parity(got, met, exp, omet)
+    # meta missing -> TSG_E_NOT_FOUND at open (the Go shim maps it to a no-op)
+    os.remove(os.path.join(p1, "search.meta.json"))
+    with pytest.raises(T.TsgError) as e:
+        engine.open_block(p1)
+    assert e.value.code == 1
+
+
+def test_corrupt_blocks_are_rejected(engine, tmp_path):
+    ents = [{"id": ref_id(i), "tags": gen_search_data(i)} for i in range(2000)]
+    p = write_block(str(tmp_path), "c", ents, page_size=4096)
+    idx = os.path.join(p, "search-index")
+    b = bytearray(open(idx, "rb").read())
+    b[30] ^= 1
+    open(idx, "wb").write(bytes(b))
+    with pytest.raises(T.TsgError) as e:
+        engine.open_block(p)
+    assert e.value.code == 2
+
+
+def test_tags_and_tag_values(engine, tmp_path):
+    ents = [{"id": ref_id(i), "tags": {"a": ["x%d" % (i % 3)], "b": ["y"]}} for i in range(30)]
+    blk = engine.open_block(write_block(str(tmp_path), "t", ents))
+    assert sorted(blk.tags()) == [b"a", b"b"]
+    assert sorted(blk.tag_values(b"a")) == [b"x0", b"x1", b"x2"]
+    assert blk.tag_values(b"zz") == []
+
+
+def test_combine_matches_oracle(engine, tmp_path):
+    rng = random.Random(11)
+    shared = random_entries(rng, 40, nkeys=1, nvals=1)
+    paths = []
+    for b in range(3):
+        ents = random_entries(rng, 500, nkeys=1, nvals=2)
+        ids = {e["id"] for e in ents}
+        ents += [dict(e, start=e["start"] + b) for e in shared if e["id"] not in ids]
+        paths.append(write_block(str(tmp_path), "b%d" % b, ents))
+    blocks = [engine.open_block(p) for p in paths]
+    for lim in [0, 3, 20]:
+        got, _ = engine.search_request(blocks, T.SearchRequest(tags={"k0": "v"}, limit=lim))
+        exp, _, _ = O.search([O.Block(p) for p in paths], tags={"k0": "v"}, limit=lim or 20, combine=lim or 20)
+        assert [(m.trace_id, m.start_time_unix_nano, m.duration_ms, m.root_service_name.encode())
+                for m in got] == [(e["id"], e["start_ns"], e["duration_ms"], e["root_service"]) for e in exp]
+
+
+def test_synthetic_block_full_scan(engine, tmp_path):
+    p = os.path.join(str(tmp_path), "syn")
+    T.synth_search_block(p, 60_000, seed=3)
+    q = dict(tags={"service.name": "svc-07", "http.method": "get", "status.code": "error"}, min_ms=10,
+             max_ms=1000, start=1_700_000_900, end=1_700_002_700)
+    for qq in [q, dict(tags={"service.name": "svc-07"}), dict(tags={"name": "span-001"}),
+               dict(tags={"http.url": "/users/12"})]:
+        got, met, exp, omet = both(engine, [p], **qq)
+        assert_parity(got, met, exp, omet)
