@@ -1,0 +1,145 @@
+// devctx.hip — device contexts, HBM residency of search blocks (host code using the
+// HIP runtime; the search kernels are in search.hip, the lookup kernels in lookup.hip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "devctx.hpp"
+
+namespace tsg {
+
+int device_ordinal(const DeviceCtx &dc) { return dc.ordinal; }
+
+void ctx_init(Ctx &c, const tsg_options *opts) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) fail(TSG_E_DEVICE, "no HIP device visible (libtsg has no CPU path)");
+  std::vector<int> ords;
+  if (opts && opts->devices && opts->num_devices > 0) {
+    for (int i = 0; i < opts->num_devices; i++) ords.push_back(opts->devices[i]);
+  } else {
+    int m = (opts && opts->num_devices > 0) ? std::min(opts->num_devices, n) : n;
+    for (int i = 0; i < m; i++) ords.push_back(i);
+  }
+  for (int o : ords) {
+    if (o < 0 || o >= n) fail(TSG_E_INVALID, "device ordinal out of range");
+    auto dc = std::make_unique<DeviceCtx>();
+    dc->ordinal = o;
+    HIP_OK(hipSetDevice(o));
+    HIP_OK(hipStreamCreateWithFlags(&dc->stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&dc->ev0));
+    HIP_OK(hipEventCreate(&dc->ev1));
+    HIP_OK(hipEventCreate(&dc->es0));
+    HIP_OK(hipEventCreate(&dc->es1));
+    dc->ticket.ensure(64);
+    HIP_OK(hipMemset(dc->ticket.p, 0, 64));
+    dc->err.ensure(64);
+    HIP_OK(hipMemset(dc->err.p, 0, 64));
+    c.devs.push_back(dc.release());
+  }
+}
+
+void ctx_shutdown(Ctx &c) {
+  for (auto &dc : c.devs) {
+    (void)hipSetDevice(dc->ordinal);
+    (void)hipStreamSynchronize(dc->stream);
+    for (DevBuf *b : {&dc->desc, &dc->vmatch, &dc->bitmaps, &dc->gran, &dc->ticket, &dc->out, &dc->regions,
+                      &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->tile_counts, &dc->wg_sums})
+      b->release();
+    dc->hdesc.release();
+    dc->hout.release();
+    (void)hipEventDestroy(dc->ev0);
+    (void)hipEventDestroy(dc->ev1);
+    (void)hipEventDestroy(dc->es0);
+    (void)hipEventDestroy(dc->es1);
+    (void)hipStreamDestroy(dc->stream);
+    delete dc;
+  }
+  c.devs.clear();
+}
+
+template <typename T>
+static T *dev_upload(DevBlock &b, const T *src, size_t count, hipStream_t s) {
+  void *p = nullptr;
+  size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  HIP_OK(hipMalloc(&p, bytes));
+  b.allocs.push_back(p);
+  b.bytes += bytes;
+  if (count) HIP_OK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+  return static_cast<T *>(p);
+}
+
+void block_upload(Ctx &c, Block &b, int device_hint) {
+  if (c.devs.empty()) fail(TSG_E_DEVICE, "no device");
+  DeviceCtx &dc = *c.devs[size_t(std::max(device_hint, 0)) % c.devs.size()];
+  b.dc = &dc;
+  DevBlock &d = b.dev;
+  const HostBlock &h = b.host;
+  d.device = dc.ordinal;
+  d.n = h.n;
+  std::lock_guard<std::mutex> lk(dc.mu);
+  HIP_OK(hipSetDevice(dc.ordinal));
+  hipStream_t s = dc.stream;
+  size_t n = h.n;
+  std::vector<uint32_t> dur32(n), ss(n), es(n);
+  std::vector<uint64_t> dur64(n);
+  for (size_t i = 0; i < n; i++) {
+    uint64_t dd = h.end[i] - h.start[i];  // uint64 wrap (pitfall P2)
+    dur64[i] = dd;
+    dur32[i] = dd >= 0xffffffffULL ? 0xffffffffu : uint32_t(dd);
+    ss[i] = uint32_t(h.start[i] / 1000000000ULL);
+    es[i] = uint32_t(h.end[i] / 1000000000ULL);
+  }
+  d.dur32 = dev_upload(d, dur32.data(), n, s);
+  d.dur64 = dev_upload(d, dur64.data(), n, s);
+  d.start_s = dev_upload(d, ss.data(), n, s);
+  d.end_s = dev_upload(d, es.data(), n, s);
+  d.ids = dev_upload(d, h.ids.data(), n * 16, s);
+  d.start_ns = dev_upload(d, h.start.data(), n, s);
+  d.end_ns = dev_upload(d, h.end.data(), n, s);
+  // the staging vectors must outlive the async copies
+  HIP_OK(hipStreamSynchronize(s));
+  for (const KeyColumn &kc : h.keys) {
+    DevKey k;
+    k.name = kc.name;
+    k.width = kc.width();
+    k.nvals = kc.nvals();
+    k.nsets = kc.nsets();
+    k.identity = kc.identity;
+    if (k.width == 1) {
+      std::vector<uint8_t> col(n);
+      for (size_t i = 0; i < n; i++) col[i] = kc.col[i] == kNone ? 0xff : uint8_t(kc.col[i]);
+      k.col = dev_upload(d, col.data(), n, s);
+      HIP_OK(hipStreamSynchronize(s));
+    } else if (k.width == 2) {
+      std::vector<uint16_t> col(n);
+      for (size_t i = 0; i < n; i++) col[i] = kc.col[i] == kNone ? 0xffff : uint16_t(kc.col[i]);
+      k.col = dev_upload(d, col.data(), n, s);
+      HIP_OK(hipStreamSynchronize(s));
+    } else {
+      k.col = dev_upload(d, kc.col.data(), n, s);
+    }
+    k.dict_bytes = dev_upload(d, kc.dict_bytes.data(), kc.dict_bytes.size(), s);
+    k.dict_off = dev_upload(d, kc.dict_off.data(), kc.dict_off.size(), s);
+    k.dict_nbytes = kc.dict_bytes.size();
+    if (!kc.identity) {
+      k.set_off = dev_upload(d, kc.set_off.data(), kc.set_off.size(), s);
+      k.set_vals = dev_upload(d, kc.set_vals.data(), kc.set_vals.size(), s);
+    }
+    d.keys.push_back(k);
+  }
+  HIP_OK(hipStreamSynchronize(s));
+}
+
+void block_free(Block &b) {
+  if (!b.dc) return;
+  std::lock_guard<std::mutex> lk(b.dc->mu);
+  (void)hipSetDevice(b.dc->ordinal);
+  (void)hipStreamSynchronize(b.dc->stream);
+  for (void *p : b.dev.allocs) (void)hipFree(p);
+  b.dev.allocs.clear();
+  b.dc = nullptr;
+}
+
+}  // namespace tsg

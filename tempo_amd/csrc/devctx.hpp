@@ -50,10 +50,15 @@ struct HostBuf {
 
 struct DeviceCtx {
   int ordinal = 0;
+  int num_cu = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, es0 = nullptr, es1 = nullptr;
   std::mutex mu;
+  // search scratch: descriptors, dictionary matches, value-set bitmaps, match
+  // bitmasks (one bit per entry of tiles that matched), per-tile / per-workgroup
+  // counts, [header | records] output. lookup reuses desc/gran/ticket/out/hdr/err.
   DevBuf desc, vmatch, bitmaps, gran, ticket, out, regions, seg_counts, hdr, err;
+  DevBuf maskbits, tile_counts, wg_sums;
   HostBuf hdesc, hout;
   unsigned long long epoch = 0, ticket_base = 0;
   size_t gran_tiles = 0;

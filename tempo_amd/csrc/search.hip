@@ -1,0 +1,836 @@
+// search.hip — MI355X (gfx950) search pipeline for Tempo backend search blocks.
+//
+// Per query, on each device, for the blocks resident there:
+//   dict_match   substring test of each term's needle against the block's value
+//                dictionary for that key (bytes.Contains of ContainsTag,
+//                pkg/tempofb/searchdata_util.go:47-61) -> value-set bitmap;
+//                one lane per dictionary value, 64-value wave ballots -> words
+//   dict_sets    value matches -> value-set bitmap (multi-valued keys only)
+//   scan         one streaming pass over the resident filter columns: trace
+//                filters (tempodb/search/pipeline.go:29-66) AND tag terms via
+//                LDS-staged bitmap lookups. Workgroups own contiguous tile ranges
+//                of one block; a tile that matches stores its 4096-bit match mask
+//   emit         order-preserving compaction: workgroup prefix over the per-
+//                workgroup counts (no atomics, no inter-workgroup waits), ranks
+//                inside a tile from packed wave scans, records written in the
+//                reference scan order (pages ascending, entry index ascending)
+// Everything is integer, HBM-bound streaming; no MFMA (no dense contraction).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "devctx.hpp"
+
+namespace tsg {
+
+// ------------------------------------------------------------------------------------
+// descriptors (POD, one H2D copy per query)
+struct DictJob {
+  const uint8_t *bytes;
+  const uint32_t *off;
+  const uint32_t *set_off;
+  const uint32_t *set_vals;
+  uint32_t nvals, nsets;
+  uint32_t needle_off, needle_len;
+  uint32_t vmatch_base;  // u8 per value (non-identity jobs)
+  uint32_t bm_base;      // bitmap word base
+  uint32_t identity, item_base;  // first item (64-aligned) of this job
+};
+struct ScanTerm {
+  const void *col;
+  const uint32_t *bm;  // bitmap in global memory
+  uint32_t width, nsets;
+  uint32_t lds_off;    // word offset of the LDS copy, or ~0u (read global)
+  uint32_t bm_words;
+};
+struct ScanSeg {
+  uint64_t n;
+  const uint32_t *dur32;
+  const uint64_t *dur64;
+  const uint32_t *start_s, *end_s;
+  const uint8_t *ids;
+  const uint64_t *start_ns, *end_ns;
+  uint32_t first_tile, ntiles;  // global tile numbering
+  uint32_t first_wg, nwg, tpw;  // workgroups owning this block, tiles per workgroup
+  uint32_t term0, nterms, lds_words;
+  uint32_t block_idx, pad;
+  uint64_t cap;  // limit mode: records kept from this block
+};
+struct MatchRec {  // == SearchOut::Rec
+  uint8_t id[16];
+  uint64_t start, end;
+  uint64_t entry;
+  uint32_t block, pad;
+};
+static_assert(sizeof(MatchRec) == 48, "record layout");
+static_assert(sizeof(MatchRec) == sizeof(SearchOut::Rec), "record layout");
+
+struct ScanParams {
+  const ScanSeg *segs;
+  const ScanTerm *terms;
+  uint32_t nsegs, nwg;
+  uint32_t has_min, has_max, need64, limit_mode;
+  uint64_t min_ns, max_ns;
+  uint32_t start_s, end_s;
+  uint16_t *mask;          // per global tile: 256 x u16 (only tiles with matches are written)
+  uint32_t *tile_counts;   // per global tile
+  uint32_t *wg_sums;       // per workgroup
+  uint8_t *out;            // [header | records]
+  uint64_t hdr_bytes, out_cap;
+};
+
+constexpr int kThreads = 256;
+constexpr int kSteps = 4;                     // 16 entries per thread per tile
+constexpr int kTile = kThreads * 4 * kSteps;  // 4096 entries
+constexpr uint32_t kNoLds = 0xffffffffu;
+
+// ------------------------------------------------------------------------------------
+// dictionary match
+__device__ __forceinline__ bool dev_contains(const uint8_t *h, uint32_t hl, const uint8_t *nd, uint32_t nl) {
+  if (nl == 0) return true;  // bytes.Contains(x, "") (pitfall P7)
+  if (nl > hl) return false;
+  const uint8_t f = nd[0];
+  for (uint32_t i = 0; i + nl <= hl; i++) {
+    if (h[i] != f) continue;
+    uint32_t k = 1;
+    while (k < nl && h[i + k] == nd[k]) k++;
+    if (k == nl) return true;
+  }
+  return false;
+}
+
+// One lane per dictionary value; every job's item range is 64-aligned so a wave
+// never straddles two jobs, and identity jobs turn the wave's matches into two
+// bitmap words with one ballot.
+extern "C" __global__ void __launch_bounds__(256) dict_match_kernel(const DictJob *jobs, uint32_t njobs,
+                                                                    uint32_t total, const uint8_t *needles,
+                                                                    uint8_t *vmatch, uint32_t *bitmaps) {
+  const uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t wave_item = __builtin_amdgcn_readfirstlane(item & ~63u);
+  if (wave_item >= total) return;
+  uint32_t lo = 0, hi = njobs;
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (jobs[mid].item_base <= wave_item) lo = mid;
+    else hi = mid;
+  }
+  const DictJob &jb = jobs[lo];
+  const uint32_t v = item - jb.item_base;
+  bool m = false;
+  if (v < jb.nvals) {
+    uint32_t o0 = jb.off[v], o1 = jb.off[v + 1];
+    m = dev_contains(jb.bytes + o0, o1 - o0, needles + jb.needle_off, jb.needle_len);
+  }
+  if (jb.identity) {
+    unsigned long long b = __ballot(m);
+    const int lane = threadIdx.x & 63;
+    const uint32_t w0 = (v - lane) >> 5;  // first word of this wave
+    const uint32_t words = (jb.nsets + 31) >> 5;
+    if (lane == 0 && w0 < words) bitmaps[jb.bm_base + w0] = uint32_t(b);
+    if (lane == 32 && w0 + 1 < words) bitmaps[jb.bm_base + w0 + 1] = uint32_t(b >> 32);
+  } else if (v < jb.nvals) {
+    vmatch[jb.vmatch_base + v] = m ? 1 : 0;
+  }
+}
+
+// multi-valued keys: a value set matches iff any of its values does
+extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob *jobs, const uint32_t *set_jobs,
+                                                                   const uint32_t *prefix, uint32_t nsj,
+                                                                   uint32_t total, const uint8_t *vmatch,
+                                                                   uint32_t *bitmaps) {
+  uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= total) return;
+  uint32_t lo = 0, hi = nsj;
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (prefix[mid] <= item) lo = mid;
+    else hi = mid;
+  }
+  const DictJob &jb = jobs[set_jobs[lo]];
+  uint32_t w = item - prefix[lo];
+  uint32_t word = 0;
+  for (uint32_t b = 0; b < 32; b++) {
+    uint32_t s = w * 32 + b;
+    if (s >= jb.nsets) break;
+    for (uint32_t i = jb.set_off[s]; i < jb.set_off[s + 1]; i++)
+      if (vmatch[jb.vmatch_base + jb.set_vals[i]]) {
+        word |= 1u << b;
+        break;
+      }
+  }
+  bitmaps[jb.bm_base + w] = word;
+}
+
+// ------------------------------------------------------------------------------------
+// scan
+// Pointers inside descriptors are generic to the compiler; casting them to the
+// global address space turns flat loads (which wait on vmcnt AND lgkmcnt) into
+// global_load_dword{,x2,x4}.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *G(const T *p) {
+  return (const __attribute__((address_space(1))) T *)(p);
+}
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *G(const void *p) {
+  return (const __attribute__((address_space(1))) T *)(p);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool FULL>
+__device__ __forceinline__ uint4 load4_u32(const uint32_t *p, uint64_t e, uint64_t n) {
+  uint4 r;
+  if (FULL) {
+    const u32x4 v = *G<u32x4>(p + e);
+    r.x = v.x;
+    r.y = v.y;
+    r.z = v.z;
+    r.w = v.w;
+    return r;
+  }
+  r.x = e < n ? G(p)[e] : 0u;
+  r.y = e + 1 < n ? G(p)[e + 1] : 0u;
+  r.z = e + 2 < n ? G(p)[e + 2] : 0u;
+  r.w = e + 3 < n ? G(p)[e + 3] : 0u;
+  return r;
+}
+// 4 consecutive column values, raw (decoded by col_at); absent slots read as "key absent"
+template <bool FULL>
+__device__ __forceinline__ uint4 load_col(const void *col, uint32_t width, uint64_t e, uint64_t n) {
+  uint4 r = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+  if (FULL) {
+    // branch-free over the (wave-uniform) width: 4 dword loads whose addresses
+    // collapse onto the first dword for narrow columns (same cache line, no
+    // extra HBM bytes). A width switch here makes hipcc merge the three load
+    // shapes with vmcnt(0) waits that serialise every outstanding load.
+    const auto *c = G<uint32_t>(static_cast<const uint8_t *>(col) + e * width);
+    r.x = c[0];
+    r.y = c[width >= 2 ? 1 : 0];
+    r.z = c[width == 4 ? 2 : 0];
+    r.w = c[width == 4 ? 3 : 0];
+    return r;
+  }
+  if (width == 1) {
+    const auto *c = G<uint8_t>(col);
+    uint32_t x = 0;
+    for (int j = 0; j < 4; j++) x |= uint32_t(e + j < n ? c[e + j] : 0xffu) << (8 * j);
+    r.x = x;
+  } else if (width == 2) {
+    const auto *c = G<uint16_t>(col);
+    uint32_t v[4];
+    for (int j = 0; j < 4; j++) v[j] = e + j < n ? c[e + j] : 0xffffu;
+    r.x = v[0] | (v[1] << 16);
+    r.y = v[2] | (v[3] << 16);
+  } else {
+    const auto *c = G<uint32_t>(col);
+    r.x = e < n ? c[e] : 0xffffffffu;
+    r.y = e + 1 < n ? c[e + 1] : 0xffffffffu;
+    r.z = e + 2 < n ? c[e + 2] : 0xffffffffu;
+    r.w = e + 3 < n ? c[e + 3] : 0xffffffffu;
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t col_at(uint4 r, uint32_t width, int j) {
+  if (width == 1) return (r.x >> (8 * j)) & 0xffu;
+  if (width == 2) return ((j < 2 ? r.x : r.y) >> (16 * (j & 1))) & 0xffffu;
+  return j == 0 ? r.x : j == 1 ? r.y : j == 2 ? r.z : r.w;
+}
+__device__ __forceinline__ bool term_ok(const ScanTerm &T, const uint32_t *lds_bm, uint32_t x) {
+  if (x >= T.nsets) return false;  // all-ones sentinel = key absent (FindTag fails)
+  uint32_t w = T.lds_off != kNoLds ? lds_bm[T.lds_off + (x >> 5)] : G(T.bm)[x >> 5];
+  return (w >> (x & 31)) & 1u;
+}
+
+// Match mask of one tile for this thread: bit (4k+j) <-> entry tile0 + 1024k + 4*tid + j.
+// NT >= 0: every load of the tile is issued before the first use; NT < 0: runtime term loop.
+// FULL: the whole tile lies inside the block (no bounds checks).
+template <int NT, bool DUR, bool RANGE, bool FULL, bool W1>
+__device__ __forceinline__ uint32_t tile_mask(const ScanParams &P, const ScanSeg &S, const ScanTerm *T,
+                                              const uint32_t *lds_bm, uint64_t tile0, int tid) {
+  const uint64_t n = S.n;
+  uint64_t ebase[kSteps];
+  uint32_t mask = FULL ? 0xffffu : 0u;
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) {
+    ebase[k] = tile0 + uint64_t(k) * (kThreads * 4) + uint64_t(tid) * 4;
+    if (!FULL)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (ebase[k] + j < n) mask |= 1u << (4 * k + j);
+  }
+  uint4 d[kSteps], s[kSteps], e[kSteps];
+  constexpr int NTA = NT > 0 ? NT : 1;
+  uint4 tv[NTA][kSteps];
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) {
+    if (DUR) d[k] = load4_u32<FULL>(S.dur32, ebase[k], n);
+    if (RANGE) {
+      s[k] = load4_u32<FULL>(S.start_s, ebase[k], n);
+      e[k] = load4_u32<FULL>(S.end_s, ebase[k], n);
+    }
+  }
+  if (NT > 0) {
+#pragma unroll
+    for (int q = 0; q < NTA; q++)
+#pragma unroll
+      for (int k = 0; k < kSteps; k++) {
+        if (W1 && FULL) tv[q][k].x = *G<uint32_t>(static_cast<const uint8_t *>(T[q].col) + ebase[k]);
+        else tv[q][k] = load_col<FULL>(T[q].col, T[q].width, ebase[k], n);
+      }
+  }
+  if (DUR) {
+    if (!P.need64) {  // both thresholds < 2^32-1 ns: the saturated u32 column is exact
+      const uint32_t mn = uint32_t(P.min_ns), mx = uint32_t(P.max_ns);
+#pragma unroll
+      for (int k = 0; k < kSteps; k++) {
+        const uint32_t dv[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (!((!P.has_min || dv[j] >= mn) && (!P.has_max || dv[j] <= mx))) mask &= ~(1u << (4 * k + j));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kSteps; k++) {
+        const uint32_t dv[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          uint64_t dd = dv[j];
+          if (dv[j] == 0xffffffffu && (FULL || ebase[k] + j < n)) dd = G(S.dur64)[ebase[k] + j];
+          if (!((!P.has_min || dd >= P.min_ns) && (!P.has_max || dd <= P.max_ns))) mask &= ~(1u << (4 * k + j));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) {
+    if (RANGE) {
+      const uint32_t sv[4] = {s[k].x, s[k].y, s[k].z, s[k].w}, ev[4] = {e[k].x, e[k].y, e[k].z, e[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; j++)  // req.Start <= endSeconds && req.End >= startSeconds
+        if (!(P.start_s <= ev[j] && P.end_s >= sv[j])) mask &= ~(1u << (4 * k + j));
+    }
+    if (NT > 0) {
+#pragma unroll
+      for (int q = 0; q < NTA; q++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          bool ok;
+          if (W1) {  // u8 column, bitmap in LDS padded to 8 words: branch-free lookup
+            const uint32_t x = (tv[q][k].x >> (8 * j)) & 0xffu;
+            const uint32_t w = lds_bm[T[q].lds_off + (x >> 5)];
+            ok = (x < T[q].nsets) & ((w >> (x & 31)) & 1u);
+          } else {
+            ok = term_ok(T[q], lds_bm, col_at(tv[q][k], T[q].width, j));
+          }
+          if (!ok) mask &= ~(1u << (4 * k + j));
+        }
+    }
+  }
+  if (NT < 0) {
+    for (uint32_t q = 0; q < S.nterms; q++) {
+      const ScanTerm Tq = P.terms[S.term0 + q];
+      uint4 c[kSteps];
+#pragma unroll
+      for (int k = 0; k < kSteps; k++) c[k] = load_col<FULL>(Tq.col, Tq.width, ebase[k], n);
+#pragma unroll
+      for (int k = 0; k < kSteps; k++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (!term_ok(Tq, lds_bm, col_at(c[k], Tq.width, j))) mask &= ~(1u << (4 * k + j));
+    }
+  }
+  return mask;
+}
+
+__device__ __forceinline__ uint32_t find_seg(const ScanSeg *segs, uint32_t nsegs, uint32_t wg) {
+  uint32_t lo = 0, hi = nsegs;
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (segs[mid].first_wg <= wg) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <int NT, bool DUR, bool RANGE, bool W1>
+__global__ void __launch_bounds__(kThreads) scan_kernel(ScanParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_bm[];
+  __shared__ uint32_t s_wcnt[2][kThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t wg = blockIdx.x;
+  const ScanSeg S = P.segs[find_seg(P.segs, P.nsegs, wg)];
+  constexpr int NTA = NT > 0 ? NT : 1;
+  ScanTerm T[NTA];
+  if (NT > 0)
+#pragma unroll
+    for (int q = 0; q < NTA; q++) T[q] = P.terms[S.term0 + q];
+  for (uint32_t q = 0; q < S.nterms; q++) {  // stage the small bitmaps in LDS
+    const ScanTerm &Tq = P.terms[S.term0 + q];
+    if (Tq.lds_off != kNoLds)
+      for (uint32_t w = tid; w < Tq.bm_words; w += kThreads) lds_bm[Tq.lds_off + w] = Tq.bm[w];
+  }
+  __syncthreads();
+  const uint32_t lt0 = (wg - S.first_wg) * S.tpw;
+  const uint32_t lt1 = min(lt0 + S.tpw, S.ntiles);
+  uint32_t wsum = 0;
+  for (uint32_t lt = lt0; lt < lt1; lt++) {
+    const uint64_t tile0 = uint64_t(lt) * kTile;
+    const uint32_t mask = tile0 + kTile <= S.n ? tile_mask<NT, DUR, RANGE, true, W1>(P, S, T, lds_bm, tile0, tid)
+                                               : tile_mask<NT, DUR, RANGE, false, W1>(P, S, T, lds_bm, tile0, tid);
+    uint32_t c = __popc(mask);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
+    const int buf = lt & 1;
+    if (lane == 0) s_wcnt[buf][wid] = c;
+    __syncthreads();
+    uint32_t tc = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; w++) tc += s_wcnt[buf][w];
+    const uint32_t gt = S.first_tile + lt;
+    if (tc) P.mask[uint64_t(gt) * kThreads + tid] = uint16_t(mask);
+    if (tid == 0) P.tile_counts[gt] = tc;
+    wsum += tc;
+  }
+  if (tid == 0) P.wg_sums[wg] = wsum;
+}
+
+// ------------------------------------------------------------------------------------
+// emit
+__device__ __forceinline__ unsigned long long block_sum(unsigned long long v, unsigned long long *red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  unsigned long long t = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; w++) t += red[w];
+  return t;
+}
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) {
+  return a < b ? a : b;
+}
+
+constexpr uint32_t kMaxWg = 4096;  // emit keeps the workgroup prefix in LDS (16 KiB)
+
+extern "C" __global__ void __launch_bounds__(kThreads) emit_kernel(ScanParams P) {
+  __shared__ unsigned long long red[kThreads / 64];
+  __shared__ unsigned long long s_wsum[kThreads / 64];
+  __shared__ uint32_t pre[kMaxWg + 1];  // exclusive prefix of wg_sums (fits: counts <= 4096 per tile)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t wg = blockIdx.x;
+  const uint32_t si = find_seg(P.segs, P.nsegs, wg);
+  const ScanSeg S = P.segs[si];
+  const uint32_t mine = P.wg_sums[wg];
+  if (mine == 0 && wg != 0) return;
+  // ---- exclusive prefix over all workgroup sums, in LDS (thread-blocked scan)
+  {
+    const uint32_t per = (P.nwg + kThreads - 1) / kThreads;
+    const uint32_t i0 = tid * per, i1 = min(i0 + per, P.nwg);
+    unsigned long long loc = 0;
+    for (uint32_t i = i0; i < i1; i++) loc += P.wg_sums[i];
+    unsigned long long inc = loc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      unsigned long long o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    if (lane == 63) s_wsum[wid] = inc;
+    __syncthreads();
+    unsigned long long run = inc - loc;
+    for (int w = 0; w < wid; w++) run += s_wsum[w];
+    for (uint32_t i = i0; i < i1; i++) {
+      pre[i] = uint32_t(run);  // total matches per device launch < 2^32 (checked on the host)
+      run += P.wg_sums[i];
+    }
+    if (i1 == P.nwg && i0 < i1) pre[P.nwg] = uint32_t(run);
+    if (P.nwg == 0 && tid == 0) pre[0] = 0;
+    __syncthreads();
+  }
+  auto seg_total = [&](uint32_t s) -> unsigned long long {
+    const ScanSeg &Ss = P.segs[s];
+    unsigned long long c = pre[Ss.first_wg + Ss.nwg] - pre[Ss.first_wg];
+    return P.limit_mode ? umin64(c, Ss.cap) : c;
+  };
+  unsigned long long *hdr = reinterpret_cast<unsigned long long *>(P.out);
+  if (wg == 0) {  // header: records written + per-block counts
+    unsigned long long t = 0;
+    for (uint32_t s = tid; s < P.nsegs; s += kThreads) {
+      unsigned long long c = seg_total(s);
+      hdr[8 + s] = c;
+      t += c;
+    }
+    t = block_sum(t, red);
+    if (tid == 0) hdr[0] = t;
+    if (mine == 0) return;
+  }
+  const unsigned long long seg_rank0 = pre[wg] - pre[S.first_wg];
+  unsigned long long base;  // output slot of this workgroup's first match
+  if (P.limit_mode) {
+    unsigned long long b = 0;
+    for (uint32_t s = tid; s < si; s += kThreads) b += seg_total(s);
+    base = block_sum(b, red);
+  } else {
+    base = pre[wg];
+  }
+  MatchRec *out = reinterpret_cast<MatchRec *>(P.out + P.hdr_bytes);
+  const uint32_t lt0 = (wg - S.first_wg) * S.tpw, lt1 = min(lt0 + S.tpw, S.ntiles);
+  unsigned long long run = 0;
+  for (uint32_t lt = lt0; lt < lt1; lt++) {
+    const uint32_t gt = S.first_tile + lt;
+    const uint32_t tc = P.tile_counts[gt];
+    if (tc == 0) continue;
+    const uint32_t mask = P.mask[uint64_t(gt) * kThreads + tid];
+    // ranks in scan order (k, tid, j): wave scan of 4 packed 16-bit per-step counts
+    unsigned long long pc = 0;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) pc |= (unsigned long long)__popc((mask >> (4 * k)) & 0xfu) << (16 * k);
+    unsigned long long inc = pc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      unsigned long long o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    __syncthreads();
+    if (lane == 63) s_wsum[wid] = inc;
+    __syncthreads();
+    unsigned long long before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; w++) {
+      if (w < wid) before += s_wsum[w];
+      tot += s_wsum[w];
+    }
+    const unsigned long long mine_ex = before + inc - pc;
+    uint32_t step_base = 0;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) {
+      const uint32_t nib = (mask >> (4 * k)) & 0xfu;
+      uint32_t r = step_base + uint32_t((mine_ex >> (16 * k)) & 0xffff);
+      step_base += uint32_t((tot >> (16 * k)) & 0xffff);
+      for (int j = 0; j < 4; j++) {
+        if (!(nib & (1u << j))) continue;
+        const unsigned long long rank_seg = seg_rank0 + run + r++;
+        unsigned long long slot;
+        if (P.limit_mode) {
+          if (rank_seg >= S.cap) continue;
+          slot = base + rank_seg;
+        } else {
+          slot = base + (rank_seg - seg_rank0);
+          if (slot >= P.out_cap) continue;
+        }
+        const uint64_t ei = uint64_t(lt) * kTile + uint64_t(k) * (kThreads * 4) + uint64_t(tid) * 4 + j;
+        MatchRec *dst = out + slot;
+        *reinterpret_cast<uint4 *>(dst->id) = *reinterpret_cast<const uint4 *>(S.ids + ei * 16);
+        dst->start = S.start_ns[ei];
+        dst->end = S.end_ns[ei];
+        dst->entry = ei;
+        dst->block = S.block_idx;
+        dst->pad = 0;
+      }
+    }
+    run += tc;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// host
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+using ScanFn = void (*)(ScanParams);
+template <int NT, bool W1>
+static ScanFn pick3(bool dur, bool range) {
+  if (dur && range) return scan_kernel<NT, true, true, W1>;
+  if (dur) return scan_kernel<NT, true, false, W1>;
+  if (range) return scan_kernel<NT, false, true, W1>;
+  return scan_kernel<NT, false, false, W1>;
+}
+// w1: every term column of every block in this launch is one byte wide
+static ScanFn pick_scan(uint32_t nterms, bool dur, bool range, bool w1) {
+  switch (nterms) {
+    case 0: return pick3<0, false>(dur, range);
+    case 1: return w1 ? pick3<1, true>(dur, range) : pick3<1, false>(dur, range);
+    case 2: return w1 ? pick3<2, true>(dur, range) : pick3<2, false>(dur, range);
+    case 3: return w1 ? pick3<3, true>(dur, range) : pick3<3, false>(dur, range);
+    case 4: return w1 ? pick3<4, true>(dur, range) : pick3<4, false>(dur, range);
+    default: return pick3<-1, false>(dur, range);
+  }
+}
+
+struct Tracer {
+  bool on;
+  std::chrono::steady_clock::time_point t0, last;
+  char buf[512];
+  int len = 0;
+  Tracer() : on(std::getenv("TSG_TRACE") != nullptr) {
+    if (on) t0 = last = std::chrono::steady_clock::now();
+  }
+  void mark(const char *name) {
+    if (!on) return;
+    auto now = std::chrono::steady_clock::now();
+    len += std::snprintf(buf + len, sizeof buf - size_t(len), " %s=%.1f", name,
+                         std::chrono::duration<double, std::micro>(now - last).count());
+    last = now;
+  }
+  ~Tracer() {
+    if (on && len) std::fprintf(stderr, "[tsg] device_search us:%s\n", buf);
+  }
+};
+
+void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
+                   uint32_t limit, SearchOut &out) {
+  Tracer tr;
+  std::lock_guard<std::mutex> lk(dc.mu);
+  HIP_OK(hipSetDevice(dc.ordinal));
+  hipStream_t s = dc.stream;
+  if (dc.num_cu == 0) {
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, dc.ordinal));
+    dc.num_cu = prop.multiProcessorCount;
+  }
+
+  // ---- plan
+  std::vector<ScanSeg> segs;
+  std::vector<ScanTerm> terms;
+  std::vector<DictJob> jobs;
+  std::vector<uint32_t> set_jobs, set_items(1, 0), term_bm_base;
+  std::vector<uint8_t> needles;
+  std::vector<uint32_t> needle_off(q.nterms);
+  for (uint32_t t = 0; t < q.nterms; t++) {
+    needle_off[t] = uint32_t(needles.size());
+    needles.insert(needles.end(), q.values[t], q.values[t] + q.value_lens[t]);
+  }
+  const bool has_dur = q.has_min || q.has_max;
+  uint32_t vmatch_total = 0, bm_total = 0, items = 0, tiles = 0, max_lds_words = 0;
+  uint64_t dict_bytes = 0, scan_bytes = 0, n_all = 0;
+  bool all_w1 = true;
+  constexpr uint32_t kLdsBudgetWords = 8192;  // 32 KiB per workgroup
+  for (auto &bp : blocks) {
+    Block &b = *bp.second;
+    const DevBlock &d = b.dev;
+    if (d.n == 0 || q.exhaustive) continue;
+    std::vector<int> kidx(q.nterms);
+    bool dead = false;  // a key absent from the block: FindTag fails for every entry
+    for (uint32_t t = 0; t < q.nterms && !dead; t++) {
+      auto it = b.host.key_index.find(std::string(reinterpret_cast<const char *>(q.keys[t]), q.key_lens[t]));
+      if (it == b.host.key_index.end()) dead = true;
+      else kidx[t] = it->second;
+    }
+    if (dead) continue;
+    ScanSeg sg{};
+    sg.n = d.n;
+    sg.dur32 = d.dur32;
+    sg.dur64 = d.dur64;
+    sg.start_s = d.start_s;
+    sg.end_s = d.end_s;
+    sg.ids = d.ids;
+    sg.start_ns = d.start_ns;
+    sg.end_ns = d.end_ns;
+    sg.block_idx = bp.first;
+    sg.term0 = uint32_t(terms.size());
+    sg.nterms = q.nterms;
+    uint64_t per = (has_dur ? 4 : 0) + (q.has_range ? 8 : 0);
+    for (uint32_t t = 0; t < q.nterms; t++) {
+      const DevKey &k = d.keys[size_t(kidx[t])];
+      DictJob jb{};
+      jb.bytes = k.dict_bytes;
+      jb.off = k.dict_off;
+      jb.set_off = k.set_off;
+      jb.set_vals = k.set_vals;
+      jb.nvals = k.nvals;
+      jb.nsets = k.nsets;
+      jb.needle_off = needle_off[t];
+      jb.needle_len = q.value_lens[t];
+      jb.identity = k.identity ? 1 : 0;
+      jb.bm_base = bm_total;
+      jb.item_base = items;
+      items += uint32_t(align_up(std::max<uint32_t>(k.nvals, 1), 64));
+      const uint32_t words = (k.nsets + 31) / 32;
+      bm_total += words + 2;  // +2: a wave's ballot writes whole 64-value word pairs
+      if (!k.identity) {
+        jb.vmatch_base = vmatch_total;
+        vmatch_total += k.nvals;
+        set_jobs.push_back(uint32_t(jobs.size()));
+        set_items.push_back(set_items.back() + words);
+      }
+      jobs.push_back(jb);
+      dict_bytes += k.dict_nbytes + 4ull * (k.nvals + 1) + 4ull * words;
+      ScanTerm st{};
+      st.col = k.col;
+      st.width = uint32_t(k.width);
+      st.nsets = k.nsets;
+      st.bm_words = words;
+      const uint32_t lds_need = k.width == 1 ? 8u : words;  // u8: 256-bit table, branch-free lookups
+      if (sg.lds_words + lds_need <= kLdsBudgetWords) {
+        st.lds_off = sg.lds_words;
+        sg.lds_words += lds_need;
+      } else {
+        st.lds_off = kNoLds;  // large dictionary: bitmap lookups go to L2 / MALL
+      }
+      terms.push_back(st);
+      term_bm_base.push_back(jb.bm_base);
+      per += uint64_t(k.width);
+      all_w1 = all_w1 && k.width == 1 && st.lds_off != kNoLds;
+    }
+    max_lds_words = std::max(max_lds_words, sg.lds_words);
+    sg.first_tile = tiles;
+    sg.ntiles = uint32_t((d.n + kTile - 1) / kTile);
+    tiles += sg.ntiles;
+    sg.cap = limit ? std::min<uint64_t>(limit, d.n) : d.n;
+    scan_bytes += d.n * per;
+    n_all += d.n;
+    segs.push_back(sg);
+  }
+  out.recs.clear();
+  out.block_counts.assign(blocks.size(), 0);
+  out.device_bytes = scan_bytes + dict_bytes;
+  out.kernel_ns = out.scan_ns = 0;
+  out.scan_bytes = scan_bytes;
+  if (segs.empty()) return;
+  // workgroups: one resident wave of them (occupancy x CUs), each owning a
+  // contiguous tile range of one block
+  const ScanFn scan_fn = pick_scan(q.nterms, has_dur, q.has_range, all_w1);
+  int per_cu = 0;
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(scan_fn), kThreads,
+                                                       size_t(max_lds_words) * 4));
+  per_cu = std::max(1, std::min(per_cu, 8));
+  const uint32_t target_wg = uint32_t(dc.num_cu) * uint32_t(per_cu);
+  const uint32_t tpw = std::max<uint32_t>(1, (tiles + target_wg - 1) / target_wg);
+  uint32_t tpw_eff = tpw, nwg = 0;
+  for (;;) {
+    nwg = 0;
+    for (auto &sg : segs) {
+      sg.tpw = tpw_eff;
+      sg.first_wg = nwg;
+      sg.nwg = (sg.ntiles + tpw_eff - 1) / tpw_eff;
+      nwg += sg.nwg;
+    }
+    if (nwg <= kMaxWg) break;
+    if (segs.size() > kMaxWg / 2) fail(TSG_E_UNSUPPORTED, "too many blocks per device in one search (max 2048)");
+    tpw_eff *= 2;
+  }
+  if (n_all >= (1ull << 32)) fail(TSG_E_UNSUPPORTED, "more than 2^32 entries per device in one search");
+  tr.mark("plan");
+
+  // ---- scratch
+  dc.bitmaps.ensure(std::max<size_t>(bm_total, 1) * 4);
+  dc.vmatch.ensure(std::max<size_t>(vmatch_total, 1));
+  dc.maskbits.ensure(size_t(tiles) * kThreads * 2);
+  dc.tile_counts.ensure(size_t(tiles) * 4);
+  dc.wg_sums.ensure(size_t(nwg) * 4);
+  const size_t hdr_bytes = align_up(64 + 8 * segs.size(), 256);
+  uint64_t n_total = 0, cap_total = 0;
+  for (auto &sg : segs) {
+    n_total += sg.n;
+    cap_total += sg.cap;
+  }
+  uint64_t out_cap = limit ? cap_total : std::min<uint64_t>(n_total, 1u << 20);
+  dc.out.ensure(hdr_bytes + std::max<size_t>(out_cap, 1) * sizeof(MatchRec));
+  for (size_t i = 0; i < terms.size(); i++)
+    terms[i].bm = static_cast<const uint32_t *>(dc.bitmaps.p) + term_bm_base[i];
+
+  // ---- descriptors: one H2D copy
+  const size_t o_segs = 0, o_terms = align_up(segs.size() * sizeof(ScanSeg), 16);
+  const size_t o_jobs = align_up(o_terms + terms.size() * sizeof(ScanTerm), 16);
+  const size_t o_sj = align_up(o_jobs + jobs.size() * sizeof(DictJob), 16);
+  const size_t o_sp = align_up(o_sj + set_jobs.size() * 4, 16);
+  const size_t o_nd = align_up(o_sp + set_items.size() * 4, 16);
+  const size_t total_desc = align_up(o_nd + needles.size() + 1, 16);
+  dc.hdesc.ensure(total_desc);
+  dc.desc.ensure(total_desc);
+  auto *hd = static_cast<uint8_t *>(dc.hdesc.p);
+  std::memcpy(hd + o_segs, segs.data(), segs.size() * sizeof(ScanSeg));
+  std::memcpy(hd + o_terms, terms.data(), terms.size() * sizeof(ScanTerm));
+  std::memcpy(hd + o_jobs, jobs.data(), jobs.size() * sizeof(DictJob));
+  if (!set_jobs.empty()) std::memcpy(hd + o_sj, set_jobs.data(), set_jobs.size() * 4);
+  std::memcpy(hd + o_sp, set_items.data(), set_items.size() * 4);
+  if (!needles.empty()) std::memcpy(hd + o_nd, needles.data(), needles.size());
+  auto *dd = static_cast<uint8_t *>(dc.desc.p);
+  HIP_OK(hipMemcpyAsync(dd, hd, total_desc, hipMemcpyHostToDevice, s));
+
+  HIP_OK(hipEventRecord(dc.ev0, s));
+  if (items)
+    dict_match_kernel<<<(items + 255) / 256, 256, 0, s>>>(reinterpret_cast<const DictJob *>(dd + o_jobs),
+                                                         uint32_t(jobs.size()), items, dd + o_nd,
+                                                         static_cast<uint8_t *>(dc.vmatch.p),
+                                                         static_cast<uint32_t *>(dc.bitmaps.p));
+  if (set_items.back())
+    dict_sets_kernel<<<(set_items.back() + 255) / 256, 256, 0, s>>>(
+        reinterpret_cast<const DictJob *>(dd + o_jobs), reinterpret_cast<const uint32_t *>(dd + o_sj),
+        reinterpret_cast<const uint32_t *>(dd + o_sp), uint32_t(set_jobs.size()), set_items.back(),
+        static_cast<const uint8_t *>(dc.vmatch.p), static_cast<uint32_t *>(dc.bitmaps.p));
+  ScanParams P{};
+  P.segs = reinterpret_cast<const ScanSeg *>(dd + o_segs);
+  P.terms = reinterpret_cast<const ScanTerm *>(dd + o_terms);
+  P.nsegs = uint32_t(segs.size());
+  P.nwg = nwg;
+  P.has_min = q.has_min;
+  P.has_max = q.has_max;
+  P.need64 = (q.has_min && q.min_ns >= 0xffffffffULL) || (q.has_max && q.max_ns >= 0xffffffffULL);
+  P.limit_mode = limit ? 1 : 0;
+  P.min_ns = q.min_ns;
+  P.max_ns = q.max_ns;
+  P.start_s = q.start_s;
+  P.end_s = q.end_s;
+  P.mask = static_cast<uint16_t *>(dc.maskbits.p);
+  P.tile_counts = static_cast<uint32_t *>(dc.tile_counts.p);
+  P.wg_sums = static_cast<uint32_t *>(dc.wg_sums.p);
+  P.out = static_cast<uint8_t *>(dc.out.p);
+  P.hdr_bytes = hdr_bytes;
+  P.out_cap = out_cap;
+  HIP_OK(hipEventRecord(dc.es0, s));
+  scan_fn<<<nwg, kThreads, max_lds_words * 4, s>>>(P);
+  HIP_OK(hipEventRecord(dc.es1, s));
+  emit_kernel<<<nwg, kThreads, 0, s>>>(P);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(dc.ev1, s));
+
+  // ---- one D2H: header + the first records
+  const size_t first = std::min<uint64_t>(out_cap, 1024);
+  const size_t hbytes = hdr_bytes + first * sizeof(MatchRec);
+  dc.hout.ensure(hbytes);
+  auto *ho = static_cast<uint8_t *>(dc.hout.p);
+  HIP_OK(hipMemcpyAsync(ho, dc.out.p, hbytes, hipMemcpyDeviceToHost, s));
+  tr.mark("submit");
+  HIP_OK(hipStreamSynchronize(s));
+  tr.mark("sync");
+  uint64_t total;
+  std::memcpy(&total, ho, 8);
+  float ms = 0, sms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, dc.ev0, dc.ev1));
+  HIP_OK(hipEventElapsedTime(&sms, dc.es0, dc.es1));
+  out.kernel_ns = uint64_t(double(ms) * 1e6);
+  out.scan_ns = uint64_t(double(sms) * 1e6);
+  uint64_t nonzero_tiles_bound = std::min<uint64_t>(tiles, total);
+  out.scan_bytes += nonzero_tiles_bound * kThreads * 2 + uint64_t(tiles) * 4 + uint64_t(nwg) * 4;
+  if (!limit && total > out_cap) {
+    // more matches than the output buffer holds: grow it and re-run the emit pass only
+    out_cap = total;
+    dc.out.ensure(hdr_bytes + out_cap * sizeof(MatchRec));
+    P.out = static_cast<uint8_t *>(dc.out.p);
+    P.out_cap = out_cap;
+    emit_kernel<<<nwg, kThreads, 0, s>>>(P);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(s));
+  }
+  out.recs.resize(total);
+  if (total <= first) {
+    if (total) std::memcpy(out.recs.data(), ho + hdr_bytes, total * sizeof(MatchRec));
+  } else {
+    HIP_OK(hipMemcpy(out.recs.data(), static_cast<uint8_t *>(dc.out.p) + hdr_bytes, total * sizeof(MatchRec),
+                     hipMemcpyDeviceToHost));
+  }
+  for (size_t i = 0; i < segs.size(); i++) {
+    uint64_t c;
+    std::memcpy(&c, ho + 64 + 8 * i, 8);
+    for (size_t bi = 0; bi < blocks.size(); bi++)
+      if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = c;
+  }
+  tr.mark("post");
+}
+
+}  // namespace tsg

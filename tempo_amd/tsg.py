@@ -303,6 +303,25 @@ class Engine:
         finally:
             lib().tsg_result_free(rp)
 
+    def search_raw(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0,
+                   _cache={}):
+        """tsg_search without unpacking the matches into Python objects: returns
+        (match count, SearchMetrics). The result arrays are assembled by libtsg as
+        for any caller (what the Go shim would receive) and then freed."""
+        key = tuple(b.h.value for b in blocks)
+        arr = _cache.get(key)
+        if arr is None:
+            arr = _cache[key] = (C.c_void_p * max(len(blocks), 1))(*key)
+        opts = _SearchOpts(limit=limit)
+        rp = C.POINTER(_Result)()
+        _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
+        r = rp.contents
+        n, m = r.n, r.metrics
+        met = SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,
+                            m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
+        lib().tsg_result_free(rp)
+        return n, met
+
     def search_request(self, blocks, req: SearchRequest, limit: Optional[int] = None):
         """instance.Search: ordered matches cut at the limit, then combined + sorted."""
         p = Pipeline(req)

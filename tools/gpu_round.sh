@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: tests, bench, rocprof. Stops at the first GPU fault/abort/timeout.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STAGES="${1:-test,bench,prof}"
+has() { [[ ",$STAGES," == *",$1,"* ]]; }
+ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 0 pass, 1 test failures (no crash)
+
+if has test; then
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest gpu rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
+  ok_rc $rc || exit $rc
+fi
+if has trace; then
+  TSG_TRACE=1 timeout -k 10 600 python bench.py --steps 10 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/trace.json 2> gpurun_out/trace.err
+  rc=$?; echo "trace rc=$rc"; grep "\[tsg\]" gpurun_out/trace.err | tail -5; cat gpurun_out/trace.json
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has bench; then
+  timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
+  rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.err; cat gpurun_out/bench.json
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has prof; then
+  export TMPDIR=/tmp
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+    python3 bench.py --steps 20 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
+  rc=$?; echo "rocprof rc=$rc"; cat gpurun_out/prof/run_kernel_stats.csv
+fi
