@@ -137,9 +137,11 @@ typedef struct tsg_result {
 } tsg_result;
 
 /* Options for tsg_search. */
+#define TSG_SEARCH_TIME_SCAN 1u /* HIP events around the scan kernel -> metrics.scan_kernel_ns */
+#define TSG_SEARCH_TIME_ALL 2u  /* ... and around the whole device sequence -> metrics.kernel_ns */
 typedef struct tsg_search_opts {
   uint32_t limit;  /* 0 = no limit (every match) */
-  uint32_t flags;  /* reserved */
+  uint32_t flags;  /* TSG_SEARCH_TIME_* (timing events cost a few us per search; off by default) */
   uint64_t query_id; /* for tsg_cancel; 0 = not cancellable */
 } tsg_search_opts;
 

@@ -308,6 +308,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
   if (!ctx || !q || !out || (nblocks && !blocks)) return TSG_E_INVALID;
   return guard([&] {
     const uint32_t limit = opts ? opts->limit : 0;
+    const uint32_t flags = opts ? opts->flags : 0;
     auto *res = new ResultHolder();
     std::unique_ptr<ResultHolder> guard_res(res);
     tsg_metrics &m = res->pub.metrics;
@@ -333,7 +334,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         size_t slot = k++;
         auto work = [&, slot, &list = kv.second]() {
           try {
-            device_search(*outs[slot].first, list, *q, limit, outs[slot].second);
+            device_search(*outs[slot].first, list, *q, limit, flags, outs[slot].second);
           } catch (...) {
             errs[slot] = std::current_exception();
           }

@@ -49,6 +49,7 @@ void ctx_shutdown(Ctx &c) {
       b->release();
     dc->hdesc.release();
     dc->hout.release();
+    dc->hres.release();
     (void)hipEventDestroy(dc->ev0);
     (void)hipEventDestroy(dc->ev1);
     (void)hipEventDestroy(dc->es0);

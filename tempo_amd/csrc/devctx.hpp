@@ -34,11 +34,12 @@ struct DevBuf {
 struct HostBuf {
   void *p = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocDefault;
   void ensure(size_t n) {
     if (n <= cap) return;
     if (p) HIP_OK(hipHostFree(p));
     size_t c = std::max(n, cap * 2);
-    HIP_OK(hipHostMalloc(&p, c, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc(&p, c, flags));
     cap = c;
   }
   void release() {
@@ -60,6 +61,9 @@ struct DeviceCtx {
   DevBuf desc, vmatch, bitmaps, gran, ticket, out, regions, seg_counts, hdr, err;
   DevBuf maskbits, tile_counts, wg_sums;
   HostBuf hdesc, hout;
+  // search results, written by the emit kernel directly (coherent: the kernel's
+  // stores go over the fabric, visible to the host once the stream is synchronised)
+  HostBuf hres{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};
   unsigned long long epoch = 0, ticket_base = 0;
   size_t gran_tiles = 0;
 };

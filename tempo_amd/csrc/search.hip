@@ -582,7 +582,7 @@ struct Tracer {
 };
 
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
-                   uint32_t limit, SearchOut &out) {
+                   uint32_t limit, uint32_t flags, SearchOut &out) {
   Tracer tr;
   std::lock_guard<std::mutex> lk(dc.mu);
   HIP_OK(hipSetDevice(dc.ordinal));
@@ -728,8 +728,13 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     n_total += sg.n;
     cap_total += sg.cap;
   }
-  uint64_t out_cap = limit ? cap_total : std::min<uint64_t>(n_total, 1u << 20);
-  dc.out.ensure(hdr_bytes + std::max<size_t>(out_cap, 1) * sizeof(MatchRec));
+  // limit 0: start from the capacity the result buffer already has (>= 2^16
+  // records); a larger match count re-runs the emit pass into a grown buffer
+  const uint64_t have = dc.hres.cap > hdr_bytes ? (dc.hres.cap - hdr_bytes) / sizeof(MatchRec) : 0;
+  uint64_t out_cap = limit ? cap_total : std::min<uint64_t>(n_total, std::max<uint64_t>(have, 1u << 16));
+  // [header | records] go straight to pinned host memory (no D2H copy, no copy kernel)
+  dc.hres.ensure(hdr_bytes + std::max<size_t>(out_cap, 1) * sizeof(MatchRec));
+  uint8_t *ho = static_cast<uint8_t *>(dc.hres.p);
   for (size_t i = 0; i < terms.size(); i++)
     terms[i].bm = static_cast<const uint32_t *>(dc.bitmaps.p) + term_bm_base[i];
 
@@ -752,7 +757,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   auto *dd = static_cast<uint8_t *>(dc.desc.p);
   HIP_OK(hipMemcpyAsync(dd, hd, total_desc, hipMemcpyHostToDevice, s));
 
-  HIP_OK(hipEventRecord(dc.ev0, s));
+  const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
+  if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
   if (items)
     dict_match_kernel<<<(items + 255) / 256, 256, 0, s>>>(reinterpret_cast<const DictJob *>(dd + o_jobs),
                                                          uint32_t(jobs.size()), items, dd + o_nd,
@@ -779,51 +785,39 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   P.mask = static_cast<uint16_t *>(dc.maskbits.p);
   P.tile_counts = static_cast<uint32_t *>(dc.tile_counts.p);
   P.wg_sums = static_cast<uint32_t *>(dc.wg_sums.p);
-  P.out = static_cast<uint8_t *>(dc.out.p);
+  P.out = ho;
   P.hdr_bytes = hdr_bytes;
   P.out_cap = out_cap;
-  HIP_OK(hipEventRecord(dc.es0, s));
+  if (time_scan) HIP_OK(hipEventRecord(dc.es0, s));
   scan_fn<<<nwg, kThreads, max_lds_words * 4, s>>>(P);
-  HIP_OK(hipEventRecord(dc.es1, s));
+  if (time_scan) HIP_OK(hipEventRecord(dc.es1, s));
   emit_kernel<<<nwg, kThreads, 0, s>>>(P);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipEventRecord(dc.ev1, s));
-
-  // ---- one D2H: header + the first records
-  const size_t first = std::min<uint64_t>(out_cap, 1024);
-  const size_t hbytes = hdr_bytes + first * sizeof(MatchRec);
-  dc.hout.ensure(hbytes);
-  auto *ho = static_cast<uint8_t *>(dc.hout.p);
-  HIP_OK(hipMemcpyAsync(ho, dc.out.p, hbytes, hipMemcpyDeviceToHost, s));
+  if (time_all) HIP_OK(hipEventRecord(dc.ev1, s));
   tr.mark("submit");
   HIP_OK(hipStreamSynchronize(s));
   tr.mark("sync");
-  uint64_t total;
-  std::memcpy(&total, ho, 8);
+  uint64_t total = *reinterpret_cast<volatile uint64_t *>(ho);
   float ms = 0, sms = 0;
-  HIP_OK(hipEventElapsedTime(&ms, dc.ev0, dc.ev1));
-  HIP_OK(hipEventElapsedTime(&sms, dc.es0, dc.es1));
+  if (time_all) HIP_OK(hipEventElapsedTime(&ms, dc.ev0, dc.ev1));
+  if (time_scan) HIP_OK(hipEventElapsedTime(&sms, dc.es0, dc.es1));
   out.kernel_ns = uint64_t(double(ms) * 1e6);
   out.scan_ns = uint64_t(double(sms) * 1e6);
   uint64_t nonzero_tiles_bound = std::min<uint64_t>(tiles, total);
   out.scan_bytes += nonzero_tiles_bound * kThreads * 2 + uint64_t(tiles) * 4 + uint64_t(nwg) * 4;
   if (!limit && total > out_cap) {
-    // more matches than the output buffer holds: grow it and re-run the emit pass only
+    // more matches than the result buffer holds: grow it and re-run the emit pass only
     out_cap = total;
-    dc.out.ensure(hdr_bytes + out_cap * sizeof(MatchRec));
-    P.out = static_cast<uint8_t *>(dc.out.p);
+    dc.hres.ensure(hdr_bytes + out_cap * sizeof(MatchRec));
+    ho = static_cast<uint8_t *>(dc.hres.p);
+    P.out = ho;
     P.out_cap = out_cap;
     emit_kernel<<<nwg, kThreads, 0, s>>>(P);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(s));
   }
   out.recs.resize(total);
-  if (total <= first) {
-    if (total) std::memcpy(out.recs.data(), ho + hdr_bytes, total * sizeof(MatchRec));
-  } else {
-    HIP_OK(hipMemcpy(out.recs.data(), static_cast<uint8_t *>(dc.out.p) + hdr_bytes, total * sizeof(MatchRec),
-                     hipMemcpyDeviceToHost));
-  }
+  if (total) std::memcpy(out.recs.data(), ho + hdr_bytes, total * sizeof(MatchRec));
   for (size_t i = 0; i < segs.size(); i++) {
     uint64_t c;
     std::memcpy(&c, ho + 64 + 8 * i, 8);

@@ -37,6 +37,9 @@ TSG_E_IO = 9
 ENC_NONE = 0
 ENC_SNAPPY = 6
 
+SEARCH_TIME_SCAN = 1  # tsg_search_opts.flags: HIP events around the scan kernel
+SEARCH_TIME_ALL = 2   # ... and around the whole device sequence
+
 
 class TsgError(RuntimeError):
     def __init__(self, code, msg):
@@ -292,10 +295,10 @@ class Engine:
     def open_block(self, path: str, device: int = 0) -> "BackendSearchBlock":
         return BackendSearchBlock(self, path, device)
 
-    def search(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0):
-        """Ordered match sequence + metrics (tsg_search)."""
+    def search(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0, flags: int = 0):
+        """Ordered match sequence + metrics (tsg_search). flags: SEARCH_TIME_*."""
         arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
-        opts = _SearchOpts(limit=limit)
+        opts = _SearchOpts(limit=limit, flags=flags)
         rp = C.POINTER(_Result)()
         _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
         try:
@@ -304,7 +307,7 @@ class Engine:
             lib().tsg_result_free(rp)
 
     def search_raw(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0,
-                   _cache={}):
+                   flags: int = 0, _cache={}):
         """tsg_search without unpacking the matches into Python objects: returns
         (match count, SearchMetrics). The result arrays are assembled by libtsg as
         for any caller (what the Go shim would receive) and then freed."""
@@ -312,7 +315,7 @@ class Engine:
         arr = _cache.get(key)
         if arr is None:
             arr = _cache[key] = (C.c_void_p * max(len(blocks), 1))(*key)
-        opts = _SearchOpts(limit=limit)
+        opts = _SearchOpts(limit=limit, flags=flags)
         rp = C.POINTER(_Result)()
         _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
         r = rp.contents

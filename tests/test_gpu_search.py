@@ -210,3 +210,43 @@ def test_synthetic_block_full_scan(engine, tmp_path):
                dict(tags={"http.url": "/users/12"})]:
         got, met, exp, omet = both(engine, [p], **qq)
         assert_parity(got, met, exp, omet)
+
+
+def test_match_everything_regrows_result_buffer(tmp_path):
+    """An unfiltered query on a fresh context: the first result buffer (2^16
+    records) overflows and the emit pass re-runs into a larger one. Every entry
+    matches, in scan order."""
+    p = os.path.join(str(tmp_path), "big")
+    n = (1 << 16) * 2 + 777
+    T.synth_search_block(p, n, seed=11)
+    engine = T.Engine(devices=[0])
+    b = engine.open_block(p)
+    try:
+        got, met = engine.search([b], T.Pipeline(T.SearchRequest()))
+        assert len(got) == n and met.inspected_traces == n
+        assert all(m.entry_idx == i for i, m in enumerate(got))
+        n2, met2 = engine.search_raw([b], T.Pipeline(T.SearchRequest(tags={"service.name": "svc-07"})))
+        got3, _ = engine.search([b], T.Pipeline(T.SearchRequest(tags={"service.name": "svc-07"})))
+        assert n2 == len(got3) and 0 < n2 < n
+        exp, omet, _ = O.search([O.Block(p)], tags={"service.name": "svc-07"})
+        assert [tsg_key(m) for m in got3] == [match_key(m) for m in exp]
+    finally:
+        b.close()
+        engine.close()
+
+
+def test_timing_flags(engine, tmp_path):
+    p = os.path.join(str(tmp_path), "syn")
+    T.synth_search_block(p, 50_000, seed=5)
+    b = engine.open_block(p)
+    try:
+        pipe = T.Pipeline(T.SearchRequest(tags={"service.name": "svc-07"}, min_duration_ms=10))
+        _, m0 = engine.search_raw([b], pipe)
+        assert m0.scan_kernel_ns == 0 and m0.kernel_ns == 0
+        _, m1 = engine.search_raw([b], pipe, flags=T.SEARCH_TIME_SCAN)
+        assert m1.scan_kernel_ns > 0 and m1.kernel_ns == 0
+        _, m2 = engine.search_raw([b], pipe, flags=T.SEARCH_TIME_ALL)
+        assert m2.kernel_ns >= m2.scan_kernel_ns > 0
+        assert m1.scan_bytes == m2.scan_bytes > 0
+    finally:
+        b.close()

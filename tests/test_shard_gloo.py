@@ -1,0 +1,115 @@
+"""N>1 path on the CPU: block sharding + frontend merge over torch.distributed (gloo, world 2).
+
+Each rank searches its contiguous block range. Without a GPU the rank-local
+querier response comes from the oracle (test-side stand-in for
+`Engine.search_request`); what is under test is the sharding, the gather and the
+frontend merge (modules/frontend/searchsharding.go:32-125) in `tempo_amd.shard`.
+"""
+import os
+import random
+import socket
+import tempfile
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+import tempo_amd as T
+from tempo_amd import shard
+from helpers import random_entries, write_block
+
+QUERY = dict(tags={"k1": "v1"}, min_ms=5)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _make_blocks(tmpdir, nblocks=6, n=400):
+    rng = random.Random(7)
+    paths = []
+    for b in range(nblocks):
+        ents = random_entries(rng, n)
+        if b % 2:  # duplicate trace ids across blocks exercise first-seen-wins
+            ents[:20] = [dict(e) for e in random_entries(random.Random(99), 20)]
+            ents.sort(key=lambda e: e["id"])
+        paths.append(write_block(tmpdir, f"b{b}", ents))
+    return paths
+
+
+def _to_meta(m):
+    return T.TraceSearchMetadata(
+        trace_id=m["id"], trace_id_len=m["id_len"], root_service_name=m["root_service"].decode(),
+        root_trace_name=m["root_name"].decode(), start_time_unix_nano=m["start_ns"],
+        duration_ms=m["duration_ms"], end_time_unix_nano=m["end_ns"], block_idx=m["block_idx"],
+        entry_idx=m["entry_idx"])
+
+
+def _rank_response(paths, limit):
+    """Querier response for a set of blocks: instance.Search (limit cut, combine, sort)."""
+    blocks = [O.Block(p) for p in paths]
+    got, met, _ = O.search(blocks, limit=limit, combine=limit, **QUERY)
+    sm = T.SearchMetrics(met["traces_inspected"], met["bytes_inspected"], met["blocks_inspected"],
+                         met["blocks_skipped"])
+    return [_to_meta(m) for m in got], sm
+
+
+def _key(res):
+    traces, met = res
+    return ([(t.trace_id_hex, t.start_time_unix_nano, t.duration_ms, t.root_service_name) for t in traces],
+            (met.inspected_traces, met.inspected_bytes, met.inspected_blocks, met.skipped_blocks))
+
+
+def _worker(rank, world, port, paths, limit, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = [paths[i] for i in shard.shard_range(len(paths), world, rank)]
+        res = shard.distributed_search(lambda: _rank_response(mine, limit), limit, len(paths))
+        if rank == 0:
+            import json
+            with open(os.path.join(outdir, "merged.json"), "w") as f:
+                json.dump(_key(res), f)
+        else:
+            assert res is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("limit", [1000, 5])
+def test_gloo_two_ranks_match_single_process_merge(limit):
+    import json
+    with tempfile.TemporaryDirectory() as td:
+        paths = _make_blocks(td)
+        mp.spawn(_worker, args=(2, _free_port(), paths, limit, td), nprocs=2, join=True)
+        with open(os.path.join(td, "merged.json")) as f:
+            got = json.load(f)
+        # expected: the same frontend merge applied to the two shards' responses in order
+        world = 2
+        resp = [_rank_response([paths[i] for i in shard.shard_range(len(paths), world, r)], limit)
+                for r in range(world)]
+        exp = _key(shard.merge_responses(resp, limit, len(paths)))
+        assert got == [list(map(list, exp[0])), list(exp[1])]
+        if limit >= 1000:
+            # nothing quit: the merged set is every distinct matching trace of the whole block set
+            full, met, _ = O.search([O.Block(p) for p in paths], **QUERY)
+            assert {t[0] for t in got[0]} == {m["id"].hex().lstrip("0") for m in full}
+            assert got[1][0] == met["traces_inspected"] and got[1][1] == met["bytes_inspected"]
+            starts = [t[1] for t in got[0]]
+            assert starts == sorted(starts, reverse=True)
+        else:
+            assert len(resp[0][0]) == limit  # the querier cut: each shard returns `limit` traces
+            # shouldQuit needs len > limit, so rank 1's response is still taken
+            assert {t[0] for t in got[0]} == {t.trace_id_hex for r in resp for t in r[0]}
+
+
+def test_shard_range_partitions():
+    for n in range(0, 20):
+        for w in range(1, 9):
+            seen = [i for r in range(w) for i in shard.shard_range(n, w, r)]
+            assert seen == list(range(n))
+    with pytest.raises(ValueError):
+        shard.shard_range(4, 2, 2)
