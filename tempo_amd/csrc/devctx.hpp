@@ -18,12 +18,13 @@ namespace tsg {
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
-  void ensure(size_t n) {
-    if (n <= cap) return;
+  bool ensure(size_t n) {  // true when (re)allocated
+    if (n <= cap) return false;
     if (p) HIP_OK(hipFree(p));
     size_t c = std::max(n, cap * 2);
     HIP_OK(hipMalloc(&p, c));
     cap = c;
+    return true;
   }
   void release() {
     if (p) (void)hipFree(p);
@@ -59,12 +60,13 @@ struct DeviceCtx {
   // bitmasks (one bit per entry of tiles that matched), per-tile / per-workgroup
   // counts, [header | records] output. lookup reuses desc/gran/ticket/out/hdr/err.
   DevBuf desc, vmatch, bitmaps, gran, ticket, out, regions, seg_counts, hdr, err;
-  DevBuf maskbits, tile_counts, wg_sums;
+  DevBuf maskbits, agg;
   HostBuf hdesc, hout;
   // search results, written by the emit kernel directly (coherent: the kernel's
   // stores go over the fabric, visible to the host once the stream is synchronised)
   HostBuf hres{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};
-  unsigned long long epoch = 0, ticket_base = 0;
+  unsigned long long epoch = 0, ticket_base = 0;  // lookup launches
+  uint32_t search_epoch = 0;  // search launches: tag of the published workgroup counts
   size_t gran_tiles = 0;
 };
 

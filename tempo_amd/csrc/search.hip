@@ -15,6 +15,7 @@
 //                inside a tile from packed wave scans, records written in the
 //                reference scan order (pages ascending, entry index ascending)
 // Everything is integer, HBM-bound streaming; no MFMA (no dense contraction).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -72,14 +73,16 @@ static_assert(sizeof(MatchRec) == sizeof(SearchOut::Rec), "record layout");
 struct ScanParams {
   const ScanSeg *segs;
   const ScanTerm *terms;
+  const uint16_t *wg_seg;  // workgroup -> segment (block) index
   uint32_t nsegs, nwg;
   uint32_t has_min, has_max, need64, limit_mode;
   uint64_t min_ns, max_ns;
   uint32_t start_s, end_s;
-  uint16_t *mask;          // per global tile: 256 x u16 (only tiles with matches are written)
-  uint32_t *tile_counts;   // per global tile
-  uint32_t *wg_sums;       // per workgroup
-  uint8_t *out;            // [header | records]
+  uint16_t *mask;            // masks of tiles beyond kLdsTiles per workgroup: per global tile 256 x u16
+  unsigned long long *agg;   // per workgroup: {epoch, match count}, published once per launch
+  uint32_t epoch;            // this launch's tag (never 0)
+  uint32_t lds_bm_words;     // dynamic LDS: [bitmaps | kLdsTiles masks | per-block sums]
+  uint8_t *out;              // pinned host: [header | records]; header[0] total, [1] error, [8+s] per block
   uint64_t hdr_bytes, out_cap;
 };
 
@@ -346,60 +349,8 @@ __device__ __forceinline__ uint32_t tile_mask(const ScanParams &P, const ScanSeg
   return mask;
 }
 
-__device__ __forceinline__ uint32_t find_seg(const ScanSeg *segs, uint32_t nsegs, uint32_t wg) {
-  uint32_t lo = 0, hi = nsegs;
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (segs[mid].first_wg <= wg) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
-template <int NT, bool DUR, bool RANGE, bool W1>
-__global__ void __launch_bounds__(kThreads) scan_kernel(ScanParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds_bm[];
-  __shared__ uint32_t s_wcnt[2][kThreads / 64];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint32_t wg = blockIdx.x;
-  const ScanSeg S = P.segs[find_seg(P.segs, P.nsegs, wg)];
-  constexpr int NTA = NT > 0 ? NT : 1;
-  ScanTerm T[NTA];
-  if (NT > 0)
-#pragma unroll
-    for (int q = 0; q < NTA; q++) T[q] = P.terms[S.term0 + q];
-  for (uint32_t q = 0; q < S.nterms; q++) {  // stage the small bitmaps in LDS
-    const ScanTerm &Tq = P.terms[S.term0 + q];
-    if (Tq.lds_off != kNoLds)
-      for (uint32_t w = tid; w < Tq.bm_words; w += kThreads) lds_bm[Tq.lds_off + w] = Tq.bm[w];
-  }
-  __syncthreads();
-  const uint32_t lt0 = (wg - S.first_wg) * S.tpw;
-  const uint32_t lt1 = min(lt0 + S.tpw, S.ntiles);
-  uint32_t wsum = 0;
-  for (uint32_t lt = lt0; lt < lt1; lt++) {
-    const uint64_t tile0 = uint64_t(lt) * kTile;
-    const uint32_t mask = tile0 + kTile <= S.n ? tile_mask<NT, DUR, RANGE, true, W1>(P, S, T, lds_bm, tile0, tid)
-                                               : tile_mask<NT, DUR, RANGE, false, W1>(P, S, T, lds_bm, tile0, tid);
-    uint32_t c = __popc(mask);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
-    const int buf = lt & 1;
-    if (lane == 0) s_wcnt[buf][wid] = c;
-    __syncthreads();
-    uint32_t tc = 0;
-#pragma unroll
-    for (int w = 0; w < kThreads / 64; w++) tc += s_wcnt[buf][w];
-    const uint32_t gt = S.first_tile + lt;
-    if (tc) P.mask[uint64_t(gt) * kThreads + tid] = uint16_t(mask);
-    if (tid == 0) P.tile_counts[gt] = tc;
-    wsum += tc;
-  }
-  if (tid == 0) P.wg_sums[wg] = wsum;
-}
-
 // ------------------------------------------------------------------------------------
-// emit
+// helpers
 __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, unsigned long long *red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -416,76 +367,139 @@ __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsig
   return a < b ? a : b;
 }
 
-constexpr uint32_t kMaxWg = 4096;  // emit keeps the workgroup prefix in LDS (16 KiB)
+// ------------------------------------------------------------------------------------
+// search: scan + in-order compaction in one launch
+//
+// Phase 1 (scan): the workgroup streams its tiles; per tile a 16-bit mask per
+//   thread (LDS for the first kLdsTiles tiles, global beyond) and a count.
+// Phase 2 (publish / look-back): the workgroup publishes its match count as one
+//   8-byte {epoch, count} word (agent-scope store, bypasses the non-coherent L1/L2
+//   paths), then sums the words of every lower-numbered workgroup, polling those
+//   not yet published. Workgroups are dispatched in index order, so every waited-on
+//   workgroup is resident or done; the poll is bounded anyway (error flag, the host
+//   fails the query loudly). Only workgroups with matches (and the last one, which
+//   writes the header) look back.
+// Phase 3 (emit): records in scan order straight into the pinned host buffer.
+constexpr uint32_t kLdsTiles = 16;      // tiles per workgroup whose masks stay in LDS
+constexpr uint32_t kMaxTpw = 1024;      // tiles per workgroup (per-tile counts in LDS)
+constexpr uint32_t kSpinMax = 1u << 22; // look-back poll bound (~seconds): never reached unless broken
+constexpr uint32_t kMaxSegs = 2048;
 
-extern "C" __global__ void __launch_bounds__(kThreads) emit_kernel(ScanParams P) {
-  __shared__ unsigned long long red[kThreads / 64];
+template <int NT, bool DUR, bool RANGE, bool W1>
+__global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t *lds_bm = lds;                                              // [lds_bm_words]
+  uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + P.lds_bm_words);  // [kLdsTiles][kThreads]
+  uint32_t *lds_seg = lds + P.lds_bm_words + kLdsTiles * kThreads / 2;  // [nsegs]
+  __shared__ uint16_t s_tc[kMaxTpw];
+  __shared__ uint32_t s_wcnt[2][kThreads / 64];
+  __shared__ unsigned long long s_red[kThreads / 64];
   __shared__ unsigned long long s_wsum[kThreads / 64];
-  __shared__ uint32_t pre[kMaxWg + 1];  // exclusive prefix of wg_sums (fits: counts <= 4096 per tile)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint32_t wg = blockIdx.x;
-  const uint32_t si = find_seg(P.segs, P.nsegs, wg);
+  const uint32_t si = P.wg_seg[wg];
   const ScanSeg S = P.segs[si];
-  const uint32_t mine = P.wg_sums[wg];
-  if (mine == 0 && wg != 0) return;
-  // ---- exclusive prefix over all workgroup sums, in LDS (thread-blocked scan)
-  {
-    const uint32_t per = (P.nwg + kThreads - 1) / kThreads;
-    const uint32_t i0 = tid * per, i1 = min(i0 + per, P.nwg);
-    unsigned long long loc = 0;
-    for (uint32_t i = i0; i < i1; i++) loc += P.wg_sums[i];
-    unsigned long long inc = loc;
+  constexpr int NTA = NT > 0 ? NT : 1;
+  ScanTerm T[NTA];
+  if (NT > 0)
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      unsigned long long o = __shfl_up(inc, d, 64);
-      if (lane >= d) inc += o;
-    }
-    if (lane == 63) s_wsum[wid] = inc;
-    __syncthreads();
-    unsigned long long run = inc - loc;
-    for (int w = 0; w < wid; w++) run += s_wsum[w];
-    for (uint32_t i = i0; i < i1; i++) {
-      pre[i] = uint32_t(run);  // total matches per device launch < 2^32 (checked on the host)
-      run += P.wg_sums[i];
-    }
-    if (i1 == P.nwg && i0 < i1) pre[P.nwg] = uint32_t(run);
-    if (P.nwg == 0 && tid == 0) pre[0] = 0;
-    __syncthreads();
+    for (int q = 0; q < NTA; q++) T[q] = P.terms[S.term0 + q];
+  for (uint32_t q = 0; q < S.nterms; q++) {  // stage the small bitmaps in LDS
+    const ScanTerm &Tq = P.terms[S.term0 + q];
+    if (Tq.lds_off != kNoLds)
+      for (uint32_t w = tid; w < Tq.bm_words; w += kThreads) lds_bm[Tq.lds_off + w] = Tq.bm[w];
   }
-  auto seg_total = [&](uint32_t s) -> unsigned long long {
-    const ScanSeg &Ss = P.segs[s];
-    unsigned long long c = pre[Ss.first_wg + Ss.nwg] - pre[Ss.first_wg];
-    return P.limit_mode ? umin64(c, Ss.cap) : c;
-  };
+  for (uint32_t i = tid; i < P.nsegs; i += kThreads) lds_seg[i] = 0;
+  __syncthreads();
+
+  // ---- phase 1: scan
+  const uint32_t lt0 = (wg - S.first_wg) * S.tpw;
+  const uint32_t ntl = min(lt0 + S.tpw, S.ntiles) - lt0;
+  uint32_t wsum = 0;
+  for (uint32_t t = 0; t < ntl; t++) {
+    const uint32_t lt = lt0 + t;
+    const uint64_t tile0 = uint64_t(lt) * kTile;
+    const uint32_t mask = tile0 + kTile <= S.n ? tile_mask<NT, DUR, RANGE, true, W1>(P, S, T, lds_bm, tile0, tid)
+                                               : tile_mask<NT, DUR, RANGE, false, W1>(P, S, T, lds_bm, tile0, tid);
+    uint32_t c = __popc(mask);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
+    const int buf = t & 1;
+    if (lane == 0) s_wcnt[buf][wid] = c;
+    __syncthreads();
+    uint32_t tc = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; w++) tc += s_wcnt[buf][w];
+    if (t < kLdsTiles) lds_mask[t * kThreads + tid] = uint16_t(mask);
+    else if (tc) P.mask[uint64_t(S.first_tile + lt) * kThreads + tid] = uint16_t(mask);
+    if (tid == 0) s_tc[t] = uint16_t(tc);
+    wsum += tc;
+  }
+
+  // ---- phase 2: publish, look back
+  const unsigned long long tag = (unsigned long long)P.epoch << 32;
+  if (tid == 0) __hip_atomic_store(&P.agg[wg], tag | wsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool last = wg + 1 == P.nwg;
+  if (wsum == 0 && !last) return;
+  const bool per_seg = P.limit_mode || last;
+  unsigned long long loc = 0;
+  for (uint32_t i = tid; i < wg; i += kThreads) {
+    unsigned long long w;
+    uint32_t spins = 0;
+    while (((w = __hip_atomic_load(&P.agg[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~0xffffffffull) != tag) {
+      if (++spins > kSpinMax) {
+        reinterpret_cast<volatile unsigned long long *>(P.out)[1] = 1;  // host fails the query
+        w = tag;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    const uint32_t v = uint32_t(w);
+    if (per_seg) atomicAdd(&lds_seg[P.wg_seg[i]], v);
+    else loc += v;
+  }
   unsigned long long *hdr = reinterpret_cast<unsigned long long *>(P.out);
-  if (wg == 0) {  // header: records written + per-block counts
-    unsigned long long t = 0;
-    for (uint32_t s = tid; s < P.nsegs; s += kThreads) {
-      unsigned long long c = seg_total(s);
-      hdr[8 + s] = c;
-      t += c;
-    }
-    t = block_sum(t, red);
-    if (tid == 0) hdr[0] = t;
-    if (mine == 0) return;
-  }
-  const unsigned long long seg_rank0 = pre[wg] - pre[S.first_wg];
-  unsigned long long base;  // output slot of this workgroup's first match
-  if (P.limit_mode) {
-    unsigned long long b = 0;
-    for (uint32_t s = tid; s < si; s += kThreads) b += seg_total(s);
-    base = block_sum(b, red);
+  unsigned long long seg_rank0, base;  // rank of this workgroup's first match in its block; output slot of rank 0
+  if (!per_seg) {
+    const unsigned long long excl = block_sum(loc, s_red);
+    seg_rank0 = 0;  // unused in this mode
+    base = excl;
   } else {
-    base = pre[wg];
+    __syncthreads();
+    seg_rank0 = lds_seg[si];  // lower workgroups of the same block
+    unsigned long long b = 0;
+    for (uint32_t s2 = tid; s2 < si; s2 += kThreads) {
+      const unsigned long long c = lds_seg[s2];
+      b += P.limit_mode ? umin64(c, P.segs[s2].cap) : c;
+    }
+    base = block_sum(b, s_red);
+    if (!P.limit_mode) base += seg_rank0;
+    if (last) {  // header: records written + per-block counts (this block's total includes our own)
+      __syncthreads();
+      if (tid == 0) lds_seg[si] += wsum;
+      __syncthreads();
+      unsigned long long tot = 0;
+      for (uint32_t s2 = tid; s2 < P.nsegs; s2 += kThreads) {
+        const unsigned long long c = P.limit_mode ? umin64(lds_seg[s2], P.segs[s2].cap) : lds_seg[s2];
+        hdr[8 + s2] = c;
+        tot += c;
+      }
+      tot = block_sum(tot, s_red);
+      if (tid == 0) hdr[0] = tot;
+    }
   }
+  if (wsum == 0) return;
+  if (P.limit_mode && seg_rank0 >= S.cap) return;  // the block's first `cap` matches precede this workgroup
+
+  // ---- phase 3: emit in scan order
   MatchRec *out = reinterpret_cast<MatchRec *>(P.out + P.hdr_bytes);
-  const uint32_t lt0 = (wg - S.first_wg) * S.tpw, lt1 = min(lt0 + S.tpw, S.ntiles);
-  unsigned long long run = 0;
-  for (uint32_t lt = lt0; lt < lt1; lt++) {
-    const uint32_t gt = S.first_tile + lt;
-    const uint32_t tc = P.tile_counts[gt];
+  unsigned long long run = 0;  // matches of this workgroup before the current tile
+  for (uint32_t t = 0; t < ntl; t++) {
+    const uint32_t tc = s_tc[t];
     if (tc == 0) continue;
-    const uint32_t mask = P.mask[uint64_t(gt) * kThreads + tid];
+    const uint32_t lt = lt0 + t;
+    const uint32_t mask = t < kLdsTiles ? lds_mask[t * kThreads + tid]
+                                        : G(P.mask)[uint64_t(S.first_tile + lt) * kThreads + tid];
     // ranks in scan order (k, tid, j): wave scan of 4 packed 16-bit per-step counts
     unsigned long long pc = 0;
 #pragma unroll
@@ -514,20 +528,22 @@ extern "C" __global__ void __launch_bounds__(kThreads) emit_kernel(ScanParams P)
       step_base += uint32_t((tot >> (16 * k)) & 0xffff);
       for (int j = 0; j < 4; j++) {
         if (!(nib & (1u << j))) continue;
-        const unsigned long long rank_seg = seg_rank0 + run + r++;
+        const unsigned long long rank_wg = run + r++;  // rank among this workgroup's matches
         unsigned long long slot;
         if (P.limit_mode) {
-          if (rank_seg >= S.cap) continue;
-          slot = base + rank_seg;
+          if (seg_rank0 + rank_wg >= S.cap) continue;
+          slot = base + seg_rank0 + rank_wg;
         } else {
-          slot = base + (rank_seg - seg_rank0);
+          slot = base + rank_wg;
           if (slot >= P.out_cap) continue;
         }
         const uint64_t ei = uint64_t(lt) * kTile + uint64_t(k) * (kThreads * 4) + uint64_t(tid) * 4 + j;
         MatchRec *dst = out + slot;
-        *reinterpret_cast<uint4 *>(dst->id) = *reinterpret_cast<const uint4 *>(S.ids + ei * 16);
-        dst->start = S.start_ns[ei];
-        dst->end = S.end_ns[ei];
+        const u32x4 id = *G<u32x4>(S.ids + ei * 16);
+        const uint64_t st = G(S.start_ns)[ei], en = G(S.end_ns)[ei];
+        *reinterpret_cast<u32x4 *>(dst->id) = id;
+        dst->start = st;
+        dst->end = en;
         dst->entry = ei;
         dst->block = S.block_idx;
         dst->pad = 0;
@@ -544,10 +560,10 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 using ScanFn = void (*)(ScanParams);
 template <int NT, bool W1>
 static ScanFn pick3(bool dur, bool range) {
-  if (dur && range) return scan_kernel<NT, true, true, W1>;
-  if (dur) return scan_kernel<NT, true, false, W1>;
-  if (range) return scan_kernel<NT, false, true, W1>;
-  return scan_kernel<NT, false, false, W1>;
+  if (dur && range) return search_kernel<NT, true, true, W1>;
+  if (dur) return search_kernel<NT, true, false, W1>;
+  if (range) return search_kernel<NT, false, true, W1>;
+  return search_kernel<NT, false, false, W1>;
 }
 // w1: every term column of every block in this launch is one byte wide
 static ScanFn pick_scan(uint32_t nterms, bool dur, bool range, bool w1) {
@@ -691,27 +707,24 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   out.kernel_ns = out.scan_ns = 0;
   out.scan_bytes = scan_bytes;
   if (segs.empty()) return;
-  // workgroups: one resident wave of them (occupancy x CUs), each owning a
+  // workgroups: about one resident wave of them (occupancy x CUs), each owning a
   // contiguous tile range of one block
   const ScanFn scan_fn = pick_scan(q.nterms, has_dur, q.has_range, all_w1);
+  if (segs.size() > kMaxSegs) fail(TSG_E_UNSUPPORTED, "too many blocks per device in one search (max 2048)");
+  const uint32_t lds_words = max_lds_words + kLdsTiles * kThreads / 2 + uint32_t(segs.size());
   int per_cu = 0;
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(scan_fn), kThreads,
-                                                       size_t(max_lds_words) * 4));
+                                                       size_t(lds_words) * 4));
   per_cu = std::max(1, std::min(per_cu, 8));
   const uint32_t target_wg = uint32_t(dc.num_cu) * uint32_t(per_cu);
   const uint32_t tpw = std::max<uint32_t>(1, (tiles + target_wg - 1) / target_wg);
-  uint32_t tpw_eff = tpw, nwg = 0;
-  for (;;) {
-    nwg = 0;
-    for (auto &sg : segs) {
-      sg.tpw = tpw_eff;
-      sg.first_wg = nwg;
-      sg.nwg = (sg.ntiles + tpw_eff - 1) / tpw_eff;
-      nwg += sg.nwg;
-    }
-    if (nwg <= kMaxWg) break;
-    if (segs.size() > kMaxWg / 2) fail(TSG_E_UNSUPPORTED, "too many blocks per device in one search (max 2048)");
-    tpw_eff *= 2;
+  if (tpw > kMaxTpw) fail(TSG_E_UNSUPPORTED, "too many entries per device in one search");
+  uint32_t nwg = 0;
+  for (auto &sg : segs) {
+    sg.tpw = tpw;
+    sg.first_wg = nwg;
+    sg.nwg = (sg.ntiles + tpw - 1) / tpw;
+    nwg += sg.nwg;
   }
   if (n_all >= (1ull << 32)) fail(TSG_E_UNSUPPORTED, "more than 2^32 entries per device in one search");
   tr.mark("plan");
@@ -719,9 +732,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // ---- scratch
   dc.bitmaps.ensure(std::max<size_t>(bm_total, 1) * 4);
   dc.vmatch.ensure(std::max<size_t>(vmatch_total, 1));
-  dc.maskbits.ensure(size_t(tiles) * kThreads * 2);
-  dc.tile_counts.ensure(size_t(tiles) * 4);
-  dc.wg_sums.ensure(size_t(nwg) * 4);
+  if (tpw > kLdsTiles) dc.maskbits.ensure(size_t(tiles) * kThreads * 2);
+  if (dc.agg.ensure(size_t(nwg) * 8)) HIP_OK(hipMemsetAsync(dc.agg.p, 0, dc.agg.cap, s));  // no stale epochs
   const size_t hdr_bytes = align_up(64 + 8 * segs.size(), 256);
   uint64_t n_total = 0, cap_total = 0;
   for (auto &sg : segs) {
@@ -729,7 +741,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     cap_total += sg.cap;
   }
   // limit 0: start from the capacity the result buffer already has (>= 2^16
-  // records); a larger match count re-runs the emit pass into a grown buffer
+  // records); a larger match count re-runs the launch into a grown buffer
   const uint64_t have = dc.hres.cap > hdr_bytes ? (dc.hres.cap - hdr_bytes) / sizeof(MatchRec) : 0;
   uint64_t out_cap = limit ? cap_total : std::min<uint64_t>(n_total, std::max<uint64_t>(have, 1u << 16));
   // [header | records] go straight to pinned host memory (no D2H copy, no copy kernel)
@@ -744,7 +756,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   const size_t o_sj = align_up(o_jobs + jobs.size() * sizeof(DictJob), 16);
   const size_t o_sp = align_up(o_sj + set_jobs.size() * 4, 16);
   const size_t o_nd = align_up(o_sp + set_items.size() * 4, 16);
-  const size_t total_desc = align_up(o_nd + needles.size() + 1, 16);
+  const size_t o_ws = align_up(o_nd + needles.size() + 1, 16);
+  const size_t total_desc = align_up(o_ws + size_t(nwg) * 2, 16);
   dc.hdesc.ensure(total_desc);
   dc.desc.ensure(total_desc);
   auto *hd = static_cast<uint8_t *>(dc.hdesc.p);
@@ -754,6 +767,9 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   if (!set_jobs.empty()) std::memcpy(hd + o_sj, set_jobs.data(), set_jobs.size() * 4);
   std::memcpy(hd + o_sp, set_items.data(), set_items.size() * 4);
   if (!needles.empty()) std::memcpy(hd + o_nd, needles.data(), needles.size());
+  auto *ws = reinterpret_cast<uint16_t *>(hd + o_ws);
+  for (size_t i = 0; i < segs.size(); i++)
+    for (uint32_t w = 0; w < segs[i].nwg; w++) ws[segs[i].first_wg + w] = uint16_t(i);
   auto *dd = static_cast<uint8_t *>(dc.desc.p);
   HIP_OK(hipMemcpyAsync(dd, hd, total_desc, hipMemcpyHostToDevice, s));
 
@@ -772,6 +788,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   ScanParams P{};
   P.segs = reinterpret_cast<const ScanSeg *>(dd + o_segs);
   P.terms = reinterpret_cast<const ScanTerm *>(dd + o_terms);
+  P.wg_seg = reinterpret_cast<const uint16_t *>(dd + o_ws);
   P.nsegs = uint32_t(segs.size());
   P.nwg = nwg;
   P.has_min = q.has_min;
@@ -783,38 +800,51 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   P.start_s = q.start_s;
   P.end_s = q.end_s;
   P.mask = static_cast<uint16_t *>(dc.maskbits.p);
-  P.tile_counts = static_cast<uint32_t *>(dc.tile_counts.p);
-  P.wg_sums = static_cast<uint32_t *>(dc.wg_sums.p);
+  P.agg = static_cast<unsigned long long *>(dc.agg.p);
+  P.lds_bm_words = max_lds_words;
   P.out = ho;
   P.hdr_bytes = hdr_bytes;
   P.out_cap = out_cap;
-  if (time_scan) HIP_OK(hipEventRecord(dc.es0, s));
-  scan_fn<<<nwg, kThreads, max_lds_words * 4, s>>>(P);
-  if (time_scan) HIP_OK(hipEventRecord(dc.es1, s));
-  emit_kernel<<<nwg, kThreads, 0, s>>>(P);
-  HIP_OK(hipGetLastError());
+  auto launch = [&](bool timed) {
+    if (++dc.search_epoch == 0) dc.search_epoch = 1;  // 0 is the never-published tag of a fresh buffer
+    P.epoch = dc.search_epoch;
+    auto *h = reinterpret_cast<volatile uint64_t *>(P.out);
+    h[0] = 0;
+    h[1] = 0;  // look-back error flag
+    void *args[] = {&P};
+    // hipExtLaunchKernel stamps the events from the dispatch packet itself: no
+    // extra barrier packets between the kernels when timing is on
+    HIP_OK(hipExtLaunchKernel(reinterpret_cast<const void *>(scan_fn), dim3(nwg), dim3(kThreads), args,
+                              size_t(lds_words) * 4, s, timed ? dc.es0 : nullptr, timed ? dc.es1 : nullptr, 0));
+  };
+  launch(time_scan);
   if (time_all) HIP_OK(hipEventRecord(dc.ev1, s));
   tr.mark("submit");
   HIP_OK(hipStreamSynchronize(s));
   tr.mark("sync");
+  auto check = [&] {
+    if (reinterpret_cast<volatile uint64_t *>(ho)[1])
+      fail(TSG_E_DEVICE, "search look-back did not complete (workgroup dispatch order assumption broken)");
+  };
+  check();
   uint64_t total = *reinterpret_cast<volatile uint64_t *>(ho);
   float ms = 0, sms = 0;
   if (time_all) HIP_OK(hipEventElapsedTime(&ms, dc.ev0, dc.ev1));
   if (time_scan) HIP_OK(hipEventElapsedTime(&sms, dc.es0, dc.es1));
   out.kernel_ns = uint64_t(double(ms) * 1e6);
   out.scan_ns = uint64_t(double(sms) * 1e6);
-  uint64_t nonzero_tiles_bound = std::min<uint64_t>(tiles, total);
-  out.scan_bytes += nonzero_tiles_bound * kThreads * 2 + uint64_t(tiles) * 4 + uint64_t(nwg) * 4;
+  // + published counts, + id/start/end reads of each written record
+  out.scan_bytes += uint64_t(nwg) * 8 + std::min<uint64_t>(total, out_cap) * 32;
   if (!limit && total > out_cap) {
-    // more matches than the result buffer holds: grow it and re-run the emit pass only
+    // more matches than the result buffer holds: grow it and run the launch again
     out_cap = total;
     dc.hres.ensure(hdr_bytes + out_cap * sizeof(MatchRec));
     ho = static_cast<uint8_t *>(dc.hres.p);
     P.out = ho;
     P.out_cap = out_cap;
-    emit_kernel<<<nwg, kThreads, 0, s>>>(P);
-    HIP_OK(hipGetLastError());
+    launch(false);
     HIP_OK(hipStreamSynchronize(s));
+    check();
   }
   out.recs.resize(total);
   if (total) std::memcpy(out.recs.data(), ho + hdr_bytes, total * sizeof(MatchRec));
