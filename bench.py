@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--entries", type=int, default=1_000_000, help="entries per block")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-blocks", type=int, default=4, help="blocks in the CPU baseline sample")
+    ap.add_argument("--events", type=int, default=1,
+                    help="HIP events around the scan kernel in every timed step (roofline.achieved); 0 = off")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--keep", action="store_true")
     return ap.parse_args()
@@ -127,8 +129,9 @@ def main():
                           max_duration_ms=QUERY["max_duration_ms"], start=QUERY["start"], end=QUERY["end"])
     pipe = T.Pipeline(req)
     got, met = eng.search(blocks, pipe)  # full result once (parity spot check below)
+    sflags = T.SEARCH_TIME_SCAN if args.events else 0
     for _ in range(args.warmup):
-        eng.search_raw(blocks, pipe, flags=T.SEARCH_TIME_SCAN)
+        eng.search_raw(blocks, pipe, flags=sflags)
 
     if dist:
         dist.barrier()
@@ -136,7 +139,7 @@ def main():
     scan_ns = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        nm, met = eng.search_raw(blocks, pipe, flags=T.SEARCH_TIME_SCAN)
+        nm, met = eng.search_raw(blocks, pipe, flags=sflags)
         scan_ns.append(met.scan_kernel_ns)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -155,7 +158,7 @@ def main():
     value = total_entries * args.steps / elapsed
     scan_avg_ns = sum(scan_ns) / len(scan_ns)
     scan_bytes = met.scan_bytes
-    achieved = scan_bytes / scan_avg_ns  # bytes/ns == GB/s
+    achieved = scan_bytes / scan_avg_ns if scan_avg_ns else None  # bytes/ns == GB/s
     out = {
         "metric": METRIC,
         "value": value,
@@ -178,7 +181,7 @@ def main():
         "achieved_hbm_gbps": achieved,
         "roofline": {
             "bound": "hbm", "kernel": "scan_kernel", "achieved": achieved, "peak": PEAK_HBM_GBPS,
-            "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS, "traffic": None,
+            "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS if achieved else None, "traffic": None,
             "bytes_per_launch": scan_bytes, "avg_launch_us": scan_avg_ns / 1e3,
             "bytes_per_entry": 15,
         },

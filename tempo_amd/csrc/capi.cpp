@@ -4,6 +4,8 @@
 // there is no CPU fallback behind this ABI (the Go shim keeps its own CPU path).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <thread>
 #include <unordered_map>
@@ -306,6 +308,9 @@ int tsg_block_tag_values(const tsg_block *b, const uint8_t *key, size_t klen, ui
 int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
                const tsg_search_opts *opts, tsg_result **out) {
   if (!ctx || !q || !out || (nblocks && !blocks)) return TSG_E_INVALID;
+  static const bool trace = std::getenv("TSG_TRACE") != nullptr;
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t_in = trace ? clk::now() : clk::time_point();
   return guard([&] {
     const uint32_t limit = opts ? opts->limit : 0;
     const uint32_t flags = opts ? opts->flags : 0;
@@ -346,6 +351,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       for (auto &e : errs)
         if (e) std::rethrow_exception(e);
     }
+    const clk::time_point t_dev = trace ? clk::now() : clk::time_point();
     // per block match lists in scan order
     std::vector<std::vector<const SearchOut::Rec *>> per_block(nblocks);
     for (auto &o : outs) {
@@ -395,6 +401,13 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     }
     res->finalize();
     *out = &guard_res.release()->pub;
+    if (trace) {
+      const clk::time_point t_end = clk::now();
+      std::fprintf(stderr, "[tsg] tsg_search us: device=%.1f results=%.1f total=%.1f\n",
+                   std::chrono::duration<double, std::micro>(t_dev - t_in).count(),
+                   std::chrono::duration<double, std::micro>(t_end - t_dev).count(),
+                   std::chrono::duration<double, std::micro>(t_end - t_in).count());
+    }
   });
 }
 void tsg_result_free(tsg_result *r) { delete reinterpret_cast<ResultHolder *>(r); }

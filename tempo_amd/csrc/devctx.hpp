@@ -3,7 +3,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
+#include <utility>
 
 #include "engine.hpp"
 
@@ -66,7 +68,8 @@ struct DeviceCtx {
   // stores go over the fabric, visible to the host once the stream is synchronised)
   HostBuf hres{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};
   unsigned long long epoch = 0, ticket_base = 0;  // lookup launches
-  uint32_t search_epoch = 0;  // search launches: tag of the published workgroup counts
+  uint32_t search_epoch = 0;
+  std::map<std::pair<const void *, size_t>, int> occupancy;  // (kernel, dynamic LDS) -> blocks per CU  // search launches: tag of the published workgroup counts
   size_t gran_tiles = 0;
 };
 

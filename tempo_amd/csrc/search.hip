@@ -93,6 +93,20 @@ constexpr uint32_t kNoLds = 0xffffffffu;
 
 // ------------------------------------------------------------------------------------
 // dictionary match
+// Pointers inside descriptors are generic to the compiler; casting them to the
+// global address space turns flat loads (which wait on vmcnt AND lgkmcnt) into
+// global_load_dword{,x2,x4}.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *G(const T *p) {
+  return (const __attribute__((address_space(1))) T *)(p);
+}
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *G(const void *p) {
+  return (const __attribute__((address_space(1))) T *)(p);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ bool dev_contains(const uint8_t *h, uint32_t hl, const uint8_t *nd, uint32_t nl) {
   if (nl == 0) return true;  // bytes.Contains(x, "") (pitfall P7)
   if (nl > hl) return false;
@@ -106,31 +120,54 @@ __device__ __forceinline__ bool dev_contains(const uint8_t *h, uint32_t hl, cons
   return false;
 }
 
-// One lane per dictionary value; every job's item range is 64-aligned so a wave
+// prep: (1) workgroup 0 copies the query descriptors from pinned host memory into
+// device memory for the search kernel (no H2D copy launch); (2) dictionary match,
+// one lane per dictionary value; every job's item range is 64-aligned so a wave
 // never straddles two jobs, and identity jobs turn the wave's matches into two
-// bitmap words with one ballot.
-extern "C" __global__ void __launch_bounds__(256) dict_match_kernel(const DictJob *jobs, uint32_t njobs,
-                                                                    uint32_t total, const uint8_t *needles,
-                                                                    uint8_t *vmatch, uint32_t *bitmaps) {
-  const uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
+// bitmap words with one ballot. The job table and needles are read from `src`
+// (host or device copy) once per workgroup into LDS when they fit.
+constexpr uint32_t kPrepLdsJobs = 2048, kPrepLdsNeedle = 4096;
+constexpr size_t kHostDescMax = 64 << 10;  // larger descriptor sets take one H2D copy
+extern "C" __global__ void __launch_bounds__(256) prep_kernel(const uint8_t *src, uint8_t *dst, uint32_t copy16,
+                                                              uint32_t o_jobs, uint32_t o_jb, uint32_t njobs,
+                                                              uint32_t total, uint32_t o_nd, uint32_t nd_bytes,
+                                                              uint8_t *vmatch, uint32_t *bitmaps) {
+  __shared__ uint32_t s_jb[kPrepLdsJobs];
+  __shared__ __attribute__((aligned(16))) uint8_t s_nd[kPrepLdsNeedle];
+  const int tid = threadIdx.x;
+  if (blockIdx.x == 0 && src != dst)
+    for (uint32_t i = tid; i < copy16; i += blockDim.x)
+      reinterpret_cast<u32x4 *>(dst)[i] = reinterpret_cast<const u32x4 *>(src)[i];
+  if (total == 0) return;
+  const bool stage = njobs <= kPrepLdsJobs && nd_bytes <= kPrepLdsNeedle;
+  const uint32_t *jbase = reinterpret_cast<const uint32_t *>(src + o_jb);
+  const uint8_t *needles = src + o_nd;
+  if (stage) {
+    for (uint32_t i = tid; i < njobs; i += blockDim.x) s_jb[i] = jbase[i];
+    for (uint32_t i = tid; i < nd_bytes; i += blockDim.x) s_nd[i] = needles[i];
+    __syncthreads();
+    jbase = s_jb;
+    needles = s_nd;
+  }
+  const uint32_t item = blockIdx.x * blockDim.x + tid;
   const uint32_t wave_item = __builtin_amdgcn_readfirstlane(item & ~63u);
   if (wave_item >= total) return;
   uint32_t lo = 0, hi = njobs;
   while (hi - lo > 1) {
     uint32_t mid = (lo + hi) >> 1;
-    if (jobs[mid].item_base <= wave_item) lo = mid;
+    if (jbase[mid] <= wave_item) lo = mid;
     else hi = mid;
   }
-  const DictJob &jb = jobs[lo];
+  const DictJob jb = reinterpret_cast<const DictJob *>(src + o_jobs)[lo];
   const uint32_t v = item - jb.item_base;
   bool m = false;
   if (v < jb.nvals) {
-    uint32_t o0 = jb.off[v], o1 = jb.off[v + 1];
+    uint32_t o0 = G(jb.off)[v], o1 = G(jb.off)[v + 1];
     m = dev_contains(jb.bytes + o0, o1 - o0, needles + jb.needle_off, jb.needle_len);
   }
   if (jb.identity) {
     unsigned long long b = __ballot(m);
-    const int lane = threadIdx.x & 63;
+    const int lane = tid & 63;
     const uint32_t w0 = (v - lane) >> 5;  // first word of this wave
     const uint32_t words = (jb.nsets + 31) >> 5;
     if (lane == 0 && w0 < words) bitmaps[jb.bm_base + w0] = uint32_t(b);
@@ -170,20 +207,6 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
 
 // ------------------------------------------------------------------------------------
 // scan
-// Pointers inside descriptors are generic to the compiler; casting them to the
-// global address space turns flat loads (which wait on vmcnt AND lgkmcnt) into
-// global_load_dword{,x2,x4}.
-template <typename T>
-__device__ __forceinline__ const __attribute__((address_space(1))) T *G(const T *p) {
-  return (const __attribute__((address_space(1))) T *)(p);
-}
-template <typename T>
-__device__ __forceinline__ const __attribute__((address_space(1))) T *G(const void *p) {
-  return (const __attribute__((address_space(1))) T *)(p);
-}
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
 template <bool FULL>
 __device__ __forceinline__ uint4 load4_u32(const uint32_t *p, uint64_t e, uint64_t n) {
   uint4 r;
@@ -593,7 +616,8 @@ struct Tracer {
     last = now;
   }
   ~Tracer() {
-    if (on && len) std::fprintf(stderr, "[tsg] device_search us:%s\n", buf);
+    if (on && len) std::fprintf(stderr, "[tsg] device_search us:%s total=%.1f\n", buf,
+                                std::chrono::duration<double, std::micro>(last - t0).count());
   }
 };
 
@@ -712,10 +736,12 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   const ScanFn scan_fn = pick_scan(q.nterms, has_dur, q.has_range, all_w1);
   if (segs.size() > kMaxSegs) fail(TSG_E_UNSUPPORTED, "too many blocks per device in one search (max 2048)");
   const uint32_t lds_words = max_lds_words + kLdsTiles * kThreads / 2 + uint32_t(segs.size());
-  int per_cu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(scan_fn), kThreads,
-                                                       size_t(lds_words) * 4));
-  per_cu = std::max(1, std::min(per_cu, 8));
+  int &per_cu = dc.occupancy[{reinterpret_cast<const void *>(scan_fn), size_t(lds_words) * 4}];
+  if (per_cu == 0) {
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(scan_fn), kThreads,
+                                                         size_t(lds_words) * 4));
+    per_cu = std::max(1, std::min(per_cu, 8));
+  }
   const uint32_t target_wg = uint32_t(dc.num_cu) * uint32_t(per_cu);
   const uint32_t tpw = std::max<uint32_t>(1, (tiles + target_wg - 1) / target_wg);
   if (tpw > kMaxTpw) fail(TSG_E_UNSUPPORTED, "too many entries per device in one search");
@@ -750,10 +776,12 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   for (size_t i = 0; i < terms.size(); i++)
     terms[i].bm = static_cast<const uint32_t *>(dc.bitmaps.p) + term_bm_base[i];
 
-  // ---- descriptors: one H2D copy
+  // ---- descriptors: written to pinned host memory; the prep kernel copies them
+  // into device memory (small descriptor sets) or one H2D copy (large ones)
   const size_t o_segs = 0, o_terms = align_up(segs.size() * sizeof(ScanSeg), 16);
   const size_t o_jobs = align_up(o_terms + terms.size() * sizeof(ScanTerm), 16);
-  const size_t o_sj = align_up(o_jobs + jobs.size() * sizeof(DictJob), 16);
+  const size_t o_jb = align_up(o_jobs + jobs.size() * sizeof(DictJob), 16);
+  const size_t o_sj = align_up(o_jb + jobs.size() * 4, 16);
   const size_t o_sp = align_up(o_sj + set_jobs.size() * 4, 16);
   const size_t o_nd = align_up(o_sp + set_items.size() * 4, 16);
   const size_t o_ws = align_up(o_nd + needles.size() + 1, 16);
@@ -764,6 +792,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   std::memcpy(hd + o_segs, segs.data(), segs.size() * sizeof(ScanSeg));
   std::memcpy(hd + o_terms, terms.data(), terms.size() * sizeof(ScanTerm));
   std::memcpy(hd + o_jobs, jobs.data(), jobs.size() * sizeof(DictJob));
+  auto *jbase = reinterpret_cast<uint32_t *>(hd + o_jb);
+  for (size_t i = 0; i < jobs.size(); i++) jbase[i] = jobs[i].item_base;
   if (!set_jobs.empty()) std::memcpy(hd + o_sj, set_jobs.data(), set_jobs.size() * 4);
   std::memcpy(hd + o_sp, set_items.data(), set_items.size() * 4);
   if (!needles.empty()) std::memcpy(hd + o_nd, needles.data(), needles.size());
@@ -771,20 +801,25 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   for (size_t i = 0; i < segs.size(); i++)
     for (uint32_t w = 0; w < segs[i].nwg; w++) ws[segs[i].first_wg + w] = uint16_t(i);
   auto *dd = static_cast<uint8_t *>(dc.desc.p);
-  HIP_OK(hipMemcpyAsync(dd, hd, total_desc, hipMemcpyHostToDevice, s));
+  const uint8_t *src = hd;
+  if (total_desc > kHostDescMax) {
+    HIP_OK(hipMemcpyAsync(dd, hd, total_desc, hipMemcpyHostToDevice, s));
+    src = dd;
+  }
+  tr.mark("desc");
 
   const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
   if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
-  if (items)
-    dict_match_kernel<<<(items + 255) / 256, 256, 0, s>>>(reinterpret_cast<const DictJob *>(dd + o_jobs),
-                                                         uint32_t(jobs.size()), items, dd + o_nd,
-                                                         static_cast<uint8_t *>(dc.vmatch.p),
-                                                         static_cast<uint32_t *>(dc.bitmaps.p));
+  prep_kernel<<<std::max<uint32_t>(1, (items + 255) / 256), 256, 0, s>>>(
+      src, dd, uint32_t(total_desc / 16), uint32_t(o_jobs), uint32_t(o_jb), uint32_t(jobs.size()), items,
+      uint32_t(o_nd), uint32_t(needles.size()), static_cast<uint8_t *>(dc.vmatch.p),
+      static_cast<uint32_t *>(dc.bitmaps.p));
   if (set_items.back())
     dict_sets_kernel<<<(set_items.back() + 255) / 256, 256, 0, s>>>(
         reinterpret_cast<const DictJob *>(dd + o_jobs), reinterpret_cast<const uint32_t *>(dd + o_sj),
         reinterpret_cast<const uint32_t *>(dd + o_sp), uint32_t(set_jobs.size()), set_items.back(),
         static_cast<const uint8_t *>(dc.vmatch.p), static_cast<uint32_t *>(dc.bitmaps.p));
+  tr.mark("dict");
   ScanParams P{};
   P.segs = reinterpret_cast<const ScanSeg *>(dd + o_segs);
   P.terms = reinterpret_cast<const ScanTerm *>(dd + o_terms);
@@ -819,7 +854,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   };
   launch(time_scan);
   if (time_all) HIP_OK(hipEventRecord(dc.ev1, s));
-  tr.mark("submit");
+  tr.mark("search");
   HIP_OK(hipStreamSynchronize(s));
   tr.mark("sync");
   auto check = [&] {
@@ -833,6 +868,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   if (time_scan) HIP_OK(hipEventElapsedTime(&sms, dc.es0, dc.es1));
   out.kernel_ns = uint64_t(double(ms) * 1e6);
   out.scan_ns = uint64_t(double(sms) * 1e6);
+  tr.mark("events");
   // + published counts, + id/start/end reads of each written record
   out.scan_bytes += uint64_t(nwg) * 8 + std::min<uint64_t>(total, out_cap) * 32;
   if (!limit && total > out_cap) {

@@ -14,7 +14,10 @@ if has test; then
 fi
 if has trace; then
   TSG_TRACE=1 timeout -k 10 600 python bench.py --steps 10 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/trace.json 2> gpurun_out/trace.err
-  rc=$?; echo "trace rc=$rc"; grep "\[tsg\]" gpurun_out/trace.err | tail -5; cat gpurun_out/trace.json
+  rc=$?; echo "trace rc=$rc"; grep "\[tsg\]" gpurun_out/trace.err | tail -6; cat gpurun_out/trace.json
+  [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 600 python bench.py --steps 50 --warmup 5 --cpu-baseline 0 --events 0 ${BENCH_ARGS:-} > gpurun_out/noevents.json 2> gpurun_out/noevents.err
+  rc=$?; echo "noevents rc=$rc"; cat gpurun_out/noevents.json
   [ $rc -eq 0 ] || exit $rc
 fi
 if has bench; then
