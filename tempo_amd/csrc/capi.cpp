@@ -57,10 +57,22 @@ struct ResultHolder {
   std::vector<uint8_t> ids, id_len;
   std::vector<uint64_t> start, end, entry;
   std::vector<uint32_t> dur, block, svc_len, name_len;
-  std::vector<std::string> svc, name;
+  std::vector<uint64_t> svc_off, name_off;  // into `arena` (one allocation for every name)
+  std::vector<char> arena;
   std::vector<const char *> svc_p, name_p;
-  void push(const uint8_t *id, uint8_t il, uint64_t s, uint64_t e, uint32_t b, uint64_t en, std::string sv,
-            std::string nm) {
+  void reserve(size_t n) {
+    ids.reserve(16 * n);
+    for (auto *v : {&start, &end, &entry, &svc_off, &name_off}) v->reserve(n);
+    for (auto *v : {&dur, &block, &svc_len, &name_len}) v->reserve(n);
+    id_len.reserve(n);
+  }
+  void set_str(std::vector<uint64_t> &off, std::vector<uint32_t> &len, size_t i, const char *p, size_t l) {
+    off[i] = arena.size();
+    len[i] = uint32_t(l);
+    arena.insert(arena.end(), p, p + l);
+  }
+  void push(const uint8_t *id, uint8_t il, uint64_t s, uint64_t e, uint32_t b, uint64_t en, const char *sv,
+            size_t svl, const char *nm, size_t nml) {
     ids.insert(ids.end(), id, id + 16);
     id_len.push_back(il);
     start.push_back(s);
@@ -68,23 +80,25 @@ struct ResultHolder {
     dur.push_back(uint32_t((e - s) / 1000000ULL));  // util.go:33
     block.push_back(b);
     entry.push_back(en);
-    svc.push_back(std::move(sv));
-    name.push_back(std::move(nm));
+    svc_off.push_back(0);
+    svc_len.push_back(0);
+    name_off.push_back(0);
+    name_len.push_back(0);
+    const size_t i = start.size() - 1;
+    set_str(svc_off, svc_len, i, sv, svl);
+    set_str(name_off, name_len, i, nm, nml);
   }
+  const char *svc(size_t i) const { return arena.data() + svc_off[i]; }
+  const char *name(size_t i) const { return arena.data() + name_off[i]; }
   void finalize() {
-    svc_p.clear();
-    name_p.clear();
-    svc_len.clear();
-    name_len.clear();
-    for (auto &s : svc) {
-      svc_p.push_back(s.c_str());
-      svc_len.push_back(uint32_t(s.size()));
+    const size_t n = start.size();
+    svc_p.resize(n);
+    name_p.resize(n);
+    for (size_t i = 0; i < n; i++) {
+      svc_p[i] = svc(i);
+      name_p[i] = name(i);
     }
-    for (auto &s : name) {
-      name_p.push_back(s.c_str());
-      name_len.push_back(uint32_t(s.size()));
-    }
-    pub.n = start.size();
+    pub.n = n;
     pub.trace_id = reinterpret_cast<const uint8_t(*)[16]>(ids.data());
     pub.trace_id_len = id_len.data();
     pub.start_ns = start.data();
@@ -354,6 +368,9 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     const clk::time_point t_dev = trace ? clk::now() : clk::time_point();
     // per block match lists in scan order
     std::vector<std::vector<const SearchOut::Rec *>> per_block(nblocks);
+    size_t nrec = 0;
+    for (auto &o : outs) nrec += o.second.recs.size();
+    res->reserve(nrec);
     for (auto &o : outs) {
       m.device_bytes_read += o.second.device_bytes;
       m.kernel_ns = std::max<uint64_t>(m.kernel_ns, o.second.kernel_ns);
@@ -375,11 +392,11 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       m.blocks_inspected++;
       uint64_t stop_entry = UINT64_MAX;
       for (const SearchOut::Rec *r : per_block[i]) {
-        std::string sv, nm;
-        if (h.svc_key >= 0 && h.svc_vid[r->entry] != kNone) sv = std::string(h.dict_value(h.svc_key, h.svc_vid[r->entry]));
-        if (h.name_key >= 0 && h.name_vid[r->entry] != kNone)
-          nm = std::string(h.dict_value(h.name_key, h.name_vid[r->entry]));
-        res->push(r->id, h.id_len[r->entry], r->start, r->end, uint32_t(i), r->entry, std::move(sv), std::move(nm));
+        std::string_view sv, nm;
+        if (h.svc_key >= 0 && h.svc_vid[r->entry] != kNone) sv = h.dict_value(h.svc_key, h.svc_vid[r->entry]);
+        if (h.name_key >= 0 && h.name_vid[r->entry] != kNone) nm = h.dict_value(h.name_key, h.name_vid[r->entry]);
+        res->push(r->id, h.id_len[r->entry], r->start, r->end, uint32_t(i), r->entry, sv.data(), sv.size(),
+                  nm.data(), nm.size());
         if (limit) {
           distinct.insert(std::string(reinterpret_cast<const char *>(r->id), 16));
           if (distinct.size() >= limit) {
@@ -429,16 +446,16 @@ int tsg_results_combine(const tsg_result *in, uint32_t max_results, tsg_result *
       auto it = map.find(key);
       if (it != map.end()) {  // CombineSearchResults (util.go:40-62)
         size_t e = it->second;
-        if (res->svc[e].empty()) res->svc[e] = std::string(in->root_service[i], in->root_service_len[i]);
-        if (res->name[e].empty()) res->name[e] = std::string(in->root_name[i], in->root_name_len[i]);
+        if (res->svc_len[e] == 0) res->set_str(res->svc_off, res->svc_len, e, in->root_service[i], in->root_service_len[i]);
+        if (res->name_len[e] == 0) res->set_str(res->name_off, res->name_len, e, in->root_name[i], in->root_name_len[i]);
         if (res->start[e] > in->start_ns[i]) res->start[e] = in->start_ns[i];
         if (res->dur[e] < in->duration_ms[i]) res->dur[e] = in->duration_ms[i];
       } else {
         map.emplace(key, res->start.size());
         order.push_back({i, res->start.size()});
         res->push(in->trace_id[i], in->trace_id_len[i], in->start_ns[i], in->end_ns[i], in->block_idx[i],
-                  in->entry_idx[i], std::string(in->root_service[i], in->root_service_len[i]),
-                  std::string(in->root_name[i], in->root_name_len[i]));
+                  in->entry_idx[i], in->root_service[i], in->root_service_len[i], in->root_name[i],
+                  in->root_name_len[i]);
         res->dur.back() = in->duration_ms[i];
       }
       if (map.size() >= max_results) break;
@@ -451,7 +468,7 @@ int tsg_results_combine(const tsg_result *in, uint32_t max_results, tsg_result *
     for (auto &f : order) {
       size_t e = f.idx;
       fin->push(&res->ids[e * 16], res->id_len[e], res->start[e], res->end[e], res->block[e], res->entry[e],
-                res->svc[e], res->name[e]);
+                res->svc(e), res->svc_len[e], res->name(e), res->name_len[e]);
       fin->dur.back() = res->dur[e];
     }
     fin->pub.metrics = in->metrics;

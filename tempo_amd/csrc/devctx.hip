@@ -30,8 +30,9 @@ void ctx_init(Ctx &c, const tsg_options *opts) {
     HIP_OK(hipStreamCreateWithFlags(&dc->stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&dc->ev0));
     HIP_OK(hipEventCreate(&dc->ev1));
-    HIP_OK(hipEventCreate(&dc->es0));
-    HIP_OK(hipEventCreate(&dc->es1));
+    // scan timing events: no system-scope fence (no L2 writeback between kernels)
+    HIP_OK(hipEventCreateWithFlags(&dc->es0, hipEventDisableSystemFence));
+    HIP_OK(hipEventCreateWithFlags(&dc->es1, hipEventDisableSystemFence));
     dc->ticket.ensure(64);
     HIP_OK(hipMemset(dc->ticket.p, 0, 64));
     dc->err.ensure(64);

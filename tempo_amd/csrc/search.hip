@@ -15,7 +15,6 @@
 //                inside a tile from packed wave scans, records written in the
 //                reference scan order (pages ascending, entry index ascending)
 // Everything is integer, HBM-bound streaming; no MFMA (no dense contraction).
-#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -126,39 +125,45 @@ __device__ __forceinline__ bool dev_contains(const uint8_t *h, uint32_t hl, cons
 // never straddles two jobs, and identity jobs turn the wave's matches into two
 // bitmap words with one ballot. The job table and needles are read from `src`
 // (host or device copy) once per workgroup into LDS when they fit.
-constexpr uint32_t kPrepLdsJobs = 2048, kPrepLdsNeedle = 4096;
+constexpr uint32_t kPrepLdsJobs = 128, kPrepLdsNeedle = 4096;
 constexpr size_t kHostDescMax = 64 << 10;  // larger descriptor sets take one H2D copy
+static_assert(sizeof(DictJob) % 16 == 0, "DictJob staged as 16-byte words");
 extern "C" __global__ void __launch_bounds__(256) prep_kernel(const uint8_t *src, uint8_t *dst, uint32_t copy16,
                                                               uint32_t o_jobs, uint32_t o_jb, uint32_t njobs,
                                                               uint32_t total, uint32_t o_nd, uint32_t nd_bytes,
                                                               uint8_t *vmatch, uint32_t *bitmaps) {
-  __shared__ uint32_t s_jb[kPrepLdsJobs];
+  __shared__ __attribute__((aligned(16))) DictJob s_jobs[kPrepLdsJobs];
   __shared__ __attribute__((aligned(16))) uint8_t s_nd[kPrepLdsNeedle];
   const int tid = threadIdx.x;
   if (blockIdx.x == 0 && src != dst)
     for (uint32_t i = tid; i < copy16; i += blockDim.x)
       reinterpret_cast<u32x4 *>(dst)[i] = reinterpret_cast<const u32x4 *>(src)[i];
   if (total == 0) return;
+  // one round trip for the whole job table + needles when they fit in LDS
   const bool stage = njobs <= kPrepLdsJobs && nd_bytes <= kPrepLdsNeedle;
-  const uint32_t *jbase = reinterpret_cast<const uint32_t *>(src + o_jb);
+  const DictJob *jobs = reinterpret_cast<const DictJob *>(src + o_jobs);
   const uint8_t *needles = src + o_nd;
   if (stage) {
-    for (uint32_t i = tid; i < njobs; i += blockDim.x) s_jb[i] = jbase[i];
-    for (uint32_t i = tid; i < nd_bytes; i += blockDim.x) s_nd[i] = needles[i];
+    constexpr uint32_t w16 = sizeof(DictJob) / 16;
+    for (uint32_t i = tid; i < njobs * w16; i += blockDim.x)
+      reinterpret_cast<u32x4 *>(s_jobs)[i] = reinterpret_cast<const u32x4 *>(jobs)[i];
+    for (uint32_t i = tid; i < (nd_bytes + 3) / 4; i += blockDim.x)
+      reinterpret_cast<uint32_t *>(s_nd)[i] = reinterpret_cast<const uint32_t *>(needles)[i];
     __syncthreads();
-    jbase = s_jb;
+    jobs = s_jobs;
     needles = s_nd;
   }
   const uint32_t item = blockIdx.x * blockDim.x + tid;
   const uint32_t wave_item = __builtin_amdgcn_readfirstlane(item & ~63u);
   if (wave_item >= total) return;
+  const uint32_t *jbase = reinterpret_cast<const uint32_t *>(src + o_jb);
   uint32_t lo = 0, hi = njobs;
   while (hi - lo > 1) {
     uint32_t mid = (lo + hi) >> 1;
-    if (jbase[mid] <= wave_item) lo = mid;
+    if ((stage ? s_jobs[mid].item_base : jbase[mid]) <= wave_item) lo = mid;
     else hi = mid;
   }
-  const DictJob jb = reinterpret_cast<const DictJob *>(src + o_jobs)[lo];
+  const DictJob jb = jobs[lo];
   const uint32_t v = item - jb.item_base;
   bool m = false;
   if (v < jb.nvals) {
@@ -846,11 +851,10 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     auto *h = reinterpret_cast<volatile uint64_t *>(P.out);
     h[0] = 0;
     h[1] = 0;  // look-back error flag
-    void *args[] = {&P};
-    // hipExtLaunchKernel stamps the events from the dispatch packet itself: no
-    // extra barrier packets between the kernels when timing is on
-    HIP_OK(hipExtLaunchKernel(reinterpret_cast<const void *>(scan_fn), dim3(nwg), dim3(kThreads), args,
-                              size_t(lds_words) * 4, s, timed ? dc.es0 : nullptr, timed ? dc.es1 : nullptr, 0));
+    if (timed) HIP_OK(hipEventRecord(dc.es0, s));
+    scan_fn<<<nwg, kThreads, size_t(lds_words) * 4, s>>>(P);
+    HIP_OK(hipGetLastError());
+    if (timed) HIP_OK(hipEventRecord(dc.es1, s));
   };
   launch(time_scan);
   if (time_all) HIP_OK(hipEventRecord(dc.ev1, s));
