@@ -147,8 +147,11 @@ static void open_common(tsg_ctx *ctx, const uint8_t *meta, size_t ml, bool has_m
     }
   }
   std::vector<uint8_t>().swap(b->b.host.ids);
+  std::vector<uint8_t>().swap(b->b.host.id_len);
   std::vector<uint64_t>().swap(b->b.host.start);
   std::vector<uint64_t>().swap(b->b.host.end);
+  std::vector<uint32_t>().swap(b->b.host.svc_vid);
+  std::vector<uint32_t>().swap(b->b.host.name_vid);
   *out = b;
 }
 
@@ -376,7 +379,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       m.kernel_ns = std::max<uint64_t>(m.kernel_ns, o.second.kernel_ns);
       m.scan_kernel_ns = std::max<uint64_t>(m.scan_kernel_ns, o.second.scan_ns);
       m.scan_bytes += o.second.scan_bytes;
-      for (auto &r : o.second.recs) per_block[r.block].push_back(&r);
+      for (auto &r : o.second.recs) per_block[r.block_il & 0xffffffu].push_back(&r);
     }
     // consume in caller block order (deterministic refinement of instance.Search)
     std::unordered_set<std::string> distinct;
@@ -393,9 +396,9 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       uint64_t stop_entry = UINT64_MAX;
       for (const SearchOut::Rec *r : per_block[i]) {
         std::string_view sv, nm;
-        if (h.svc_key >= 0 && h.svc_vid[r->entry] != kNone) sv = h.dict_value(h.svc_key, h.svc_vid[r->entry]);
-        if (h.name_key >= 0 && h.name_vid[r->entry] != kNone) nm = h.dict_value(h.name_key, h.name_vid[r->entry]);
-        res->push(r->id, h.id_len[r->entry], r->start, r->end, uint32_t(i), r->entry, sv.data(), sv.size(),
+        if (h.svc_key >= 0 && r->svc != kNone) sv = h.dict_value(h.svc_key, r->svc);
+        if (h.name_key >= 0 && r->name != kNone) nm = h.dict_value(h.name_key, r->name);
+        res->push(r->id, uint8_t(r->block_il >> 24), r->start, r->end, uint32_t(i), r->entry, sv.data(), sv.size(),
                   nm.data(), nm.size());
         if (limit) {
           distinct.insert(std::string(reinterpret_cast<const char *>(r->id), 16));

@@ -64,7 +64,8 @@ void ctx_shutdown(Ctx &c) {
 template <typename T>
 static T *dev_upload(DevBlock &b, const T *src, size_t count, hipStream_t s) {
   void *p = nullptr;
-  size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  // whole 16-byte words: kernels may read a dictionary's last bytes as a word
+  size_t bytes = std::max<size_t>((count * sizeof(T) + 15) / 16 * 16, 16);
   HIP_OK(hipMalloc(&p, bytes));
   b.allocs.push_back(p);
   b.bytes += bytes;
@@ -100,6 +101,13 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
   d.ids = dev_upload(d, h.ids.data(), n * 16, s);
   d.start_ns = dev_upload(d, h.start.data(), n, s);
   d.end_ns = dev_upload(d, h.end.data(), n, s);
+  std::vector<uint32_t> names(2 * n);
+  for (size_t i = 0; i < n; i++) {
+    names[2 * i] = h.svc_vid.empty() ? kNone : h.svc_vid[i];
+    names[2 * i + 1] = h.name_vid.empty() ? kNone : h.name_vid[i];
+  }
+  d.names = dev_upload(d, names.data(), 2 * n, s);
+  d.id_len = dev_upload(d, h.id_len.data(), n, s);
   // the staging vectors must outlive the async copies
   HIP_OK(hipStreamSynchronize(s));
   for (const KeyColumn &kc : h.keys) {
@@ -128,9 +136,40 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     if (!kc.identity) {
       k.set_off = dev_upload(d, kc.set_off.data(), kc.set_off.size(), s);
       k.set_vals = dev_upload(d, kc.set_vals.data(), kc.set_vals.size(), s);
+      k.nsetvals = uint32_t(kc.set_vals.size());
     }
     d.keys.push_back(k);
   }
+  // resident descriptor (one-launch search path)
+  std::vector<uint8_t> desc(sizeof(DevBlockDesc) + d.keys.size() * sizeof(DevKeyDesc));
+  auto *bd = reinterpret_cast<DevBlockDesc *>(desc.data());
+  bd->n = n;
+  bd->dur32 = d.dur32;
+  bd->dur64 = d.dur64;
+  bd->start_s = d.start_s;
+  bd->end_s = d.end_s;
+  bd->ids = d.ids;
+  bd->start_ns = d.start_ns;
+  bd->end_ns = d.end_ns;
+  bd->names = d.names;
+  bd->id_len = d.id_len;
+  bd->nkeys = uint32_t(d.keys.size());
+  auto *kd = reinterpret_cast<DevKeyDesc *>(bd + 1);
+  for (size_t i = 0; i < d.keys.size(); i++) {
+    const DevKey &k = d.keys[i];
+    kd[i].col = k.col;
+    kd[i].dict_bytes = k.dict_bytes;
+    kd[i].dict_off = k.dict_off;
+    kd[i].set_off = k.set_off;
+    kd[i].set_vals = k.set_vals;
+    kd[i].width = uint32_t(k.width);
+    kd[i].nvals = k.nvals;
+    kd[i].nsets = k.nsets;
+    kd[i].identity = k.identity ? 1u : 0u;
+    kd[i].dict_nbytes = uint32_t(std::min<uint64_t>(k.dict_nbytes, 0xffffffffu));
+    kd[i].nsetvals = k.nsetvals;
+  }
+  d.desc = reinterpret_cast<const DevBlockDesc *>(dev_upload(d, desc.data(), desc.size(), s));
   HIP_OK(hipStreamSynchronize(s));
 }
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -69,6 +70,7 @@ struct DeviceCtx {
   HostBuf hres{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};
   unsigned long long epoch = 0, ticket_base = 0;  // lookup launches
   uint32_t search_epoch = 0;
+  bool fast_off = std::getenv("TSG_NO_FAST") != nullptr;  // force the general (prep + search) path
   std::map<std::pair<const void *, size_t>, int> occupancy;  // (kernel, dynamic LDS) -> blocks per CU  // search launches: tag of the published workgroup counts
   size_t gran_tiles = 0;
 };

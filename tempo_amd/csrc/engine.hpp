@@ -13,6 +13,7 @@ namespace tsg {
 struct DevKey {
   std::string name;
   int width = 4;
+  uint32_t nsetvals = 0;
   void *col = nullptr;  // n entries of `width` bytes; all-ones = key absent
   uint8_t *dict_bytes = nullptr;
   uint32_t *dict_off = nullptr;
@@ -22,6 +23,28 @@ struct DevKey {
   bool identity = true;
   uint64_t dict_nbytes = 0;
 };
+
+// Resident descriptors (device memory, written once at upload): the one-launch
+// search path finds a block's columns and dictionaries through these.
+struct DevKeyDesc {  // 64 B
+  const void *col;
+  const uint8_t *dict_bytes;  // allocation padded to whole words
+  const uint32_t *dict_off, *set_off, *set_vals;
+  uint32_t width, nvals, nsets, identity;
+  uint32_t dict_nbytes, nsetvals;
+};
+struct DevBlockDesc {  // 128 B, followed by nkeys DevKeyDesc
+  uint64_t n;
+  const uint32_t *dur32;
+  const uint64_t *dur64;
+  const uint32_t *start_s, *end_s;
+  const uint8_t *ids;
+  const uint64_t *start_ns, *end_ns;
+  const uint32_t *names;  // per entry: {root.service.name value id, root.name value id}, ~0u = absent
+  const uint8_t *id_len;
+  uint32_t nkeys, pad[11];
+};
+static_assert(sizeof(DevKeyDesc) == 64 && sizeof(DevBlockDesc) == 128, "descriptor layout");
 
 // One backend search block resident in HBM (DESIGN.md "Data layout in HBM").
 struct DevBlock {
@@ -33,6 +56,9 @@ struct DevBlock {
   uint32_t *end_s = nullptr;   // uint32(end/1e9)
   uint8_t *ids = nullptr;      // n x 16, right aligned
   uint64_t *start_ns = nullptr, *end_ns = nullptr;
+  uint32_t *names = nullptr;   // n x {svc vid, name vid}: record fields resolved on the host
+  uint8_t *id_len = nullptr;
+  const DevBlockDesc *desc = nullptr;
   std::vector<DevKey> keys;
   uint64_t bytes = 0;
   std::vector<void *> allocs;
@@ -60,9 +86,9 @@ struct SearchOut {
   struct Rec {
     uint8_t id[16];
     uint64_t start, end;
-    uint64_t entry;
-    uint32_t block;
-    uint32_t pad;
+    uint32_t entry;
+    uint32_t block_il;  // block index | id length << 24
+    uint32_t svc, name; // value ids of root.service.name / root.name (~0u = absent)
   };
   std::vector<Rec> recs;  // ordered (before the limit cut across blocks)
   std::vector<uint64_t> block_counts;

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -54,6 +55,8 @@ struct ScanSeg {
   const uint32_t *start_s, *end_s;
   const uint8_t *ids;
   const uint64_t *start_ns, *end_ns;
+  const uint32_t *names;
+  const uint8_t *id_len;
   uint32_t first_tile, ntiles;  // global tile numbering
   uint32_t first_wg, nwg, tpw;  // workgroups owning this block, tiles per workgroup
   uint32_t term0, nterms, lds_words;
@@ -63,8 +66,9 @@ struct ScanSeg {
 struct MatchRec {  // == SearchOut::Rec
   uint8_t id[16];
   uint64_t start, end;
-  uint64_t entry;
-  uint32_t block, pad;
+  uint32_t entry;
+  uint32_t block_il;  // block index | id length << 24
+  uint32_t svc, name;
 };
 static_assert(sizeof(MatchRec) == 48, "record layout");
 static_assert(sizeof(MatchRec) == sizeof(SearchOut::Rec), "record layout");
@@ -413,32 +417,41 @@ constexpr uint32_t kMaxTpw = 1024;      // tiles per workgroup (per-tile counts 
 constexpr uint32_t kSpinMax = 1u << 22; // look-back poll bound (~seconds): never reached unless broken
 constexpr uint32_t kMaxSegs = 2048;
 
-template <int NT, bool DUR, bool RANGE, bool W1>
-__global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t *lds_bm = lds;                                              // [lds_bm_words]
-  uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + P.lds_bm_words);  // [kLdsTiles][kThreads]
-  uint32_t *lds_seg = lds + P.lds_bm_words + kLdsTiles * kThreads / 2;  // [nsegs]
+// workgroup -> block and per-block record caps, from the device descriptors
+struct DescSegs {
+  const uint16_t *wg_seg;
+  const ScanSeg *segs;
+  __device__ uint32_t seg_of(uint32_t i) const { return G(wg_seg)[i]; }
+  __device__ unsigned long long cap_of(uint32_t s) const { return segs[s].cap; }
+};
+// ... from LDS copies of the kernel-argument tables (one-launch path)
+struct ArgSegs {
+  const uint32_t *first_wg;  // nsegs + 1
+  const unsigned long long *cap;
+  uint32_t nsegs;
+  __device__ uint32_t seg_of(uint32_t i) const {
+    uint32_t lo = 0, hi = nsegs;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (first_wg[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  }
+  __device__ unsigned long long cap_of(uint32_t s) const { return cap[s]; }
+};
+
+// Phases 1-3 for one workgroup of block `si` (bitmaps already in LDS, lds_seg zeroed).
+template <int NT, bool DUR, bool RANGE, bool W1, class Segs>
+__device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S, const ScanTerm *T, uint32_t si,
+                                          const Segs &segs, const uint32_t *lds_bm, uint16_t *lds_mask,
+                                          uint32_t *lds_seg) {
   __shared__ uint16_t s_tc[kMaxTpw];
   __shared__ uint32_t s_wcnt[2][kThreads / 64];
   __shared__ unsigned long long s_red[kThreads / 64];
   __shared__ unsigned long long s_wsum[kThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint32_t wg = blockIdx.x;
-  const uint32_t si = P.wg_seg[wg];
-  const ScanSeg S = P.segs[si];
-  constexpr int NTA = NT > 0 ? NT : 1;
-  ScanTerm T[NTA];
-  if (NT > 0)
-#pragma unroll
-    for (int q = 0; q < NTA; q++) T[q] = P.terms[S.term0 + q];
-  for (uint32_t q = 0; q < S.nterms; q++) {  // stage the small bitmaps in LDS
-    const ScanTerm &Tq = P.terms[S.term0 + q];
-    if (Tq.lds_off != kNoLds)
-      for (uint32_t w = tid; w < Tq.bm_words; w += kThreads) lds_bm[Tq.lds_off + w] = Tq.bm[w];
-  }
-  for (uint32_t i = tid; i < P.nsegs; i += kThreads) lds_seg[i] = 0;
-  __syncthreads();
 
   // ---- phase 1: scan
   const uint32_t lt0 = (wg - S.first_wg) * S.tpw;
@@ -483,22 +496,21 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
       __builtin_amdgcn_s_sleep(8);
     }
     const uint32_t v = uint32_t(w);
-    if (per_seg) atomicAdd(&lds_seg[P.wg_seg[i]], v);
+    if (per_seg) atomicAdd(&lds_seg[segs.seg_of(i)], v);
     else loc += v;
   }
   unsigned long long *hdr = reinterpret_cast<unsigned long long *>(P.out);
   unsigned long long seg_rank0, base;  // rank of this workgroup's first match in its block; output slot of rank 0
   if (!per_seg) {
-    const unsigned long long excl = block_sum(loc, s_red);
     seg_rank0 = 0;  // unused in this mode
-    base = excl;
+    base = block_sum(loc, s_red);
   } else {
     __syncthreads();
     seg_rank0 = lds_seg[si];  // lower workgroups of the same block
     unsigned long long b = 0;
     for (uint32_t s2 = tid; s2 < si; s2 += kThreads) {
       const unsigned long long c = lds_seg[s2];
-      b += P.limit_mode ? umin64(c, P.segs[s2].cap) : c;
+      b += P.limit_mode ? umin64(c, segs.cap_of(s2)) : c;
     }
     base = block_sum(b, s_red);
     if (!P.limit_mode) base += seg_rank0;
@@ -508,7 +520,7 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
       __syncthreads();
       unsigned long long tot = 0;
       for (uint32_t s2 = tid; s2 < P.nsegs; s2 += kThreads) {
-        const unsigned long long c = P.limit_mode ? umin64(lds_seg[s2], P.segs[s2].cap) : lds_seg[s2];
+        const unsigned long long c = P.limit_mode ? umin64(lds_seg[s2], segs.cap_of(s2)) : lds_seg[s2];
         hdr[8 + s2] = c;
         tot += c;
       }
@@ -569,16 +581,208 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
         MatchRec *dst = out + slot;
         const u32x4 id = *G<u32x4>(S.ids + ei * 16);
         const uint64_t st = G(S.start_ns)[ei], en = G(S.end_ns)[ei];
+        const uint64_t nm = G(reinterpret_cast<const uint64_t *>(S.names))[ei];
+        const uint32_t il = G(S.id_len)[ei];
         *reinterpret_cast<u32x4 *>(dst->id) = id;
         dst->start = st;
         dst->end = en;
-        dst->entry = ei;
-        dst->block = S.block_idx;
-        dst->pad = 0;
+        dst->entry = uint32_t(ei);
+        dst->block_il = S.block_idx | (il << 24);
+        *reinterpret_cast<uint64_t *>(&dst->svc) = nm;
       }
     }
     run += tc;
   }
+}
+
+// General path: descriptors in device memory (copied by prep_kernel), value-set
+// bitmaps precomputed by prep/dict_sets.
+template <int NT, bool DUR, bool RANGE, bool W1>
+__global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t *lds_bm = lds;                                                   // [lds_bm_words]
+  uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + P.lds_bm_words);  // [kLdsTiles][kThreads]
+  uint32_t *lds_seg = lds + P.lds_bm_words + kLdsTiles * kThreads / 2;      // [nsegs]
+  const int tid = threadIdx.x;
+  const uint32_t si = P.wg_seg[blockIdx.x];
+  const ScanSeg S = P.segs[si];
+  constexpr int NTA = NT > 0 ? NT : 1;
+  ScanTerm T[NTA];
+  if (NT > 0)
+#pragma unroll
+    for (int q = 0; q < NTA; q++) T[q] = P.terms[S.term0 + q];
+  for (uint32_t q = 0; q < S.nterms; q++) {  // stage the small bitmaps in LDS
+    const ScanTerm &Tq = P.terms[S.term0 + q];
+    if (Tq.lds_off != kNoLds)
+      for (uint32_t w = tid; w < Tq.bm_words; w += kThreads) lds_bm[Tq.lds_off + w] = Tq.bm[w];
+  }
+  for (uint32_t i = tid; i < P.nsegs; i += kThreads) lds_seg[i] = 0;
+  __syncthreads();
+  scan_emit<NT, DUR, RANGE, W1>(P, S, T, si, DescSegs{P.wg_seg, P.segs}, lds_bm, lds_mask, lds_seg);
+}
+
+// ------------------------------------------------------------------------------------
+// one-launch path: the whole query travels in the kernel arguments, block columns
+// and dictionaries are found through the block's resident descriptor, and every
+// workgroup matches its block's (small) dictionaries itself, in LDS, before
+// scanning. Used when every dictionary of the query fits kFast* (the host decides).
+constexpr int kArgSegs = 32, kArgTerms = 8, kArgNeedle = 256;
+constexpr uint32_t kFastStageWords = 6144;  // 24 KiB: offsets + bytes + value bits + set CSR of all terms
+struct QArgs {
+  const DevBlockDesc *blk[kArgSegs];
+  unsigned long long cap[kArgSegs];  // records kept per block (limit mode)
+  uint32_t first_wg[kArgSegs + 1];
+  uint32_t first_tile[kArgSegs];
+  uint32_t block_idx[kArgSegs];
+  uint16_t key_of[kArgSegs][kArgTerms];
+  uint16_t nd_off[kArgTerms + 1];
+  uint8_t needles[kArgNeedle];
+  uint32_t nsegs, nterms, tpw, bm_words, stage_words;
+  ScanParams P;  // thresholds, outputs (segs/terms/wg_seg unused)
+};
+
+// LDS addresses: contains() runs over staged bytes; needles come from LDS too
+__device__ __forceinline__ bool lds_contains(const uint8_t *h, uint32_t hl, const uint8_t *nd, uint32_t nl) {
+  if (nl == 0) return true;  // bytes.Contains(x, "") (pitfall P7)
+  if (nl > hl) return false;
+  const uint8_t f = nd[0];
+  for (uint32_t i = 0; i + nl <= hl; i++) {
+    if (h[i] != f) continue;
+    uint32_t k = 1;
+    while (k < nl && h[i + k] == nd[k]) k++;
+    if (k == nl) return true;
+  }
+  return false;
+}
+
+template <int NT, bool DUR, bool RANGE, bool W1>
+__global__ void __launch_bounds__(kThreads) search_fast_kernel(QArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  // [bitmaps bm_words | stage (dictionaries, then kLdsTiles masks) | seg sums nsegs | first_wg nsegs+1 | caps]
+  const uint32_t stage_w = max(A.stage_words, kLdsTiles * kThreads / 2);
+  uint32_t *lds_bm = lds;
+  uint32_t *stage = lds + A.bm_words;
+  uint32_t *lds_seg = stage + stage_w;
+  uint32_t *lds_fw = lds_seg + A.nsegs;
+  unsigned long long *lds_cap = reinterpret_cast<unsigned long long *>(lds_fw + ((A.nsegs + 2) & ~1u));
+  __shared__ __attribute__((aligned(16))) uint8_t s_nd[kArgNeedle];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wg = blockIdx.x;
+  uint32_t si = 0;
+  for (uint32_t s2 = 1; s2 < A.nsegs; s2++)
+    if (A.first_wg[s2] <= wg) si = s2;
+  const DevBlockDesc *B = A.blk[si];
+  ScanSeg S;
+  S.n = B->n;
+  S.dur32 = B->dur32;
+  S.dur64 = B->dur64;
+  S.start_s = B->start_s;
+  S.end_s = B->end_s;
+  S.ids = B->ids;
+  S.start_ns = B->start_ns;
+  S.end_ns = B->end_ns;
+  S.names = B->names;
+  S.id_len = B->id_len;
+  S.first_tile = A.first_tile[si];
+  S.ntiles = uint32_t((S.n + kTile - 1) / kTile);
+  S.first_wg = A.first_wg[si];
+  S.nwg = A.first_wg[si + 1] - S.first_wg;
+  S.tpw = A.tpw;
+  S.term0 = 0;
+  S.nterms = A.nterms;
+  S.lds_words = A.bm_words;
+  S.block_idx = A.block_idx[si];
+  S.cap = A.cap[si];
+  for (uint32_t i = tid; i < A.nsegs; i += kThreads) {
+    lds_seg[i] = 0;
+    lds_fw[i] = A.first_wg[i];
+    lds_cap[i] = A.cap[i];
+  }
+  if (tid == 0) lds_fw[A.nsegs] = A.first_wg[A.nsegs];
+  for (uint32_t i = tid; i < A.nd_off[A.nterms]; i += kThreads) s_nd[i] = A.needles[i];
+
+  // ---- dictionaries: stage every term's offsets, bytes and set CSR in one round trip
+  constexpr int NTA = NT > 0 ? NT : 1;
+  ScanTerm T[NTA];
+  uint32_t so[NTA + 1];  // stage word offset per term
+  uint32_t bmo = 0;
+  so[0] = 0;
+#pragma unroll
+  for (int q = 0; q < NTA; q++) {
+    if (q >= int(A.nterms)) break;
+    const DevKeyDesc &K = reinterpret_cast<const DevKeyDesc *>(B + 1)[A.key_of[si][q]];
+    T[q].col = K.col;
+    T[q].bm = nullptr;
+    T[q].width = K.width;
+    T[q].nsets = K.nsets;
+    T[q].lds_off = bmo;
+    T[q].bm_words = (K.nsets + 31) / 32;
+    bmo += W1 ? 8u : T[q].bm_words;
+    // stage layout: off[nvals+1] | bytes (padded to words) | [vbits nvals/32 | set_off nsets+1 | set_vals]
+    uint32_t w = K.nvals + 1 + (K.dict_nbytes + 3) / 4;
+    if (!K.identity) w += (K.nvals + 31) / 32 + K.nsets + 1 + K.nsetvals;
+    so[q + 1] = so[q] + w;
+  }
+#pragma unroll
+  for (int q = 0; q < NTA; q++) {
+    if (q >= int(A.nterms)) break;
+    const DevKeyDesc &K = reinterpret_cast<const DevKeyDesc *>(B + 1)[A.key_of[si][q]];
+    uint32_t *st = stage + so[q];
+    for (uint32_t i = tid; i <= K.nvals; i += kThreads) st[i] = G(K.dict_off)[i];
+    uint32_t *by = st + K.nvals + 1;
+    for (uint32_t i = tid; i < (K.dict_nbytes + 3) / 4; i += kThreads)
+      by[i] = G(reinterpret_cast<const uint32_t *>(K.dict_bytes))[i];  // dict_bytes allocations are padded
+    if (!K.identity) {
+      uint32_t *so2 = by + (K.dict_nbytes + 3) / 4 + (K.nvals + 31) / 32;
+      for (uint32_t i = tid; i <= K.nsets; i += kThreads) so2[i] = G(K.set_off)[i];
+      for (uint32_t i = tid; i < K.nsetvals; i += kThreads) so2[K.nsets + 1 + i] = G(K.set_vals)[i];
+    }
+  }
+  __syncthreads();
+  // ---- match: value bits (ballots), then value-set bits
+#pragma unroll
+  for (int q = 0; q < NTA; q++) {
+    if (q >= int(A.nterms)) break;
+    const DevKeyDesc &K = reinterpret_cast<const DevKeyDesc *>(B + 1)[A.key_of[si][q]];
+    const uint32_t *off = stage + so[q];
+    const uint8_t *by = reinterpret_cast<const uint8_t *>(off + K.nvals + 1);
+    uint32_t *vbits = const_cast<uint32_t *>(off) + K.nvals + 1 + (K.dict_nbytes + 3) / 4;
+    uint32_t *bits = K.identity ? lds_bm + T[q].lds_off : vbits;
+    const uint8_t *nd = s_nd + A.nd_off[q];
+    const uint32_t nl = A.nd_off[q + 1] - A.nd_off[q];
+    for (uint32_t v0 = 0; v0 < K.nvals; v0 += kThreads) {
+      const uint32_t v = v0 + tid;
+      bool m = false;
+      if (v < K.nvals) m = lds_contains(by + off[v], off[v + 1] - off[v], nd, nl);
+      const unsigned long long b = __ballot(m);
+      const uint32_t w0 = (v - lane) >> 5;
+      if (lane == 0 && w0 * 32 < K.nvals) bits[w0] = uint32_t(b);
+      if (lane == 32 && (w0 + 1) * 32 < K.nvals) bits[w0 + 1] = uint32_t(b >> 32);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NTA; q++) {
+    if (q >= int(A.nterms)) break;
+    const DevKeyDesc &K = reinterpret_cast<const DevKeyDesc *>(B + 1)[A.key_of[si][q]];
+    if (K.identity) continue;
+    const uint32_t *vbits = stage + so[q] + K.nvals + 1 + (K.dict_nbytes + 3) / 4;
+    const uint32_t *soff = vbits + (K.nvals + 31) / 32;
+    const uint32_t *svals = soff + K.nsets + 1;
+    for (uint32_t s0 = 0; s0 < K.nsets; s0 += kThreads) {
+      const uint32_t sid = s0 + tid;
+      bool m = false;
+      if (sid < K.nsets)
+        for (uint32_t i = soff[sid]; i < soff[sid + 1] && !m; i++) m = (vbits[svals[i] >> 5] >> (svals[i] & 31)) & 1u;
+      const unsigned long long b = __ballot(m);
+      const uint32_t w0 = (sid - lane) >> 5;
+      if (lane == 0 && w0 * 32 < K.nsets) lds_bm[T[q].lds_off + w0] = uint32_t(b);
+      if (lane == 32 && (w0 + 1) * 32 < K.nsets) lds_bm[T[q].lds_off + w0 + 1] = uint32_t(b >> 32);
+    }
+  }
+  __syncthreads();  // the stage region is reused for the tile masks from here on
+  scan_emit<NT, DUR, RANGE, W1>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, A.nsegs}, lds_bm,
+                                reinterpret_cast<uint16_t *>(stage), lds_seg);
 }
 
 // ------------------------------------------------------------------------------------
@@ -586,6 +790,23 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 using ScanFn = void (*)(ScanParams);
+using FastFn = void (*)(QArgs);
+template <int NT, bool W1>
+static FastFn pick3_fast(bool dur, bool range) {
+  if (dur && range) return search_fast_kernel<NT, true, true, W1>;
+  if (dur) return search_fast_kernel<NT, true, false, W1>;
+  if (range) return search_fast_kernel<NT, false, true, W1>;
+  return search_fast_kernel<NT, false, false, W1>;
+}
+static FastFn pick_fast(uint32_t nterms, bool dur, bool range, bool w1) {
+  switch (nterms) {
+    case 0: return pick3_fast<0, false>(dur, range);
+    case 1: return w1 ? pick3_fast<1, true>(dur, range) : pick3_fast<1, false>(dur, range);
+    case 2: return w1 ? pick3_fast<2, true>(dur, range) : pick3_fast<2, false>(dur, range);
+    case 3: return w1 ? pick3_fast<3, true>(dur, range) : pick3_fast<3, false>(dur, range);
+    default: return w1 ? pick3_fast<4, true>(dur, range) : pick3_fast<4, false>(dur, range);
+  }
+}
 template <int NT, bool W1>
 static ScanFn pick3(bool dur, bool range) {
   if (dur && range) return search_kernel<NT, true, true, W1>;
@@ -654,6 +875,11 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   uint64_t dict_bytes = 0, scan_bytes = 0, n_all = 0;
   bool all_w1 = true;
   constexpr uint32_t kLdsBudgetWords = 8192;  // 32 KiB per workgroup
+  // one-launch path bookkeeping: per block key indices and LDS words its
+  // workgroups need to match the dictionaries themselves
+  std::vector<std::array<uint16_t, kArgTerms>> seg_keys;
+  std::vector<const DevBlockDesc *> seg_desc;
+  uint32_t fast_stage = 0, fast_bm = 0, fast_bm8 = 0;
   for (auto &bp : blocks) {
     Block &b = *bp.second;
     const DevBlock &d = b.dev;
@@ -675,6 +901,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     sg.ids = d.ids;
     sg.start_ns = d.start_ns;
     sg.end_ns = d.end_ns;
+    sg.names = d.names;
+    sg.id_len = d.id_len;
     sg.block_idx = bp.first;
     sg.term0 = uint32_t(terms.size());
     sg.nterms = q.nterms;
@@ -722,6 +950,25 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       all_w1 = all_w1 && k.width == 1 && st.lds_off != kNoLds;
     }
     max_lds_words = std::max(max_lds_words, sg.lds_words);
+    {
+      std::array<uint16_t, kArgTerms> ks{};
+      uint32_t stage = 0, bmw = 0, bmw8 = 0;
+      for (uint32_t t = 0; t < q.nterms && t < kArgTerms; t++) {
+        const DevKey &k = d.keys[size_t(kidx[t])];
+        ks[t] = uint16_t(kidx[t]);
+        stage += k.nvals + 1 + uint32_t((k.dict_nbytes + 3) / 4);
+        if (!k.identity) stage += (k.nvals + 31) / 32 + k.nsets + 1 + k.nsetvals;
+        if (k.dict_nbytes > (1u << 20) || k.nvals > (1u << 20)) stage = 0xfffffffu;
+        bmw += (k.nsets + 31) / 32;
+        bmw8 += k.width == 1 ? 8u : (k.nsets + 31) / 32;
+      }
+      if (kidx.size() && std::any_of(kidx.begin(), kidx.end(), [](int x) { return x > 0xffff; })) stage = 0xfffffffu;
+      seg_keys.push_back(ks);
+      seg_desc.push_back(d.desc);
+      fast_stage = std::max(fast_stage, stage);
+      fast_bm = std::max(fast_bm, bmw);
+      fast_bm8 = std::max(fast_bm8, bmw8);
+    }
     sg.first_tile = tiles;
     sg.ntiles = uint32_t((d.n + kTile - 1) / kTile);
     tiles += sg.ntiles;
@@ -736,15 +983,24 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   out.kernel_ns = out.scan_ns = 0;
   out.scan_bytes = scan_bytes;
   if (segs.empty()) return;
+  if (segs.size() > kMaxSegs) fail(TSG_E_UNSUPPORTED, "too many blocks per device in one search (max 2048)");
+  const uint32_t nsegs = uint32_t(segs.size());
+  // one launch when the whole query fits the kernel arguments and every block's
+  // dictionaries for it can be matched in LDS by the scanning workgroups
+  const bool fast = !dc.fast_off && nsegs <= uint32_t(kArgSegs) && q.nterms <= 4 && needles.size() <= size_t(kArgNeedle) &&
+                    fast_stage <= kFastStageWords;
   // workgroups: about one resident wave of them (occupancy x CUs), each owning a
   // contiguous tile range of one block
-  const ScanFn scan_fn = pick_scan(q.nterms, has_dur, q.has_range, all_w1);
-  if (segs.size() > kMaxSegs) fail(TSG_E_UNSUPPORTED, "too many blocks per device in one search (max 2048)");
-  const uint32_t lds_words = max_lds_words + kLdsTiles * kThreads / 2 + uint32_t(segs.size());
-  int &per_cu = dc.occupancy[{reinterpret_cast<const void *>(scan_fn), size_t(lds_words) * 4}];
+  const ScanFn scan_fn = fast ? nullptr : pick_scan(q.nterms, has_dur, q.has_range, all_w1);
+  const FastFn fast_fn = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1) : nullptr;
+  const void *kfn = fast ? reinterpret_cast<const void *>(fast_fn) : reinterpret_cast<const void *>(scan_fn);
+  const uint32_t fast_bm_words = align_up(all_w1 ? fast_bm8 : fast_bm, 2);
+  const uint32_t fast_stage_words = std::max<uint32_t>(align_up(fast_stage, 2), kLdsTiles * kThreads / 2);
+  const uint32_t lds_words = fast ? fast_bm_words + fast_stage_words + nsegs + ((nsegs + 2) & ~1u) + 2 * nsegs
+                                  : max_lds_words + kLdsTiles * kThreads / 2 + nsegs;
+  int &per_cu = dc.occupancy[{kfn, size_t(lds_words) * 4}];
   if (per_cu == 0) {
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(scan_fn), kThreads,
-                                                         size_t(lds_words) * 4));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kThreads, size_t(lds_words) * 4));
     per_cu = std::max(1, std::min(per_cu, 8));
   }
   const uint32_t target_wg = uint32_t(dc.num_cu) * uint32_t(per_cu);
@@ -761,8 +1017,6 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   tr.mark("plan");
 
   // ---- scratch
-  dc.bitmaps.ensure(std::max<size_t>(bm_total, 1) * 4);
-  dc.vmatch.ensure(std::max<size_t>(vmatch_total, 1));
   if (tpw > kLdsTiles) dc.maskbits.ensure(size_t(tiles) * kThreads * 2);
   if (dc.agg.ensure(size_t(nwg) * 8)) HIP_OK(hipMemsetAsync(dc.agg.p, 0, dc.agg.cap, s));  // no stale epochs
   const size_t hdr_bytes = align_up(64 + 8 * segs.size(), 256);
@@ -778,58 +1032,10 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // [header | records] go straight to pinned host memory (no D2H copy, no copy kernel)
   dc.hres.ensure(hdr_bytes + std::max<size_t>(out_cap, 1) * sizeof(MatchRec));
   uint8_t *ho = static_cast<uint8_t *>(dc.hres.p);
-  for (size_t i = 0; i < terms.size(); i++)
-    terms[i].bm = static_cast<const uint32_t *>(dc.bitmaps.p) + term_bm_base[i];
-
-  // ---- descriptors: written to pinned host memory; the prep kernel copies them
-  // into device memory (small descriptor sets) or one H2D copy (large ones)
-  const size_t o_segs = 0, o_terms = align_up(segs.size() * sizeof(ScanSeg), 16);
-  const size_t o_jobs = align_up(o_terms + terms.size() * sizeof(ScanTerm), 16);
-  const size_t o_jb = align_up(o_jobs + jobs.size() * sizeof(DictJob), 16);
-  const size_t o_sj = align_up(o_jb + jobs.size() * 4, 16);
-  const size_t o_sp = align_up(o_sj + set_jobs.size() * 4, 16);
-  const size_t o_nd = align_up(o_sp + set_items.size() * 4, 16);
-  const size_t o_ws = align_up(o_nd + needles.size() + 1, 16);
-  const size_t total_desc = align_up(o_ws + size_t(nwg) * 2, 16);
-  dc.hdesc.ensure(total_desc);
-  dc.desc.ensure(total_desc);
-  auto *hd = static_cast<uint8_t *>(dc.hdesc.p);
-  std::memcpy(hd + o_segs, segs.data(), segs.size() * sizeof(ScanSeg));
-  std::memcpy(hd + o_terms, terms.data(), terms.size() * sizeof(ScanTerm));
-  std::memcpy(hd + o_jobs, jobs.data(), jobs.size() * sizeof(DictJob));
-  auto *jbase = reinterpret_cast<uint32_t *>(hd + o_jb);
-  for (size_t i = 0; i < jobs.size(); i++) jbase[i] = jobs[i].item_base;
-  if (!set_jobs.empty()) std::memcpy(hd + o_sj, set_jobs.data(), set_jobs.size() * 4);
-  std::memcpy(hd + o_sp, set_items.data(), set_items.size() * 4);
-  if (!needles.empty()) std::memcpy(hd + o_nd, needles.data(), needles.size());
-  auto *ws = reinterpret_cast<uint16_t *>(hd + o_ws);
-  for (size_t i = 0; i < segs.size(); i++)
-    for (uint32_t w = 0; w < segs[i].nwg; w++) ws[segs[i].first_wg + w] = uint16_t(i);
-  auto *dd = static_cast<uint8_t *>(dc.desc.p);
-  const uint8_t *src = hd;
-  if (total_desc > kHostDescMax) {
-    HIP_OK(hipMemcpyAsync(dd, hd, total_desc, hipMemcpyHostToDevice, s));
-    src = dd;
-  }
-  tr.mark("desc");
-
   const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
-  if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
-  prep_kernel<<<std::max<uint32_t>(1, (items + 255) / 256), 256, 0, s>>>(
-      src, dd, uint32_t(total_desc / 16), uint32_t(o_jobs), uint32_t(o_jb), uint32_t(jobs.size()), items,
-      uint32_t(o_nd), uint32_t(needles.size()), static_cast<uint8_t *>(dc.vmatch.p),
-      static_cast<uint32_t *>(dc.bitmaps.p));
-  if (set_items.back())
-    dict_sets_kernel<<<(set_items.back() + 255) / 256, 256, 0, s>>>(
-        reinterpret_cast<const DictJob *>(dd + o_jobs), reinterpret_cast<const uint32_t *>(dd + o_sj),
-        reinterpret_cast<const uint32_t *>(dd + o_sp), uint32_t(set_jobs.size()), set_items.back(),
-        static_cast<const uint8_t *>(dc.vmatch.p), static_cast<uint32_t *>(dc.bitmaps.p));
-  tr.mark("dict");
+
   ScanParams P{};
-  P.segs = reinterpret_cast<const ScanSeg *>(dd + o_segs);
-  P.terms = reinterpret_cast<const ScanTerm *>(dd + o_terms);
-  P.wg_seg = reinterpret_cast<const uint16_t *>(dd + o_ws);
-  P.nsegs = uint32_t(segs.size());
+  P.nsegs = nsegs;
   P.nwg = nwg;
   P.has_min = q.has_min;
   P.has_max = q.has_max;
@@ -845,6 +1051,78 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   P.out = ho;
   P.hdr_bytes = hdr_bytes;
   P.out_cap = out_cap;
+  QArgs A;
+  if (fast) {
+    std::memset(&A, 0, sizeof A);
+    for (uint32_t i = 0; i < nsegs; i++) {
+      A.blk[i] = seg_desc[i];
+      A.cap[i] = segs[i].cap;
+      A.first_wg[i] = segs[i].first_wg;
+      A.first_tile[i] = segs[i].first_tile;
+      A.block_idx[i] = segs[i].block_idx;
+      for (int t = 0; t < kArgTerms; t++) A.key_of[i][t] = seg_keys[i][size_t(t)];
+    }
+    A.first_wg[nsegs] = nwg;
+    for (uint32_t t = 0; t <= q.nterms; t++) A.nd_off[t] = uint16_t(t < q.nterms ? needle_off[t] : needles.size());
+    if (!needles.empty()) std::memcpy(A.needles, needles.data(), needles.size());
+    A.nsegs = nsegs;
+    A.nterms = q.nterms;
+    A.tpw = tpw;
+    A.bm_words = fast_bm_words;
+    A.stage_words = fast_stage_words;
+    tr.mark("desc");
+    if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
+  } else {
+    dc.bitmaps.ensure(std::max<size_t>(bm_total, 1) * 4);
+    dc.vmatch.ensure(std::max<size_t>(vmatch_total, 1));
+    for (size_t i = 0; i < terms.size(); i++)
+      terms[i].bm = static_cast<const uint32_t *>(dc.bitmaps.p) + term_bm_base[i];
+    // ---- descriptors: written to pinned host memory; the prep kernel copies them
+    // into device memory (small descriptor sets) or one H2D copy (large ones)
+    const size_t o_segs = 0, o_terms = align_up(segs.size() * sizeof(ScanSeg), 16);
+    const size_t o_jobs = align_up(o_terms + terms.size() * sizeof(ScanTerm), 16);
+    const size_t o_jb = align_up(o_jobs + jobs.size() * sizeof(DictJob), 16);
+    const size_t o_sj = align_up(o_jb + jobs.size() * 4, 16);
+    const size_t o_sp = align_up(o_sj + set_jobs.size() * 4, 16);
+    const size_t o_nd = align_up(o_sp + set_items.size() * 4, 16);
+    const size_t o_ws = align_up(o_nd + needles.size() + 1, 16);
+    const size_t total_desc = align_up(o_ws + size_t(nwg) * 2, 16);
+    dc.hdesc.ensure(total_desc);
+    dc.desc.ensure(total_desc);
+    auto *hd = static_cast<uint8_t *>(dc.hdesc.p);
+    std::memcpy(hd + o_segs, segs.data(), segs.size() * sizeof(ScanSeg));
+    std::memcpy(hd + o_terms, terms.data(), terms.size() * sizeof(ScanTerm));
+    std::memcpy(hd + o_jobs, jobs.data(), jobs.size() * sizeof(DictJob));
+    auto *jbase = reinterpret_cast<uint32_t *>(hd + o_jb);
+    for (size_t i = 0; i < jobs.size(); i++) jbase[i] = jobs[i].item_base;
+    if (!set_jobs.empty()) std::memcpy(hd + o_sj, set_jobs.data(), set_jobs.size() * 4);
+    std::memcpy(hd + o_sp, set_items.data(), set_items.size() * 4);
+    if (!needles.empty()) std::memcpy(hd + o_nd, needles.data(), needles.size());
+    auto *ws = reinterpret_cast<uint16_t *>(hd + o_ws);
+    for (size_t i = 0; i < segs.size(); i++)
+      for (uint32_t w = 0; w < segs[i].nwg; w++) ws[segs[i].first_wg + w] = uint16_t(i);
+    auto *dd = static_cast<uint8_t *>(dc.desc.p);
+    const uint8_t *src = hd;
+    if (total_desc > kHostDescMax) {
+      HIP_OK(hipMemcpyAsync(dd, hd, total_desc, hipMemcpyHostToDevice, s));
+      src = dd;
+    }
+    tr.mark("desc");
+    if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
+    prep_kernel<<<std::max<uint32_t>(1, (items + 255) / 256), 256, 0, s>>>(
+        src, dd, uint32_t(total_desc / 16), uint32_t(o_jobs), uint32_t(o_jb), uint32_t(jobs.size()), items,
+        uint32_t(o_nd), uint32_t(needles.size()), static_cast<uint8_t *>(dc.vmatch.p),
+        static_cast<uint32_t *>(dc.bitmaps.p));
+    if (set_items.back())
+      dict_sets_kernel<<<(set_items.back() + 255) / 256, 256, 0, s>>>(
+          reinterpret_cast<const DictJob *>(dd + o_jobs), reinterpret_cast<const uint32_t *>(dd + o_sj),
+          reinterpret_cast<const uint32_t *>(dd + o_sp), uint32_t(set_jobs.size()), set_items.back(),
+          static_cast<const uint8_t *>(dc.vmatch.p), static_cast<uint32_t *>(dc.bitmaps.p));
+    P.segs = reinterpret_cast<const ScanSeg *>(dd + o_segs);
+    P.terms = reinterpret_cast<const ScanTerm *>(dd + o_terms);
+    P.wg_seg = reinterpret_cast<const uint16_t *>(dd + o_ws);
+    tr.mark("dict");
+  }
   auto launch = [&](bool timed) {
     if (++dc.search_epoch == 0) dc.search_epoch = 1;  // 0 is the never-published tag of a fresh buffer
     P.epoch = dc.search_epoch;
@@ -852,7 +1130,12 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     h[0] = 0;
     h[1] = 0;  // look-back error flag
     if (timed) HIP_OK(hipEventRecord(dc.es0, s));
-    scan_fn<<<nwg, kThreads, size_t(lds_words) * 4, s>>>(P);
+    if (fast) {
+      A.P = P;
+      fast_fn<<<nwg, kThreads, size_t(lds_words) * 4, s>>>(A);
+    } else {
+      scan_fn<<<nwg, kThreads, size_t(lds_words) * 4, s>>>(P);
+    }
     HIP_OK(hipGetLastError());
     if (timed) HIP_OK(hipEventRecord(dc.es1, s));
   };

@@ -250,3 +250,16 @@ def test_timing_flags(engine, tmp_path):
         assert m1.scan_bytes == m2.scan_bytes > 0
     finally:
         b.close()
+
+
+def test_many_blocks_general_path(engine, tmp_path):
+    """More blocks than the one-launch path's kernel arguments carry (32): the
+    descriptor path runs, with the same results."""
+    rng = random.Random(42)
+    paths = [write_block(str(tmp_path), f"b{i}", random_entries(rng, 150)) for i in range(40)]
+    for q in [dict(tags={"k1": "v1"}), dict(tags={"k2": "v3-x", "root.service.name": "svc"}, min_ms=1),
+              dict(min_ms=3, max_ms=5000)]:
+        got, met, exp, omet = both(engine, paths, **q)
+        assert_parity(got, met, exp, omet)
+    got, met, exp, omet = both(engine, paths, tags={"k1": "v"}, limit=7)
+    assert_parity(got, met, exp, omet)

@@ -11,6 +11,10 @@ if has test; then
   timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
   ok_rc $rc || exit $rc
+  # the general (prep kernel + descriptor) search path, forced
+  TSG_NO_FAST=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_nofast.log 2>&1
+  rc=$?; echo "pytest gpu (TSG_NO_FAST) rc=$rc"; tail -5 gpurun_out/pytest_gpu_nofast.log
+  ok_rc $rc || exit $rc
 fi
 if has trace; then
   TSG_TRACE=1 timeout -k 10 600 python bench.py --steps 10 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/trace.json 2> gpurun_out/trace.err
