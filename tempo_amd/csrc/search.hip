@@ -86,6 +86,7 @@ struct ScanParams {
   uint32_t epoch;            // this launch's tag (never 0)
   uint32_t lds_bm_words;     // dynamic LDS: [bitmaps | kLdsTiles masks | per-block sums]
   uint8_t *out;              // pinned host: [header | records]; header[0] total, [1] error, [8+s] per block
+  unsigned long long *stamps;  // TSG_STAMPS: per workgroup s_memrealtime at phase boundaries (else null)
   uint64_t hdr_bytes, out_cap;
 };
 
@@ -445,13 +446,18 @@ struct ArgSegs {
 template <int NT, bool DUR, bool RANGE, bool W1, class Segs>
 __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S, const ScanTerm *T, uint32_t si,
                                           const Segs &segs, const uint32_t *lds_bm, uint16_t *lds_mask,
-                                          uint32_t *lds_seg) {
+                                          uint32_t *lds_seg, unsigned long long t_start) {
   __shared__ uint16_t s_tc[kMaxTpw];
   __shared__ uint32_t s_wcnt[2][kThreads / 64];
   __shared__ unsigned long long s_red[kThreads / 64];
   __shared__ unsigned long long s_wsum[kThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint32_t wg = blockIdx.x;
+  auto stamp = [&](int k) {
+    if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * 5 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * 5] = t_start;
+  stamp(1);
 
   // ---- phase 1: scan
   const uint32_t lt0 = (wg - S.first_wg) * S.tpw;
@@ -478,10 +484,15 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
   }
 
   // ---- phase 2: publish, look back
+  stamp(2);
   const unsigned long long tag = (unsigned long long)P.epoch << 32;
   if (tid == 0) __hip_atomic_store(&P.agg[wg], tag | wsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool last = wg + 1 == P.nwg;
-  if (wsum == 0 && !last) return;
+  if (wsum == 0 && !last) {
+    stamp(3);
+    stamp(4);
+    return;
+  }
   const bool per_seg = P.limit_mode || last;
   unsigned long long loc = 0;
   for (uint32_t i = tid; i < wg; i += kThreads) {
@@ -528,8 +539,11 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
       if (tid == 0) hdr[0] = tot;
     }
   }
-  if (wsum == 0) return;
-  if (P.limit_mode && seg_rank0 >= S.cap) return;  // the block's first `cap` matches precede this workgroup
+  stamp(3);
+  if (wsum == 0 || (P.limit_mode && seg_rank0 >= S.cap)) {  // (the block's first `cap` matches precede us)
+    stamp(4);
+    return;
+  }
 
   // ---- phase 3: emit in scan order
   MatchRec *out = reinterpret_cast<MatchRec *>(P.out + P.hdr_bytes);
@@ -593,12 +607,14 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
     }
     run += tc;
   }
+  stamp(4);
 }
 
 // General path: descriptors in device memory (copied by prep_kernel), value-set
 // bitmaps precomputed by prep/dict_sets.
 template <int NT, bool DUR, bool RANGE, bool W1>
 __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
+  const unsigned long long t_start = P.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t *lds_bm = lds;                                                   // [lds_bm_words]
   uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + P.lds_bm_words);  // [kLdsTiles][kThreads]
@@ -618,7 +634,7 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
   }
   for (uint32_t i = tid; i < P.nsegs; i += kThreads) lds_seg[i] = 0;
   __syncthreads();
-  scan_emit<NT, DUR, RANGE, W1>(P, S, T, si, DescSegs{P.wg_seg, P.segs}, lds_bm, lds_mask, lds_seg);
+  scan_emit<NT, DUR, RANGE, W1>(P, S, T, si, DescSegs{P.wg_seg, P.segs}, lds_bm, lds_mask, lds_seg, t_start);
 }
 
 // ------------------------------------------------------------------------------------
@@ -657,6 +673,7 @@ __device__ __forceinline__ bool lds_contains(const uint8_t *h, uint32_t hl, cons
 
 template <int NT, bool DUR, bool RANGE, bool W1>
 __global__ void __launch_bounds__(kThreads) search_fast_kernel(QArgs A) {
+  const unsigned long long t_start = A.P.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   // [bitmaps bm_words | stage (dictionaries, then kLdsTiles masks) | seg sums nsegs | first_wg nsegs+1 | caps]
   const uint32_t stage_w = max(A.stage_words, kLdsTiles * kThreads / 2);
@@ -782,7 +799,7 @@ __global__ void __launch_bounds__(kThreads) search_fast_kernel(QArgs A) {
   }
   __syncthreads();  // the stage region is reused for the tile masks from here on
   scan_emit<NT, DUR, RANGE, W1>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, A.nsegs}, lds_bm,
-                                reinterpret_cast<uint16_t *>(stage), lds_seg);
+                                reinterpret_cast<uint16_t *>(stage), lds_seg, t_start);
 }
 
 // ------------------------------------------------------------------------------------
@@ -846,6 +863,26 @@ struct Tracer {
                                 std::chrono::duration<double, std::micro>(last - t0).count());
   }
 };
+
+// TSG_STAMPS: where a launch's time goes (us from the first workgroup start; 100 MHz clock)
+static void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast) {
+  std::vector<unsigned long long> st(size_t(nwg) * 5);
+  HIP_OK(hipMemcpy(st.data(), dc.stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
+  unsigned long long t0 = ~0ull;
+  for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, st[size_t(w) * 5]);
+  const char *names[5] = {"start", "setup", "scan", "lookback", "end"};
+  std::fprintf(stderr, "[tsg] stamps (%s, %u wg) us avg/max:", fast ? "one-launch" : "general", nwg);
+  for (int k = 0; k < 5; k++) {
+    double sum = 0, mx = 0;
+    for (uint32_t w = 0; w < nwg; w++) {
+      const double v = double(st[size_t(w) * 5 + k] - t0) / 100.0;
+      sum += v;
+      mx = std::max(mx, v);
+    }
+    std::fprintf(stderr, " %s=%.1f/%.1f", names[k], sum / nwg, mx);
+  }
+  std::fprintf(stderr, "\n");
+}
 
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
                    uint32_t limit, uint32_t flags, SearchOut &out) {
@@ -1051,6 +1088,12 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   P.out = ho;
   P.hdr_bytes = hdr_bytes;
   P.out_cap = out_cap;
+  static const bool want_stamps = std::getenv("TSG_STAMPS") != nullptr;
+  if (want_stamps) {
+    dc.stamps.ensure(size_t(nwg) * 5 * 8);
+    HIP_OK(hipMemsetAsync(dc.stamps.p, 0, size_t(nwg) * 5 * 8, s));
+    P.stamps = static_cast<unsigned long long *>(dc.stamps.p);
+  }
   QArgs A;
   if (fast) {
     std::memset(&A, 0, sizeof A);
@@ -1149,6 +1192,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       fail(TSG_E_DEVICE, "search look-back did not complete (workgroup dispatch order assumption broken)");
   };
   check();
+  if (want_stamps) print_stamps(dc, nwg, fast);
   uint64_t total = *reinterpret_cast<volatile uint64_t *>(ho);
   float ms = 0, sms = 0;
   if (time_all) HIP_OK(hipEventElapsedTime(&ms, dc.ev0, dc.ev1));

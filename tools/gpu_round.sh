@@ -24,6 +24,13 @@ if has trace; then
   rc=$?; echo "noevents rc=$rc"; cat gpurun_out/noevents.json
   [ $rc -eq 0 ] || exit $rc
 fi
+if has stamps; then
+  TSG_STAMPS=1 TSG_TRACE=1 timeout -k 10 600 python bench.py --steps 5 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/stamps.json 2> gpurun_out/stamps.err
+  rc=$?; echo "stamps rc=$rc"; grep "stamps" gpurun_out/stamps.err | tail -3
+  TSG_NO_FAST=1 TSG_STAMPS=1 TSG_TRACE=1 timeout -k 10 600 python bench.py --steps 5 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/stamps_nofast.json 2> gpurun_out/stamps_nofast.err
+  rc=$?; echo "stamps nofast rc=$rc"; grep "stamps\|tsg_search\|device_search" gpurun_out/stamps_nofast.err | tail -4
+  [ $rc -eq 0 ] || exit $rc
+fi
 if has bench; then
   timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
   rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.err; cat gpurun_out/bench.json
