@@ -46,7 +46,7 @@ void ctx_shutdown(Ctx &c) {
     (void)hipSetDevice(dc->ordinal);
     (void)hipStreamSynchronize(dc->stream);
     for (DevBuf *b : {&dc->desc, &dc->vmatch, &dc->bitmaps, &dc->gran, &dc->ticket, &dc->out, &dc->regions,
-                      &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps})
+                      &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps, &dc->gbm})
       b->release();
     dc->hdesc.release();
     dc->hout.release();

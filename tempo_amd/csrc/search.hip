@@ -58,7 +58,7 @@ struct ScanSeg {
   const uint32_t *names;
   const uint8_t *id_len;
   uint32_t first_tile, ntiles;  // global tile numbering
-  uint32_t first_wg, nwg, tpw;  // workgroups owning this block, tiles per workgroup
+  uint32_t first_wg, nwg, tpw;  // workgroups owning this block (tiles split evenly), max tiles per workgroup
   uint32_t term0, nterms, lds_words;
   uint32_t block_idx, pad;
   uint64_t cap;  // limit mode: records kept from this block
@@ -446,13 +446,12 @@ struct ArgSegs {
 template <int NT, bool DUR, bool RANGE, bool W1, class Segs>
 __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S, const ScanTerm *T, uint32_t si,
                                           const Segs &segs, const uint32_t *lds_bm, uint16_t *lds_mask,
-                                          uint32_t *lds_seg, unsigned long long t_start) {
+                                          uint32_t *lds_seg, unsigned long long t_start, uint32_t wg) {
   __shared__ uint16_t s_tc[kMaxTpw];
   __shared__ uint32_t s_wcnt[2][kThreads / 64];
   __shared__ unsigned long long s_red[kThreads / 64];
   __shared__ unsigned long long s_wsum[kThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint32_t wg = blockIdx.x;
   auto stamp = [&](int k) {
     if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * 5 + k] = __builtin_amdgcn_s_memrealtime();
   };
@@ -460,8 +459,9 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
   stamp(1);
 
   // ---- phase 1: scan
-  const uint32_t lt0 = (wg - S.first_wg) * S.tpw;
-  const uint32_t ntl = min(lt0 + S.tpw, S.ntiles) - lt0;
+  const uint32_t lw = wg - S.first_wg;  // tiles split evenly over the block's workgroups
+  const uint32_t lt0 = uint32_t(uint64_t(lw) * S.ntiles / S.nwg);
+  const uint32_t ntl = uint32_t(uint64_t(lw + 1) * S.ntiles / S.nwg) - lt0;
   uint32_t wsum = 0;
   for (uint32_t t = 0; t < ntl; t++) {
     const uint32_t lt = lt0 + t;
@@ -634,30 +634,37 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
   }
   for (uint32_t i = tid; i < P.nsegs; i += kThreads) lds_seg[i] = 0;
   __syncthreads();
-  scan_emit<NT, DUR, RANGE, W1>(P, S, T, si, DescSegs{P.wg_seg, P.segs}, lds_bm, lds_mask, lds_seg, t_start);
+  scan_emit<NT, DUR, RANGE, W1>(P, S, T, si, DescSegs{P.wg_seg, P.segs}, lds_bm, lds_mask, lds_seg, t_start,
+                                blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------
-// one-launch path: the whole query travels in the kernel arguments, block columns
-// and dictionaries are found through the block's resident descriptor, and every
-// workgroup matches its block's (small) dictionaries itself, in LDS, before
-// scanning. Used when every dictionary of the query fits kFast* (the host decides).
+// one-launch path: the whole query travels in the kernel arguments and block
+// columns / dictionaries are found through the blocks' resident descriptors.
+// The grid's first njobs workgroups are dictionary workgroups, one per (block,
+// term): each stages that dictionary in LDS, matches every value against the
+// needle and publishes the value-set bitmap as 8-byte {epoch, word} granules
+// (agent-scope stores: untorn, no fences needed). The scan workgroups behind them
+// poll the granules of their block's terms, then scan. Dispatch is in index
+// order, so the producers are resident or done; polls are bounded.
 constexpr int kArgSegs = 32, kArgTerms = 8, kArgNeedle = 256;
-constexpr uint32_t kFastStageWords = 6144;  // 24 KiB: offsets + bytes + value bits + set CSR of all terms
+constexpr uint32_t kFastStageWords = 6144;  // 24 KiB: one dictionary's offsets + bytes + value bits + set CSR
 struct QArgs {
   const DevBlockDesc *blk[kArgSegs];
   unsigned long long cap[kArgSegs];  // records kept per block (limit mode)
-  uint32_t first_wg[kArgSegs + 1];
+  uint32_t first_wg[kArgSegs + 1];   // scan workgroup numbering (without the dictionary workgroups)
   uint32_t first_tile[kArgSegs];
   uint32_t block_idx[kArgSegs];
   uint16_t key_of[kArgSegs][kArgTerms];
   uint16_t nd_off[kArgTerms + 1];
   uint8_t needles[kArgNeedle];
-  uint32_t nsegs, nterms, tpw, bm_words, stage_words;
-  ScanParams P;  // thresholds, outputs (segs/terms/wg_seg unused)
+  uint32_t nsegs, nterms, njobs, gstride;  // dictionary jobs = nsegs x nterms, granules per job
+  uint32_t bm_words, stage_words;
+  unsigned long long *gbm;  // njobs x gstride granules
+  ScanParams P;             // thresholds, outputs (segs/terms/wg_seg unused)
 };
 
-// LDS addresses: contains() runs over staged bytes; needles come from LDS too
+// bytes.Contains over LDS-staged bytes
 __device__ __forceinline__ bool lds_contains(const uint8_t *h, uint32_t hl, const uint8_t *nd, uint32_t nl) {
   if (nl == 0) return true;  // bytes.Contains(x, "") (pitfall P7)
   if (nl > hl) return false;
@@ -671,20 +678,76 @@ __device__ __forceinline__ bool lds_contains(const uint8_t *h, uint32_t hl, cons
   return false;
 }
 
+__device__ __forceinline__ const DevKeyDesc &key_desc(const DevBlockDesc *B, uint32_t k) {
+  return reinterpret_cast<const DevKeyDesc *>(B + 1)[k];
+}
+
+// One dictionary workgroup: job j = (block s, term q).
+__device__ __forceinline__ void dict_job(const QArgs &A, uint32_t j, uint32_t *stage, uint32_t *bits) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_nd[kArgNeedle];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t s = j / A.nterms, q = j % A.nterms;
+  const DevKeyDesc K = key_desc(A.blk[s], A.key_of[s][q]);
+  const uint32_t nl = A.nd_off[q + 1] - A.nd_off[q];
+  for (uint32_t i = tid; i < nl; i += kThreads) s_nd[i] = A.needles[A.nd_off[q] + i];
+  // stage: off[nvals+1] | bytes (whole words) | [set_off nsets+1 | set_vals]; value bits in `bits`
+  const uint32_t bw = (K.dict_nbytes + 3) / 4;
+  uint32_t *off = stage, *by = stage + K.nvals + 1, *soff = by + bw, *svals = soff + K.nsets + 1;
+  for (uint32_t i = tid; i <= K.nvals; i += kThreads) off[i] = G(K.dict_off)[i];
+  for (uint32_t i = tid; i < bw; i += kThreads) by[i] = G(reinterpret_cast<const uint32_t *>(K.dict_bytes))[i];
+  if (!K.identity) {
+    for (uint32_t i = tid; i <= K.nsets; i += kThreads) soff[i] = G(K.set_off)[i];
+    for (uint32_t i = tid; i < K.nsetvals; i += kThreads) svals[i] = G(K.set_vals)[i];
+  }
+  __syncthreads();
+  const uint8_t *b8 = reinterpret_cast<const uint8_t *>(by);
+  for (uint32_t v0 = 0; v0 < K.nvals; v0 += kThreads) {
+    const uint32_t v = v0 + tid;
+    bool m = false;
+    if (v < K.nvals) m = lds_contains(b8 + off[v], off[v + 1] - off[v], s_nd, nl);
+    const unsigned long long b = __ballot(m);
+    const uint32_t w0 = (v - lane) >> 5;
+    if (lane == 0 && w0 * 32 < K.nvals) bits[w0] = uint32_t(b);
+    if (lane == 32 && (w0 + 1) * 32 < K.nvals) bits[w0 + 1] = uint32_t(b >> 32);
+  }
+  __syncthreads();
+  const uint32_t words = (K.nsets + 31) / 32;
+  const unsigned long long tag = (unsigned long long)A.P.epoch << 32;
+  unsigned long long *g = A.gbm + uint64_t(j) * A.gstride;
+  if (K.identity) {  // value set == value
+    for (uint32_t w = tid; w < words; w += kThreads)
+      __hip_atomic_store(&g[w], tag | bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {  // a set matches iff one of its values does
+    for (uint32_t s0 = 0; s0 < K.nsets; s0 += kThreads) {
+      const uint32_t sid = s0 + tid;
+      bool m = false;
+      if (sid < K.nsets)
+        for (uint32_t i = soff[sid]; i < soff[sid + 1] && !m; i++) m = (bits[svals[i] >> 5] >> (svals[i] & 31)) & 1u;
+      const unsigned long long b = __ballot(m);
+      const uint32_t w0 = (sid - lane) >> 5;
+      if (lane == 0 && w0 < words) __hip_atomic_store(&g[w0], tag | uint32_t(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 32 && w0 + 1 < words)
+        __hip_atomic_store(&g[w0 + 1], tag | uint32_t(b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <int NT, bool DUR, bool RANGE, bool W1>
 __global__ void __launch_bounds__(kThreads) search_fast_kernel(QArgs A) {
   const unsigned long long t_start = A.P.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  // [bitmaps bm_words | stage (dictionaries, then kLdsTiles masks) | seg sums nsegs | first_wg nsegs+1 | caps]
-  const uint32_t stage_w = max(A.stage_words, kLdsTiles * kThreads / 2);
+  if (blockIdx.x < A.njobs) {  // dictionary workgroup: [value bits | stage]
+    dict_job(A, blockIdx.x, lds + A.bm_words, lds);
+    return;
+  }
+  // scan workgroup: [bitmaps bm_words | kLdsTiles masks | seg sums nsegs | first_wg nsegs+1 | caps]
   uint32_t *lds_bm = lds;
-  uint32_t *stage = lds + A.bm_words;
-  uint32_t *lds_seg = stage + stage_w;
+  uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + A.bm_words);
+  uint32_t *lds_seg = lds + A.bm_words + kLdsTiles * kThreads / 2;
   uint32_t *lds_fw = lds_seg + A.nsegs;
   unsigned long long *lds_cap = reinterpret_cast<unsigned long long *>(lds_fw + ((A.nsegs + 2) & ~1u));
-  __shared__ __attribute__((aligned(16))) uint8_t s_nd[kArgNeedle];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t wg = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint32_t wg = blockIdx.x - A.njobs;
   uint32_t si = 0;
   for (uint32_t s2 = 1; s2 < A.nsegs; s2++)
     if (A.first_wg[s2] <= wg) si = s2;
@@ -704,7 +767,7 @@ __global__ void __launch_bounds__(kThreads) search_fast_kernel(QArgs A) {
   S.ntiles = uint32_t((S.n + kTile - 1) / kTile);
   S.first_wg = A.first_wg[si];
   S.nwg = A.first_wg[si + 1] - S.first_wg;
-  S.tpw = A.tpw;
+  S.tpw = 0;
   S.term0 = 0;
   S.nterms = A.nterms;
   S.lds_words = A.bm_words;
@@ -716,18 +779,15 @@ __global__ void __launch_bounds__(kThreads) search_fast_kernel(QArgs A) {
     lds_cap[i] = A.cap[i];
   }
   if (tid == 0) lds_fw[A.nsegs] = A.first_wg[A.nsegs];
-  for (uint32_t i = tid; i < A.nd_off[A.nterms]; i += kThreads) s_nd[i] = A.needles[i];
-
-  // ---- dictionaries: stage every term's offsets, bytes and set CSR in one round trip
   constexpr int NTA = NT > 0 ? NT : 1;
   ScanTerm T[NTA];
-  uint32_t so[NTA + 1];  // stage word offset per term
+  uint32_t gw[NTA + 1];  // granule prefix over this block's terms
+  gw[0] = 0;
   uint32_t bmo = 0;
-  so[0] = 0;
 #pragma unroll
   for (int q = 0; q < NTA; q++) {
     if (q >= int(A.nterms)) break;
-    const DevKeyDesc &K = reinterpret_cast<const DevKeyDesc *>(B + 1)[A.key_of[si][q]];
+    const DevKeyDesc &K = key_desc(B, A.key_of[si][q]);
     T[q].col = K.col;
     T[q].bm = nullptr;
     T[q].width = K.width;
@@ -735,71 +795,36 @@ __global__ void __launch_bounds__(kThreads) search_fast_kernel(QArgs A) {
     T[q].lds_off = bmo;
     T[q].bm_words = (K.nsets + 31) / 32;
     bmo += W1 ? 8u : T[q].bm_words;
-    // stage layout: off[nvals+1] | bytes (padded to words) | [vbits nvals/32 | set_off nsets+1 | set_vals]
-    uint32_t w = K.nvals + 1 + (K.dict_nbytes + 3) / 4;
-    if (!K.identity) w += (K.nvals + 31) / 32 + K.nsets + 1 + K.nsetvals;
-    so[q + 1] = so[q] + w;
+    gw[q + 1] = gw[q] + T[q].bm_words;
   }
+  // bitmaps: poll this block's granules (one per thread), then LDS
+  if (NT > 0) {
+    const unsigned long long tag = (unsigned long long)A.P.epoch << 32;
+    for (uint32_t i = tid; i < gw[A.nterms]; i += kThreads) {
+      uint32_t q = 0;
 #pragma unroll
-  for (int q = 0; q < NTA; q++) {
-    if (q >= int(A.nterms)) break;
-    const DevKeyDesc &K = reinterpret_cast<const DevKeyDesc *>(B + 1)[A.key_of[si][q]];
-    uint32_t *st = stage + so[q];
-    for (uint32_t i = tid; i <= K.nvals; i += kThreads) st[i] = G(K.dict_off)[i];
-    uint32_t *by = st + K.nvals + 1;
-    for (uint32_t i = tid; i < (K.dict_nbytes + 3) / 4; i += kThreads)
-      by[i] = G(reinterpret_cast<const uint32_t *>(K.dict_bytes))[i];  // dict_bytes allocations are padded
-    if (!K.identity) {
-      uint32_t *so2 = by + (K.dict_nbytes + 3) / 4 + (K.nvals + 31) / 32;
-      for (uint32_t i = tid; i <= K.nsets; i += kThreads) so2[i] = G(K.set_off)[i];
-      for (uint32_t i = tid; i < K.nsetvals; i += kThreads) so2[K.nsets + 1 + i] = G(K.set_vals)[i];
+      for (int q2 = 1; q2 < NTA; q2++)
+        if (i >= gw[q2]) q = q2;
+      const unsigned long long *g = A.gbm + uint64_t(si * A.nterms + q) * A.gstride + (i - gw[q]);
+      unsigned long long v;
+      uint32_t spins = 0;
+      while (((v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~0xffffffffull) != tag) {
+        if (++spins > kSpinMax) {
+          reinterpret_cast<volatile unsigned long long *>(A.P.out)[1] = 1;  // host fails the query
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      uint32_t lo = 0;
+#pragma unroll
+      for (int q2 = 0; q2 < NTA; q2++)
+        if (q2 == int(q)) lo = T[q2].lds_off;
+      lds_bm[lo + (i - gw[q])] = uint32_t(v);
     }
   }
   __syncthreads();
-  // ---- match: value bits (ballots), then value-set bits
-#pragma unroll
-  for (int q = 0; q < NTA; q++) {
-    if (q >= int(A.nterms)) break;
-    const DevKeyDesc &K = reinterpret_cast<const DevKeyDesc *>(B + 1)[A.key_of[si][q]];
-    const uint32_t *off = stage + so[q];
-    const uint8_t *by = reinterpret_cast<const uint8_t *>(off + K.nvals + 1);
-    uint32_t *vbits = const_cast<uint32_t *>(off) + K.nvals + 1 + (K.dict_nbytes + 3) / 4;
-    uint32_t *bits = K.identity ? lds_bm + T[q].lds_off : vbits;
-    const uint8_t *nd = s_nd + A.nd_off[q];
-    const uint32_t nl = A.nd_off[q + 1] - A.nd_off[q];
-    for (uint32_t v0 = 0; v0 < K.nvals; v0 += kThreads) {
-      const uint32_t v = v0 + tid;
-      bool m = false;
-      if (v < K.nvals) m = lds_contains(by + off[v], off[v + 1] - off[v], nd, nl);
-      const unsigned long long b = __ballot(m);
-      const uint32_t w0 = (v - lane) >> 5;
-      if (lane == 0 && w0 * 32 < K.nvals) bits[w0] = uint32_t(b);
-      if (lane == 32 && (w0 + 1) * 32 < K.nvals) bits[w0 + 1] = uint32_t(b >> 32);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < NTA; q++) {
-    if (q >= int(A.nterms)) break;
-    const DevKeyDesc &K = reinterpret_cast<const DevKeyDesc *>(B + 1)[A.key_of[si][q]];
-    if (K.identity) continue;
-    const uint32_t *vbits = stage + so[q] + K.nvals + 1 + (K.dict_nbytes + 3) / 4;
-    const uint32_t *soff = vbits + (K.nvals + 31) / 32;
-    const uint32_t *svals = soff + K.nsets + 1;
-    for (uint32_t s0 = 0; s0 < K.nsets; s0 += kThreads) {
-      const uint32_t sid = s0 + tid;
-      bool m = false;
-      if (sid < K.nsets)
-        for (uint32_t i = soff[sid]; i < soff[sid + 1] && !m; i++) m = (vbits[svals[i] >> 5] >> (svals[i] & 31)) & 1u;
-      const unsigned long long b = __ballot(m);
-      const uint32_t w0 = (sid - lane) >> 5;
-      if (lane == 0 && w0 * 32 < K.nsets) lds_bm[T[q].lds_off + w0] = uint32_t(b);
-      if (lane == 32 && (w0 + 1) * 32 < K.nsets) lds_bm[T[q].lds_off + w0 + 1] = uint32_t(b >> 32);
-    }
-  }
-  __syncthreads();  // the stage region is reused for the tile masks from here on
-  scan_emit<NT, DUR, RANGE, W1>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, A.nsegs}, lds_bm,
-                                reinterpret_cast<uint16_t *>(stage), lds_seg, t_start);
+  scan_emit<NT, DUR, RANGE, W1>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, A.nsegs}, lds_bm, lds_mask, lds_seg,
+                                t_start, wg);
 }
 
 // ------------------------------------------------------------------------------------
@@ -916,7 +941,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // workgroups need to match the dictionaries themselves
   std::vector<std::array<uint16_t, kArgTerms>> seg_keys;
   std::vector<const DevBlockDesc *> seg_desc;
-  uint32_t fast_stage = 0, fast_bm = 0, fast_bm8 = 0;
+  uint32_t fast_stage = 0, fast_bm = 0, fast_bm8 = 0, fast_vbits = 0, fast_words = 1;
   for (auto &bp : blocks) {
     Block &b = *bp.second;
     const DevBlock &d = b.dev;
@@ -989,20 +1014,21 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     max_lds_words = std::max(max_lds_words, sg.lds_words);
     {
       std::array<uint16_t, kArgTerms> ks{};
-      uint32_t stage = 0, bmw = 0, bmw8 = 0;
+      uint32_t bmw = 0, bmw8 = 0;
       for (uint32_t t = 0; t < q.nterms && t < kArgTerms; t++) {
         const DevKey &k = d.keys[size_t(kidx[t])];
         ks[t] = uint16_t(kidx[t]);
-        stage += k.nvals + 1 + uint32_t((k.dict_nbytes + 3) / 4);
-        if (!k.identity) stage += (k.nvals + 31) / 32 + k.nsets + 1 + k.nsetvals;
-        if (k.dict_nbytes > (1u << 20) || k.nvals > (1u << 20)) stage = 0xfffffffu;
+        uint32_t stage = k.nvals + 1 + uint32_t((k.dict_nbytes + 3) / 4);
+        if (!k.identity) stage += k.nsets + 1 + k.nsetvals;
+        if (k.dict_nbytes > (1u << 20) || k.nvals > (1u << 20) || kidx[t] > 0xffff) stage = 0xfffffffu;
+        fast_stage = std::max(fast_stage, stage);
+        fast_vbits = std::max(fast_vbits, (k.nvals + 63) / 32);
+        fast_words = std::max(fast_words, (k.nsets + 31) / 32);
         bmw += (k.nsets + 31) / 32;
         bmw8 += k.width == 1 ? 8u : (k.nsets + 31) / 32;
       }
-      if (kidx.size() && std::any_of(kidx.begin(), kidx.end(), [](int x) { return x > 0xffff; })) stage = 0xfffffffu;
       seg_keys.push_back(ks);
       seg_desc.push_back(d.desc);
-      fast_stage = std::max(fast_stage, stage);
       fast_bm = std::max(fast_bm, bmw);
       fast_bm8 = std::max(fast_bm8, bmw8);
     }
@@ -1031,9 +1057,11 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   const ScanFn scan_fn = fast ? nullptr : pick_scan(q.nterms, has_dur, q.has_range, all_w1);
   const FastFn fast_fn = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1) : nullptr;
   const void *kfn = fast ? reinterpret_cast<const void *>(fast_fn) : reinterpret_cast<const void *>(scan_fn);
-  const uint32_t fast_bm_words = align_up(all_w1 ? fast_bm8 : fast_bm, 2);
-  const uint32_t fast_stage_words = std::max<uint32_t>(align_up(fast_stage, 2), kLdsTiles * kThreads / 2);
-  const uint32_t lds_words = fast ? fast_bm_words + fast_stage_words + nsegs + ((nsegs + 2) & ~1u) + 2 * nsegs
+  // fast LDS: scan workgroups [bitmaps | masks | seg sums | first_wg | caps], dictionary
+  // workgroups [value bits | stage]; the launch takes the larger
+  const uint32_t fast_bm_words = uint32_t(align_up(std::max(all_w1 ? fast_bm8 : fast_bm, fast_vbits), 2));
+  const uint32_t fast_scan_words = kLdsTiles * kThreads / 2 + nsegs + ((nsegs + 2) & ~1u) + 2 * nsegs;
+  const uint32_t lds_words = fast ? fast_bm_words + std::max<uint32_t>(fast_scan_words, uint32_t(align_up(fast_stage, 4)))
                                   : max_lds_words + kLdsTiles * kThreads / 2 + nsegs;
   int &per_cu = dc.occupancy[{kfn, size_t(lds_words) * 4}];
   if (per_cu == 0) {
@@ -1041,15 +1069,19 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     per_cu = std::max(1, std::min(per_cu, 8));
   }
   const uint32_t target_wg = uint32_t(dc.num_cu) * uint32_t(per_cu);
-  const uint32_t tpw = std::max<uint32_t>(1, (tiles + target_wg - 1) / target_wg);
-  if (tpw > kMaxTpw) fail(TSG_E_UNSUPPORTED, "too many entries per device in one search");
-  uint32_t nwg = 0;
+  // workgroups per block in proportion to its tiles, the tiles of a block split
+  // evenly over its workgroups: every CU gets the same load (+-1 tile)
+  uint32_t nwg = 0, tpw = 1;
   for (auto &sg : segs) {
-    sg.tpw = tpw;
+    uint64_t w = (uint64_t(target_wg) * sg.ntiles + tiles / 2) / tiles;
+    w = std::max<uint64_t>(1, std::min<uint64_t>(w, sg.ntiles));
     sg.first_wg = nwg;
-    sg.nwg = (sg.ntiles + tpw - 1) / tpw;
+    sg.nwg = uint32_t(w);
+    sg.tpw = uint32_t((sg.ntiles + w - 1) / w);
+    tpw = std::max(tpw, sg.tpw);
     nwg += sg.nwg;
   }
+  if (tpw > kMaxTpw) fail(TSG_E_UNSUPPORTED, "too many entries per device in one search");
   if (n_all >= (1ull << 32)) fail(TSG_E_UNSUPPORTED, "more than 2^32 entries per device in one search");
   tr.mark("plan");
 
@@ -1110,9 +1142,13 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     if (!needles.empty()) std::memcpy(A.needles, needles.data(), needles.size());
     A.nsegs = nsegs;
     A.nterms = q.nterms;
-    A.tpw = tpw;
+    A.njobs = nsegs * q.nterms;
+    A.gstride = fast_words;
     A.bm_words = fast_bm_words;
-    A.stage_words = fast_stage_words;
+    A.stage_words = fast_stage;
+    if (A.njobs && dc.gbm.ensure(size_t(A.njobs) * fast_words * 8))
+      HIP_OK(hipMemsetAsync(dc.gbm.p, 0, dc.gbm.cap, s));  // tag 0: never published
+    A.gbm = static_cast<unsigned long long *>(dc.gbm.p);
     tr.mark("desc");
     if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
   } else {
@@ -1175,7 +1211,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     if (timed) HIP_OK(hipEventRecord(dc.es0, s));
     if (fast) {
       A.P = P;
-      fast_fn<<<nwg, kThreads, size_t(lds_words) * 4, s>>>(A);
+      fast_fn<<<A.njobs + nwg, kThreads, size_t(lds_words) * 4, s>>>(A);
     } else {
       scan_fn<<<nwg, kThreads, size_t(lds_words) * 4, s>>>(P);
     }

@@ -263,3 +263,17 @@ def test_many_blocks_general_path(engine, tmp_path):
         assert_parity(got, met, exp, omet)
     got, met, exp, omet = both(engine, paths, tags={"k1": "v"}, limit=7)
     assert_parity(got, met, exp, omet)
+
+
+def test_high_cardinality_config4(engine, tmp_path):
+    """BASELINE config 4 shape: ~unique http.url and long db.statement values
+    (substring terms over large dictionaries: the prep-kernel path)."""
+    p = os.path.join(str(tmp_path), "hc")
+    T.synth_search_block(p, 20_000, seed=4, profile=1)
+    for q in [dict(tags={"http.url": "/api/v1/users/12"}),
+              dict(tags={"db.statement": "select"}),
+              dict(tags={"http.url": "/api/v1/users/12", "db.statement": "from orders"}, min_ms=1),
+              dict(tags={"db.statement": "where id = 77"}, start=1_700_000_900, end=1_700_002_700)]:
+        got, met, exp, omet = both(engine, [p], **q)
+        assert_parity(got, met, exp, omet)
+        assert len(exp) > 0

@@ -36,6 +36,11 @@ if has bench; then
   rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.err; cat gpurun_out/bench.json
   [ $rc -eq 0 ] || exit $rc
 fi
+if has lookup; then
+  timeout -k 10 600 python tools/bench_lookup.py ${LOOKUP_ARGS:-} > gpurun_out/lookup.json 2> gpurun_out/lookup.err
+  rc=$?; echo "lookup rc=$rc"; tail -3 gpurun_out/lookup.err; cat gpurun_out/lookup.json
+  [ $rc -eq 0 ] || exit $rc
+fi
 if has prof; then
   export TMPDIR=/tmp
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
