@@ -733,7 +733,7 @@ __device__ __forceinline__ void dict_job(const QArgs &A, uint32_t j, uint32_t *s
 }
 
 template <int NT, bool DUR, bool RANGE, bool W1>
-__global__ void __launch_bounds__(kThreads) search_fast_kernel(QArgs A) {
+__global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   const unsigned long long t_start = A.P.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   if (blockIdx.x < A.njobs) {  // dictionary workgroup: [value bits | stage]
