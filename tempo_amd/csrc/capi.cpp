@@ -65,28 +65,37 @@ struct ResultHolder {
     for (auto *v : {&start, &end, &entry, &svc_off, &name_off}) v->reserve(n);
     for (auto *v : {&dur, &block, &svc_len, &name_len}) v->reserve(n);
     id_len.reserve(n);
+    arena.reserve(24 * n);
   }
   void set_str(std::vector<uint64_t> &off, std::vector<uint32_t> &len, size_t i, const char *p, size_t l) {
     off[i] = arena.size();
     len[i] = uint32_t(l);
     arena.insert(arena.end(), p, p + l);
   }
-  void push(const uint8_t *id, uint8_t il, uint64_t s, uint64_t e, uint32_t b, uint64_t en, const char *sv,
-            size_t svl, const char *nm, size_t nml) {
-    ids.insert(ids.end(), id, id + 16);
-    id_len.push_back(il);
-    start.push_back(s);
-    end.push_back(e);
-    dur.push_back(uint32_t((e - s) / 1000000ULL));  // util.go:33
-    block.push_back(b);
-    entry.push_back(en);
-    svc_off.push_back(0);
-    svc_len.push_back(0);
-    name_off.push_back(0);
-    name_len.push_back(0);
-    const size_t i = start.size() - 1;
+  size_t size() const { return start.size(); }
+  void resize(size_t n) {
+    ids.resize(16 * n);
+    for (auto *v : {&start, &end, &entry, &svc_off, &name_off}) v->resize(n);
+    for (auto *v : {&dur, &block, &svc_len, &name_len}) v->resize(n);
+    id_len.resize(n);
+  }
+  void set(size_t i, const uint8_t *id, uint8_t il, uint64_t s, uint64_t e, uint32_t b, uint64_t en, const char *sv,
+           size_t svl, const char *nm, size_t nml) {
+    std::memcpy(&ids[16 * i], id, 16);
+    id_len[i] = il;
+    start[i] = s;
+    end[i] = e;
+    dur[i] = uint32_t((e - s) / 1000000ULL);  // util.go:33
+    block[i] = b;
+    entry[i] = en;
     set_str(svc_off, svc_len, i, sv, svl);
     set_str(name_off, name_len, i, nm, nml);
+  }
+  void push(const uint8_t *id, uint8_t il, uint64_t s, uint64_t e, uint32_t b, uint64_t en, const char *sv,
+            size_t svl, const char *nm, size_t nml) {
+    const size_t i = size();
+    resize(i + 1);
+    set(i, id, il, s, e, b, en, sv, svl, nm, nml);
   }
   const char *svc(size_t i) const { return arena.data() + svc_off[i]; }
   const char *name(size_t i) const { return arena.data() + name_off[i]; }
@@ -369,18 +378,27 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         if (e) std::rethrow_exception(e);
     }
     const clk::time_point t_dev = trace ? clk::now() : clk::time_point();
-    // per block match lists in scan order
-    std::vector<std::vector<const SearchOut::Rec *>> per_block(nblocks);
+    // per block match lists in scan order (each device's records are grouped by block already)
+    std::vector<std::pair<const SearchOut::Rec *, size_t>> per_block(nblocks, {nullptr, 0});
     size_t nrec = 0;
-    for (auto &o : outs) nrec += o.second.recs.size();
-    res->reserve(nrec);
     for (auto &o : outs) {
       m.device_bytes_read += o.second.device_bytes;
       m.kernel_ns = std::max<uint64_t>(m.kernel_ns, o.second.kernel_ns);
       m.scan_kernel_ns = std::max<uint64_t>(m.scan_kernel_ns, o.second.scan_ns);
       m.scan_bytes += o.second.scan_bytes;
-      for (auto &r : o.second.recs) per_block[r.block_il & 0xffffffu].push_back(&r);
+      const auto &recs = o.second.recs;
+      for (size_t r = 0; r < recs.size();) {
+        const uint32_t bi = recs[r].block_il & 0xffffffu;
+        size_t e = r;
+        while (e < recs.size() && (recs[e].block_il & 0xffffffu) == bi) e++;
+        per_block[bi] = {&recs[r], e - r};
+        r = e;
+      }
+      nrec += recs.size();
     }
+    res->reserve(nrec);
+    res->resize(nrec);
+    size_t nout = 0;
     // consume in caller block order (deterministic refinement of instance.Search)
     std::unordered_set<std::string> distinct;
     bool stopped = false;
@@ -394,12 +412,13 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       }
       m.blocks_inspected++;
       uint64_t stop_entry = UINT64_MAX;
-      for (const SearchOut::Rec *r : per_block[i]) {
+      for (size_t ri = 0; ri < per_block[i].second; ri++) {
+        const SearchOut::Rec *r = per_block[i].first + ri;
         std::string_view sv, nm;
         if (h.svc_key >= 0 && r->svc != kNone) sv = h.dict_value(h.svc_key, r->svc);
         if (h.name_key >= 0 && r->name != kNone) nm = h.dict_value(h.name_key, r->name);
-        res->push(r->id, uint8_t(r->block_il >> 24), r->start, r->end, uint32_t(i), r->entry, sv.data(), sv.size(),
-                  nm.data(), nm.size());
+        res->set(nout++, r->id, uint8_t(r->block_il >> 24), r->start, r->end, uint32_t(i), r->entry, sv.data(),
+                 sv.size(), nm.data(), nm.size());
         if (limit) {
           distinct.insert(std::string(reinterpret_cast<const char *>(r->id), 16));
           if (distinct.size() >= limit) {
@@ -419,6 +438,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
           m.bytes_inspected += h.page_fb_bytes[p];
       }
     }
+    res->resize(nout);
     res->finalize();
     *out = &guard_res.release()->pub;
     if (trace) {
