@@ -15,6 +15,7 @@
 //                inside a tile from packed wave scans, records written in the
 //                reference scan order (pages ascending, entry index ascending)
 // Everything is integer, HBM-bound streaming; no MFMA (no dense contraction).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1208,6 +1209,14 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     auto *h = reinterpret_cast<volatile uint64_t *>(P.out);
     h[0] = 0;
     h[1] = 0;  // look-back error flag
+    static const bool ext_events = std::getenv("TSG_EXT_EVENTS") != nullptr;
+    if (timed && ext_events) {  // events stamped from the dispatch packet (hipExtLaunchKernel)
+      if (fast) A.P = P;
+      void *args[] = {fast ? static_cast<void *>(&A) : static_cast<void *>(&P)};
+      HIP_OK(hipExtLaunchKernel(kfn, dim3(fast ? A.njobs + nwg : nwg), dim3(kThreads), args,
+                                size_t(lds_words) * 4, s, dc.es0, dc.es1, 0));
+      return;
+    }
     if (timed) HIP_OK(hipEventRecord(dc.es0, s));
     if (fast) {
       A.P = P;

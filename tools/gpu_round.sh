@@ -23,6 +23,9 @@ if has trace; then
   timeout -k 10 600 python bench.py --steps 50 --warmup 5 --cpu-baseline 0 --events 0 ${BENCH_ARGS:-} > gpurun_out/noevents.json 2> gpurun_out/noevents.err
   rc=$?; echo "noevents rc=$rc"; cat gpurun_out/noevents.json
   [ $rc -eq 0 ] || exit $rc
+  TSG_EXT_EVENTS=1 timeout -k 10 600 python bench.py --steps 50 --warmup 5 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/extevents.json 2> gpurun_out/extevents.err
+  rc=$?; echo "extevents rc=$rc"; cat gpurun_out/extevents.json
+  [ $rc -eq 0 ] || exit $rc
 fi
 if has stamps; then
   TSG_STAMPS=1 TSG_TRACE=1 timeout -k 10 600 python bench.py --steps 5 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/stamps.json 2> gpurun_out/stamps.err
