@@ -50,3 +50,14 @@ if has prof; then
     python3 bench.py --steps 20 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
   rc=$?; echo "rocprof rc=$rc"; cat gpurun_out/prof/run_kernel_stats.csv
 fi
+if has pmc; then
+  export TMPDIR=/tmp
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 900 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv -- \
+      python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err
+    rc=$?; echo "pmc $c rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+  done
+  python3 tools/pmc_summary.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE | tee gpurun_out/pmc_summary.txt
+fi
+
