@@ -32,6 +32,27 @@ T0 = 1_700_000_000
 QUERY = dict(tags={"service.name": "svc-07", "http.method": "get", "status.code": "error"},
              min_duration_ms=10, max_duration_ms=1000, start=T0 + 900, end=T0 + 2700)
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# The config-2 query (3 u8 term columns, duration + range filters, 10 blocks) runs
+# the one-launch path; TSG_NO_FAST=1 forces the general path (prep + search kernels).
+KERNEL = ("search_kernel<3, true, true, true>" if os.environ.get("TSG_NO_FAST")
+          else "search_fast_kernel<3, true, true, true>")
+# HBM-side bytes per launch of KERNEL from separate rocprofv3 --pmc passes
+# (FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE), written by
+# tools/pmc_summary.py --out; keyed by workload so other sizes report null.
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(workload_key):
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    w = d.get(workload_key, {})
+    for name, ent in w.items():
+        if KERNEL.replace(" ", "") in name.replace(" ", ""):  # rocprof: "void tsg::search_fast_kernel<...>(tsg::QArgs)"
+            return ent.get("traffic_bytes_per_launch"), w.get("_source")
+    return None, None
 
 
 def parse():
@@ -159,6 +180,7 @@ def main():
     scan_avg_ns = sum(scan_ns) / len(scan_ns)
     scan_bytes = met.scan_bytes
     achieved = scan_bytes / scan_avg_ns if scan_avg_ns else None  # bytes/ns == GB/s
+    traffic, traffic_src = pmc_traffic(f"blocks={args.blocks},entries={args.entries}")
     out = {
         "metric": METRIC,
         "value": value,
@@ -180,9 +202,9 @@ def main():
         },
         "achieved_hbm_gbps": achieved,
         "roofline": {
-            "bound": "hbm", "kernel": "scan_kernel", "achieved": achieved, "peak": PEAK_HBM_GBPS,
-            "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS if achieved else None, "traffic": None,
-            "bytes_per_launch": scan_bytes, "avg_launch_us": scan_avg_ns / 1e3,
+            "bound": "hbm", "kernel": KERNEL, "achieved": achieved, "peak": PEAK_HBM_GBPS,
+            "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS if achieved else None, "traffic": traffic,
+            "traffic_source": traffic_src, "bytes_per_launch": scan_bytes, "avg_launch_us": scan_avg_ns / 1e3,
             "bytes_per_entry": 15,
         },
         "load_s": load_s,

@@ -58,6 +58,7 @@ if has pmc; then
     rc=$?; echo "pmc $c rc=$rc"
     [ $rc -eq 0 ] || exit $rc
   done
-  python3 tools/pmc_summary.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE | tee gpurun_out/pmc_summary.txt
+  python3 tools/pmc_summary.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE --out gpurun_out/pmc_traffic.json \
+    --workload "${PMC_WORKLOAD:-blocks=10,entries=1000000}" --source "${PMC_SOURCE:-gpu_round.sh pmc}" | tee gpurun_out/pmc_summary.txt
 fi
 

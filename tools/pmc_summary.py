@@ -4,8 +4,9 @@
 FETCH_SIZE / WRITE_SIZE are kilobytes at the L2's memory side (Infinity Cache
 hits included). On gfx950 FETCH_SIZE reports half the bytes of wide coalesced
 streaming reads (MI355X_MICROARCH.md, HBM section), so reads are doubled.
-Usage: pmc_summary.py <FETCH_SIZE run dir> <WRITE_SIZE run dir>
+Usage: pmc_summary.py <FETCH_SIZE run dir> <WRITE_SIZE run dir> [--out profiles/pmc_traffic.json]
 """
+import argparse
 import csv
 import glob
 import json
@@ -26,8 +27,15 @@ def per_kernel(d, counter):
 
 
 def main():
-    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
-    write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--out", help="merge into this JSON file (profiles/pmc_traffic.json) under --workload")
+    ap.add_argument("--workload", default="blocks=10,entries=1000000")
+    ap.add_argument("--source", default="", help="where the passes came from (recorded next to the numbers)")
+    args = ap.parse_args()
+    fetch = per_kernel(args.fetch_dir, "FETCH_SIZE")
+    write = per_kernel(args.write_dir, "WRITE_SIZE")
     out = {}
     for k in sorted(set(fetch) | set(write)):
         if "search" not in k and "prep" not in k:
@@ -41,6 +49,16 @@ def main():
         out[k] = {"launches": len(f), "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                   "traffic_bytes_per_launch": (rd or 0) + (wr or 0)}
     print(json.dumps(out, indent=1))
+    if args.out:
+        try:
+            with open(args.out) as f:
+                merged = json.load(f)
+        except (OSError, ValueError):
+            merged = {}
+        out["_source"] = args.source
+        merged[args.workload] = out
+        with open(args.out, "w") as f:
+            json.dump(merged, f, indent=1)
 
 
 if __name__ == "__main__":
