@@ -139,6 +139,8 @@ typedef struct tsg_result {
 /* Options for tsg_search. */
 #define TSG_SEARCH_TIME_SCAN 1u /* HIP events around the scan kernel -> metrics.scan_kernel_ns */
 #define TSG_SEARCH_TIME_ALL 2u  /* ... and around the whole device sequence -> metrics.kernel_ns */
+#define TSG_SEARCH_TIME_DEFER 4u /* HIP events around the search kernel, read later with
+                                    tsg_kernel_times (the search does not wait for them) */
 typedef struct tsg_search_opts {
   uint32_t limit;  /* 0 = no limit (every match) */
   uint32_t flags;  /* TSG_SEARCH_TIME_* (timing events cost a few us per search; off by default) */
@@ -200,6 +202,11 @@ void tsg_free(void *p);
 int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
                const tsg_search_opts *opts, tsg_result **out);
 void tsg_result_free(tsg_result *r);
+
+/* Durations (ns) of the search kernels launched with TSG_SEARCH_TIME_DEFER since
+ * the last call, in launch order per device (devices in context order). Waits for
+ * every device's stream. At most cap values are written; *n = values written. */
+int tsg_kernel_times(tsg_ctx *ctx, uint64_t *ns, size_t cap, size_t *n);
 
 /* instance.Search consumer on an ordered match sequence: dedupe by trace ID with
  * CombineSearchResults, stop at max_results distinct (0 -> 20), then sort by

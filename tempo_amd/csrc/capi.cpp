@@ -452,6 +452,17 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
 }
 void tsg_result_free(tsg_result *r) { delete reinterpret_cast<ResultHolder *>(r); }
 
+int tsg_kernel_times(tsg_ctx *ctx, uint64_t *ns, size_t cap, size_t *n) {
+  if (!ctx || !n || (cap && !ns)) return TSG_E_INVALID;
+  return guard([&] {
+    std::vector<uint64_t> v;
+    for (DeviceCtx *dc : ctx->c.devs) device_kernel_times(*dc, v);
+    const size_t k = std::min(cap, v.size());
+    if (k) std::memcpy(ns, v.data(), k * sizeof(uint64_t));
+    *n = k;
+  });
+}
+
 int tsg_results_combine(const tsg_result *in, uint32_t max_results, tsg_result **out) {
   if (!in || !out) return TSG_E_INVALID;
   return guard([&] {

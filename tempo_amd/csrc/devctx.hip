@@ -46,8 +46,10 @@ void ctx_shutdown(Ctx &c) {
     (void)hipSetDevice(dc->ordinal);
     (void)hipStreamSynchronize(dc->stream);
     for (DevBuf *b : {&dc->desc, &dc->vmatch, &dc->bitmaps, &dc->gran, &dc->ticket, &dc->out, &dc->regions,
-                      &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps, &dc->gbm})
+                      &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps, &dc->gbm,
+                      &dc->done})
       b->release();
+    for (hipEvent_t e : dc->tring) (void)hipEventDestroy(e);
     dc->hdesc.release();
     dc->hout.release();
     dc->hres.release();
@@ -61,15 +63,20 @@ void ctx_shutdown(Ctx &c) {
   c.devs.clear();
 }
 
+// pad_to: allocate a multiple of that many elements (scan columns: kColPad) and
+// zero the tail, so whole-tile loads past the last entry stay in bounds.
 template <typename T>
-static T *dev_upload(DevBlock &b, const T *src, size_t count, hipStream_t s) {
+static T *dev_upload(DevBlock &b, const T *src, size_t count, hipStream_t s, size_t pad_to = 1) {
   void *p = nullptr;
+  const size_t elems = (count + pad_to - 1) / pad_to * pad_to;
   // whole 16-byte words: kernels may read a dictionary's last bytes as a word
-  size_t bytes = std::max<size_t>((count * sizeof(T) + 15) / 16 * 16, 16);
+  size_t bytes = std::max<size_t>((elems * sizeof(T) + 15) / 16 * 16, 16);
   HIP_OK(hipMalloc(&p, bytes));
   b.allocs.push_back(p);
   b.bytes += bytes;
   if (count) HIP_OK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+  if (bytes > count * sizeof(T))
+    HIP_OK(hipMemsetAsync(static_cast<uint8_t *>(p) + count * sizeof(T), 0, bytes - count * sizeof(T), s));
   return static_cast<T *>(p);
 }
 
@@ -94,10 +101,10 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     ss[i] = uint32_t(h.start[i] / 1000000000ULL);
     es[i] = uint32_t(h.end[i] / 1000000000ULL);
   }
-  d.dur32 = dev_upload(d, dur32.data(), n, s);
+  d.dur32 = dev_upload(d, dur32.data(), n, s, kColPad);
   d.dur64 = dev_upload(d, dur64.data(), n, s);
-  d.start_s = dev_upload(d, ss.data(), n, s);
-  d.end_s = dev_upload(d, es.data(), n, s);
+  d.start_s = dev_upload(d, ss.data(), n, s, kColPad);
+  d.end_s = dev_upload(d, es.data(), n, s, kColPad);
   d.ids = dev_upload(d, h.ids.data(), n * 16, s);
   d.start_ns = dev_upload(d, h.start.data(), n, s);
   d.end_ns = dev_upload(d, h.end.data(), n, s);
@@ -120,23 +127,38 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     if (k.width == 1) {
       std::vector<uint8_t> col(n);
       for (size_t i = 0; i < n; i++) col[i] = kc.col[i] == kNone ? 0xff : uint8_t(kc.col[i]);
-      k.col = dev_upload(d, col.data(), n, s);
+      k.col = dev_upload(d, col.data(), n, s, kColPad);
       HIP_OK(hipStreamSynchronize(s));
     } else if (k.width == 2) {
       std::vector<uint16_t> col(n);
       for (size_t i = 0; i < n; i++) col[i] = kc.col[i] == kNone ? 0xffff : uint16_t(kc.col[i]);
-      k.col = dev_upload(d, col.data(), n, s);
+      k.col = dev_upload(d, col.data(), n, s, kColPad);
       HIP_OK(hipStreamSynchronize(s));
     } else {
-      k.col = dev_upload(d, kc.col.data(), n, s);
+      k.col = dev_upload(d, kc.col.data(), n, s, kColPad);
     }
-    k.dict_bytes = dev_upload(d, kc.dict_bytes.data(), kc.dict_bytes.size(), s);
-    k.dict_off = dev_upload(d, kc.dict_off.data(), kc.dict_off.size(), s);
+    // one contiguous blob per key, in the order a workgroup stages it into LDS:
+    // [value offsets nvals+1 | value bytes (whole words) | set offsets nsets+1 | set values]
+    // (set arrays only for non-identity keys)
+    const size_t bw = (kc.dict_bytes.size() + 3) / 4;
+    const size_t nso = kc.identity ? 0 : kc.set_off.size(), nsv = kc.identity ? 0 : kc.set_vals.size();
+    std::vector<uint32_t> blob(kc.dict_off.size() + bw + nso + nsv, 0);
+    uint32_t *bp = blob.data();
+    std::memcpy(bp, kc.dict_off.data(), kc.dict_off.size() * 4);
+    bp += kc.dict_off.size();
+    if (!kc.dict_bytes.empty()) std::memcpy(bp, kc.dict_bytes.data(), kc.dict_bytes.size());
+    bp += bw;
+    if (nso) std::memcpy(bp, kc.set_off.data(), nso * 4);
+    if (nsv) std::memcpy(bp + nso, kc.set_vals.data(), nsv * 4);
+    uint32_t *dblob = dev_upload(d, blob.data(), blob.size(), s);
+    HIP_OK(hipStreamSynchronize(s));  // (blob is a temporary)
+    k.dict_off = dblob;
+    k.dict_bytes = reinterpret_cast<uint8_t *>(dblob + kc.dict_off.size());
     k.dict_nbytes = kc.dict_bytes.size();
     if (!kc.identity) {
-      k.set_off = dev_upload(d, kc.set_off.data(), kc.set_off.size(), s);
-      k.set_vals = dev_upload(d, kc.set_vals.data(), kc.set_vals.size(), s);
-      k.nsetvals = uint32_t(kc.set_vals.size());
+      k.set_off = dblob + kc.dict_off.size() + bw;
+      k.set_vals = k.set_off + nso;
+      k.nsetvals = uint32_t(nsv);
     }
     d.keys.push_back(k);
   }

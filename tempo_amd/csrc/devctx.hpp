@@ -71,9 +71,36 @@ struct DeviceCtx {
   unsigned long long epoch = 0, ticket_base = 0;  // lookup launches
   uint32_t search_epoch = 0;
   bool fast_off = std::getenv("TSG_NO_FAST") != nullptr;  // force the general (prep + search) path
+  bool self_off = std::getenv("TSG_NO_SELF_DICT") != nullptr;  // one-launch path: always use dictionary workgroups
   std::map<std::pair<const void *, size_t>, int> occupancy;  // (kernel, dynamic LDS) -> blocks per CU  // search launches: tag of the published workgroup counts
   size_t gran_tiles = 0;
+  // one-launch search path: per-XCD-group completion counters + top counter, 128 B
+  // apart; monotonic: a launch advances each by an amount the host knows, mirrored
+  // in done_base
+  DevBuf done;
+  uint32_t done_base[9] = {};
+  uint32_t seg_cap = 16;                                  // segment-mode records per workgroup (limit 0), adaptive
+  bool seg_off = std::getenv("TSG_NO_SEG") != nullptr;    // one-launch path: always look-back mode
+  // TSG_SEARCH_TIME_DEFER: event pairs recorded around search kernels, read by tsg_kernel_times
+  std::vector<hipEvent_t> tring;
+  size_t tring_used = 0;
+  bool defer_slot(hipEvent_t &a, hipEvent_t &b) {
+    constexpr size_t kMaxDeferred = 4096;
+    if (tring_used == kMaxDeferred) return false;
+    if (2 * tring_used == tring.size()) {
+      hipEvent_t e0, e1;
+      HIP_OK(hipEventCreateWithFlags(&e0, hipEventDisableSystemFence));
+      HIP_OK(hipEventCreateWithFlags(&e1, hipEventDisableSystemFence));
+      tring.push_back(e0);
+      tring.push_back(e1);
+    }
+    a = tring[2 * tring_used];
+    b = tring[2 * tring_used + 1];
+    tring_used++;
+    return true;
+  }
 };
+
 
 
 }  // namespace tsg

@@ -10,6 +10,10 @@
 
 namespace tsg {
 
+// Scan columns (dur32, start_s, end_s, term value-set columns) are allocated to a
+// multiple of kColPad entries so the scan kernels load whole tiles unconditionally.
+constexpr uint64_t kColPad = 4096;
+
 struct DevKey {
   std::string name;
   int width = 4;
@@ -29,6 +33,7 @@ struct DevKey {
 struct DevKeyDesc {  // 64 B
   const void *col;
   const uint8_t *dict_bytes;  // allocation padded to whole words
+  // dict_off starts the key's contiguous blob [dict_off | dict_bytes | set_off | set_vals]
   const uint32_t *dict_off, *set_off, *set_vals;
   uint32_t width, nvals, nsets, identity;
   uint32_t dict_nbytes, nsetvals;
@@ -134,5 +139,7 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
                    size_t nids, const tsg_lookup_opts *opts, LookupOut &out);
 
 int device_ordinal(const DeviceCtx &dc);
+// Durations of the TSG_SEARCH_TIME_DEFER launches since the last call (waits for the stream).
+void device_kernel_times(DeviceCtx &dc, std::vector<uint64_t> &ns);
 
 }  // namespace tsg

@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "devctx.hpp"
 
@@ -58,8 +59,8 @@ struct ScanSeg {
   const uint64_t *start_ns, *end_ns;
   const uint32_t *names;
   const uint8_t *id_len;
-  uint32_t first_tile, ntiles;  // global tile numbering
-  uint32_t first_wg, nwg, tpw;  // workgroups owning this block (tiles split evenly), max tiles per workgroup
+  uint32_t pad1, nunits;        // scan units (kUnit entries) in the block
+  uint32_t first_wg, nwg, tpw;  // workgroups owning this block (units split evenly), max tiles per workgroup
   uint32_t term0, nterms, lds_words;
   uint32_t block_idx, pad;
   uint64_t cap;  // limit mode: records kept from this block
@@ -82,18 +83,27 @@ struct ScanParams {
   uint32_t has_min, has_max, need64, limit_mode;
   uint64_t min_ns, max_ns;
   uint32_t start_s, end_s;
-  uint16_t *mask;            // masks of tiles beyond kLdsTiles per workgroup: per global tile 256 x u16
+  uint16_t *mask;            // masks of tiles beyond kLdsTiles per workgroup: [workgroup][mask_tpw][256] u16
+  uint32_t mask_tpw, pad2;
   unsigned long long *agg;   // per workgroup: {epoch, match count}, published once per launch
   uint32_t epoch;            // this launch's tag (never 0)
   uint32_t lds_bm_words;     // dynamic LDS: [bitmaps | kLdsTiles masks | per-block sums]
-  uint8_t *out;              // pinned host: [header | records]; header[0] total, [1] error, [8+s] per block
+  uint8_t *out;              // pinned host: [header | (segment mode) tile counts | records];
+                             // header[0] total, [1] error, [2] done epoch, [8+s] per block
   unsigned long long *stamps;  // TSG_STAMPS: per workgroup s_memrealtime at phase boundaries (else null)
-  uint64_t hdr_bytes, out_cap;
+  uint64_t hdr_bytes, out_cap;  // records start at out + hdr_bytes
+  uint32_t *counts;          // segment mode: match count of every tile (pinned host)
+  unsigned *done;            // one-launch path: completion counters (device; 8 XCD groups + top, 32 words apart)
+  uint32_t seg_cap;          // segment mode (> 0): records per tile segment; 0 = look-back mode
+  uint32_t done_top;         // top counter value once every XCD group has finished
+  uint32_t done_target[8];   // group counter values once every scan workgroup of the group has finished
 };
 
 constexpr int kThreads = 256;
-constexpr int kSteps = 4;                     // 16 entries per thread per tile
-constexpr int kTile = kThreads * 4 * kSteps;  // 4096 entries
+constexpr int kSteps = 2;                     // 8 entries per thread per tile
+constexpr int kTile = kThreads * 4 * kSteps;  // 2048 entries
+constexpr uint32_t kMaskAll = (1u << (4 * kSteps)) - 1;
+constexpr int kUnit = kThreads * 4;           // 1024 entries: workgroup ranges are whole units
 constexpr uint32_t kNoLds = 0xffffffffu;
 
 // ------------------------------------------------------------------------------------
@@ -218,60 +228,29 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
 
 // ------------------------------------------------------------------------------------
 // scan
-template <bool FULL>
-__device__ __forceinline__ uint4 load4_u32(const uint32_t *p, uint64_t e, uint64_t n) {
-  uint4 r;
-  if (FULL) {
-    const u32x4 v = *G<u32x4>(p + e);
-    r.x = v.x;
-    r.y = v.y;
-    r.z = v.z;
-    r.w = v.w;
-    return r;
-  }
-  r.x = e < n ? G(p)[e] : 0u;
-  r.y = e + 1 < n ? G(p)[e + 1] : 0u;
-  r.z = e + 2 < n ? G(p)[e + 2] : 0u;
-  r.w = e + 3 < n ? G(p)[e + 3] : 0u;
+// Scan columns are allocated to whole kColPad-entry multiples (devctx.hip), so every
+// tile load is in bounds; entries past n are only masked off.
+static_assert(kColPad % (kThreads * 4 * kSteps) == 0, "column padding covers whole tiles");
+
+// (tile registers are kept as 128-bit vectors, not 4 scalars: a quad returned by one
+// dwordx4 load then stays one register tuple across the loop, instead of being
+// copied into scalar registers right after the load, which waits for it)
+__device__ __forceinline__ u32x4 load4_u32(const uint32_t *p, uint64_t e) { return *G<u32x4>(p + e); }
+// 4 consecutive column values, raw (decoded by col_at). Branch-free over the
+// (wave-uniform) width: 4 dword loads whose addresses collapse onto the first
+// dword for narrow columns (same cache line, no extra HBM bytes). A width switch
+// here makes hipcc merge the three load shapes with vmcnt(0) waits that serialise
+// every outstanding load.
+__device__ __forceinline__ u32x4 load_col(const void *col, uint32_t width, uint64_t e) {
+  const auto *c = G<uint32_t>(static_cast<const uint8_t *>(col) + e * width);
+  u32x4 r;
+  r.x = c[0];
+  r.y = c[width >= 2 ? 1 : 0];
+  r.z = c[width == 4 ? 2 : 0];
+  r.w = c[width == 4 ? 3 : 0];
   return r;
 }
-// 4 consecutive column values, raw (decoded by col_at); absent slots read as "key absent"
-template <bool FULL>
-__device__ __forceinline__ uint4 load_col(const void *col, uint32_t width, uint64_t e, uint64_t n) {
-  uint4 r = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-  if (FULL) {
-    // branch-free over the (wave-uniform) width: 4 dword loads whose addresses
-    // collapse onto the first dword for narrow columns (same cache line, no
-    // extra HBM bytes). A width switch here makes hipcc merge the three load
-    // shapes with vmcnt(0) waits that serialise every outstanding load.
-    const auto *c = G<uint32_t>(static_cast<const uint8_t *>(col) + e * width);
-    r.x = c[0];
-    r.y = c[width >= 2 ? 1 : 0];
-    r.z = c[width == 4 ? 2 : 0];
-    r.w = c[width == 4 ? 3 : 0];
-    return r;
-  }
-  if (width == 1) {
-    const auto *c = G<uint8_t>(col);
-    uint32_t x = 0;
-    for (int j = 0; j < 4; j++) x |= uint32_t(e + j < n ? c[e + j] : 0xffu) << (8 * j);
-    r.x = x;
-  } else if (width == 2) {
-    const auto *c = G<uint16_t>(col);
-    uint32_t v[4];
-    for (int j = 0; j < 4; j++) v[j] = e + j < n ? c[e + j] : 0xffffu;
-    r.x = v[0] | (v[1] << 16);
-    r.y = v[2] | (v[3] << 16);
-  } else {
-    const auto *c = G<uint32_t>(col);
-    r.x = e < n ? c[e] : 0xffffffffu;
-    r.y = e + 1 < n ? c[e + 1] : 0xffffffffu;
-    r.z = e + 2 < n ? c[e + 2] : 0xffffffffu;
-    r.w = e + 3 < n ? c[e + 3] : 0xffffffffu;
-  }
-  return r;
-}
-__device__ __forceinline__ uint32_t col_at(uint4 r, uint32_t width, int j) {
+__device__ __forceinline__ uint32_t col_at(u32x4 r, uint32_t width, int j) {
   if (width == 1) return (r.x >> (8 * j)) & 0xffu;
   if (width == 2) return ((j < 2 ? r.x : r.y) >> (16 * (j & 1))) & 0xffffu;
   return j == 0 ? r.x : j == 1 ? r.y : j == 2 ? r.z : r.w;
@@ -282,49 +261,70 @@ __device__ __forceinline__ bool term_ok(const ScanTerm &T, const uint32_t *lds_b
   return (w >> (x & 31)) & 1u;
 }
 
-// Match mask of one tile for this thread: bit (4k+j) <-> entry tile0 + 1024k + 4*tid + j.
-// NT >= 0: every load of the tile is issued before the first use; NT < 0: runtime term loop.
-// FULL: the whole tile lies inside the block (no bounds checks).
-template <int NT, bool DUR, bool RANGE, bool FULL, bool W1>
-__device__ __forceinline__ uint32_t tile_mask(const ScanParams &P, const ScanSeg &S, const ScanTerm *T,
-                                              const uint32_t *lds_bm, uint64_t tile0, int tid) {
-  const uint64_t n = S.n;
-  uint64_t ebase[kSteps];
-  uint32_t mask = FULL ? 0xffffu : 0u;
+// One tile's filter-column registers for this thread: entries
+// tile0 + 1024k + 4*tid + j (k < kSteps, j < 4). Loaded one tile ahead of use.
+template <int NT, bool W1>
+struct TileRegs {
+  u32x4 d[kSteps], s[kSteps], e[kSteps];
+  typename std::conditional<W1, uint32_t, u32x4>::type tv[NT > 0 ? NT : 1][kSteps];  // u8 columns: one dword
+};
+
+__device__ __forceinline__ uint64_t step_base(uint64_t tile0, int k, int tid) {
+  return tile0 + uint64_t(k) * (kThreads * 4) + uint64_t(tid) * 4;
+}
+
+// Issue every load of one tile (NT < 0: the term columns are loaded in eval_tile).
+// Steps of a tile that start at or past `lim` (the workgroup's range end) re-load
+// step 0's addresses (cache hits, no extra HBM bytes) and are masked off in eval.
+__device__ __forceinline__ uint64_t load_base(uint64_t tile0, int k, int tid, uint64_t lim) {
+  const uint64_t s0 = tile0 + uint64_t(k) * kUnit;
+  return (s0 < lim ? s0 : tile0) + uint64_t(tid) * 4;
+}
+template <int NT, bool DUR, bool RANGE, bool W1>
+__device__ __forceinline__ void load_tile(TileRegs<NT, W1> &R, const ScanSeg &S, const ScanTerm *T, uint64_t tile0,
+                                          uint64_t lim, int tid) {
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
-    ebase[k] = tile0 + uint64_t(k) * (kThreads * 4) + uint64_t(tid) * 4;
-    if (!FULL)
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (ebase[k] + j < n) mask |= 1u << (4 * k + j);
-  }
-  uint4 d[kSteps], s[kSteps], e[kSteps];
-  constexpr int NTA = NT > 0 ? NT : 1;
-  uint4 tv[NTA][kSteps];
-#pragma unroll
-  for (int k = 0; k < kSteps; k++) {
-    if (DUR) d[k] = load4_u32<FULL>(S.dur32, ebase[k], n);
+    const uint64_t e = load_base(tile0, k, tid, lim);
+    if (DUR) R.d[k] = load4_u32(S.dur32, e);
     if (RANGE) {
-      s[k] = load4_u32<FULL>(S.start_s, ebase[k], n);
-      e[k] = load4_u32<FULL>(S.end_s, ebase[k], n);
+      R.s[k] = load4_u32(S.start_s, e);
+      R.e[k] = load4_u32(S.end_s, e);
     }
   }
   if (NT > 0) {
 #pragma unroll
-    for (int q = 0; q < NTA; q++)
+    for (int q = 0; q < (NT > 0 ? NT : 1); q++)
 #pragma unroll
       for (int k = 0; k < kSteps; k++) {
-        if (W1 && FULL) tv[q][k].x = *G<uint32_t>(static_cast<const uint8_t *>(T[q].col) + ebase[k]);
-        else tv[q][k] = load_col<FULL>(T[q].col, T[q].width, ebase[k], n);
+        const uint64_t e = load_base(tile0, k, tid, lim);
+        if constexpr (W1) R.tv[q][k] = *G<uint32_t>(static_cast<const uint8_t *>(T[q].col) + e);
+        else R.tv[q][k] = load_col(T[q].col, T[q].width, e);
       }
+  }
+}
+
+// Match mask of one loaded tile: bit (4k+j) <-> entry tile0 + 1024k + 4*tid + j.
+template <int NT, bool DUR, bool RANGE, bool W1>
+__device__ __forceinline__ uint32_t eval_tile(const TileRegs<NT, W1> &R, const ScanParams &P, const ScanSeg &S,
+                                              const ScanTerm *T, const uint32_t *lds_bm, uint64_t tile0,
+                                              uint64_t lim, int tid) {
+  const uint64_t n = lim;  // entries of this workgroup's range (<= the block's n)
+  uint32_t mask = kMaskAll;
+  if (tile0 + kTile > n) {  // last tile of the range
+    mask = 0;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (step_base(tile0, k, tid) + j < n) mask |= 1u << (4 * k + j);
   }
   if (DUR) {
     if (!P.need64) {  // both thresholds < 2^32-1 ns: the saturated u32 column is exact
       const uint32_t mn = uint32_t(P.min_ns), mx = uint32_t(P.max_ns);
 #pragma unroll
       for (int k = 0; k < kSteps; k++) {
-        const uint32_t dv[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+        const uint32_t dv[4] = {R.d[k].x, R.d[k].y, R.d[k].z, R.d[k].w};
 #pragma unroll
         for (int j = 0; j < 4; j++)
           if (!((!P.has_min || dv[j] >= mn) && (!P.has_max || dv[j] <= mx))) mask &= ~(1u << (4 * k + j));
@@ -332,11 +332,12 @@ __device__ __forceinline__ uint32_t tile_mask(const ScanParams &P, const ScanSeg
     } else {
 #pragma unroll
       for (int k = 0; k < kSteps; k++) {
-        const uint32_t dv[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+        const uint32_t dv[4] = {R.d[k].x, R.d[k].y, R.d[k].z, R.d[k].w};
+        const uint64_t eb = step_base(tile0, k, tid);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           uint64_t dd = dv[j];
-          if (dv[j] == 0xffffffffu && (FULL || ebase[k] + j < n)) dd = G(S.dur64)[ebase[k] + j];
+          if (dv[j] == 0xffffffffu && eb + j < n) dd = G(S.dur64)[eb + j];
           if (!((!P.has_min || dd >= P.min_ns) && (!P.has_max || dd <= P.max_ns))) mask &= ~(1u << (4 * k + j));
         }
       }
@@ -345,23 +346,24 @@ __device__ __forceinline__ uint32_t tile_mask(const ScanParams &P, const ScanSeg
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
     if (RANGE) {
-      const uint32_t sv[4] = {s[k].x, s[k].y, s[k].z, s[k].w}, ev[4] = {e[k].x, e[k].y, e[k].z, e[k].w};
+      const uint32_t sv[4] = {R.s[k].x, R.s[k].y, R.s[k].z, R.s[k].w};
+      const uint32_t ev[4] = {R.e[k].x, R.e[k].y, R.e[k].z, R.e[k].w};
 #pragma unroll
       for (int j = 0; j < 4; j++)  // req.Start <= endSeconds && req.End >= startSeconds
         if (!(P.start_s <= ev[j] && P.end_s >= sv[j])) mask &= ~(1u << (4 * k + j));
     }
     if (NT > 0) {
 #pragma unroll
-      for (int q = 0; q < NTA; q++)
+      for (int q = 0; q < (NT > 0 ? NT : 1); q++)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           bool ok;
-          if (W1) {  // u8 column, bitmap in LDS padded to 8 words: branch-free lookup
-            const uint32_t x = (tv[q][k].x >> (8 * j)) & 0xffu;
+          if constexpr (W1) {  // u8 column, bitmap in LDS padded to 8 words: branch-free lookup
+            const uint32_t x = (R.tv[q][k] >> (8 * j)) & 0xffu;
             const uint32_t w = lds_bm[T[q].lds_off + (x >> 5)];
             ok = (x < T[q].nsets) & ((w >> (x & 31)) & 1u);
           } else {
-            ok = term_ok(T[q], lds_bm, col_at(tv[q][k], T[q].width, j));
+            ok = term_ok(T[q], lds_bm, col_at(R.tv[q][k], T[q].width, j));
           }
           if (!ok) mask &= ~(1u << (4 * k + j));
         }
@@ -370,9 +372,9 @@ __device__ __forceinline__ uint32_t tile_mask(const ScanParams &P, const ScanSeg
   if (NT < 0) {
     for (uint32_t q = 0; q < S.nterms; q++) {
       const ScanTerm Tq = P.terms[S.term0 + q];
-      uint4 c[kSteps];
+      u32x4 c[kSteps];
 #pragma unroll
-      for (int k = 0; k < kSteps; k++) c[k] = load_col<FULL>(Tq.col, Tq.width, ebase[k], n);
+      for (int k = 0; k < kSteps; k++) c[k] = load_col(Tq.col, Tq.width, load_base(tile0, k, tid, lim));
 #pragma unroll
       for (int k = 0; k < kSteps; k++)
 #pragma unroll
@@ -401,6 +403,69 @@ __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsig
   return a < b ? a : b;
 }
 
+// Stores to pinned host memory (records, counts, header): relaxed system-scope
+// stores, i.e. write-through, no cache maintenance. A workgroup makes them complete
+// with one s_waitcnt before it arrives at the completion counter; no L2 writeback /
+// invalidate fence (a per-workgroup __threadfence_system() stalls the whole L2 of
+// its XCD while the other workgroups stream).
+template <typename T>
+__device__ __forceinline__ void host_store(T *p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The matches of one tile (bit 4k+j of `mask` <-> entry tile0 + 1024k + 4*tid + j)
+// in scan order (k, thread, j): ranks from a wave scan of kSteps packed 16-bit
+// per-step counts; rank r -> output slot slot_of(run + r) (~0 = not kept). Record
+// fields are gathered from the cold columns; sink(slot, words) stores one record
+// (6 x u64).
+template <class Slot, class Sink>
+__device__ __forceinline__ void emit_tile(const ScanSeg &S, uint32_t mask, uint64_t tile0, unsigned long long run,
+                                          unsigned long long *s_wsum, Slot &&slot_of, Sink &&sink) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  unsigned long long pc = 0;
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) pc |= (unsigned long long)__popc((mask >> (4 * k)) & 0xfu) << (16 * k);
+  unsigned long long inc = pc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    unsigned long long o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  __syncthreads();
+  if (lane == 63) s_wsum[wid] = inc;
+  __syncthreads();
+  unsigned long long before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; w++) {
+    if (w < wid) before += s_wsum[w];
+    tot += s_wsum[w];
+  }
+  const unsigned long long mine_ex = before + inc - pc;
+  uint32_t step_base = 0;
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) {
+    const uint32_t nib = (mask >> (4 * k)) & 0xfu;
+    uint32_t r = step_base + uint32_t((mine_ex >> (16 * k)) & 0xffff);
+    step_base += uint32_t((tot >> (16 * k)) & 0xffff);
+    for (int j = 0; j < 4; j++) {
+      if (!(nib & (1u << j))) continue;
+      const unsigned long long slot = slot_of(run + r++);
+      if (slot == ~0ull) continue;
+      const uint64_t ei = tile0 + uint64_t(k) * kUnit + uint64_t(tid) * 4 + j;
+      const u32x4 id = *G<u32x4>(S.ids + ei * 16);
+      const uint64_t st = G(S.start_ns)[ei], en = G(S.end_ns)[ei];
+      const uint64_t nm = G(reinterpret_cast<const uint64_t *>(S.names))[ei];
+      const uint32_t il = G(S.id_len)[ei];
+      const unsigned long long w[6] = {(unsigned long long)id.x | (unsigned long long)id.y << 32,
+                                       (unsigned long long)id.z | (unsigned long long)id.w << 32,
+                                       (unsigned long long)st, (unsigned long long)en,
+                                       (unsigned long long)uint32_t(ei) | (unsigned long long)(S.block_idx | (il << 24)) << 32,
+                                       (unsigned long long)nm};
+      sink(slot, w);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // search: scan + in-order compaction in one launch
 //
@@ -415,7 +480,7 @@ __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsig
 //   writes the header) look back.
 // Phase 3 (emit): records in scan order straight into the pinned host buffer.
 constexpr uint32_t kLdsTiles = 16;      // tiles per workgroup whose masks stay in LDS
-constexpr uint32_t kMaxTpw = 1024;      // tiles per workgroup (per-tile counts in LDS)
+constexpr uint32_t kMaxTpw = 2048;      // tiles per workgroup (per-tile counts in LDS)
 constexpr uint32_t kSpinMax = 1u << 22; // look-back poll bound (~seconds): never reached unless broken
 constexpr uint32_t kMaxSegs = 2048;
 
@@ -443,11 +508,16 @@ struct ArgSegs {
   __device__ unsigned long long cap_of(uint32_t s) const { return cap[s]; }
 };
 
-// Phases 1-3 for one workgroup of block `si` (bitmaps already in LDS, lds_seg zeroed).
-template <int NT, bool DUR, bool RANGE, bool W1, class Segs>
+// Phases 1-3 for one workgroup of block `si`. `init_segs` zeroes lds_seg (and
+// stages the block tables) after the scan. `issue_stage` issues
+// the loads the bitmaps need (before the first tile's loads), `wait_bitmaps` brings
+// the term bitmaps into LDS and ends with a barrier; it runs after the first tile's
+// loads are issued, so dictionary latency hides under the stream.
+template <int NT, bool DUR, bool RANGE, bool W1, bool SEG, class Segs, class Issue, class Wait, class Init>
 __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S, const ScanTerm *T, uint32_t si,
                                           const Segs &segs, const uint32_t *lds_bm, uint16_t *lds_mask,
-                                          uint32_t *lds_seg, unsigned long long t_start, uint32_t wg) {
+                                          uint32_t *lds_seg, unsigned long long *lds_rec, unsigned long long t_start,
+                                          uint32_t wg, Issue &&issue_stage, Wait &&wait_bitmaps, Init &&init_segs) {
   __shared__ uint16_t s_tc[kMaxTpw];
   __shared__ uint32_t s_wcnt[2][kThreads / 64];
   __shared__ unsigned long long s_red[kThreads / 64];
@@ -457,35 +527,91 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
     if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * 5 + k] = __builtin_amdgcn_s_memrealtime();
   };
   if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * 5] = t_start;
-  stamp(1);
 
-  // ---- phase 1: scan
-  const uint32_t lw = wg - S.first_wg;  // tiles split evenly over the block's workgroups
-  const uint32_t lt0 = uint32_t(uint64_t(lw) * S.ntiles / S.nwg);
-  const uint32_t ntl = uint32_t(uint64_t(lw + 1) * S.ntiles / S.nwg) - lt0;
+  // ---- phase 1: scan, one tile of loads in flight ahead of the tile evaluated
+  const uint32_t lw = wg - S.first_wg;  // units split evenly over the block's workgroups (+-1 unit)
+  const uint32_t u0 = uint32_t(uint64_t(lw) * S.nunits / S.nwg);
+  const uint32_t u1 = uint32_t(uint64_t(lw + 1) * S.nunits / S.nwg);
+  const uint32_t ntl = (u1 - u0 + kSteps - 1) / kSteps;
+  const uint64_t tbase = uint64_t(u0) * kUnit;
+  const uint64_t lim = min(uint64_t(u1) * kUnit, S.n);
   uint32_t wsum = 0;
-  for (uint32_t t = 0; t < ntl; t++) {
-    const uint32_t lt = lt0 + t;
-    const uint64_t tile0 = uint64_t(lt) * kTile;
-    const uint32_t mask = tile0 + kTile <= S.n ? tile_mask<NT, DUR, RANGE, true, W1>(P, S, T, lds_bm, tile0, tid)
-                                               : tile_mask<NT, DUR, RANGE, false, W1>(P, S, T, lds_bm, tile0, tid);
+  auto finish = [&](uint32_t t, uint32_t mask) {
     uint32_t c = __popc(mask);
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
     const int buf = t & 1;
     if (lane == 0) s_wcnt[buf][wid] = c;
-    __syncthreads();
+    __syncthreads();  // (LDS only: hipcc waits lgkmcnt here, the next tile's loads stay in flight)
     uint32_t tc = 0;
 #pragma unroll
     for (int w = 0; w < kThreads / 64; w++) tc += s_wcnt[buf][w];
     if (t < kLdsTiles) lds_mask[t * kThreads + tid] = uint16_t(mask);
-    else if (tc) P.mask[uint64_t(S.first_tile + lt) * kThreads + tid] = uint16_t(mask);
+    else if (tc) P.mask[(uint64_t(wg) * P.mask_tpw + t) * kThreads + tid] = uint16_t(mask);
     if (tid == 0) s_tc[t] = uint16_t(tc);
     wsum += tc;
+  };
+  TileRegs<NT, W1> ra, rb;
+  // two register sets, unrolled by two (no dynamic register indexing). Both
+  // are loaded before the bitmaps are waited for (the setup chain — descriptors,
+  // dictionary staging, match — hides under two tiles of stream); afterwards each
+  // set is refilled right after its tile is evaluated. A prefetch past the last
+  // tile re-reads the last tile (cache hit) so the load sequence stays
+  // unconditional and hipcc's vmcnt counting stays exact.
+  auto tile0 = [&](uint32_t t) { return tbase + uint64_t(min(t, ntl - 1)) * kTile; };
+  issue_stage();
+  load_tile<NT, DUR, RANGE, W1>(ra, S, T, tile0(0), lim, tid);  // (ntl >= 1: never more workgroups than units)
+  load_tile<NT, DUR, RANGE, W1>(rb, S, T, tile0(1), lim, tid);
+  wait_bitmaps();
+  stamp(1);
+  for (uint32_t t = 0;; t += 2) {
+    finish(t, eval_tile<NT, DUR, RANGE, W1>(ra, P, S, T, lds_bm, tile0(t), lim, tid));
+    if (t + 1 >= ntl) break;
+    load_tile<NT, DUR, RANGE, W1>(ra, S, T, tile0(t + 2), lim, tid);
+    finish(t + 1, eval_tile<NT, DUR, RANGE, W1>(rb, P, S, T, lds_bm, tile0(t + 1), lim, tid));
+    if (t + 2 >= ntl) break;
+    load_tile<NT, DUR, RANGE, W1>(rb, S, T, tile0(t + 3), lim, tid);
   }
 
   // ---- phase 2: publish, look back
+  // (the per-block tables the look-back needs are staged only now: their loads
+  // would otherwise sit in front of the dictionary and tile loads)
+  init_segs();
+  __syncthreads();
   stamp(2);
+  if constexpr (SEG) {
+    // segment mode: the first min(seg_cap, cap) matches of this workgroup go to its
+    // own segment of the pinned buffer, its count to counts[wg]; the host concatenates
+    // the segments in workgroup order (= scan order). No workgroup waits on another.
+    if (tid == 0) host_store(P.counts + wg, wsum);
+    stamp(3);
+    if (wsum) {
+      // records are gathered into LDS first (no gather load waits behind a host store:
+      // loads and stores share vmcnt), then copied out in one burst of write-through
+      // stores, the only host traffic the completion protocol waits for
+      const unsigned long long keep = umin64(P.seg_cap, S.cap);
+      unsigned long long run = 0;
+      for (uint32_t t = 0; t < ntl; t++) {
+        const uint32_t tc = s_tc[t];
+        if (tc == 0) continue;
+        const uint32_t mask = t < kLdsTiles ? lds_mask[t * kThreads + tid]
+                                            : G(P.mask)[(uint64_t(wg) * P.mask_tpw + t) * kThreads + tid];
+        emit_tile(S, mask, tbase + uint64_t(t) * kTile, run, s_wsum,
+                  [&](unsigned long long r) { return r < keep ? r : ~0ull; },
+                  [&](unsigned long long slot, const unsigned long long *w) {
+#pragma unroll
+                    for (int i = 0; i < 6; i++) lds_rec[slot * 6 + i] = w[i];
+                  });
+        run += tc;
+      }
+      __syncthreads();
+      const uint32_t nw = uint32_t(umin64(wsum, keep)) * 6;
+      auto *dst = reinterpret_cast<unsigned long long *>(P.out + P.hdr_bytes) + (unsigned long long)wg * P.seg_cap * 6;
+      for (uint32_t i = tid; i < nw; i += kThreads) host_store(dst + i, lds_rec[i]);
+    }
+    stamp(4);
+    return;
+  }
   const unsigned long long tag = (unsigned long long)P.epoch << 32;
   if (tid == 0) __hip_atomic_store(&P.agg[wg], tag | wsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool last = wg + 1 == P.nwg;
@@ -533,11 +659,11 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
       unsigned long long tot = 0;
       for (uint32_t s2 = tid; s2 < P.nsegs; s2 += kThreads) {
         const unsigned long long c = P.limit_mode ? umin64(lds_seg[s2], segs.cap_of(s2)) : lds_seg[s2];
-        hdr[8 + s2] = c;
+        host_store(hdr + 8 + s2, c);
         tot += c;
       }
       tot = block_sum(tot, s_red);
-      if (tid == 0) hdr[0] = tot;
+      if (tid == 0) host_store(hdr + 0, tot);
     }
   }
   stamp(3);
@@ -552,60 +678,18 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
   for (uint32_t t = 0; t < ntl; t++) {
     const uint32_t tc = s_tc[t];
     if (tc == 0) continue;
-    const uint32_t lt = lt0 + t;
     const uint32_t mask = t < kLdsTiles ? lds_mask[t * kThreads + tid]
-                                        : G(P.mask)[uint64_t(S.first_tile + lt) * kThreads + tid];
-    // ranks in scan order (k, tid, j): wave scan of 4 packed 16-bit per-step counts
-    unsigned long long pc = 0;
+                                        : G(P.mask)[(uint64_t(wg) * P.mask_tpw + t) * kThreads + tid];
+    emit_tile(S, mask, tbase + uint64_t(t) * kTile, run, s_wsum,
+              [&](unsigned long long rank_wg) -> unsigned long long {  // rank among this workgroup's matches
+                if (P.limit_mode) return seg_rank0 + rank_wg < S.cap ? base + seg_rank0 + rank_wg : ~0ull;
+                return base + rank_wg < P.out_cap ? base + rank_wg : ~0ull;
+              },
+              [&](unsigned long long slot, const unsigned long long *w) {
+                auto *d = reinterpret_cast<unsigned long long *>(out + slot);
 #pragma unroll
-    for (int k = 0; k < kSteps; k++) pc |= (unsigned long long)__popc((mask >> (4 * k)) & 0xfu) << (16 * k);
-    unsigned long long inc = pc;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      unsigned long long o = __shfl_up(inc, d, 64);
-      if (lane >= d) inc += o;
-    }
-    __syncthreads();
-    if (lane == 63) s_wsum[wid] = inc;
-    __syncthreads();
-    unsigned long long before = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kThreads / 64; w++) {
-      if (w < wid) before += s_wsum[w];
-      tot += s_wsum[w];
-    }
-    const unsigned long long mine_ex = before + inc - pc;
-    uint32_t step_base = 0;
-#pragma unroll
-    for (int k = 0; k < kSteps; k++) {
-      const uint32_t nib = (mask >> (4 * k)) & 0xfu;
-      uint32_t r = step_base + uint32_t((mine_ex >> (16 * k)) & 0xffff);
-      step_base += uint32_t((tot >> (16 * k)) & 0xffff);
-      for (int j = 0; j < 4; j++) {
-        if (!(nib & (1u << j))) continue;
-        const unsigned long long rank_wg = run + r++;  // rank among this workgroup's matches
-        unsigned long long slot;
-        if (P.limit_mode) {
-          if (seg_rank0 + rank_wg >= S.cap) continue;
-          slot = base + seg_rank0 + rank_wg;
-        } else {
-          slot = base + rank_wg;
-          if (slot >= P.out_cap) continue;
-        }
-        const uint64_t ei = uint64_t(lt) * kTile + uint64_t(k) * (kThreads * 4) + uint64_t(tid) * 4 + j;
-        MatchRec *dst = out + slot;
-        const u32x4 id = *G<u32x4>(S.ids + ei * 16);
-        const uint64_t st = G(S.start_ns)[ei], en = G(S.end_ns)[ei];
-        const uint64_t nm = G(reinterpret_cast<const uint64_t *>(S.names))[ei];
-        const uint32_t il = G(S.id_len)[ei];
-        *reinterpret_cast<u32x4 *>(dst->id) = id;
-        dst->start = st;
-        dst->end = en;
-        dst->entry = uint32_t(ei);
-        dst->block_il = S.block_idx | (il << 24);
-        *reinterpret_cast<uint64_t *>(&dst->svc) = nm;
-      }
-    }
+                for (int i = 0; i < 6; i++) d[i] = w[i];
+              });
     run += tc;
   }
   stamp(4);
@@ -628,15 +712,19 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
   if (NT > 0)
 #pragma unroll
     for (int q = 0; q < NTA; q++) T[q] = P.terms[S.term0 + q];
-  for (uint32_t q = 0; q < S.nterms; q++) {  // stage the small bitmaps in LDS
-    const ScanTerm &Tq = P.terms[S.term0 + q];
-    if (Tq.lds_off != kNoLds)
-      for (uint32_t w = tid; w < Tq.bm_words; w += kThreads) lds_bm[Tq.lds_off + w] = Tq.bm[w];
-  }
-  for (uint32_t i = tid; i < P.nsegs; i += kThreads) lds_seg[i] = 0;
-  __syncthreads();
-  scan_emit<NT, DUR, RANGE, W1>(P, S, T, si, DescSegs{P.wg_seg, P.segs}, lds_bm, lds_mask, lds_seg, t_start,
-                                blockIdx.x);
+  scan_emit<NT, DUR, RANGE, W1, false>(P, S, T, si, DescSegs{P.wg_seg, P.segs}, lds_bm, lds_mask, lds_seg, nullptr, t_start,
+                                blockIdx.x, [] {}, [&] {
+                                  for (uint32_t q = 0; q < S.nterms; q++) {  // stage the small bitmaps in LDS
+                                    const ScanTerm &Tq = P.terms[S.term0 + q];
+                                    if (Tq.lds_off != kNoLds)
+                                      for (uint32_t w = tid; w < Tq.bm_words; w += kThreads)
+                                        lds_bm[Tq.lds_off + w] = Tq.bm[w];
+                                  }
+                                  __syncthreads();
+                                },
+                                [&] {
+                                  for (uint32_t i = tid; i < P.nsegs; i += kThreads) lds_seg[i] = 0;
+                                });
 }
 
 // ------------------------------------------------------------------------------------
@@ -654,16 +742,18 @@ struct QArgs {
   const DevBlockDesc *blk[kArgSegs];
   unsigned long long cap[kArgSegs];  // records kept per block (limit mode)
   uint32_t first_wg[kArgSegs + 1];   // scan workgroup numbering (without the dictionary workgroups)
-  uint32_t first_tile[kArgSegs];
   uint32_t block_idx[kArgSegs];
   uint16_t key_of[kArgSegs][kArgTerms];
   uint16_t nd_off[kArgTerms + 1];
-  uint8_t needles[kArgNeedle];
+  alignas(16) uint8_t needles[kArgNeedle];  // (aligned: read as dwords by scalar loads)
   uint32_t nsegs, nterms, njobs, gstride;  // dictionary jobs = nsegs x nterms, granules per job
   uint32_t bm_words, stage_words;
+  uint32_t mask_words;      // LDS words between the bitmaps and the block sums: tile masks / self-match stage
+  uint32_t self_dict;       // 1: every scan workgroup matches its block's (small) dictionaries itself, njobs = 0
   unsigned long long *gbm;  // njobs x gstride granules
   ScanParams P;             // thresholds, outputs (segs/terms/wg_seg unused)
 };
+static_assert(sizeof(QArgs) <= 4096, "kernel arguments");
 
 // bytes.Contains over LDS-staged bytes
 __device__ __forceinline__ bool lds_contains(const uint8_t *h, uint32_t hl, const uint8_t *nd, uint32_t nl) {
@@ -679,8 +769,28 @@ __device__ __forceinline__ bool lds_contains(const uint8_t *h, uint32_t hl, cons
   return false;
 }
 
-__device__ __forceinline__ const DevKeyDesc &key_desc(const DevBlockDesc *B, uint32_t k) {
-  return reinterpret_cast<const DevKeyDesc *>(B + 1)[k];
+// Resident descriptors are immutable while a search runs: read them through the
+// constant address space so uniform reads become scalar loads (s_load, one round
+// trip for all fields) instead of vector loads serialised by vmcnt.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T *K4(const T *p) {
+  return (const __attribute__((address_space(4))) T *)(p);
+}
+__device__ __forceinline__ DevKeyDesc key_desc(const DevBlockDesc *B, uint32_t k) {
+  const auto *p = K4(reinterpret_cast<const DevKeyDesc *>(B + 1)) + k;
+  DevKeyDesc r;
+  r.col = p->col;
+  r.dict_bytes = p->dict_bytes;
+  r.dict_off = p->dict_off;
+  r.set_off = p->set_off;
+  r.set_vals = p->set_vals;
+  r.width = p->width;
+  r.nvals = p->nvals;
+  r.nsets = p->nsets;
+  r.identity = p->identity;
+  r.dict_nbytes = p->dict_nbytes;
+  r.nsetvals = p->nsetvals;
+  return r;
 }
 
 // One dictionary workgroup: job j = (block s, term q).
@@ -733,7 +843,131 @@ __device__ __forceinline__ void dict_job(const QArgs &A, uint32_t j, uint32_t *s
   }
 }
 
-template <int NT, bool DUR, bool RANGE, bool W1>
+// Small dictionaries (every term's blob of the block fits kSelfWords in all): the
+// scan workgroup matches them itself, straight into its LDS bitmaps, with no
+// cross-workgroup wait. Same per-value test and set rule as dict_job.
+// The staging loads go into registers (kSelfPer words per thread, no loop) and are
+// issued BEFORE the first tile's loads: vmcnt retires loads in order, so waiting
+// for the dictionary words does not wait for the tile stream behind them.
+constexpr uint32_t kSelfWords = 4096;
+constexpr int kSelfPer = int(kSelfWords / kThreads);
+template <int NTA>
+struct SelfStage {
+  const uint32_t *src[NTA];  // key blobs [off | bytes | set_off | set_vals]
+  uint32_t cum[NTA + 1];     // blob word prefix over the terms
+  uint32_t base[NTA];        // LDS word offset of each term's staged blob (+ value bits after it)
+  uint32_t nvals[NTA], nsets[NTA], bw[NTA], identity[NTA];
+  uint32_t w[kSelfPer];
+};
+
+template <int NTA>
+__device__ __forceinline__ void self_issue(SelfStage<NTA> &X, const DevKeyDesc *KD) {
+  const int tid = threadIdx.x;
+  uint32_t c = 0, o = 0;
+#pragma unroll
+  for (int q = 0; q < NTA; q++) {  // (one-launch kernels: NTA == nterms)
+    const DevKeyDesc &K = KD[q];
+    X.cum[q] = c;
+    X.base[q] = o;
+    X.src[q] = K.dict_off;
+    X.nvals[q] = K.nvals;
+    X.nsets[q] = K.nsets;
+    X.identity[q] = K.identity;
+    X.bw[q] = (K.dict_nbytes + 3) / 4;
+    const uint32_t words = K.nvals + 1 + X.bw[q] + (K.identity ? 0u : K.nsets + 1 + K.nsetvals);
+    c += words;
+    o += words + (K.identity ? 0u : (K.nvals + 63) / 32);  // + value bits of a non-identity key
+  }
+  X.cum[NTA] = c;
+  // lanes past the staged total skip their load (every workgroup of the block
+  // reads the same few lines: redundant requests queue on one L2 channel)
+#pragma unroll
+  for (int r = 0; r < kSelfPer; r++) {
+    const uint32_t i = uint32_t(tid) + uint32_t(r) * kThreads;
+    if (i >= c) continue;
+    const uint32_t *src = X.src[0];
+    uint32_t cq = 0;
+#pragma unroll
+    for (int q2 = 1; q2 < NTA; q2++)
+      if (i >= X.cum[q2]) {
+        src = X.src[q2];
+        cq = X.cum[q2];
+      }
+    X.w[r] = G(src)[i - cq];
+  }
+}
+
+template <int NTA>
+__device__ __forceinline__ void self_finish(SelfStage<NTA> &X, const QArgs &A, const ScanTerm *T, uint32_t *lds_bm,
+                                            uint32_t *scratch) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_nd2w[kArgNeedle / 4];
+  const uint8_t *s_nd2 = reinterpret_cast<const uint8_t *>(s_nd2w);
+  const int tid = threadIdx.x, lane = tid & 63;
+  // needles: uniform loop, scalar kernel-argument loads (lgkmcnt, not behind the
+  // tile loads in the vmcnt queue)
+  if (tid == 0) {
+    const uint32_t nw = (uint32_t(A.nd_off[NTA]) + 3) / 4;
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (uint32_t w = 0; w < nw; w++) s_nd2w[w] = reinterpret_cast<const uint32_t *>(A.needles)[w];
+  }
+#pragma unroll
+  for (int r = 0; r < kSelfPer; r++) {
+    const uint32_t i = uint32_t(tid) + uint32_t(r) * kThreads;
+    if (i < X.cum[NTA]) {
+      uint32_t dst = X.base[0] + i - X.cum[0];
+#pragma unroll
+      for (int q2 = 1; q2 < NTA; q2++)
+        if (i >= X.cum[q2]) dst = X.base[q2] + i - X.cum[q2];
+      scratch[dst] = X.w[r];
+    }
+  }
+  __syncthreads();
+  bool sets = false;
+#pragma unroll
+  for (int q = 0; q < NTA; q++) {
+    {
+      const uint32_t *off = scratch + X.base[q];
+      const uint8_t *b8 = reinterpret_cast<const uint8_t *>(off + X.nvals[q] + 1);
+      const uint8_t *nd = s_nd2 + A.nd_off[q];
+      const uint32_t nl = A.nd_off[q + 1] - A.nd_off[q];
+      // value set == value: straight into the term bitmap; else value bits after the blob
+      uint32_t *bits = X.identity[q] ? lds_bm + T[q].lds_off : scratch + X.base[q] + (X.cum[q + 1] - X.cum[q]);
+      sets |= !X.identity[q];
+      for (uint32_t v0 = 0; v0 < X.nvals[q]; v0 += kThreads) {
+        const uint32_t v = v0 + tid;
+        bool m = false;
+        if (v < X.nvals[q]) m = lds_contains(b8 + off[v], off[v + 1] - off[v], nd, nl);
+        const unsigned long long b = __ballot(m);
+        const uint32_t w0 = (v - lane) >> 5;
+        if (lane == 0 && w0 * 32 < X.nvals[q]) bits[w0] = uint32_t(b);
+        if (lane == 32 && (w0 + 1) * 32 < X.nvals[q]) bits[w0 + 1] = uint32_t(b >> 32);
+      }
+    }
+  }
+  __syncthreads();
+  if (!sets) return;
+#pragma unroll
+  for (int q = 0; q < NTA; q++) {  // a set matches iff one of its values does
+    if (!X.identity[q]) {
+      const uint32_t *soff = scratch + X.base[q] + X.nvals[q] + 1 + X.bw[q];
+      const uint32_t *svals = soff + X.nsets[q] + 1;
+      const uint32_t *vbits = scratch + X.base[q] + (X.cum[q + 1] - X.cum[q]);
+      for (uint32_t s0 = 0; s0 < X.nsets[q]; s0 += kThreads) {
+        const uint32_t sid = s0 + tid;
+        bool m = false;
+        if (sid < X.nsets[q])
+          for (uint32_t i = soff[sid]; i < soff[sid + 1] && !m; i++) m = (vbits[svals[i] >> 5] >> (svals[i] & 31)) & 1u;
+        const unsigned long long b = __ballot(m);
+        const uint32_t w0 = (sid - lane) >> 5;
+        if (lane == 0 && w0 * 32 < X.nsets[q]) lds_bm[T[q].lds_off + w0] = uint32_t(b);
+        if (lane == 32 && (w0 + 1) * 32 < X.nsets[q]) lds_bm[T[q].lds_off + w0 + 1] = uint32_t(b >> 32);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int NT, bool DUR, bool RANGE, bool W1, bool SEG>
 __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   const unsigned long long t_start = A.P.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -744,28 +978,38 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   // scan workgroup: [bitmaps bm_words | kLdsTiles masks | seg sums nsegs | first_wg nsegs+1 | caps]
   uint32_t *lds_bm = lds;
   uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + A.bm_words);
-  uint32_t *lds_seg = lds + A.bm_words + kLdsTiles * kThreads / 2;
+  uint32_t *lds_seg = lds + A.bm_words + A.mask_words;
   uint32_t *lds_fw = lds_seg + A.nsegs;
   unsigned long long *lds_cap = reinterpret_cast<unsigned long long *>(lds_fw + ((A.nsegs + 2) & ~1u));
+  unsigned long long *lds_rec = lds_cap + A.nsegs;  // segment mode: kSegMax staged records
   const int tid = threadIdx.x;
   const uint32_t wg = blockIdx.x - A.njobs;
-  uint32_t si = 0;
-  for (uint32_t s2 = 1; s2 < A.nsegs; s2++)
-    if (A.first_wg[s2] <= wg) si = s2;
+  uint32_t si = 0;  // (fixed trip count: every first_wg load issues in one round trip)
+#pragma unroll
+  for (int s2 = 1; s2 < kArgSegs; s2++) si += (uint32_t(s2) < A.nsegs && A.first_wg[s2] <= wg) ? 1u : 0u;
+  // wave-uniform: descriptor reads become scalar loads (one round trip, not vmcnt-serialised)
+  si = __builtin_amdgcn_readfirstlane(si);
   const DevBlockDesc *B = A.blk[si];
+  constexpr int NTA = NT > 0 ? NT : 1;
+  DevKeyDesc KD[NTA];  // scalar loads, all issued together (one-launch kernels: NT == nterms)
+  if (NT > 0)
+#pragma unroll
+    for (int q = 0; q < NTA; q++) KD[q] = key_desc(B, A.key_of[si][q]);
   ScanSeg S;
-  S.n = B->n;
-  S.dur32 = B->dur32;
-  S.dur64 = B->dur64;
-  S.start_s = B->start_s;
-  S.end_s = B->end_s;
-  S.ids = B->ids;
-  S.start_ns = B->start_ns;
-  S.end_ns = B->end_ns;
-  S.names = B->names;
-  S.id_len = B->id_len;
-  S.first_tile = A.first_tile[si];
-  S.ntiles = uint32_t((S.n + kTile - 1) / kTile);
+  {
+    const auto *Bc = K4(B);
+    S.n = Bc->n;
+    S.dur32 = Bc->dur32;
+    S.dur64 = Bc->dur64;
+    S.start_s = Bc->start_s;
+    S.end_s = Bc->end_s;
+    S.ids = Bc->ids;
+    S.start_ns = Bc->start_ns;
+    S.end_ns = Bc->end_ns;
+    S.names = Bc->names;
+    S.id_len = Bc->id_len;
+  }
+  S.nunits = uint32_t((S.n + kUnit - 1) / kUnit);
   S.first_wg = A.first_wg[si];
   S.nwg = A.first_wg[si + 1] - S.first_wg;
   S.tpw = 0;
@@ -774,21 +1018,14 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   S.lds_words = A.bm_words;
   S.block_idx = A.block_idx[si];
   S.cap = A.cap[si];
-  for (uint32_t i = tid; i < A.nsegs; i += kThreads) {
-    lds_seg[i] = 0;
-    lds_fw[i] = A.first_wg[i];
-    lds_cap[i] = A.cap[i];
-  }
-  if (tid == 0) lds_fw[A.nsegs] = A.first_wg[A.nsegs];
-  constexpr int NTA = NT > 0 ? NT : 1;
   ScanTerm T[NTA];
   uint32_t gw[NTA + 1];  // granule prefix over this block's terms
   gw[0] = 0;
   uint32_t bmo = 0;
 #pragma unroll
   for (int q = 0; q < NTA; q++) {
-    if (q >= int(A.nterms)) break;
-    const DevKeyDesc &K = key_desc(B, A.key_of[si][q]);
+    if (NT <= 0) break;
+    const DevKeyDesc &K = KD[q];
     T[q].col = K.col;
     T[q].bm = nullptr;
     T[q].width = K.width;
@@ -798,34 +1035,74 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
     bmo += W1 ? 8u : T[q].bm_words;
     gw[q + 1] = gw[q] + T[q].bm_words;
   }
-  // bitmaps: poll this block's granules (one per thread), then LDS
-  if (NT > 0) {
-    const unsigned long long tag = (unsigned long long)A.P.epoch << 32;
-    for (uint32_t i = tid; i < gw[A.nterms]; i += kThreads) {
-      uint32_t q = 0;
+  // bitmaps: poll this block's granules (one per thread) into LDS, after the first
+  // tile's loads are in flight
+  SelfStage<NTA> X;
+  auto issue_stage = [&] {
+    if (NT > 0 && A.self_dict) self_issue<NTA>(X, KD);
+  };
+  auto wait_bitmaps = [&] {
+    if (NT > 0 && A.self_dict) {  // (self_finish ends with a barrier)
+      self_finish<NTA>(X, A, T, lds_bm, lds + A.bm_words);
+      return;
+    }
+    if (NT > 0) {
+      const unsigned long long tag = (unsigned long long)A.P.epoch << 32;
+      for (uint32_t i = tid; i < gw[A.nterms]; i += kThreads) {
+        uint32_t q = 0;
 #pragma unroll
-      for (int q2 = 1; q2 < NTA; q2++)
-        if (i >= gw[q2]) q = q2;
-      const unsigned long long *g = A.gbm + uint64_t(si * A.nterms + q) * A.gstride + (i - gw[q]);
-      unsigned long long v;
-      uint32_t spins = 0;
-      while (((v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~0xffffffffull) != tag) {
-        if (++spins > kSpinMax) {
-          reinterpret_cast<volatile unsigned long long *>(A.P.out)[1] = 1;  // host fails the query
-          break;
+        for (int q2 = 1; q2 < NTA; q2++)
+          if (i >= gw[q2]) q = q2;
+        const unsigned long long *g = A.gbm + uint64_t(si * A.nterms + q) * A.gstride + (i - gw[q]);
+        unsigned long long v;
+        uint32_t spins = 0;
+        while (((v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~0xffffffffull) != tag) {
+          if (++spins > kSpinMax) {
+            reinterpret_cast<volatile unsigned long long *>(A.P.out)[1] = 1;  // host fails the query
+            break;
+          }
+          __builtin_amdgcn_s_sleep(4);
         }
-        __builtin_amdgcn_s_sleep(4);
-      }
-      uint32_t lo = 0;
+        uint32_t lo = 0;
 #pragma unroll
-      for (int q2 = 0; q2 < NTA; q2++)
-        if (q2 == int(q)) lo = T[q2].lds_off;
-      lds_bm[lo + (i - gw[q])] = uint32_t(v);
+        for (int q2 = 0; q2 < NTA; q2++)
+          if (q2 == int(q)) lo = T[q2].lds_off;
+        lds_bm[lo + (i - gw[q])] = uint32_t(v);
+      }
+    }
+    __syncthreads();
+  };
+  scan_emit<NT, DUR, RANGE, W1, SEG>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, A.nsegs}, lds_bm, lds_mask, lds_seg,
+                                     lds_rec, t_start, wg, issue_stage, wait_bitmaps, [&] {
+                                       if constexpr (!SEG) {
+                                         for (uint32_t i = tid; i < A.nsegs; i += kThreads) {
+                                           lds_seg[i] = 0;
+                                           lds_fw[i] = A.first_wg[i];
+                                           lds_cap[i] = A.cap[i];
+                                         }
+                                         if (tid == 0) lds_fw[A.nsegs] = A.first_wg[A.nsegs];
+                                       }
+                                     });
+  // completion: the last scan workgroup raises the flag the host polls (header word 2 =
+  // epoch). Arrivals are counted per XCD group (blockIdx % 8: a group label, speed
+  // only) and the last of each group arrives at the top counter, so no single word
+  // takes a thousand atomics at the end of the launch. Every workgroup's record and
+  // count stores (system-scope write-through) have completed before it arrives.
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t g = blockIdx.x & 7u;
+    // (relaxed: the only data behind the flag is host memory written through at system
+    // scope, already complete; an acquire/release here would write back / invalidate L2)
+    const unsigned prev = __hip_atomic_fetch_add(A.P.done + 32 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1u == A.P.done_target[g]) {
+      const unsigned top = __hip_atomic_fetch_add(A.P.done + 32 * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (top + 1u == A.P.done_top) {
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(A.P.out) + 2, (unsigned long long)A.P.epoch,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
-  __syncthreads();
-  scan_emit<NT, DUR, RANGE, W1>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, A.nsegs}, lds_bm, lds_mask, lds_seg,
-                                t_start, wg);
 }
 
 // ------------------------------------------------------------------------------------
@@ -834,21 +1111,26 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 using ScanFn = void (*)(ScanParams);
 using FastFn = void (*)(QArgs);
-template <int NT, bool W1>
+template <int NT, bool W1, bool SEG>
 static FastFn pick3_fast(bool dur, bool range) {
-  if (dur && range) return search_fast_kernel<NT, true, true, W1>;
-  if (dur) return search_fast_kernel<NT, true, false, W1>;
-  if (range) return search_fast_kernel<NT, false, true, W1>;
-  return search_fast_kernel<NT, false, false, W1>;
+  if (dur && range) return search_fast_kernel<NT, true, true, W1, SEG>;
+  if (dur) return search_fast_kernel<NT, true, false, W1, SEG>;
+  if (range) return search_fast_kernel<NT, false, true, W1, SEG>;
+  return search_fast_kernel<NT, false, false, W1, SEG>;
 }
-static FastFn pick_fast(uint32_t nterms, bool dur, bool range, bool w1) {
+template <bool SEG>
+static FastFn pick_fast_t(uint32_t nterms, bool dur, bool range, bool w1) {
   switch (nterms) {
-    case 0: return pick3_fast<0, false>(dur, range);
-    case 1: return w1 ? pick3_fast<1, true>(dur, range) : pick3_fast<1, false>(dur, range);
-    case 2: return w1 ? pick3_fast<2, true>(dur, range) : pick3_fast<2, false>(dur, range);
-    case 3: return w1 ? pick3_fast<3, true>(dur, range) : pick3_fast<3, false>(dur, range);
-    default: return w1 ? pick3_fast<4, true>(dur, range) : pick3_fast<4, false>(dur, range);
+    case 0: return pick3_fast<0, false, SEG>(dur, range);
+    case 1: return w1 ? pick3_fast<1, true, SEG>(dur, range) : pick3_fast<1, false, SEG>(dur, range);
+    case 2: return w1 ? pick3_fast<2, true, SEG>(dur, range) : pick3_fast<2, false, SEG>(dur, range);
+    case 3: return w1 ? pick3_fast<3, true, SEG>(dur, range) : pick3_fast<3, false, SEG>(dur, range);
+    default: return w1 ? pick3_fast<4, true, SEG>(dur, range) : pick3_fast<4, false, SEG>(dur, range);
   }
+}
+// seg: segment-mode kernel (dynamic tiles, per-tile segments) vs look-back mode
+static FastFn pick_fast(uint32_t nterms, bool dur, bool range, bool w1, bool seg) {
+  return seg ? pick_fast_t<true>(nterms, dur, range, w1) : pick_fast_t<false>(nterms, dur, range, w1);
 }
 template <int NT, bool W1>
 static ScanFn pick3(bool dur, bool range) {
@@ -934,7 +1216,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     needles.insert(needles.end(), q.values[t], q.values[t] + q.value_lens[t]);
   }
   const bool has_dur = q.has_min || q.has_max;
-  uint32_t vmatch_total = 0, bm_total = 0, items = 0, tiles = 0, max_lds_words = 0;
+  uint32_t vmatch_total = 0, bm_total = 0, items = 0, units = 0, max_lds_words = 0;
   uint64_t dict_bytes = 0, scan_bytes = 0, n_all = 0;
   bool all_w1 = true;
   constexpr uint32_t kLdsBudgetWords = 8192;  // 32 KiB per workgroup
@@ -942,7 +1224,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // workgroups need to match the dictionaries themselves
   std::vector<std::array<uint16_t, kArgTerms>> seg_keys;
   std::vector<const DevBlockDesc *> seg_desc;
-  uint32_t fast_stage = 0, fast_bm = 0, fast_bm8 = 0, fast_vbits = 0, fast_words = 1;
+  uint32_t fast_stage = 0, fast_bm = 0, fast_bm8 = 0, fast_vbits = 0, fast_words = 1, fast_self = 0;
   for (auto &bp : blocks) {
     Block &b = *bp.second;
     const DevBlock &d = b.dev;
@@ -1015,7 +1297,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     max_lds_words = std::max(max_lds_words, sg.lds_words);
     {
       std::array<uint16_t, kArgTerms> ks{};
-      uint32_t bmw = 0, bmw8 = 0;
+      uint32_t bmw = 0, bmw8 = 0, selfw = 0;
       for (uint32_t t = 0; t < q.nterms && t < kArgTerms; t++) {
         const DevKey &k = d.keys[size_t(kidx[t])];
         ks[t] = uint16_t(kidx[t]);
@@ -1023,6 +1305,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
         if (!k.identity) stage += k.nsets + 1 + k.nsetvals;
         if (k.dict_nbytes > (1u << 20) || k.nvals > (1u << 20) || kidx[t] > 0xffff) stage = 0xfffffffu;
         fast_stage = std::max(fast_stage, stage);
+        selfw += stage + (k.identity ? 0u : (k.nvals + 63) / 32);
         fast_vbits = std::max(fast_vbits, (k.nvals + 63) / 32);
         fast_words = std::max(fast_words, (k.nsets + 31) / 32);
         bmw += (k.nsets + 31) / 32;
@@ -1032,10 +1315,10 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       seg_desc.push_back(d.desc);
       fast_bm = std::max(fast_bm, bmw);
       fast_bm8 = std::max(fast_bm8, bmw8);
+      fast_self = std::max(fast_self, std::min(selfw, 0xfffffffu));
     }
-    sg.first_tile = tiles;
-    sg.ntiles = uint32_t((d.n + kTile - 1) / kTile);
-    tiles += sg.ntiles;
+    sg.nunits = uint32_t((d.n + kUnit - 1) / kUnit);
+    units += sg.nunits;
     sg.cap = limit ? std::min<uint64_t>(limit, d.n) : d.n;
     scan_bytes += d.n * per;
     n_all += d.n;
@@ -1056,12 +1339,30 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // workgroups: about one resident wave of them (occupancy x CUs), each owning a
   // contiguous tile range of one block
   const ScanFn scan_fn = fast ? nullptr : pick_scan(q.nterms, has_dur, q.has_range, all_w1);
-  const FastFn fast_fn = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1) : nullptr;
-  const void *kfn = fast ? reinterpret_cast<const void *>(fast_fn) : reinterpret_cast<const void *>(scan_fn);
+  // result mode, decided before the kernel is picked (see "Result modes" below)
+  constexpr uint32_t kSegMax = 256;
+  constexpr uint64_t kSegBudget = 64ull << 20;  // pinned bytes of segment records (workgroups <= 8 per CU)
+  auto seg_fits = [&](uint32_t c) {
+    return fast && !dc.seg_off && c > 0 && c <= kSegMax &&
+           uint64_t(dc.num_cu) * 8 * c * sizeof(MatchRec) <= kSegBudget;
+  };
+  uint32_t seg = limit ? limit : dc.seg_cap;
+  if (!seg_fits(seg)) seg = 0;
+  const FastFn fast_seg = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, true) : nullptr;
+  const FastFn fast_lb = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, false) : nullptr;
+  const void *kfn = fast ? reinterpret_cast<const void *>(seg ? fast_seg : fast_lb)
+                         : reinterpret_cast<const void *>(scan_fn);
   // fast LDS: scan workgroups [bitmaps | masks | seg sums | first_wg | caps], dictionary
   // workgroups [value bits | stage]; the launch takes the larger
-  const uint32_t fast_bm_words = uint32_t(align_up(std::max(all_w1 ? fast_bm8 : fast_bm, fast_vbits), 2));
-  const uint32_t fast_scan_words = kLdsTiles * kThreads / 2 + nsegs + ((nsegs + 2) & ~1u) + 2 * nsegs;
+  // self-match: every block's dictionaries for this query fit one workgroup's LDS
+  // stage, so no dictionary workgroups and no cross-workgroup wait
+  const bool self_dict = fast && !dc.self_off && q.nterms > 0 && fast_self <= kSelfWords;
+  const uint32_t fast_bm_words =
+      uint32_t(align_up(std::max(all_w1 ? fast_bm8 : fast_bm, self_dict ? 0u : fast_vbits), 2));
+  const uint32_t fast_mask_words =
+      std::max<uint32_t>(kLdsTiles * kThreads / 2, self_dict ? uint32_t(align_up(fast_self, 4)) : 0u);
+  const uint32_t fast_scan_words = fast_mask_words + nsegs + ((nsegs + 2) & ~1u) + 2 * nsegs +
+                                   (seg ? kSegMax * uint32_t(sizeof(MatchRec) / 4) : 0u);
   const uint32_t lds_words = fast ? fast_bm_words + std::max<uint32_t>(fast_scan_words, uint32_t(align_up(fast_stage, 4)))
                                   : max_lds_words + kLdsTiles * kThreads / 2 + nsegs;
   int &per_cu = dc.occupancy[{kfn, size_t(lds_words) * 4}];
@@ -1069,16 +1370,27 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kThreads, size_t(lds_words) * 4));
     per_cu = std::max(1, std::min(per_cu, 8));
   }
-  const uint32_t target_wg = uint32_t(dc.num_cu) * uint32_t(per_cu);
-  // workgroups per block in proportion to its tiles, the tiles of a block split
-  // evenly over its workgroups: every CU gets the same load (+-1 tile)
+  // every workgroup of the launch resident at once: a workgroup dispatched only
+  // when another retires starts a full scan slice late and the in-order look-back
+  // waits for it. The one-launch grid also holds the dictionary workgroups.
+  const uint32_t slots = uint32_t(dc.num_cu) * uint32_t(per_cu);
+  const uint32_t njobs_fast = fast && !self_dict ? nsegs * q.nterms : 0;
+  const uint32_t target_wg = slots > njobs_fast + uint32_t(dc.num_cu) ? slots - njobs_fast : uint32_t(dc.num_cu);
+  // workgroups per block in proportion to its units, the units of a block split
+  // evenly over its workgroups: every CU gets the same load (+-1 unit of 1024 entries)
   uint32_t nwg = 0, tpw = 1;
+  uint64_t units_before = 0;
   for (auto &sg : segs) {
-    uint64_t w = (uint64_t(target_wg) * sg.ntiles + tiles / 2) / tiles;
-    w = std::max<uint64_t>(1, std::min<uint64_t>(w, sg.ntiles));
+    // cumulative rounding: the block gets round(target * units_through / units)
+    // minus what earlier blocks got, so the grid never exceeds target_wg (+1 per
+    // block only where a block would otherwise get none)
+    const uint64_t hi = (uint64_t(target_wg) * (units_before + sg.nunits) + units / 2) / units;
+    units_before += sg.nunits;
+    uint64_t w = hi > nwg ? hi - nwg : 0;
+    w = std::max<uint64_t>(1, std::min<uint64_t>(w, (sg.nunits + kSteps - 1) / kSteps));  // <= its tiles
     sg.first_wg = nwg;
     sg.nwg = uint32_t(w);
-    sg.tpw = uint32_t((sg.ntiles + w - 1) / w);
+    sg.tpw = uint32_t(((sg.nunits + w - 1) / w + kSteps - 1) / kSteps);
     tpw = std::max(tpw, sg.tpw);
     nwg += sg.nwg;
   }
@@ -1087,22 +1399,32 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   tr.mark("plan");
 
   // ---- scratch
-  if (tpw > kLdsTiles) dc.maskbits.ensure(size_t(tiles) * kThreads * 2);
+  if (tpw > kLdsTiles) dc.maskbits.ensure(size_t(nwg) * tpw * kThreads * 2);
   if (dc.agg.ensure(size_t(nwg) * 8)) HIP_OK(hipMemsetAsync(dc.agg.p, 0, dc.agg.cap, s));  // no stale epochs
+  if (fast && dc.done.ensure(9 * 128)) {  // completion counters: zeroed once, then monotonic
+    HIP_OK(hipMemsetAsync(dc.done.p, 0, dc.done.cap, s));
+    std::fill(std::begin(dc.done_base), std::end(dc.done_base), 0u);
+  }
   const size_t hdr_bytes = align_up(64 + 8 * segs.size(), 256);
   uint64_t n_total = 0, cap_total = 0;
-  for (auto &sg : segs) {
-    n_total += sg.n;
-    cap_total += sg.cap;
+  for (size_t i = 0; i < segs.size(); i++) {
+    n_total += segs[i].n;
+    cap_total += segs[i].cap;
   }
-  // limit 0: start from the capacity the result buffer already has (>= 2^16
-  // records); a larger match count re-runs the launch into a grown buffer
-  const uint64_t have = dc.hres.cap > hdr_bytes ? (dc.hres.cap - hdr_bytes) / sizeof(MatchRec) : 0;
-  uint64_t out_cap = limit ? cap_total : std::min<uint64_t>(n_total, std::max<uint64_t>(have, 1u << 16));
-  // [header | records] go straight to pinned host memory (no D2H copy, no copy kernel)
-  dc.hres.ensure(hdr_bytes + std::max<size_t>(out_cap, 1) * sizeof(MatchRec));
-  uint8_t *ho = static_cast<uint8_t *>(dc.hres.p);
+  const size_t cnt_bytes = align_up(size_t(nwg) * 4, 256);
+  // Result modes (the records go straight to pinned host memory: no D2H copy).
+  //  segment (one-launch path): a segment of seg_cap records per workgroup, no
+  //    look-back; limit L: segments of L; limit 0: seg_cap follows the largest
+  //    per-workgroup count seen on this device (an overflow re-runs with larger
+  //    segments, or in look-back mode beyond kSegMax)
+  //  look-back: one record array; limit 0 starts from the capacity the buffer already
+  //    has (>= 2^16 records) and a larger match count re-runs into a grown buffer
+  auto lb_cap = [&]() -> uint64_t {
+    const uint64_t have = dc.hres.cap > hdr_bytes ? (dc.hres.cap - hdr_bytes) / sizeof(MatchRec) : 0;
+    return limit ? cap_total : std::min<uint64_t>(n_total, std::max<uint64_t>(have, 1u << 16));
+  };
   const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
+  const bool time_defer = flags & TSG_SEARCH_TIME_DEFER;
 
   ScanParams P{};
   P.nsegs = nsegs;
@@ -1116,11 +1438,19 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   P.start_s = q.start_s;
   P.end_s = q.end_s;
   P.mask = static_cast<uint16_t *>(dc.maskbits.p);
+  P.mask_tpw = tpw;
   P.agg = static_cast<unsigned long long *>(dc.agg.p);
   P.lds_bm_words = max_lds_words;
-  P.out = ho;
-  P.hdr_bytes = hdr_bytes;
-  P.out_cap = out_cap;
+  // [header | tile counts (segment mode) | records]
+  auto configure = [&](uint32_t sg, uint64_t out_cap) {
+    P.seg_cap = sg;
+    P.hdr_bytes = sg ? hdr_bytes + cnt_bytes : hdr_bytes;
+    P.out_cap = sg ? uint64_t(nwg) * sg : out_cap;
+    dc.hres.ensure(P.hdr_bytes + std::max<uint64_t>(P.out_cap, 1) * sizeof(MatchRec));
+    P.out = static_cast<uint8_t *>(dc.hres.p);
+    P.counts = reinterpret_cast<uint32_t *>(P.out + hdr_bytes);
+  };
+  configure(seg, seg ? 0 : lb_cap());
   static const bool want_stamps = std::getenv("TSG_STAMPS") != nullptr;
   if (want_stamps) {
     dc.stamps.ensure(size_t(nwg) * 5 * 8);
@@ -1134,7 +1464,6 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       A.blk[i] = seg_desc[i];
       A.cap[i] = segs[i].cap;
       A.first_wg[i] = segs[i].first_wg;
-      A.first_tile[i] = segs[i].first_tile;
       A.block_idx[i] = segs[i].block_idx;
       for (int t = 0; t < kArgTerms; t++) A.key_of[i][t] = seg_keys[i][size_t(t)];
     }
@@ -1143,13 +1472,16 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     if (!needles.empty()) std::memcpy(A.needles, needles.data(), needles.size());
     A.nsegs = nsegs;
     A.nterms = q.nterms;
-    A.njobs = nsegs * q.nterms;
+    A.njobs = njobs_fast;
+    A.self_dict = self_dict ? 1u : 0u;
+    A.mask_words = fast_mask_words;
     A.gstride = fast_words;
     A.bm_words = fast_bm_words;
     A.stage_words = fast_stage;
     if (A.njobs && dc.gbm.ensure(size_t(A.njobs) * fast_words * 8))
       HIP_OK(hipMemsetAsync(dc.gbm.p, 0, dc.gbm.cap, s));  // tag 0: never published
     A.gbm = static_cast<unsigned long long *>(dc.gbm.p);
+    P.done = static_cast<unsigned *>(dc.done.p);
     tr.mark("desc");
     if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
   } else {
@@ -1203,70 +1535,189 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     P.wg_seg = reinterpret_cast<const uint16_t *>(dd + o_ws);
     tr.mark("dict");
   }
-  auto launch = [&](bool timed) {
+  // XCD groups of the scan workgroups (blockIdx % 8 over [njobs, njobs + nwg))
+  const uint32_t grid = fast ? A.njobs + nwg : nwg;
+  uint32_t group_n[8] = {};
+  for (uint32_t g = 0; g < 8; g++) {
+    const uint32_t lo = fast ? A.njobs : 0u;
+    // blocks b in [lo, grid) with b % 8 == g
+    const uint32_t first = lo + ((g + 8 - lo % 8) % 8);
+    group_n[g] = first < grid ? (grid - first + 7) / 8 : 0;
+  }
+  auto launch = [&](bool first) {
     if (++dc.search_epoch == 0) dc.search_epoch = 1;  // 0 is the never-published tag of a fresh buffer
     P.epoch = dc.search_epoch;
     auto *h = reinterpret_cast<volatile uint64_t *>(P.out);
     h[0] = 0;
-    h[1] = 0;  // look-back error flag
+    h[1] = 0;  // look-back / granule poll error flag
+    h[2] = 0;  // completion flag (one-launch path)
+    if (fast) {
+      uint32_t ng = 0;
+      for (uint32_t g = 0; g < 8; g++) {
+        P.done_target[g] = dc.done_base[g] + group_n[g];
+        ng += group_n[g] ? 1u : 0u;
+      }
+      P.done_top = dc.done_base[8] + ng;
+    }
+    hipEvent_t e0 = dc.es0, e1 = dc.es1;
+    const bool timed = first && time_scan;
+    const bool defer = first && !timed && time_defer && dc.defer_slot(e0, e1);
     static const bool ext_events = std::getenv("TSG_EXT_EVENTS") != nullptr;
-    if (timed && ext_events) {  // events stamped from the dispatch packet (hipExtLaunchKernel)
+    if ((timed || defer) && ext_events) {  // events stamped from the dispatch packet (hipExtLaunchKernel)
       if (fast) A.P = P;
       void *args[] = {fast ? static_cast<void *>(&A) : static_cast<void *>(&P)};
-      HIP_OK(hipExtLaunchKernel(kfn, dim3(fast ? A.njobs + nwg : nwg), dim3(kThreads), args,
-                                size_t(lds_words) * 4, s, dc.es0, dc.es1, 0));
+      const void *f = fast ? reinterpret_cast<const void *>(P.seg_cap ? fast_seg : fast_lb) : kfn;
+      HIP_OK(hipExtLaunchKernel(f, dim3(grid), dim3(kThreads), args, size_t(lds_words) * 4, s, e0, e1, 0));
+    } else {
+      if (timed || defer) HIP_OK(hipEventRecord(e0, s));
+      if (fast) {
+        A.P = P;
+        (P.seg_cap ? fast_seg : fast_lb)<<<grid, kThreads, size_t(lds_words) * 4, s>>>(A);
+      } else {
+        scan_fn<<<grid, kThreads, size_t(lds_words) * 4, s>>>(P);
+      }
+      HIP_OK(hipGetLastError());
+      if (timed || defer) HIP_OK(hipEventRecord(e1, s));
+    }
+    if (fast) {  // the launch advances every counter by a known amount
+      for (uint32_t g = 0; g < 8; g++) dc.done_base[g] = P.done_target[g];
+      dc.done_base[8] = P.done_top;
+    }
+  };
+  // segment mode: poll the completion flag the last workgroup raises in the pinned
+  // header instead of waiting for the stream (the end-of-kernel signal comes later);
+  // the stream is queried now and then, so a kernel that dies without raising the
+  // flag fails the search instead of hanging the host
+  auto wait = [&] {
+    if (!fast || !P.seg_cap) {  // (look-back mode writes its records with plain stores)
+      HIP_OK(hipStreamSynchronize(s));
       return;
     }
-    if (timed) HIP_OK(hipEventRecord(dc.es0, s));
-    if (fast) {
-      A.P = P;
-      fast_fn<<<A.njobs + nwg, kThreads, size_t(lds_words) * 4, s>>>(A);
-    } else {
-      scan_fn<<<nwg, kThreads, size_t(lds_words) * 4, s>>>(P);
+    const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(P.out);
+    for (uint32_t it = 1;; it++) {
+      if (h[2] == P.epoch) return;
+      if ((it & 255u) == 0) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) {
+          if (h[2] == P.epoch) return;
+          fail(TSG_E_DEVICE, "search kernel completed without raising its completion flag");
+        }
+        if (e != hipErrorNotReady) HIP_OK(e);
+      }
+      __builtin_ia32_pause();
     }
-    HIP_OK(hipGetLastError());
-    if (timed) HIP_OK(hipEventRecord(dc.es1, s));
   };
-  launch(time_scan);
-  if (time_all) HIP_OK(hipEventRecord(dc.ev1, s));
-  tr.mark("search");
-  HIP_OK(hipStreamSynchronize(s));
-  tr.mark("sync");
   auto check = [&] {
-    if (reinterpret_cast<volatile uint64_t *>(ho)[1])
+    if (reinterpret_cast<volatile uint64_t *>(P.out)[1])
       fail(TSG_E_DEVICE, "search look-back did not complete (workgroup dispatch order assumption broken)");
   };
+  launch(true);
+  if (time_all) HIP_OK(hipEventRecord(dc.ev1, s));
+  tr.mark("search");
+  wait();
+  tr.mark("sync");
   check();
   if (want_stamps) print_stamps(dc, nwg, fast);
-  uint64_t total = *reinterpret_cast<volatile uint64_t *>(ho);
   float ms = 0, sms = 0;
-  if (time_all) HIP_OK(hipEventElapsedTime(&ms, dc.ev0, dc.ev1));
-  if (time_scan) HIP_OK(hipEventElapsedTime(&sms, dc.es0, dc.es1));
+  if (time_all) {
+    HIP_OK(hipEventSynchronize(dc.ev1));
+    HIP_OK(hipEventElapsedTime(&ms, dc.ev0, dc.ev1));
+  }
+  if (time_scan) {
+    HIP_OK(hipEventSynchronize(dc.es1));
+    HIP_OK(hipEventElapsedTime(&sms, dc.es0, dc.es1));
+  }
   out.kernel_ns = uint64_t(double(ms) * 1e6);
   out.scan_ns = uint64_t(double(sms) * 1e6);
   tr.mark("events");
-  // + published counts, + id/start/end reads of each written record
-  out.scan_bytes += uint64_t(nwg) * 8 + std::min<uint64_t>(total, out_cap) * 32;
-  if (!limit && total > out_cap) {
-    // more matches than the result buffer holds: grow it and run the launch again
-    out_cap = total;
-    dc.hres.ensure(hdr_bytes + out_cap * sizeof(MatchRec));
-    ho = static_cast<uint8_t *>(dc.hres.p);
-    P.out = ho;
-    P.out_cap = out_cap;
-    launch(false);
-    HIP_OK(hipStreamSynchronize(s));
-    check();
+
+  // ---- results
+  if (P.seg_cap) {
+    const uint32_t *cnt = P.counts;  // (every scan workgroup writes its count)
+    for (uint32_t w = 0; w < nwg; w += 16) __builtin_prefetch(cnt + w);
+    uint32_t maxc = 0;
+    uint64_t total = 0;
+    for (uint32_t w = 0; w < nwg; w++) {
+      maxc = std::max(maxc, cnt[w]);
+      total += cnt[w];
+    }
+    tr.mark("counts");
+    if (!limit && maxc > P.seg_cap) {
+      // a workgroup overflowed its segment: remember the size and run again with
+      // larger segments, or in look-back mode
+      uint32_t want = 16;
+      while (want < maxc && want < (1u << 30)) want <<= 1;
+      dc.seg_cap = want;
+      configure(seg_fits(want) ? want : 0u, total);
+      launch(false);
+      wait();
+      check();
+    }
   }
-  out.recs.resize(total);
-  if (total) std::memcpy(out.recs.data(), ho + hdr_bytes, total * sizeof(MatchRec));
-  for (size_t i = 0; i < segs.size(); i++) {
-    uint64_t c;
-    std::memcpy(&c, ho + 64 + 8 * i, 8);
-    for (size_t bi = 0; bi < blocks.size(); bi++)
-      if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = c;
+  uint64_t nrec = 0;
+  if (P.seg_cap) {
+    // concatenate the workgroup segments in scan order; limit L: each block's first L
+    const uint32_t *cnt = P.counts;
+    const uint8_t *rec = P.out + P.hdr_bytes;
+    // the GPU's writes evicted these lines from the CPU caches: touch every non-empty
+    // segment once (prefetch) before copying, so the misses overlap
+    uint64_t upper = 0;
+    for (uint32_t w = 0; w < nwg; w++) {
+      const uint32_t c = std::min(cnt[w], P.seg_cap);
+      if (!c) continue;
+      upper += c;
+      const uint8_t *p0 = rec + uint64_t(w) * P.seg_cap * sizeof(MatchRec);
+      for (uint64_t o = 0; o < c * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
+    }
+    out.recs.resize(upper);
+    for (size_t i = 0; i < segs.size(); i++) {
+      uint64_t kept = 0;
+      for (uint32_t w = segs[i].first_wg; w < segs[i].first_wg + segs[i].nwg && kept < segs[i].cap; w++) {
+        const uint64_t c = std::min<uint64_t>(std::min(cnt[w], P.seg_cap), segs[i].cap - kept);
+        if (!c) continue;
+        std::memcpy(&out.recs[nrec], rec + uint64_t(w) * P.seg_cap * sizeof(MatchRec), c * sizeof(MatchRec));
+        nrec += c;
+        kept += c;
+      }
+      for (size_t bi = 0; bi < blocks.size(); bi++)
+        if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = kept;
+    }
+    out.recs.resize(nrec);
+    out.scan_bytes += uint64_t(nwg) * 4 + nrec * 32;  // + workgroup counts, + id/start/end of each record
+  } else {
+    uint64_t total = *reinterpret_cast<volatile uint64_t *>(P.out);
+    if (!limit && total > P.out_cap) {
+      // more matches than the result buffer holds: grow it and run the launch again
+      configure(0, total);
+      launch(false);
+      wait();
+      check();
+    }
+    if (!limit && fast && total <= 64) dc.seg_cap = 16;  // sparse again: back to segment mode
+    nrec = total;
+    out.recs.resize(total);
+    if (total) std::memcpy(out.recs.data(), P.out + P.hdr_bytes, total * sizeof(MatchRec));
+    for (size_t i = 0; i < segs.size(); i++) {
+      uint64_t c;
+      std::memcpy(&c, P.out + 64 + 8 * i, 8);
+      for (size_t bi = 0; bi < blocks.size(); bi++)
+        if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = c;
+    }
+    out.scan_bytes += uint64_t(nwg) * 8 + nrec * 32;  // + published counts, + id/start/end of each record
   }
   tr.mark("post");
+}
+
+void device_kernel_times(DeviceCtx &dc, std::vector<uint64_t> &ns) {
+  std::lock_guard<std::mutex> lk(dc.mu);
+  HIP_OK(hipSetDevice(dc.ordinal));
+  HIP_OK(hipStreamSynchronize(dc.stream));
+  for (size_t i = 0; i < dc.tring_used; i++) {
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, dc.tring[2 * i], dc.tring[2 * i + 1]));
+    ns.push_back(uint64_t(double(ms) * 1e6));
+  }
+  dc.tring_used = 0;
 }
 
 }  // namespace tsg

@@ -39,6 +39,7 @@ ENC_SNAPPY = 6
 
 SEARCH_TIME_SCAN = 1  # tsg_search_opts.flags: HIP events around the scan kernel
 SEARCH_TIME_ALL = 2   # ... and around the whole device sequence
+SEARCH_TIME_DEFER = 4  # events around the search kernel, read later by Engine.kernel_times()
 
 
 class TsgError(RuntimeError):
@@ -112,7 +113,7 @@ EXPORTED = [
     "tsg_init", "tsg_shutdown", "tsg_device_count", "tsg_last_error", "tsg_abi_version", "tsg_cancel",
     "tsg_pipeline_new", "tsg_pipeline_query", "tsg_pipeline_free", "tsg_pipeline_matches_header",
     "tsg_block_open", "tsg_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
-    "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_results_combine",
+    "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_kernel_times", "tsg_results_combine",
     "tsg_v2block_open", "tsg_v2block_close", "tsg_lookup_ids", "tsg_lookup_result_free",
     "tsg_write_search_block", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
     "tsg_synth_v2_block",
@@ -148,6 +149,7 @@ def lib():
         L.tsg_search.argtypes = [vp, C.POINTER(vp), C.c_size_t, C.POINTER(_Query), C.POINTER(_SearchOpts),
                                  C.POINTER(C.POINTER(_Result))]
         L.tsg_result_free.argtypes = [C.POINTER(_Result)]
+        L.tsg_kernel_times.argtypes = [vp, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_size_t)]
         L.tsg_results_combine.argtypes = [C.POINTER(_Result), C.c_uint32, C.POINTER(C.POINTER(_Result))]
         L.tsg_v2block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
         L.tsg_v2block_close.argtypes = [vp]
@@ -324,6 +326,14 @@ class Engine:
                             m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
         lib().tsg_result_free(rp)
         return n, met
+
+    def kernel_times(self, cap: int = 65536) -> List[int]:
+        """Durations (ns) of the searches run with SEARCH_TIME_DEFER since the last
+        call, in launch order (tsg_kernel_times; waits for the device streams)."""
+        buf = (C.c_uint64 * cap)()
+        n = C.c_size_t()
+        _check(lib().tsg_kernel_times(self.h, buf, cap, C.byref(n)))
+        return list(buf[:n.value])
 
     def search_request(self, blocks, req: SearchRequest, limit: Optional[int] = None):
         """instance.Search: ordered matches cut at the limit, then combined + sorted."""

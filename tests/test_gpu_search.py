@@ -248,8 +248,43 @@ def test_timing_flags(engine, tmp_path):
         _, m2 = engine.search_raw([b], pipe, flags=T.SEARCH_TIME_ALL)
         assert m2.kernel_ns >= m2.scan_kernel_ns > 0
         assert m1.scan_bytes == m2.scan_bytes > 0
+        engine.kernel_times()  # drain
+        for _ in range(3):
+            _, m3 = engine.search_raw([b], pipe, flags=T.SEARCH_TIME_DEFER)
+            assert m3.scan_kernel_ns == 0
+        ts = engine.kernel_times()
+        assert len(ts) == 3 and all(t > 0 for t in ts)
+        assert engine.kernel_times() == []
     finally:
         b.close()
+
+
+def test_result_modes_switch_with_match_density(tmp_path):
+    """Segment mode (per-tile record segments) grows its segments when a tile
+    overflows, hands dense queries to look-back mode and returns to segments when
+    results are sparse again: the same ordered matches as the oracle throughout."""
+    p = os.path.join(str(tmp_path), "dens")
+    T.synth_search_block(p, 300_000, seed=21)
+    engine = T.Engine(devices=[0])
+    b = engine.open_block(p)
+    ob = O.Block(p)
+    try:
+        for tags in [{"service.name": "svc-07"},   # ~40 per tile: 16-record segments overflow
+                     {"span.kind": "s"},           # dense: look-back mode
+                     {"service.name": "svc-07"},
+                     {"service.name": "svc-07", "http.method": "get", "status.code": "error"},  # sparse
+                     {"service.name": "svc-1"},
+                     {"http.method": "post"}]:
+            got, _ = engine.search([b], T.Pipeline(T.SearchRequest(tags=tags)))
+            exp, _, _ = O.search([ob], tags=tags)
+            assert [tsg_key(m) for m in got] == [match_key(m) for m in exp], tags
+            for lim in (3, 20):
+                got, _ = engine.search([b], T.Pipeline(T.SearchRequest(tags=tags)), limit=lim)
+                exp, _, _ = O.search([ob], tags=tags, limit=lim)
+                assert [tsg_key(m) for m in got] == [match_key(m) for m in exp], (tags, lim)
+    finally:
+        b.close()
+        engine.close()
 
 
 def test_many_blocks_general_path(engine, tmp_path):

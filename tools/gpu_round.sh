@@ -8,12 +8,20 @@ has() { [[ ",$STAGES," == *",$1,"* ]]; }
 ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 0 pass, 1 test failures (no crash)
 
 if has test; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
   ok_rc $rc || exit $rc
   # the general (prep kernel + descriptor) search path, forced
   TSG_NO_FAST=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_nofast.log 2>&1
   rc=$?; echo "pytest gpu (TSG_NO_FAST) rc=$rc"; tail -5 gpurun_out/pytest_gpu_nofast.log
+  ok_rc $rc || exit $rc
+  # the one-launch path with dictionary workgroups (granule hand-off) instead of per-workgroup matching
+  TSG_NO_SELF_DICT=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_noself.log 2>&1
+  rc=$?; echo "pytest gpu (TSG_NO_SELF_DICT) rc=$rc"; tail -5 gpurun_out/pytest_gpu_noself.log
+  ok_rc $rc || exit $rc
+  # the one-launch path in look-back mode only (no per-tile segments)
+  TSG_NO_SEG=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_noseg.log 2>&1
+  rc=$?; echo "pytest gpu (TSG_NO_SEG) rc=$rc"; tail -5 gpurun_out/pytest_gpu_noseg.log
   ok_rc $rc || exit $rc
 fi
 if has trace; then
@@ -30,6 +38,7 @@ fi
 if has stamps; then
   TSG_STAMPS=1 TSG_TRACE=1 timeout -k 10 600 python bench.py --steps 5 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/stamps.json 2> gpurun_out/stamps.err
   rc=$?; echo "stamps rc=$rc"; grep "stamps" gpurun_out/stamps.err | tail -3
+  [ $rc -eq 0 ] || exit $rc
   TSG_NO_FAST=1 TSG_STAMPS=1 TSG_TRACE=1 timeout -k 10 600 python bench.py --steps 5 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/stamps_nofast.json 2> gpurun_out/stamps_nofast.err
   rc=$?; echo "stamps nofast rc=$rc"; grep "stamps\|tsg_search\|device_search" gpurun_out/stamps_nofast.err | tail -4
   [ $rc -eq 0 ] || exit $rc
