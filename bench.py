@@ -34,8 +34,10 @@ QUERY = dict(tags={"service.name": "svc-07", "http.method": "get", "status.code"
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # The config-2 query (3 u8 term columns, duration + range filters, 10 blocks) runs
 # the one-launch path; TSG_NO_FAST=1 forces the general path (prep + search kernels).
+# The last template argument of the one-launch kernel is segment mode (per-workgroup
+# record segments; TSG_NO_SEG=1 forces look-back mode).
 KERNEL = ("search_kernel<3, true, true, true>" if os.environ.get("TSG_NO_FAST")
-          else "search_fast_kernel<3, true, true, true>")
+          else "search_fast_kernel<3, true, true, true, %s>" % ("false" if os.environ.get("TSG_NO_SEG") else "true"))
 # HBM-side bytes per launch of KERNEL from separate rocprofv3 --pmc passes
 # (FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE), written by
 # tools/pmc_summary.py --out; keyed by workload so other sizes report null.

@@ -1190,6 +1190,24 @@ static void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast) {
     std::fprintf(stderr, " %s=%.1f/%.1f", names[k], sum / nwg, mx);
   }
   std::fprintf(stderr, "\n");
+  // spread of the scan ends: percentiles, and per XCD group (workgroup index % 8)
+  std::vector<double> se(nwg), su(nwg);
+  double gsum[8] = {}, gmax[8] = {};
+  uint32_t gn[8] = {};
+  for (uint32_t w = 0; w < nwg; w++) {
+    se[w] = double(st[size_t(w) * 5 + 2] - t0) / 100.0;
+    su[w] = double(st[size_t(w) * 5 + 1] - t0) / 100.0;
+    gsum[w & 7] += se[w];
+    gmax[w & 7] = std::max(gmax[w & 7], se[w]);
+    gn[w & 7]++;
+  }
+  std::sort(se.begin(), se.end());
+  std::sort(su.begin(), su.end());
+  auto pct = [&](const std::vector<double> &v, double p) { return v[std::min(v.size() - 1, size_t(p * v.size()))]; };
+  std::fprintf(stderr, "[tsg] stamps scan-end p10/p50/p90/p99 %.1f/%.1f/%.1f/%.1f setup p50/p90 %.1f/%.1f | group avg/max:",
+               pct(se, 0.1), pct(se, 0.5), pct(se, 0.9), pct(se, 0.99), pct(su, 0.5), pct(su, 0.9));
+  for (int g = 0; g < 8; g++) std::fprintf(stderr, " %.1f/%.1f", gn[g] ? gsum[g] / gn[g] : 0.0, gmax[g]);
+  std::fprintf(stderr, "\n");
 }
 
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
