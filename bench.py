@@ -57,17 +57,29 @@ def pmc_traffic(workload_key):
     return None, None
 
 
+def pct(xs):
+    """p10 / median / p90 of a sample (SURVEY.md §8(d) timing rules)."""
+    if not xs:
+        return None
+    v = sorted(xs)
+    at = lambda q: v[min(len(v) - 1, int(q * (len(v) - 1) + 0.5))]  # noqa: E731
+    return {"p10": at(0.1), "p50": at(0.5), "p90": at(0.9)}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--blocks", type=int, default=10, help="blocks per GPU")
     ap.add_argument("--entries", type=int, default=1_000_000, help="entries per block")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-blocks", type=int, default=4, help="blocks in the CPU baseline sample")
-    ap.add_argument("--events", type=int, default=1,
-                    help="HIP events around the scan kernel in every timed step (roofline.achieved); 0 = off")
+    ap.add_argument("--events", type=int, default=4,
+                    help="HIP events around the search kernel of every N-th timed step (roofline.achieved: "
+                         "the average over those launches); 0 = off")
+    ap.add_argument("--limit-steps", type=int, default=20,
+                    help="extra timed searches with limit=20 (early exit, config-3 mode); 0 = skip")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--keep", action="store_true")
     return ap.parse_args()
@@ -81,7 +93,8 @@ def gen_blocks(workdir, rank, nblocks, n, threads):
     import tempo_amd as T
     paths = [os.path.join(workdir, f"r{rank}b{i}") for i in range(nblocks)]
     errs = []
-    todo = list(enumerate(paths))
+    # (a --workdir kept from an earlier run is reused: its blocks are seeded the same)
+    todo = [(i, p) for i, p in enumerate(paths) if not os.path.exists(os.path.join(p, "search.meta.json"))]
     lock = threading.Lock()
 
     def work():
@@ -152,8 +165,9 @@ def main():
                           max_duration_ms=QUERY["max_duration_ms"], start=QUERY["start"], end=QUERY["end"])
     pipe = T.Pipeline(req)
     got, met = eng.search(blocks, pipe)  # full result once (parity spot check below)
-    # HIP events around the search kernel of every timed step, on the library's
-    # stream; read after the timed region (the search does not wait for them)
+    # HIP events around the search kernel of every --events-th timed step, on the
+    # library's stream; read after the timed region (the search does not wait for them).
+    # A pair of event records costs the host ~10 us, so not every step carries one.
     sflags = T.SEARCH_TIME_DEFER if args.events else 0
     for _ in range(args.warmup):
         eng.search_raw(blocks, pipe, flags=0)
@@ -162,9 +176,12 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    step_s = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        nm, met = eng.search_raw(blocks, pipe, flags=sflags)
+    for i in range(args.steps):  # (tsg_search is synchronous: results are on the host when it returns)
+        ts = time.perf_counter()
+        nm, met = eng.search_raw(blocks, pipe, flags=sflags if args.events and i % args.events == 0 else 0)
+        step_s.append(time.perf_counter() - ts)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     scan_ns = eng.kernel_times() if args.events else []
@@ -214,6 +231,23 @@ def main():
         "load_s": load_s,
         "flatbuffer_gb_per_gpu": fb_bytes / 1e9,
     }
+
+    out["latency_us"] = {"step": pct([x * 1e6 for x in step_s]), "kernel": pct([x / 1e3 for x in scan_ns])}
+    if args.limit_steps:
+        # SURVEY.md §8(d) config-3 mode on this rank's set: limit=20 (ingester default),
+        # the deterministic early-exit rule, same query; reported beside the full scan
+        for _ in range(3):
+            eng.search_raw(blocks, pipe, limit=20)
+        eng.kernel_times()
+        ls = []
+        for i in range(args.limit_steps):
+            ts = time.perf_counter()
+            nl, metl = eng.search_raw(blocks, pipe, limit=20, flags=sflags if args.events and i % args.events == 0 else 0)
+            ls.append(time.perf_counter() - ts)
+        lk = eng.kernel_times() if args.events else []
+        out["limit20"] = {"steps": args.limit_steps, "matches": nl, "traces_inspected": metl.inspected_traces,
+                          "step_us": pct([x * 1e6 for x in ls]), "kernel_us": pct([x / 1e3 for x in lk]),
+                          "entries_per_s": entries / (sum(ls) / len(ls))}
 
     if rank == 0 and world == 1 and args.cpu_baseline:
         from oracle import oracle as O

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define TSG_ABI_VERSION 1
+#define TSG_ABI_VERSION 2
 
 /* Status codes. */
 #define TSG_OK 0
@@ -175,6 +175,21 @@ int tsg_block_open_mem(tsg_ctx *ctx, const uint8_t *meta_json, size_t meta_len,
                        tsg_block **out);
 void tsg_block_close(tsg_block *b);
 
+/* ---- WAL search blocks (StreamingSearchBlock) -------------------------------------- */
+/* Replaces search.RescanBlocks' per-file replay + StreamingSearchBlock.Search's
+ * iterator (tempodb/search/rescan_blocks.go:74-107, streaming_search_block.go:118-237):
+ * path names a search WAL file "<blockID>:<tenant>:v2:<encoding>[:<dataEncoding>]"
+ * (wal.ParseFilename, tempodb/wal/wal.go:179-219). Pages are replayed in file order (the
+ * block header is SearchBlockHeaderMutable over every page), records sorted by id,
+ * equal ids combined (DataCombiner), and the entries become one resident block; a
+ * damaged page ends the replay (tsg_block_info.partial). An empty file ->
+ * TSG_E_NOT_FOUND (RescanBlocks drops it). The handle is searched with tsg_search like
+ * a backend block: block filter on the mutable header (exact-value tag Contains),
+ * bytesInspected = object bytes of the entries visited, no header bytes. */
+int tsg_wal_block_open(tsg_ctx *ctx, const char *path, int device_hint, tsg_block **out);
+int tsg_wal_block_open_mem(tsg_ctx *ctx, const uint8_t *data, size_t len, int encoding, int device_hint,
+                           tsg_block **out);
+
 typedef struct tsg_block_info {
   uint64_t entries;
   uint64_t pages;
@@ -186,6 +201,8 @@ typedef struct tsg_block_info {
   uint64_t max_dur_ns;
   int32_t device;
   int32_t encoding;        /* backend.Encoding numeric value */
+  int32_t streaming;       /* 1: a WAL (StreamingSearchBlock) replay */
+  int32_t partial;         /* 1: the WAL replay stopped at a damaged page (the reference's warning) */
 } tsg_block_info;
 int tsg_block_info_get(const tsg_block *b, tsg_block_info *out);
 
@@ -260,6 +277,9 @@ int tsg_write_search_block(const char *block_dir, const uint8_t *entries, size_t
 /* SearchEntryMutable.ToBytes (pkg/tempofb/search_entry_mutable.go:41-46) for one
  * entry in the wire format above; SearchBlockHeaderMutable.ToBytes from a list
  * of entries (pkg/tempofb/SearchBlockHeader_util.go:23-75). Free with tsg_free. */
+/* StreamingSearchBlock.Append of each entry in order (one page per entry) into a search
+ * WAL file; duplicates of an id stay separate pages (combined at replay). Test tooling. */
+int tsg_write_wal_search(const char *path, const uint8_t *entries, size_t len, int encoding);
 int tsg_fb_search_entry(const uint8_t *entry, size_t len, uint8_t **out, size_t *out_len);
 int tsg_fb_search_header(const uint8_t *entries, size_t len, uint8_t **out, size_t *out_len);
 

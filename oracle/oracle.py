@@ -58,6 +58,11 @@ def lib():
         L = C.CDLL(LIB_PATH)
         vp = C.c_void_p
         L.orc_block_load.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.orc_wal_block_load.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.orc_entry_to_bytes.argtypes = [C.c_char_p, C.c_size_t, C.c_uint64, C.c_uint64, C.c_uint32,
+                                         C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.POINTER(C.c_char_p),
+                                         C.POINTER(C.c_uint32), C.POINTER(C.POINTER(C.c_uint8)),
+                                         C.POINTER(C.c_size_t)]
         L.orc_block_free.argtypes = [vp]
         L.orc_block_bytes.argtypes = [vp]
         L.orc_block_bytes.restype = C.c_uint64
@@ -115,11 +120,12 @@ def make_request(tags=None, min_ms=0, max_ms=0, start=0, end=0, limit=0):
 
 
 class Block:
-    def __init__(self, path):
+    def __init__(self, path, wal=False):
         self.h = C.c_void_p()
-        rc = lib().orc_block_load(path.encode(), C.byref(self.h))
+        load = lib().orc_wal_block_load if wal else lib().orc_block_load
+        rc = load(path.encode(), C.byref(self.h))
         if rc != 0:
-            raise OSError(f"orc_block_load({path}) -> {rc}")
+            raise OSError(f"orc_{'wal_' if wal else ''}block_load({path}) -> {rc}")
 
     def nbytes(self):
         return lib().orc_block_bytes(self.h)
@@ -210,6 +216,26 @@ def lookup(blocks, ids, ts=0, te=0, bstart=None, bend=None, nthreads=1):
            for i in range(n.value)]
     lib().orc_free(hp)
     return rc, out
+
+
+def entry_to_bytes(entry):
+    """SearchEntryMutable.ToBytes of {"id", "start", "end", "tags": {k: [v]}} (oracle builder)."""
+    pairs = []
+    for k, vs in entry.get("tags", {}).items():
+        for v in ([vs] if isinstance(vs, (str, bytes)) else vs):
+            pairs.append((k.encode() if isinstance(k, str) else k, v.encode() if isinstance(v, str) else v))
+    n = len(pairs)
+    K = (C.c_char_p * max(n, 1))(*[k for k, _ in pairs])
+    V = (C.c_char_p * max(n, 1))(*[v for _, v in pairs])
+    KL = (C.c_uint32 * max(n, 1))(*[len(k) for k, _ in pairs])
+    VL = (C.c_uint32 * max(n, 1))(*[len(v) for _, v in pairs])
+    out, ol = C.POINTER(C.c_uint8)(), C.c_size_t()
+    tid = entry["id"]
+    lib().orc_entry_to_bytes(tid, len(tid), entry.get("start", 0), entry.get("end", 0), n, K, KL, V, VL,
+                             C.byref(out), C.byref(ol))
+    b = C.string_at(out, ol.value)
+    lib().orc_free(out)
+    return b
 
 
 def xxhash64(b):

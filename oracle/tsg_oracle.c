@@ -12,6 +12,7 @@
 #define _GNU_SOURCE
 #include "tsg_oracle.h"
 
+#include <ctype.h>
 #include <dirent.h>
 #include <errno.h>
 #include <pthread.h>
@@ -838,6 +839,7 @@ static int unmarshal_advance(const uint8_t **buf, size_t *len, const uint8_t **i
 /* ------------------------------------------------------------------------- */
 /* backend search block                                                        */
 struct orc_block {
+  int wal; /* a search WAL file (StreamingSearchBlock): data = the file, enc from its name */
   int has_meta;
   int enc;
   char version[16];
@@ -951,12 +953,42 @@ static int idset_add(idset *s, const uint8_t *id16) { /* 1 if new */
   return 1;
 }
 
+/* GetSearchResultFromData (tempodb/search/util.go:27-35) for entry e -> m */
+static int result_from_entry(const fbt *e, uint32_t bidx, uint64_t scan_pos, mlist *out, orc_match **mo) {
+  orc_match *m = ml_push(out);
+  memset(m, 0, sizeof *m);
+  uint32_t il = 0;
+  const uint8_t *tid = NULL;
+  uint16_t io = fb_offset(e, VT_ENTRY_ID);
+  if (io) tid = fb_byte_vector(e, io + e->pos, &il);
+  if (il > 16) return ORC_CORRUPT;
+  if (il) memcpy(m->id + 16 - il, tid, il);
+  m->id_len = il;
+  m->block_idx = bidx;
+  m->entry_idx = scan_pos;
+  m->start_ns = fb_u64(e, VT_ENTRY_START);
+  m->end_ns = fb_u64(e, VT_ENTRY_END);
+  m->duration_ms = (uint32_t)((m->end_ns - m->start_ns) / 1000000ULL);
+  uint32_t sl, nl;
+  const uint8_t *sv = entry_get(e, "root.service.name", &sl);
+  const uint8_t *nv = entry_get(e, "root.name", &nl);
+  m->svc_off = ml_str(out, sv, sl);
+  m->svc_len = sl;
+  m->name_off = ml_str(out, nv, nl);
+  m->name_len = nl;
+  *mo = m;
+  return ORC_OK;
+}
+
 /* BackendSearchBlock.Search (tempodb/search/backend_search_block.go:184-298).
  * `stop` (optional) = consumer: called per match, returns 1 when the consumer
  * closed (the L-th distinct id arrived) -> the block stops right there. */
 typedef int (*consume_fn)(void *ctx, const orc_match *m);
+static int wal_search(const orc_block *b, uint32_t bidx, const orc_pipeline *p, mlist *out, consume_fn consume,
+                      void *cctx, int *quit);
 static int block_search(const orc_block *b, uint32_t bidx, const orc_pipeline *p, mlist *out,
                         consume_fn consume, void *cctx, int *quit) {
+  if (b->wal) return wal_search(b, bidx, p, out, consume, cctx, quit);
   if (!b->has_meta) return ORC_OK; /* ErrDoesNotExist -> nil (:191-203) */
   if (strcmp(b->version, "v2") != 0) return ORC_UNSUPPORTED_ENCODING; /* encoding.FromVersion */
   out->met.bytes_inspected += b->header_len; /* :217 */
@@ -1485,4 +1517,459 @@ int orc_lookup_ids(orc_v2block *const *blocks, uint32_t nblocks, const uint8_t (
   *out = h;
   *nout = total;
   return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* WAL search blocks (StreamingSearchBlock)                                    */
+
+/* Go flatbuffers Builder (vendor/github.com/google/flatbuffers/go/builder.go, v2.0.0):
+ * the bytes grow toward the front; offsets are measured from the end. Only what
+ * SearchEntryMutable.ToBytes needs (pkg/tempofb/search_entry_mutable.go:41-63). */
+typedef struct gob {
+  uint8_t *b;
+  size_t cap, head;
+  int minalign;
+  uint32_t vt[8];
+  int nvt;
+  uint32_t obj_end;
+  uint32_t *vts;
+  size_t nvts, cvts;
+  /* CreateSharedString's map */
+  uint8_t **ssk;
+  size_t *ssl;
+  uint32_t *sso;
+  size_t nss, css;
+} gob;
+static uint32_t gob_off(const gob *f) { return (uint32_t)(f->cap - f->head); } /* Offset() */
+static void gob_grow(gob *f) {                                                  /* growByteBuffer */
+  size_t nc = f->cap ? f->cap * 2 : 1;
+  uint8_t *nb = (uint8_t *)calloc(nc, 1);
+  memcpy(nb + (nc - f->cap), f->b, f->cap);
+  free(f->b);
+  f->head += nc - f->cap;
+  f->b = nb;
+  f->cap = nc;
+}
+static void gob_prep(gob *f, int size, size_t extra) { /* Prep */
+  if (size > f->minalign) f->minalign = size;
+  size_t align = (size_t)(-(int64_t)(gob_off(f) + extra)) & (size_t)(size - 1);
+  while (f->head <= align + (size_t)size + extra) gob_grow(f);
+  for (size_t i = 0; i < align; i++) f->b[--f->head] = 0; /* Pad */
+}
+static void gob_place32(gob *f, uint32_t x) {
+  f->head -= 4;
+  memcpy(f->b + f->head, &x, 4);
+}
+static void gob_place16(gob *f, uint16_t x) {
+  f->head -= 2;
+  memcpy(f->b + f->head, &x, 2);
+}
+static void gob_prepend_uoff(gob *f, uint32_t off) { /* PrependUOffsetT */
+  gob_prep(f, 4, 0);
+  gob_place32(f, gob_off(f) - off + 4);
+}
+static void gob_prepend_voff(gob *f, uint16_t x) { /* PrependVOffsetT */
+  gob_prep(f, 2, 0);
+  gob_place16(f, x);
+}
+static uint32_t gob_start_vector(gob *f, int elem, size_t n, int align) {
+  gob_prep(f, 4, (size_t)elem * n);
+  gob_prep(f, align, (size_t)elem * n);
+  return gob_off(f);
+}
+static uint32_t gob_end_vector(gob *f, size_t n) {
+  gob_place32(f, (uint32_t)n);
+  return gob_off(f);
+}
+static uint32_t gob_bytes(gob *f, const uint8_t *s, size_t l) { /* CreateString / CreateByteString */
+  gob_prep(f, 4, l + 1);
+  f->b[--f->head] = 0;
+  f->head -= l;
+  if (l) memcpy(f->b + f->head, s, l);
+  return gob_end_vector(f, l);
+}
+static uint32_t gob_shared(gob *f, const uint8_t *s, size_t l) { /* CreateSharedString */
+  for (size_t i = 0; i < f->nss; i++)
+    if (f->ssl[i] == l && memcmp(f->ssk[i], s, l) == 0) return f->sso[i];
+  uint32_t o = gob_bytes(f, s, l);
+  if (f->nss == f->css) {
+    f->css = f->css ? f->css * 2 : 64;
+    f->ssk = (uint8_t **)realloc(f->ssk, f->css * sizeof(uint8_t *));
+    f->ssl = (size_t *)realloc(f->ssl, f->css * sizeof(size_t));
+    f->sso = (uint32_t *)realloc(f->sso, f->css * sizeof(uint32_t));
+  }
+  f->ssk[f->nss] = (uint8_t *)malloc(l ? l : 1);
+  if (l) memcpy(f->ssk[f->nss], s, l);
+  f->ssl[f->nss] = l;
+  f->sso[f->nss++] = o;
+  return o;
+}
+static void gob_start_object(gob *f, int n) {
+  memset(f->vt, 0, sizeof f->vt);
+  f->nvt = n;
+  f->obj_end = gob_off(f);
+}
+static void gob_uoff_slot(gob *f, int o, uint32_t x) { /* PrependUOffsetTSlot(o, x, 0) */
+  if (x == 0) return;
+  gob_prepend_uoff(f, x);
+  f->vt[o] = gob_off(f);
+}
+static void gob_u64_slot(gob *f, int o, uint64_t x) { /* PrependUint64Slot(o, x, 0) */
+  if (x == 0) return;
+  gob_prep(f, 8, 0);
+  f->head -= 8;
+  memcpy(f->b + f->head, &x, 8);
+  f->vt[o] = gob_off(f);
+}
+static uint32_t gob_end_object(gob *f) { /* WriteVtable */
+  gob_prep(f, 4, 0); /* PrependSOffsetT(0) (overwritten below with the vtable's offset) */
+  gob_place32(f, gob_off(f) + 4u);
+  uint32_t obj = gob_off(f);
+  int n = f->nvt;
+  while (n > 0 && f->vt[n - 1] == 0) n--;
+  uint32_t existing = 0;
+  for (size_t i = f->nvts; i-- > 0;) {
+    const uint8_t *v2 = f->b + (f->cap - f->vts[i]);
+    uint16_t v2len = le16(v2);
+    if ((size_t)n * 2 != (size_t)v2len - 4) continue;
+    int eq = 1;
+    for (int k = 0; k < n && eq; k++) {
+      uint16_t x = le16(v2 + 4 + 2 * k);
+      if (x == 0 && f->vt[k] == 0) continue;
+      if ((int32_t)x != (int32_t)obj - (int32_t)f->vt[k]) eq = 0;
+    }
+    if (eq) { existing = f->vts[i]; break; }
+  }
+  if (!existing) {
+    for (int k = n - 1; k >= 0; k--) gob_prepend_voff(f, (uint16_t)(f->vt[k] ? obj - f->vt[k] : 0));
+    gob_prepend_voff(f, (uint16_t)(obj - f->obj_end));
+    gob_prepend_voff(f, (uint16_t)((n + 2) * 2));
+    int32_t so = (int32_t)gob_off(f) - (int32_t)obj;
+    memcpy(f->b + (f->cap - obj), &so, 4);
+    if (f->nvts == f->cvts) {
+      f->cvts = f->cvts ? f->cvts * 2 : 16;
+      f->vts = (uint32_t *)realloc(f->vts, f->cvts * sizeof(uint32_t));
+    }
+    f->vts[f->nvts++] = gob_off(f);
+  } else {
+    f->head = f->cap - obj;
+    int32_t so = (int32_t)existing - (int32_t)obj;
+    memcpy(f->b + f->head, &so, 4);
+  }
+  return obj;
+}
+static void gob_free(gob *f) {
+  for (size_t i = 0; i < f->nss; i++) free(f->ssk[i]);
+  free(f->ssk); free(f->ssl); free(f->sso); free(f->vts); free(f->b);
+}
+
+/* a (key, value) string pair of a SearchDataMap */
+typedef struct kvp {
+  uint8_t *k, *v;
+  size_t kl, vl;
+} kvp;
+static int bcmp_go(const uint8_t *a, size_t al, const uint8_t *b, size_t bl) { /* Go string < */
+  size_t n = al < bl ? al : bl;
+  int c = n ? memcmp(a, b, n) : 0;
+  if (c) return c;
+  return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+static int kvp_cmp(const void *x, const void *y) {
+  const kvp *a = (const kvp *)x, *b = (const kvp *)y;
+  int c = bcmp_go(a->k, a->kl, b->k, b->kl);
+  return c ? c : bcmp_go(a->v, a->vl, b->v, b->vl);
+}
+typedef struct kvset {
+  kvp *p;
+  size_t n, cap;
+} kvset;
+static void kvset_add(kvset *s, const uint8_t *k, size_t kl, const uint8_t *v, size_t vl) {
+  if (s->n == s->cap) {
+    s->cap = s->cap ? s->cap * 2 : 64;
+    s->p = (kvp *)realloc(s->p, s->cap * sizeof(kvp));
+  }
+  kvp *e = &s->p[s->n++];
+  e->k = (uint8_t *)malloc(kl ? kl : 1);
+  e->v = (uint8_t *)malloc(vl ? vl : 1);
+  if (kl) memcpy(e->k, k, kl);
+  if (vl) memcpy(e->v, v, vl);
+  e->kl = kl;
+  e->vl = vl;
+}
+static void kvset_unique(kvset *s) { /* sorted, one copy of each pair (the map's semantics) */
+  if (!s->n) return;
+  qsort(s->p, s->n, sizeof(kvp), kvp_cmp);
+  size_t w = 1;
+  for (size_t i = 1; i < s->n; i++) {
+    if (kvp_cmp(&s->p[i], &s->p[w - 1]) == 0) { free(s->p[i].k); free(s->p[i].v); continue; }
+    s->p[w++] = s->p[i];
+  }
+  s->n = w;
+}
+static void kvset_free(kvset *s) {
+  for (size_t i = 0; i < s->n; i++) { free(s->p[i].k); free(s->p[i].v); }
+  free(s->p);
+}
+/* every (key, value) of an entry's tags (SearchEntry.Tags / KeyValues.Value loops) */
+static void entry_pairs(const fbt *e, kvset *s) {
+  uint16_t to = fb_offset(e, VT_ENTRY_TAGS);
+  uint32_t nt = to ? fb_vector_len(e, to) : 0;
+  for (uint32_t t = 0; t < nt; t++) {
+    fbt kv;
+    if (!tc_tag(e, VT_ENTRY_TAGS, t, &kv)) continue;
+    uint32_t kl = 0;
+    uint16_t ko = fb_offset(&kv, VT_KV_KEY);
+    const uint8_t *k = ko ? fb_byte_vector(&kv, ko + kv.pos, &kl) : (const uint8_t *)"";
+    uint16_t vo = fb_offset(&kv, VT_KV_VALUE);
+    uint32_t vn = vo ? fb_vector_len(&kv, vo) : 0;
+    for (uint32_t j = 0; j < vn; j++) {
+      uint32_t vl = 0;
+      const uint8_t *v = fb_byte_vector(&kv, fb_vector(&kv, vo) + 4 * j, &vl);
+      kvset_add(s, k, kl, v, vl);
+    }
+  }
+}
+static int str_cmp_ptr(const void *x, const void *y) {
+  const kvp *a = (const kvp *)x, *b = (const kvp *)y;
+  return bcmp_go(a->v, a->vl, b->v, b->vl);
+}
+/* DataCombiner.Combine's SearchEntryMutable -> ToBytes: CreateByteString(id),
+ * WriteSearchDataMap (keys sorted, writeKeyValues lowercases + sorts values, shared
+ * strings), SearchEntry{id, start, end, tags} (searchdatamap.go:71-152). */
+static uint8_t *combined_to_bytes(const uint8_t *id, size_t idl, kvset *tags, uint64_t st, uint64_t en, size_t *len) {
+  gob f;
+  memset(&f, 0, sizeof f);
+  f.minalign = 1;
+  uint32_t ido = gob_bytes(&f, id, idl);
+  kvset_unique(tags); /* (key, value) sorted: keys ascending as sort.Strings(keys) */
+  uint32_t *offs = (uint32_t *)calloc(tags->n + 1, sizeof(uint32_t));
+  size_t nk = 0;
+  for (size_t i = 0; i < tags->n;) {
+    size_t j = i;
+    while (j < tags->n && bcmp_go(tags->p[j].k, tags->p[j].kl, tags->p[i].k, tags->p[i].kl) == 0) j++;
+    uint8_t *lk = (uint8_t *)malloc(3 * tags->p[i].kl + 1);
+    size_t lkl = go_to_lower(tags->p[i].k, tags->p[i].kl, lk);
+    kvp *vals = (kvp *)calloc(j - i, sizeof(kvp));
+    for (size_t q = i; q < j; q++) {
+      vals[q - i].v = (uint8_t *)malloc(3 * tags->p[q].vl + 1);
+      vals[q - i].vl = go_to_lower(tags->p[q].v, tags->p[q].vl, vals[q - i].v);
+    }
+    qsort(vals, j - i, sizeof(kvp), str_cmp_ptr); /* sort.Strings(values) */
+    uint32_t ko = gob_shared(&f, lk, lkl);
+    uint32_t *vs = (uint32_t *)calloc(j - i, sizeof(uint32_t));
+    for (size_t q = 0; q < j - i; q++) vs[q] = gob_shared(&f, vals[q].v, vals[q].vl);
+    gob_start_vector(&f, 4, j - i, 4);
+    for (size_t q = 0; q < j - i; q++) gob_prepend_uoff(&f, vs[q]);
+    uint32_t vv = gob_end_vector(&f, j - i);
+    gob_start_object(&f, 2);
+    gob_uoff_slot(&f, 0, ko);
+    gob_uoff_slot(&f, 1, vv);
+    offs[nk++] = gob_end_object(&f);
+    for (size_t q = 0; q < j - i; q++) free(vals[q].v);
+    free(vals);
+    free(vs);
+    free(lk);
+    i = j;
+  }
+  gob_start_vector(&f, 4, nk, 4);
+  for (size_t q = 0; q < nk; q++) gob_prepend_uoff(&f, offs[q]);
+  uint32_t tv = gob_end_vector(&f, nk);
+  free(offs);
+  gob_start_object(&f, 4);
+  gob_uoff_slot(&f, 0, ido);
+  gob_u64_slot(&f, 2, st);
+  gob_u64_slot(&f, 3, en);
+  gob_uoff_slot(&f, 1, tv);
+  uint32_t root = gob_end_object(&f);
+  gob_prep(&f, f.minalign, 4); /* Finish */
+  gob_prepend_uoff(&f, root);
+  *len = f.cap - f.head;
+  uint8_t *out = (uint8_t *)malloc(*len);
+  memcpy(out, f.b + f.head, *len);
+  gob_free(&f);
+  return out;
+}
+
+/* wal.ParseFilename (tempodb/wal/wal.go:179-219): blockID:tenant:version:encoding[:dataEncoding] */
+static int wal_parse_name(const char *name, int *enc) {
+  char buf[512];
+  size_t n = strlen(name);
+  if (n >= sizeof buf) return ORC_INVALID;
+  memcpy(buf, name, n + 1);
+  char *parts[6];
+  int np = 0;
+  char *p = buf;
+  for (;;) {
+    if (np == 6) return ORC_INVALID;
+    parts[np++] = p;
+    char *c = strchr(p, ':');
+    if (!c) break;
+    *c = 0;
+    p = c + 1;
+  }
+  if (np != 4 && np != 5) return ORC_INVALID;
+  if (strlen(parts[0]) != 36) return ORC_INVALID;
+  for (int i = 0; i < 36; i++) {
+    int dash = i == 8 || i == 13 || i == 18 || i == 23;
+    if (dash ? parts[0][i] != '-' : !isxdigit((unsigned char)parts[0][i])) return ORC_INVALID;
+  }
+  if (!parts[1][0]) return ORC_INVALID;
+  if (strcmp(parts[2], "v2") != 0) return ORC_UNSUPPORTED_ENCODING;
+  *enc = parse_encoding(parts[3]);
+  return *enc < 0 ? ORC_INVALID : ORC_OK;
+}
+
+int orc_wal_block_load(const char *path, orc_block **out) {
+  const char *slash = strrchr(path, '/');
+  int enc = -1;
+  int rc = wal_parse_name(slash ? slash + 1 : path, &enc);
+  if (rc) return rc;
+  orc_block *b = (orc_block *)calloc(1, sizeof(*b));
+  b->wal = 1;
+  b->has_meta = 1;
+  b->enc = enc;
+  strcpy(b->version, "v2");
+  FILE *f = fopen(path, "rb");
+  if (!f) { free(b); return ORC_IO; }
+  fseek(f, 0, SEEK_END);
+  long l = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  b->data = (uint8_t *)malloc(l > 0 ? (size_t)l : 1);
+  b->data_len = l > 0 && fread(b->data, 1, (size_t)l, f) == (size_t)l ? (size_t)l : 0;
+  fclose(f);
+  *out = b;
+  return ORC_OK;
+}
+
+typedef struct walrec {
+  uint8_t *id, *obj;
+  size_t idl, objl, order;
+} walrec;
+static int walrec_cmp(const void *x, const void *y) { /* common.SortRecords: bytes.Compare on ids */
+  const walrec *a = (const walrec *)x, *b = (const walrec *)y;
+  int c = bcmp_go(a->id, a->idl, b->id, b->idl);
+  if (c) return c;
+  return a->order < b->order ? -1 : (a->order > b->order ? 1 : 0);
+}
+
+/* newStreamingSearchBlockFromWALReplay (rescan_blocks.go:74-107) + ReplayWALAndGetRecords
+ * (wal/replay.go:15-71) + StreamingSearchBlock.Search (streaming_search_block.go:118-175)
+ * through its deduping iterator (iterator_deduping.go, data_combiner.go). */
+static int wal_search(const orc_block *b, uint32_t bidx, const orc_pipeline *p, mlist *out, consume_fn consume,
+                      void *cctx, int *quit) {
+  if (b->enc != 0 && b->enc != 6) return ORC_UNSUPPORTED_ENCODING;
+  walrec *recs = NULL;
+  size_t nr = 0, cr = 0;
+  kvset hdr;
+  memset(&hdr, 0, sizeof hdr);
+  uint64_t min_dur = 0, max_dur = 0;
+  size_t off = 0;
+  while (off < b->data_len) { /* a damaged page ends the replay (warning), records kept */
+    if (b->data_len - off < 6) break;
+    uint32_t total = le32(b->data + off);
+    if (total < 6 || total > b->data_len - off) break;
+    uint8_t *page;
+    size_t pl;
+    if (data_read_page(b->data, b->data_len, b->enc, off, total, &page, &pl)) break;
+    const uint8_t *cur = page, *id, *obj;
+    size_t cl = pl, objl;
+    uint32_t idl;
+    if (unmarshal_advance(&cur, &cl, &id, &idl, &obj, &objl) != 0 || cl != 0) { free(page); break; }
+    /* handleObj: SearchBlockHeaderMutable.AddEntry (SearchBlockHeader_util.go:21-43) */
+    fbt e = fb_root(obj, objl);
+    entry_pairs(&e, &hdr);
+    uint64_t dur = fb_u64(&e, VT_ENTRY_END) - fb_u64(&e, VT_ENTRY_START);
+    if (min_dur == 0 || dur < min_dur) min_dur = dur;
+    if (dur > max_dur) max_dur = dur;
+    if (nr == cr) {
+      cr = cr ? cr * 2 : 64;
+      recs = (walrec *)realloc(recs, cr * sizeof(walrec));
+    }
+    walrec *r = &recs[nr];
+    r->id = (uint8_t *)malloc(idl ? idl : 1);
+    if (idl) memcpy(r->id, id, idl);
+    r->idl = idl;
+    r->obj = (uint8_t *)malloc(objl ? objl : 1);
+    if (objl) memcpy(r->obj, obj, objl);
+    r->objl = objl;
+    r->order = nr++;
+    free(page);
+    off += total;
+  }
+  int rc = ORC_OK;
+  if (nr == 0) goto done; /* RescanBlocks drops an empty WAL file: no block, nothing counted */
+  kvset_unique(&hdr);
+  /* MatchesBlock on the mutable header: durations, then SearchDataMap.Contains (exact) */
+  int ok = 1;
+  if (p->has_min && !(max_dur >= p->min_ns)) ok = 0;
+  if (p->has_max && !(min_dur <= p->max_ns)) ok = 0;
+  for (uint32_t t = 0; t < p->nterms && ok; t++) {
+    kvp key = {p->k[t], p->v[t], p->kl[t], p->vl[t]};
+    if (!bsearch(&key, hdr.p, hdr.n, sizeof(kvp), kvp_cmp)) ok = 0;
+  }
+  if (!ok) {
+    out->met.blocks_skipped++;
+    goto done;
+  }
+  out->met.blocks_inspected++;
+  qsort(recs, nr, sizeof(walrec), walrec_cmp);
+  uint64_t scan_pos = 0;
+  for (size_t i = 0; i < nr;) {
+    if (*quit) break; /* sr.Quit() before each entry */
+    size_t j = i + 1;
+    while (j < nr && bcmp_go(recs[j].id, recs[j].idl, recs[i].id, recs[i].idl) == 0) j++;
+    uint8_t *obj = recs[i].obj, *comb = NULL;
+    size_t objl = recs[i].objl;
+    if (j - i > 1) { /* DataCombiner.Combine */
+      kvset tags;
+      memset(&tags, 0, sizeof tags);
+      uint64_t st = 0, en = 0;
+      const uint8_t *tid = NULL;
+      uint32_t tidl = 0;
+      for (size_t k = i; k < j; k++) {
+        if (recs[k].objl == 0) continue;
+        fbt e = fb_root(recs[k].obj, recs[k].objl);
+        entry_pairs(&e, &tags);
+        uint64_t s2 = fb_u64(&e, VT_ENTRY_START), e2 = fb_u64(&e, VT_ENTRY_END);
+        if (s2 > 0 && (st == 0 || st > s2)) st = s2;
+        if (e2 > 0 && e2 > en) en = e2;
+        uint16_t io = fb_offset(&e, VT_ENTRY_ID);
+        tidl = 0;
+        tid = io ? fb_byte_vector(&e, io + e.pos, &tidl) : NULL;
+      }
+      comb = combined_to_bytes(tid ? tid : (const uint8_t *)"", tidl, &tags, st, en, &objl);
+      kvset_free(&tags);
+      obj = comb;
+    }
+    out->met.bytes_inspected += objl; /* :160-161 */
+    out->met.traces_inspected += 1;
+    fbt e = fb_root(obj, objl);
+    if (pipeline_matches(p, &e)) {
+      orc_match *m;
+      rc = result_from_entry(&e, bidx, scan_pos, out, &m);
+      if (!rc && consume && consume(cctx, m)) *quit = 1;
+    }
+    free(comb);
+    scan_pos++;
+    i = j;
+    if (rc) break;
+  }
+done:
+  for (size_t i = 0; i < nr; i++) { free(recs[i].id); free(recs[i].obj); }
+  free(recs);
+  kvset_free(&hdr);
+  return rc;
+}
+
+/* SearchEntryMutable{id, tags, start, end}.ToBytes through the builder restatement
+ * above (cross-checks the engine's writer, which restates the same builder). */
+int orc_entry_to_bytes(const uint8_t *id, size_t idl, uint64_t st, uint64_t en, uint32_t npairs,
+                       const uint8_t *const *k, const uint32_t *kl, const uint8_t *const *v, const uint32_t *vl,
+                       uint8_t **out, size_t *out_len) {
+  kvset tags;
+  memset(&tags, 0, sizeof tags);
+  for (uint32_t i = 0; i < npairs; i++) kvset_add(&tags, k[i], kl[i], v[i], vl[i]);
+  *out = combined_to_bytes(id, idl, &tags, st, en, out_len);
+  kvset_free(&tags);
+  return ORC_OK;
 }

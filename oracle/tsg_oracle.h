@@ -71,6 +71,9 @@ typedef struct orc_block orc_block; /* search block files held in memory */
 #define ORC_IO 9
 
 int orc_block_load(const char *dir, orc_block **out);
+/* A search WAL file "<blockID>:<tenant>:v2:<encoding>[:...]" (StreamingSearchBlock):
+ * orc_search replays it (header, sort, dedupe/combine) and searches it. */
+int orc_wal_block_load(const char *path, orc_block **out);
 void orc_block_free(orc_block *b);
 uint64_t orc_block_bytes(const orc_block *b);
 
@@ -124,6 +127,10 @@ int orc_lookup_ids(orc_v2block *const *blocks, uint32_t nblocks, const uint8_t (
 uint32_t orc_v2_shard_count(const orc_v2block *b);
 
 void orc_free(void *p);
+/* SearchEntryMutable.ToBytes (Go flatbuffers builder restatement); *out malloc'd */
+int orc_entry_to_bytes(const uint8_t *id, size_t idl, uint64_t st, uint64_t en, uint32_t npairs,
+                       const uint8_t *const *k, const uint32_t *kl, const uint8_t *const *v, const uint32_t *vl,
+                       uint8_t **out, size_t *out_len);
 
 #ifdef __cplusplus
 }

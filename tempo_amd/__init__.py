@@ -5,7 +5,7 @@ the drop-in boundary of tempodb/search BackendSearchBlock.Search and the v2
 bloom/index trace-ID lookup. ``tempo_amd.tsg`` is the ctypes host mirror.
 """
 from .tsg import (  # noqa: F401
-    BackendSearchBlock, Engine, Pipeline, SearchMetrics, SearchRequest, TraceSearchMetadata, TsgError, V2Block,
+    BackendSearchBlock, Engine, StreamingSearchBlock, Pipeline, SearchMetrics, SearchRequest, TraceSearchMetadata, TsgError, V2Block,
     ENC_NONE, ENC_SNAPPY, SEARCH_TIME_ALL, SEARCH_TIME_DEFER, SEARCH_TIME_SCAN, fb_search_entry, fb_search_header, lib, synth_search_block, synth_v2_block,
-    write_search_block,
+    write_search_block, write_wal_search, wal_filename,
 )

@@ -5,6 +5,9 @@
 #include "block.hpp"
 
 #include <algorithm>
+#include <cctype>
+
+#include "writer.hpp"
 #include <atomic>
 #include <thread>
 
@@ -141,10 +144,78 @@ struct PageParse {
   std::vector<uint8_t> id_len;
   std::vector<uint64_t> start, end;
   std::vector<uint32_t> tag_begin;  // nentries + 1
-  std::vector<uint32_t> tag_kv;
+  std::vector<uint32_t> tag_kv;     // the entry's KeyValues tables, vector order (SearchEntry.Get)
+  std::vector<uint32_t> tag_res;    // per table: the table FindTag(its key) lands on, or kNone
   int err = 0;
   std::string msg;
 };
+
+// One SearchEntry table -> pp (id, times, tag tables). Which table a term on key k
+// reads is what FindTag's binarySearch over this entry's vector finds for k
+// (searchdata_util.go:63-100), resolved here once per table: for keys unique and
+// strictly descending (backend blocks, pitfall P3) that is the table itself; WAL
+// entries written from mixed-case keys may be out of order or repeat a key, and then
+// a key can resolve to another table with the same key, or to none (the reference's
+// search misses it). Exact-key lookup of the resolved table is then the reference.
+void parse_entry(const FbTable &e, const uint8_t *fb, uint32_t fb_base, PageParse &pp,
+                 std::unordered_map<uint32_t, uint32_t> &memo) {
+  FbTable kv{e.b, e.n, 0};
+  uint16_t io = e.field(kEntryId);
+  std::string_view id = io ? e.byte_vector(e.pos + io) : std::string_view();
+  if (id.size() > 16) fail(TSG_E_UNSUPPORTED, "trace id longer than 16 bytes");
+  pp.id_off.push_back(uint32_t(reinterpret_cast<const uint8_t *>(id.data()) - fb) + fb_base);
+  pp.id_len.push_back(uint8_t(id.size()));
+  pp.start.push_back(e.u64(kEntryStart));
+  pp.end.push_back(e.u64(kEntryEnd));
+  uint16_t to = e.field(kEntryTags);
+  uint32_t nt = to ? e.vector_len(to) : 0, ts = to ? e.vector_start(to) : 0;
+  const size_t t0 = pp.tag_kv.size();
+  bool ordered = true;
+  for (uint32_t t = 0; t < nt; t++) {
+    uint32_t pos = e.indirect(ts + 4 * t);
+    auto it = memo.find(pos);
+    uint32_t idx;
+    if (it == memo.end()) {
+      kv.pos = pos;
+      PageKV p;
+      uint16_t ko = kv.field(kKvKey);
+      p.key = ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
+      uint16_t vo = kv.field(kKvValue);
+      uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
+      p.vals.reserve(vn);
+      for (uint32_t q = 0; q < vn; q++) p.vals.push_back(kv.byte_vector(vs + 4 * q));
+      idx = uint32_t(pp.kvs.size());
+      pp.kvs.push_back(std::move(p));
+      memo.emplace(pos, idx);
+    } else {
+      idx = it->second;
+    }
+    if (t > 0 && !(pp.kvs[pp.tag_kv.back()].key > pp.kvs[idx].key)) ordered = false;
+    pp.tag_kv.push_back(idx);
+  }
+  for (uint32_t t = 0; t < nt; t++) {
+    if (ordered) {
+      pp.tag_res.push_back(pp.tag_kv[t0 + t]);
+      continue;
+    }
+    const std::string_view k = pp.kvs[pp.tag_kv[t0 + t]].key;
+    uint32_t i = 0, j = nt, found = kNone;
+    while (i < j) {
+      const uint32_t h = (i + j) >> 1;
+      const std::string_view hk = pp.kvs[pp.tag_kv[t0 + h]].key;
+      const int c = bytes_compare(reinterpret_cast<const uint8_t *>(hk.data()), hk.size(),
+                                  reinterpret_cast<const uint8_t *>(k.data()), k.size());
+      if (c == 0) {
+        found = pp.tag_kv[t0 + h];
+        break;
+      }
+      if (c < 0) j = h;
+      else i = h + 1;
+    }
+    pp.tag_res.push_back(found);
+  }
+  pp.tag_begin.push_back(uint32_t(pp.tag_kv.size()));
+}
 
 void parse_page(const uint8_t *data, size_t dlen, int enc, const IndexRecord &rec, PageParse &pp) {
   read_data_page(data, dlen, rec, enc, pp.buf);
@@ -162,48 +233,11 @@ void parse_page(const uint8_t *data, size_t dlen, int enc, const IndexRecord &re
   std::unordered_map<uint32_t, uint32_t> memo;  // KeyValues table position -> kvs index
   pp.tag_begin.reserve(pp.nentries + 1);
   pp.tag_begin.push_back(0);
-  FbTable e{fb, fbn, 0}, kv{fb, fbn, 0};
+  FbTable e{fb, fbn, 0};
   const uint32_t fb_base = uint32_t(fb - pp.buf.data());
   for (uint32_t j = 0; j < pp.nentries; j++) {
     e.pos = page.indirect(es + 4 * j);
-    uint16_t io = e.field(kEntryId);
-    std::string_view id = io ? e.byte_vector(e.pos + io) : std::string_view();
-    if (id.size() > 16) fail(TSG_E_UNSUPPORTED, "trace id longer than 16 bytes");
-    pp.id_off.push_back(uint32_t(reinterpret_cast<const uint8_t *>(id.data()) - fb) + fb_base);
-    pp.id_len.push_back(uint8_t(id.size()));
-    pp.start.push_back(e.u64(kEntryStart));
-    pp.end.push_back(e.u64(kEntryEnd));
-    uint16_t to = e.field(kEntryTags);
-    uint32_t nt = to ? e.vector_len(to) : 0, ts = to ? e.vector_start(to) : 0;
-    std::string_view prev;
-    for (uint32_t t = 0; t < nt; t++) {
-      uint32_t pos = e.indirect(ts + 4 * t);
-      auto it = memo.find(pos);
-      uint32_t idx;
-      if (it == memo.end()) {
-        kv.pos = pos;
-        PageKV p;
-        uint16_t ko = kv.field(kKvKey);
-        p.key = ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
-        uint16_t vo = kv.field(kKvValue);
-        uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
-        p.vals.reserve(vn);
-        for (uint32_t q = 0; q < vn; q++) p.vals.push_back(kv.byte_vector(vs + 4 * q));
-        idx = uint32_t(pp.kvs.size());
-        pp.kvs.push_back(std::move(p));
-        memo.emplace(pos, idx);
-      } else {
-        idx = it->second;
-      }
-      // Contract (pitfall P3): keys unique and strictly descending, as NewBackendSearchBlock
-      // writes them (backend_search_block.go:78-89); then exact-key hashing == binarySearch.
-      std::string_view key = pp.kvs[idx].key;
-      if (t > 0 && !(prev > key))
-        fail(TSG_E_UNSUPPORTED, "entry keys not strictly descending (WAL-style entry; see DESIGN.md P3)");
-      prev = key;
-      pp.tag_kv.push_back(idx);
-    }
-    pp.tag_begin.push_back(uint32_t(pp.tag_kv.size()));
+    parse_entry(e, fb, fb_base, pp, memo);
   }
 }
 
@@ -212,6 +246,105 @@ struct KeyBuild {
   std::unordered_map<std::string, uint32_t> smap;
 };
 }  // namespace
+
+
+// Appends one parsed page to the block: its KeyValues tables resolved to (key, value
+// set) ids, then its entries' columns (scan order = pages ascending, entry index ascending).
+static void merge_page(HostBlock &hb, std::vector<KeyBuild> &kb, PageParse &pp) {
+  uint64_t base = hb.n;
+  hb.page_entries.push_back(pp.nentries);
+  hb.page_fb_bytes.push_back(pp.fb_bytes);
+  hb.page_first.push_back(base);
+  hb.fb_bytes += pp.fb_bytes;
+  // resolve the page's KeyValues tables to (key, set)
+  std::vector<std::pair<int, uint32_t>> res(pp.kvs.size());
+  for (size_t q = 0; q < pp.kvs.size(); q++) {
+    const PageKV &p = pp.kvs[q];
+    std::string key(p.key);
+    auto ki = hb.key_index.find(key);
+    int k;
+    if (ki == hb.key_index.end()) {
+      k = int(hb.keys.size());
+      hb.key_index.emplace(key, k);
+      KeyColumn kc;
+      kc.name = key;
+      kc.dict_off.push_back(0);
+      kc.set_off.push_back(0);
+      hb.keys.push_back(std::move(kc));
+      kb.emplace_back();
+      if (key == "root.service.name") hb.svc_key = k;
+      if (key == "root.name") hb.name_key = k;
+    } else {
+      k = ki->second;
+    }
+    KeyColumn &kc = hb.keys[size_t(k)];
+    KeyBuild &b = kb[size_t(k)];
+    std::string skey;
+    skey.reserve(4 * p.vals.size());
+    uint32_t first_vid = kNone;
+    for (auto &v : p.vals) {
+      std::string vs(v);
+      auto vi = b.vmap.find(vs);
+      uint32_t vid;
+      if (vi == b.vmap.end()) {
+        vid = kc.nvals();
+        kc.dict_bytes.insert(kc.dict_bytes.end(), v.begin(), v.end());
+        kc.dict_off.push_back(uint32_t(kc.dict_bytes.size()));
+        if (kc.dict_bytes.size() > 0xF0000000u) fail(TSG_E_UNSUPPORTED, "dictionary too large");
+        b.vmap.emplace(std::move(vs), vid);
+      } else {
+        vid = vi->second;
+      }
+      if (first_vid == kNone) first_vid = vid;
+      skey.append(reinterpret_cast<const char *>(&vid), 4);
+    }
+    auto si = b.smap.find(skey);
+    uint32_t sid;
+    if (si == b.smap.end()) {
+      sid = kc.nsets();
+      for (auto &v : p.vals) kc.set_vals.push_back(b.vmap[std::string(v)]);
+      kc.set_off.push_back(uint32_t(kc.set_vals.size()));
+      if (p.vals.size() != 1 || sid != first_vid) kc.identity = false;
+      b.smap.emplace(std::move(skey), sid);
+    } else {
+      sid = si->second;
+    }
+    res[q] = {k, sid};
+  }
+  // entries
+  uint64_t n1 = base + pp.nentries;
+  for (auto &kc : hb.keys) kc.col.resize(n1, kNone);
+  hb.ids.resize(n1 * 16, 0);
+  hb.id_len.resize(n1);
+  hb.start.resize(n1);
+  hb.end.resize(n1);
+  hb.svc_vid.resize(n1, kNone);
+  hb.name_vid.resize(n1, kNone);
+  for (uint32_t j = 0; j < pp.nentries; j++) {
+    uint64_t e = base + j;
+    uint8_t il = pp.id_len[j];
+    std::memcpy(&hb.ids[e * 16 + 16 - il], pp.buf.data() + pp.id_off[j], il);
+    hb.id_len[e] = il;
+    hb.start[e] = pp.start[j];
+    hb.end[e] = pp.end[j];
+    bool svc_done = false, name_done = false;
+    for (uint32_t t = pp.tag_begin[j]; t < pp.tag_begin[j + 1]; t++) {
+      auto [k, sid] = res[pp.tag_kv[t]];
+      KeyColumn &kc = hb.keys[size_t(k)];
+      if (pp.tag_res[t] != kNone) kc.col[e] = res[pp.tag_res[t]].second;
+      // SearchEntry.Get: first key match in vector order, Value(0) (searchdata_util.go:10-23)
+      if (k == hb.svc_key && !svc_done) {
+        svc_done = true;
+        if (kc.set_off[sid + 1] > kc.set_off[sid]) hb.svc_vid[e] = kc.set_vals[kc.set_off[sid]];
+      }
+      if (k == hb.name_key && !name_done) {
+        name_done = true;
+        if (kc.set_off[sid + 1] > kc.set_off[sid]) hb.name_vid[e] = kc.set_vals[kc.set_off[sid]];
+      }
+    }
+  }
+  hb.n = n1;
+}
 
 void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
                          const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
@@ -264,100 +397,149 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
     // merge pages in order (scan order = pages ascending, entry index ascending)
     for (auto &pp : pages) {
       if (pp.err) fail(pp.err, pp.msg);
-      uint64_t base = hb.n;
-      hb.page_entries.push_back(pp.nentries);
-      hb.page_fb_bytes.push_back(pp.fb_bytes);
-      hb.page_first.push_back(base);
-      hb.fb_bytes += pp.fb_bytes;
-      // resolve the page's KeyValues tables to (key, set)
-      std::vector<std::pair<int, uint32_t>> res(pp.kvs.size());
-      for (size_t q = 0; q < pp.kvs.size(); q++) {
-        const PageKV &p = pp.kvs[q];
-        std::string key(p.key);
-        auto ki = hb.key_index.find(key);
-        int k;
-        if (ki == hb.key_index.end()) {
-          k = int(hb.keys.size());
-          hb.key_index.emplace(key, k);
-          KeyColumn kc;
-          kc.name = key;
-          kc.dict_off.push_back(0);
-          kc.set_off.push_back(0);
-          hb.keys.push_back(std::move(kc));
-          kb.emplace_back();
-          if (key == "root.service.name") hb.svc_key = k;
-          if (key == "root.name") hb.name_key = k;
-        } else {
-          k = ki->second;
-        }
-        KeyColumn &kc = hb.keys[size_t(k)];
-        KeyBuild &b = kb[size_t(k)];
-        std::string skey;
-        skey.reserve(4 * p.vals.size());
-        uint32_t first_vid = kNone;
-        for (auto &v : p.vals) {
-          std::string vs(v);
-          auto vi = b.vmap.find(vs);
-          uint32_t vid;
-          if (vi == b.vmap.end()) {
-            vid = kc.nvals();
-            kc.dict_bytes.insert(kc.dict_bytes.end(), v.begin(), v.end());
-            kc.dict_off.push_back(uint32_t(kc.dict_bytes.size()));
-            if (kc.dict_bytes.size() > 0xF0000000u) fail(TSG_E_UNSUPPORTED, "dictionary too large");
-            b.vmap.emplace(std::move(vs), vid);
-          } else {
-            vid = vi->second;
-          }
-          if (first_vid == kNone) first_vid = vid;
-          skey.append(reinterpret_cast<const char *>(&vid), 4);
-        }
-        auto si = b.smap.find(skey);
-        uint32_t sid;
-        if (si == b.smap.end()) {
-          sid = kc.nsets();
-          for (auto &v : p.vals) kc.set_vals.push_back(b.vmap[std::string(v)]);
-          kc.set_off.push_back(uint32_t(kc.set_vals.size()));
-          if (p.vals.size() != 1 || sid != first_vid) kc.identity = false;
-          b.smap.emplace(std::move(skey), sid);
-        } else {
-          sid = si->second;
-        }
-        res[q] = {k, sid};
-      }
-      // entries
-      uint64_t n1 = base + pp.nentries;
-      for (auto &kc : hb.keys) kc.col.resize(n1, kNone);
-      hb.ids.resize(n1 * 16, 0);
-      hb.id_len.resize(n1);
-      hb.start.resize(n1);
-      hb.end.resize(n1);
-      hb.svc_vid.resize(n1, kNone);
-      hb.name_vid.resize(n1, kNone);
-      for (uint32_t j = 0; j < pp.nentries; j++) {
-        uint64_t e = base + j;
-        uint8_t il = pp.id_len[j];
-        std::memcpy(&hb.ids[e * 16 + 16 - il], pp.buf.data() + pp.id_off[j], il);
-        hb.id_len[e] = il;
-        hb.start[e] = pp.start[j];
-        hb.end[e] = pp.end[j];
-        bool svc_done = false, name_done = false;
-        for (uint32_t t = pp.tag_begin[j]; t < pp.tag_begin[j + 1]; t++) {
-          auto [k, sid] = res[pp.tag_kv[t]];
-          KeyColumn &kc = hb.keys[size_t(k)];
-          kc.col[e] = sid;
-          // SearchEntry.Get: first key match in vector order, Value(0) (searchdata_util.go:10-23)
-          if (k == hb.svc_key && !svc_done) {
-            svc_done = true;
-            if (kc.set_off[sid + 1] > kc.set_off[sid]) hb.svc_vid[e] = kc.set_vals[kc.set_off[sid]];
-          }
-          if (k == hb.name_key && !name_done) {
-            name_done = true;
-            if (kc.set_off[sid + 1] > kc.set_off[sid]) hb.name_vid[e] = kc.set_vals[kc.set_off[sid]];
-          }
-        }
-      }
-      hb.n = n1;
+      merge_page(hb, kb, pp);
     }
+  }
+  for (auto &kc : hb.keys) kc.col.resize(hb.n, kNone);
+}
+
+}  // namespace tsg
+
+namespace tsg {
+
+int parse_wal_filename(const std::string &name, std::string &version) {
+  std::vector<std::string> parts;
+  size_t p = 0;
+  for (;;) {
+    size_t q = name.find(':', p);
+    parts.push_back(name.substr(p, q == std::string::npos ? std::string::npos : q - p));
+    if (q == std::string::npos) break;
+    p = q + 1;
+  }
+  if (parts.size() != 4 && parts.size() != 5) fail(TSG_E_INVALID, "unable to parse " + name + ". unexpected number of segments");
+  const std::string &u = parts[0];  // uuid.Parse: the canonical 36-character form
+  bool uuid_ok = u.size() == 36;
+  for (size_t i = 0; i < u.size() && uuid_ok; i++)
+    uuid_ok = (i == 8 || i == 13 || i == 18 || i == 23) ? u[i] == '-' : std::isxdigit(uint8_t(u[i])) != 0;
+  if (!uuid_ok) fail(TSG_E_INVALID, "unable to parse " + name + ". error parsing uuid");
+  if (parts[1].empty()) fail(TSG_E_INVALID, "unable to parse " + name + ". missing fields");
+  version = parts[2];
+  if (version != "v2") fail(TSG_E_UNSUPPORTED_ENCODING, "unable to parse " + name + ". error parsing version");
+  const int enc = parse_encoding(parts[3]);
+  if (enc < 0) fail(TSG_E_INVALID, "unable to parse " + name + ". error parsing encoding");
+  return enc;
+}
+
+namespace {
+// SearchEntryMutable fields accumulated by DataCombiner.Combine (data_combiner.go:11-44)
+void combine_into(SearchEntryIn &d, const std::vector<uint8_t> &obj) {
+  FbTable e = FbTable::root(obj.data(), obj.size());
+  uint16_t to = e.field(kEntryTags);
+  uint32_t nt = to ? e.vector_len(to) : 0, ts = to ? e.vector_start(to) : 0;
+  FbTable kv{obj.data(), obj.size(), 0};
+  for (uint32_t t = 0; t < nt; t++) {
+    kv.pos = e.indirect(ts + 4 * t);
+    uint16_t ko = kv.field(kKvKey);
+    std::string key(ko ? kv.byte_vector(kv.pos + ko) : std::string_view());
+    uint16_t vo = kv.field(kKvValue);
+    uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
+    for (uint32_t q = 0; q < vn; q++) d.tags[key].insert(std::string(kv.byte_vector(vs + 4 * q)));  // AddTag
+  }
+  const uint64_t st = e.u64(kEntryStart), en = e.u64(kEntryEnd);
+  if (st > 0 && (d.start == 0 || d.start > st)) d.start = st;  // SetStartTimeUnixNano
+  if (en > 0 && en > d.end) d.end = en;                         // SetEndTimeUnixNano
+  uint16_t io = e.field(kEntryId);
+  std::string_view id = io ? e.byte_vector(e.pos + io) : std::string_view();
+  d.id.assign(id.begin(), id.end());  // data.TraceID = sd.Id()
+}
+
+// SearchBlockHeaderMutable.AddEntry (SearchBlockHeader_util.go:21-43)
+void header_add_entry(HostBlock &hb, const uint8_t *obj, size_t n) {
+  FbTable e = FbTable::root(obj, n);
+  uint16_t to = e.field(kEntryTags);
+  uint32_t nt = to ? e.vector_len(to) : 0, ts = to ? e.vector_start(to) : 0;
+  FbTable kv{obj, n, 0};
+  for (uint32_t t = 0; t < nt; t++) {
+    kv.pos = e.indirect(ts + 4 * t);
+    uint16_t ko = kv.field(kKvKey);
+    std::string key(ko ? kv.byte_vector(kv.pos + ko) : std::string_view());
+    uint16_t vo = kv.field(kKvValue);
+    uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
+    for (uint32_t q = 0; q < vn; q++) hb.stream_tags[key].insert(std::string(kv.byte_vector(vs + 4 * q)));
+  }
+  const uint64_t dur = e.u64(kEntryEnd) - e.u64(kEntryStart);  // uint64 wrap (P2)
+  if (hb.min_dur == 0 || dur < hb.min_dur) hb.min_dur = dur;    // quirk P1
+  if (dur > hb.max_dur) hb.max_dur = dur;
+}
+}  // namespace
+
+void decode_wal_search_block(const uint8_t *file, size_t len, int enc, HostBlock &hb) {
+  hb = HostBlock();
+  hb.has_meta = true;
+  hb.streaming = true;
+  hb.meta.version = "v2";
+  hb.meta.encoding = enc;
+  if (enc != 0 && enc != 6)
+    fail(TSG_E_UNSUPPORTED_ENCODING, std::string("search encoding not supported: ") + encoding_name(enc));
+  struct Rec {
+    std::string id;
+    std::vector<uint8_t> obj;
+  };
+  std::vector<Rec> recs;
+  // ReplayWALAndGetRecords: pages in file order until EOF; a damaged page ends the
+  // replay with a warning and keeps the records before it
+  std::vector<uint8_t> buf;
+  for (size_t off = 0; off < len;) {
+    try {
+      if (len - off < 6) fail(TSG_E_CORRUPT, "truncated page header");
+      const uint32_t total = le32(file + off);
+      if (total < 6 || total > len - off) fail(TSG_E_CORRUPT, "truncated page");
+      const uint8_t *hdr, *payload;
+      size_t pl;
+      unmarshal_page(file + off, total, 0, hdr, payload, pl);
+      if (enc == 0) buf.assign(payload, payload + pl);
+      else snappy_framed_decode(payload, pl, buf);
+      // exactly one object per page: [u32 total][u32 idLen][id][obj], then EOF
+      if (buf.size() < 8) fail(TSG_E_CORRUPT, "object header truncated");
+      const uint32_t ot = le32(buf.data()), il = le32(buf.data() + 4);
+      if (ot < 8 || ot - 8 > buf.size() - 8 || il > ot - 8) fail(TSG_E_CORRUPT, "object out of bounds");
+      if (buf.size() != ot) fail(TSG_E_CORRUPT, "expected EOF after the page's object");
+      Rec r;
+      r.id.assign(reinterpret_cast<const char *>(buf.data() + 8), il);
+      r.obj.assign(buf.data() + 8 + il, buf.data() + ot);
+      header_add_entry(hb, r.obj.data(), r.obj.size());  // handleObj
+      recs.push_back(std::move(r));
+      off += total;
+    } catch (const Error &) {
+      hb.partial = true;
+      break;
+    }
+  }
+  if (recs.empty()) fail(TSG_E_NOT_FOUND, "empty wal file");  // RescanBlocks drops it
+  // common.SortRecords (bytes order of ids; equal ids combine order-independently)
+  std::stable_sort(recs.begin(), recs.end(), [](const Rec &a, const Rec &b) { return a.id < b.id; });
+  std::vector<KeyBuild> kb;
+  PageParse pp;
+  for (size_t i = 0; i < recs.size();) {
+    size_t j = i + 1;
+    while (j < recs.size() && recs[j].id == recs[i].id) j++;
+    pp = PageParse();
+    if (j - i == 1) {
+      pp.buf = std::move(recs[i].obj);
+    } else {  // dedupingIterator -> DataCombiner.Combine -> SearchEntryMutable.ToBytes
+      SearchEntryIn d;
+      for (size_t k = i; k < j; k++)
+        if (!recs[k].obj.empty()) combine_into(d, recs[k].obj);
+      pp.buf = fb_search_entry_bytes(d);
+    }
+    pp.fb_bytes = pp.buf.size();  // sr.AddBytesInspected(len(obj))
+    pp.nentries = 1;
+    pp.tag_begin.push_back(0);
+    FbTable e = FbTable::root(pp.buf.data(), pp.buf.size());
+    std::unordered_map<uint32_t, uint32_t> memo;
+    parse_entry(e, pp.buf.data(), 0, pp, memo);
+    merge_page(hb, kb, pp);
+    i = j;
   }
   for (auto &kc : hb.keys) kc.col.resize(hb.n, kNone);
 }

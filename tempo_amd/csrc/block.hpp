@@ -3,6 +3,8 @@
 // value-set ids and per-entry columns, ready to upload to HBM.
 #pragma once
 #include <cstdint>
+#include <map>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -116,6 +118,11 @@ struct KeyColumn {
 
 struct HostBlock {
   bool has_meta = false;
+  // WAL (StreamingSearchBlock) form: one entry per "page", no on-disk header; the
+  // header is the SearchBlockHeaderMutable rebuilt during replay (exact-value Contains)
+  bool streaming = false;
+  bool partial = false;  // replay stopped at a damaged page (the reference's warning)
+  std::map<std::string, std::set<std::string>> stream_tags;
   SearchMeta meta;
   std::vector<uint8_t> header;  // raw search-header flatbuffer (kept for MatchesBlock/Tags)
   uint64_t min_dur = 0, max_dur = 0;
@@ -143,5 +150,15 @@ struct HostBlock {
 void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
                          const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
                          HostBlock &out);
+
+// newStreamingSearchBlockFromWALReplay + the deduping iterator of its Search
+// (tempodb/search/rescan_blocks.go:74-107, tempodb/wal/replay.go:15-71,
+// streaming_search_block.go:118-175, iterator_deduping.go, data_combiner.go):
+// pages replayed in file order (header AddEntry per page), records sorted by id,
+// equal ids combined, each resulting entry one scan position whose bytesInspected
+// is its object length.
+void decode_wal_search_block(const uint8_t *file, size_t len, int enc, HostBlock &out);
+// wal.ParseFilename (tempodb/wal/wal.go:179-219): blockID:tenant:version:encoding[:dataEncoding]
+int parse_wal_filename(const std::string &name, std::string &version);
 
 }  // namespace tsg

@@ -30,6 +30,8 @@ struct tsg_v2block {
 namespace tsg {
 tsg_pipeline *pipeline_new(const tsg_request &req);
 bool pipeline_matches_block(const tsg_query &q, const uint8_t *hdr, size_t len);
+bool pipeline_matches_stream_header(const tsg_query &q, uint64_t min_dur, uint64_t max_dur,
+                                    const std::map<std::string, std::set<std::string>> &tags);
 
 static thread_local std::string g_last_error;
 void set_last_error(const std::string &m) { g_last_error = m; }
@@ -131,13 +133,12 @@ static_assert(offsetof(LookupHolder, pub) == 0, "pub first");
 
 static std::string join(const char *dir, const char *name) { return std::string(dir) + "/" + name; }
 
-static void open_common(tsg_ctx *ctx, const uint8_t *meta, size_t ml, bool has_meta, std::vector<uint8_t> header,
-                        const uint8_t *index, size_t il, const uint8_t *data, size_t dl, int device_hint,
-                        tsg_block **out) {
+template <class Decode>
+static void open_common(tsg_ctx *ctx, Decode &&decode, int device_hint, tsg_block **out) {
   auto *b = new tsg_block();
   b->ctx = ctx;
   try {
-    decode_search_block(meta, ml, has_meta, std::move(header), index, il, data, dl, 0, b->b.host);
+    decode(b->b.host);
     if (b->b.host.has_meta) block_upload(ctx->c, b->b, device_hint);
   } catch (...) {
     block_free(b->b);
@@ -216,8 +217,10 @@ int tsg_block_open(tsg_ctx *ctx, const char *dir, int device_hint, tsg_block **o
     if (!read_file(join(dir, "search-header"), header)) fail(TSG_E_IO, "search-header missing");
     if (!read_file(join(dir, "search-index"), index)) fail(TSG_E_IO, "search-index missing");
     if (!read_file(join(dir, "search"), data)) fail(TSG_E_IO, "search missing");
-    open_common(ctx, meta.data(), meta.size(), true, std::move(header), index.data(), index.size(), data.data(),
-                data.size(), device_hint, out);
+    open_common(ctx, [&](HostBlock &h) {
+      decode_search_block(meta.data(), meta.size(), true, std::move(header), index.data(), index.size(), data.data(),
+                          data.size(), 0, h);
+    }, device_hint, out);
   });
 }
 int tsg_block_open_mem(tsg_ctx *ctx, const uint8_t *meta, size_t ml, const uint8_t *header, size_t hl,
@@ -226,8 +229,27 @@ int tsg_block_open_mem(tsg_ctx *ctx, const uint8_t *meta, size_t ml, const uint8
   if (!ctx || !out) return TSG_E_INVALID;
   return guard([&] {
     if (!meta) fail(TSG_E_NOT_FOUND, "search.meta.json not provided");
-    std::vector<uint8_t> h(header, header + hl);
-    open_common(ctx, meta, ml, true, std::move(h), index, il, data, dl, device_hint, out);
+    std::vector<uint8_t> hv(header, header + hl);
+    open_common(ctx, [&](HostBlock &h) { decode_search_block(meta, ml, true, std::move(hv), index, il, data, dl, 0, h); },
+                device_hint, out);
+  });
+}
+int tsg_wal_block_open(tsg_ctx *ctx, const char *path, int device_hint, tsg_block **out) {
+  if (!ctx || !path || !out) return TSG_E_INVALID;
+  return guard([&] {
+    std::string p(path), version;
+    const size_t slash = p.find_last_of('/');
+    const int enc = parse_wal_filename(slash == std::string::npos ? p : p.substr(slash + 1), version);
+    std::vector<uint8_t> data;
+    if (!read_file(p, data)) fail(TSG_E_IO, "wal file missing");
+    open_common(ctx, [&](HostBlock &h) { decode_wal_search_block(data.data(), data.size(), enc, h); }, device_hint, out);
+  });
+}
+int tsg_wal_block_open_mem(tsg_ctx *ctx, const uint8_t *data, size_t len, int encoding, int device_hint,
+                           tsg_block **out) {
+  if (!ctx || (len && !data) || !out) return TSG_E_INVALID;
+  return guard([&] {
+    open_common(ctx, [&](HostBlock &h) { decode_wal_search_block(data, len, encoding, h); }, device_hint, out);
   });
 }
 void tsg_block_close(tsg_block *b) {
@@ -248,6 +270,8 @@ int tsg_block_info_get(const tsg_block *b, tsg_block_info *o) {
   o->max_dur_ns = h.max_dur;
   o->device = b->b.dev.device;
   o->encoding = h.meta.encoding;
+  o->streaming = h.streaming ? 1 : 0;
+  o->partial = h.partial ? 1 : 0;
   return TSG_OK;
 }
 
@@ -273,7 +297,9 @@ int tsg_block_tags(const tsg_block *b, uint8_t **out, size_t *len, size_t *n) {
   return guard([&] {
     std::vector<std::string> keys;
     const auto &hb = b->b.host.header;
-    if (b->b.host.has_meta) {
+    if (b->b.host.streaming) {  // StreamingSearchBlock.Tags: the mutable header's keys
+      for (auto &kv : b->b.host.stream_tags) keys.push_back(kv.first);
+    } else if (b->b.host.has_meta) {
       FbTable h = FbTable::root(hb.data(), hb.size());
       uint16_t o = h.field(kHdrTags);
       uint32_t cnt = o ? h.vector_len(o) : 0, st = o ? h.vector_start(o) : 0;
@@ -295,7 +321,10 @@ int tsg_block_tag_values(const tsg_block *b, const uint8_t *key, size_t klen, ui
   return guard([&] {
     std::vector<std::string> vals;
     const auto &hb = b->b.host.header;
-    if (b->b.host.has_meta) {
+    if (b->b.host.streaming) {  // StreamingSearchBlock.TagValues
+      auto it = b->b.host.stream_tags.find(std::string(reinterpret_cast<const char *>(key), klen));
+      if (it != b->b.host.stream_tags.end()) vals.assign(it->second.begin(), it->second.end());
+    } else if (b->b.host.has_meta) {
       FbTable h = FbTable::root(hb.data(), hb.size());
       uint16_t o = h.field(kHdrTags);
       uint32_t cnt = o ? h.vector_len(o) : 0, st = o ? h.vector_start(o) : 0;
@@ -350,7 +379,9 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     for (size_t i = 0; i < nblocks; i++) {
       Block &b = blocks[i]->b;
       if (!b.host.has_meta) continue;
-      bool ok = pipeline_matches_block(*q, b.host.header.data(), b.host.header.size());
+      bool ok = b.host.streaming
+                    ? pipeline_matches_stream_header(*q, b.host.min_dur, b.host.max_dur, b.host.stream_tags)
+                    : pipeline_matches_block(*q, b.host.header.data(), b.host.header.size());
       state[i] = ok ? 2 : 1;
       if (ok && b.dc) per_dev[b.dc].push_back({uint32_t(i), &b});
     }
@@ -557,6 +588,10 @@ void tsg_lookup_result_free(tsg_lookup_result *r) { delete reinterpret_cast<Look
 int tsg_write_search_block(const char *dir, const uint8_t *entries, size_t len, int encoding, uint32_t page_size) {
   if (!dir || (len && !entries)) return TSG_E_INVALID;
   return guard([&] { write_search_block(dir, parse_entries(entries, len), encoding, page_size); });
+}
+int tsg_write_wal_search(const char *path, const uint8_t *entries, size_t len, int encoding) {
+  if (!path || (len && !entries)) return TSG_E_INVALID;
+  return guard([&] { write_wal_search(path, parse_entries(entries, len), encoding); });
 }
 int tsg_fb_search_entry(const uint8_t *entry, size_t len, uint8_t **out, size_t *out_len) {
   if (!entry || !out || !out_len) return TSG_E_INVALID;

@@ -81,6 +81,13 @@ struct DeviceCtx {
   uint32_t done_base[9] = {};
   uint32_t seg_cap = 16;                                  // segment-mode records per workgroup (limit 0), adaptive
   bool seg_off = std::getenv("TSG_NO_SEG") != nullptr;    // one-launch path: always look-back mode
+  // TSG_PER_CU=k (1..16): scan workgroups per CU in the grid plan instead of the
+  // occupancy (k above it oversubscribes: later workgroups start as earlier ones retire)
+  int per_cu_override = [] {
+    const char *e = std::getenv("TSG_PER_CU");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= 16 ? v : 0;
+  }();
   // TSG_SEARCH_TIME_DEFER: event pairs recorded around search kernels, read by tsg_kernel_times
   std::vector<hipEvent_t> tring;
   size_t tring_used = 0;

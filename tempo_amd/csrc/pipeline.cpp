@@ -79,6 +79,22 @@ bool pipeline_matches_block(const tsg_query &q, const uint8_t *hdr, size_t len) 
   return true;
 }
 
+// MatchesBlock on a StreamingSearchBlock's SearchBlockHeaderMutable
+// (streaming_search_block.go:127-134): the same duration filters, but the tag filter is
+// SearchDataMap.Contains (searchdatamap.go:43-49): the EXACT value must be present,
+// not a substring of one (the backend header's ContainsTag).
+bool pipeline_matches_stream_header(const tsg_query &q, uint64_t min_dur, uint64_t max_dur,
+                                    const std::map<std::string, std::set<std::string>> &tags) {
+  if (q.has_min && !(max_dur >= q.min_ns)) return false;
+  if (q.has_max && !(min_dur <= q.max_ns)) return false;
+  for (uint32_t t = 0; t < q.nterms; t++) {
+    auto it = tags.find(std::string(reinterpret_cast<const char *>(q.keys[t]), q.key_lens[t]));
+    if (it == tags.end()) return false;
+    if (!it->second.count(std::string(reinterpret_cast<const char *>(q.values[t]), q.value_lens[t]))) return false;
+  }
+  return true;
+}
+
 }  // namespace tsg
 
 extern "C" {

@@ -1362,7 +1362,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   constexpr uint64_t kSegBudget = 64ull << 20;  // pinned bytes of segment records (workgroups <= 8 per CU)
   auto seg_fits = [&](uint32_t c) {
     return fast && !dc.seg_off && c > 0 && c <= kSegMax &&
-           uint64_t(dc.num_cu) * 8 * c * sizeof(MatchRec) <= kSegBudget;
+           uint64_t(dc.num_cu) * std::max(8, dc.per_cu_override) * c * sizeof(MatchRec) <= kSegBudget;
   };
   uint32_t seg = limit ? limit : dc.seg_cap;
   if (!seg_fits(seg)) seg = 0;
@@ -1391,7 +1391,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // every workgroup of the launch resident at once: a workgroup dispatched only
   // when another retires starts a full scan slice late and the in-order look-back
   // waits for it. The one-launch grid also holds the dictionary workgroups.
-  const uint32_t slots = uint32_t(dc.num_cu) * uint32_t(per_cu);
+  const uint32_t slots = uint32_t(dc.num_cu) * uint32_t(dc.per_cu_override ? dc.per_cu_override : per_cu);
   const uint32_t njobs_fast = fast && !self_dict ? nsegs * q.nterms : 0;
   const uint32_t target_wg = slots > njobs_fast + uint32_t(dc.num_cu) ? slots - njobs_fast : uint32_t(dc.num_cu);
   // workgroups per block in proportion to its units, the units of a block split

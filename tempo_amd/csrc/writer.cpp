@@ -137,6 +137,24 @@ static size_t cut_data_page(std::vector<uint8_t> &file, const std::vector<uint8_
   return total;
 }
 
+// StreamingSearchBlock.Append per entry (streaming_search_block.go:80-95): one
+// SearchEntry flatbuffer per page, the page's object keyed by the entry's id, pages in
+// append order (v2.Appender: Write + CutPage).
+void write_wal_search(const std::string &path, const std::vector<SearchEntryIn> &entries, int enc) {
+  std::vector<uint8_t> file, obj;
+  for (const auto &e : entries) {
+    const std::vector<uint8_t> fb = fb_search_entry_bytes(e);
+    obj.clear();
+    marshal_object(obj, e.id.data(), e.id.size(), fb.data(), fb.size());
+    cut_data_page(file, obj, enc);
+  }
+  FILE *f = std::fopen(path.c_str(), "wb");
+  if (!f) fail(TSG_E_IO, "cannot create " + path);
+  const size_t w = file.empty() ? 0 : std::fwrite(file.data(), 1, file.size(), f);
+  std::fclose(f);
+  if (w != file.size()) fail(TSG_E_IO, "short write " + path);
+}
+
 struct Record {
   std::vector<uint8_t> id;
   uint64_t start = 0;

@@ -27,6 +27,7 @@ struct HeaderBuilder {  // SearchBlockHeaderMutable
 std::vector<SearchEntryIn> parse_entries(const uint8_t *p, size_t n);
 std::vector<uint8_t> fb_search_entry_bytes(const SearchEntryIn &e);
 void write_search_block(const std::string &dir, std::vector<SearchEntryIn> entries, int enc, uint32_t page_size);
+void write_wal_search(const std::string &path, const std::vector<SearchEntryIn> &entries, int enc);
 
 // Streaming form of NewBackendSearchBlock: entries must arrive in strictly
 // ascending trace-id order (what the deduping WAL iterator yields).

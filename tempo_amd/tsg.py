@@ -36,6 +36,7 @@ TSG_E_IO = 9
 
 ENC_NONE = 0
 ENC_SNAPPY = 6
+ENC_NAMES = ["none", "gzip", "lz4-64k", "lz4-256k", "lz4-1M", "lz4", "snappy", "zstd", "s2"]  # backend.Encoding.String
 
 SEARCH_TIME_SCAN = 1  # tsg_search_opts.flags: HIP events around the scan kernel
 SEARCH_TIME_ALL = 2   # ... and around the whole device sequence
@@ -94,7 +95,7 @@ class _BlockInfo(C.Structure):
     _fields_ = [("entries", C.c_uint64), ("pages", C.c_uint64), ("keys", C.c_uint64),
                 ("header_bytes", C.c_uint64), ("fb_bytes", C.c_uint64), ("device_bytes", C.c_uint64),
                 ("min_dur_ns", C.c_uint64), ("max_dur_ns", C.c_uint64), ("device", C.c_int32),
-                ("encoding", C.c_int32)]
+                ("encoding", C.c_int32), ("streaming", C.c_int32), ("partial", C.c_int32)]
 
 
 class _LookupOpts(C.Structure):
@@ -112,10 +113,10 @@ class _LookupResult(C.Structure):
 EXPORTED = [
     "tsg_init", "tsg_shutdown", "tsg_device_count", "tsg_last_error", "tsg_abi_version", "tsg_cancel",
     "tsg_pipeline_new", "tsg_pipeline_query", "tsg_pipeline_free", "tsg_pipeline_matches_header",
-    "tsg_block_open", "tsg_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
+    "tsg_block_open", "tsg_block_open_mem", "tsg_wal_block_open", "tsg_wal_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
     "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_kernel_times", "tsg_results_combine",
     "tsg_v2block_open", "tsg_v2block_close", "tsg_lookup_ids", "tsg_lookup_result_free",
-    "tsg_write_search_block", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
+    "tsg_write_search_block", "tsg_write_wal_search", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
     "tsg_synth_v2_block",
 ]
 
@@ -141,6 +142,9 @@ def lib():
         L.tsg_pipeline_matches_header.argtypes = [C.POINTER(_Query), C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
         L.tsg_block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
         L.tsg_block_close.argtypes = [vp]
+        L.tsg_wal_block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
+        L.tsg_wal_block_open_mem.argtypes = [vp, C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(vp)]
+        L.tsg_write_wal_search.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int]
         L.tsg_block_info_get.argtypes = [vp, C.POINTER(_BlockInfo)]
         L.tsg_block_tags.argtypes = [vp, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
         L.tsg_block_tag_values.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
@@ -294,6 +298,10 @@ class Engine:
     def device_count(self):
         return lib().tsg_device_count(self.h)
 
+    def open_wal_block(self, path: str, device: int = 0) -> "StreamingSearchBlock":
+        """Replay a search WAL file (<blockID>:<tenant>:v2:<encoding>[:...]) onto a device."""
+        return StreamingSearchBlock(self, path, device)
+
     def open_block(self, path: str, device: int = 0) -> "BackendSearchBlock":
         return BackendSearchBlock(self, path, device)
 
@@ -388,10 +396,11 @@ class Engine:
 class BackendSearchBlock:
     """A backend search block resident on one device (tsg_block)."""
 
-    def __init__(self, eng: Engine, path: str, device: int = 0):
+    def __init__(self, eng: Engine, path: str, device: int = 0, _wal: bool = False):
         self.path = path
         self.h = C.c_void_p()
-        _check(lib().tsg_block_open(eng.h, path.encode(), device, C.byref(self.h)))
+        opener = lib().tsg_wal_block_open if _wal else lib().tsg_block_open
+        _check(opener(eng.h, path.encode(), device, C.byref(self.h)))
 
     def info(self):
         i = _BlockInfo()
@@ -422,6 +431,14 @@ class BackendSearchBlock:
             self.h = None
 
     __del__ = close
+
+
+class StreamingSearchBlock(BackendSearchBlock):
+    """A search WAL file replayed into a resident block (tsg_wal_block_open): the
+    StreamingSearchBlock of search.RescanBlocks, searched through the same tsg_search."""
+
+    def __init__(self, eng: Engine, path: str, device: int = 0):
+        super().__init__(eng, path, device, _wal=True)
 
 
 class V2Block:
@@ -463,6 +480,18 @@ def encode_entries(entries: Iterable[dict]) -> bytes:
 def write_search_block(path: str, entries: Iterable[dict], encoding: int = ENC_SNAPPY, page_size: int = 0):
     buf = encode_entries(entries)
     _check(lib().tsg_write_search_block(path.encode(), buf, len(buf), encoding, page_size))
+
+
+def write_wal_search(path: str, entries: Iterable[dict], encoding: int = ENC_SNAPPY):
+    """StreamingSearchBlock.Append of each entry, in order, into a search WAL file."""
+    buf = encode_entries(entries)
+    _check(lib().tsg_write_wal_search(path.encode(), buf, len(buf), encoding))
+
+
+def wal_filename(encoding: int = ENC_SNAPPY, block_id: str = "1c505e8b-26cd-4621-ba7d-792bb55282d5",
+                 tenant: str = "single-tenant") -> str:
+    """<blockID>:<tenant>:v2:<encoding>: (the name wal.ParseFilename reads)."""
+    return f"{block_id}:{tenant}:v2:{ENC_NAMES[encoding]}:"
 
 
 def _bytes_out(fn, *args):
