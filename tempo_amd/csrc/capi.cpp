@@ -363,7 +363,7 @@ int tsg_block_tag_values(const tsg_block *b, const uint8_t *key, size_t klen, ui
 int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
                const tsg_search_opts *opts, tsg_result **out) {
   if (!ctx || !q || !out || (nblocks && !blocks)) return TSG_E_INVALID;
-  static const bool trace = std::getenv("TSG_TRACE") != nullptr;
+  static const bool trace = std::getenv("TSG_TRACE") != nullptr || prof_on();
   using clk = std::chrono::steady_clock;
   const clk::time_point t_in = trace ? clk::now() : clk::time_point();
   return guard([&] {
@@ -472,7 +472,11 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     res->resize(nout);
     res->finalize();
     *out = &guard_res.release()->pub;
-    if (trace) {
+    if (prof_on()) {
+      const clk::time_point t_end = clk::now();
+      prof_add("tsg_search.device", std::chrono::duration<double, std::micro>(t_dev - t_in).count());
+      prof_add("tsg_search.results", std::chrono::duration<double, std::micro>(t_end - t_dev).count());
+    } else if (trace) {
       const clk::time_point t_end = clk::now();
       std::fprintf(stderr, "[tsg] tsg_search us: device=%.1f results=%.1f total=%.1f\n",
                    std::chrono::duration<double, std::micro>(t_dev - t_in).count(),
@@ -481,7 +485,15 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     }
   });
 }
-void tsg_result_free(tsg_result *r) { delete reinterpret_cast<ResultHolder *>(r); }
+void tsg_result_free(tsg_result *r) {
+  if (prof_on()) {
+    const auto t0 = std::chrono::steady_clock::now();
+    delete reinterpret_cast<ResultHolder *>(r);
+    prof_add("result_free", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    return;
+  }
+  delete reinterpret_cast<ResultHolder *>(r);
+}
 
 int tsg_kernel_times(tsg_ctx *ctx, uint64_t *ns, size_t cap, size_t *n) {
   if (!ctx || !n || (cap && !ns)) return TSG_E_INVALID;

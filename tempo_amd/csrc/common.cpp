@@ -1,6 +1,7 @@
 // common.cpp — hashes, snappy framing, strings.ToLower, file helpers.
 #include "common.hpp"
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <mutex>
@@ -436,5 +437,39 @@ int parse_encoding(std::string_view s) {
   return -1;
 }
 const char *encoding_name(int e) { return (e >= 0 && e < 9) ? kEncNames[e] : "unsupported"; }
+
+namespace {
+struct ProfTable {
+  std::mutex mu;
+  std::vector<std::pair<std::string, std::vector<double>>> rows;
+  ~ProfTable() {
+    if (rows.empty()) return;
+    std::fprintf(stderr, "[tsg] prof p50 us:");
+    for (auto &r : rows) {
+      std::sort(r.second.begin(), r.second.end());
+      std::fprintf(stderr, " %s=%.2f", r.first.c_str(), r.second[r.second.size() / 2]);
+    }
+    std::fprintf(stderr, " (n=%zu)\n", rows[0].second.size());
+  }
+};
+ProfTable &prof_table() {
+  static ProfTable t;
+  return t;
+}
+}  // namespace
+bool prof_on() {
+  static const bool on = std::getenv("TSG_PROF") != nullptr;
+  return on;
+}
+void prof_add(const char *name, double us) {
+  ProfTable &t = prof_table();
+  std::lock_guard<std::mutex> lk(t.mu);
+  for (auto &r : t.rows)
+    if (r.first == name) {
+      r.second.push_back(us);
+      return;
+    }
+  t.rows.push_back({name, {us}});
+}
 
 }  // namespace tsg

@@ -94,6 +94,9 @@ void make_dirs(const std::string &path);
 
 // backend.Encoding names (tempodb/backend/encoding.go:40-62)
 int parse_encoding(std::string_view s);
+// TSG_PROF=1: host phase times accumulated per name, averages printed at exit
+bool prof_on();
+void prof_add(const char *name, double us);
 const char *encoding_name(int e);
 
 }  // namespace tsg

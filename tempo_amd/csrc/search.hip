@@ -1156,12 +1156,18 @@ struct Tracer {
   std::chrono::steady_clock::time_point t0, last;
   char buf[512];
   int len = 0;
+  bool prof = prof_on();
   Tracer() : on(std::getenv("TSG_TRACE") != nullptr) {
-    if (on) t0 = last = std::chrono::steady_clock::now();
+    if (on || prof) t0 = last = std::chrono::steady_clock::now();
   }
   void mark(const char *name) {
-    if (!on) return;
+    if (!on && !prof) return;
     auto now = std::chrono::steady_clock::now();
+    if (prof) {
+      prof_add(name, std::chrono::duration<double, std::micro>(now - last).count());
+      last = now;
+      if (!on) return;
+    }
     len += std::snprintf(buf + len, sizeof buf - size_t(len), " %s=%.1f", name,
                          std::chrono::duration<double, std::micro>(now - last).count());
     last = now;
@@ -1588,6 +1594,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       HIP_OK(hipExtLaunchKernel(f, dim3(grid), dim3(kThreads), args, size_t(lds_words) * 4, s, e0, e1, 0));
     } else {
       if (timed || defer) HIP_OK(hipEventRecord(e0, s));
+      else if (dc.mark_mode & 1) HIP_OK(hipEventRecord(dc.mk0, s));
       if (fast) {
         A.P = P;
         (P.seg_cap ? fast_seg : fast_lb)<<<grid, kThreads, size_t(lds_words) * 4, s>>>(A);
@@ -1596,6 +1603,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       }
       HIP_OK(hipGetLastError());
       if (timed || defer) HIP_OK(hipEventRecord(e1, s));
+      else if (dc.mark_mode & 2) HIP_OK(hipEventRecord(dc.mk1, s));
     }
     if (fast) {  // the launch advances every counter by a known amount
       for (uint32_t g = 0; g < 8; g++) dc.done_base[g] = P.done_target[g];

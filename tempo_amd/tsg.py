@@ -169,6 +169,18 @@ def lib():
     return _lib
 
 
+_raw = None
+
+
+def _raw_lib():
+    """A second handle on libtsg whose functions take prebuilt ctypes arguments as-is."""
+    global _raw
+    if _raw is None:
+        lib()
+        _raw = C.CDLL(LIB_PATH)
+    return _raw
+
+
 def _check(rc):
     if rc != TSG_OK:
         raise TsgError(rc, lib().tsg_last_error().decode(errors="replace"))
@@ -212,6 +224,7 @@ class Pipeline:
         self.h = C.c_void_p()
         _check(lib().tsg_pipeline_new(C.byref(self._creq), C.byref(self.h)))
         self.query = lib().tsg_pipeline_query(self.h)
+        self.query_addr = C.cast(self.query, C.c_void_p).value
 
     def terms(self):
         q = self.query.contents
@@ -320,19 +333,28 @@ class Engine:
                    flags: int = 0, _cache={}):
         """tsg_search without unpacking the matches into Python objects: returns
         (match count, SearchMetrics). The result arrays are assembled by libtsg as
-        for any caller (what the Go shim would receive) and then freed."""
-        key = tuple(b.h.value for b in blocks)
-        arr = _cache.get(key)
-        if arr is None:
-            arr = _cache[key] = (C.c_void_p * max(len(blocks), 1))(*key)
-        opts = _SearchOpts(limit=limit, flags=flags)
-        rp = C.POINTER(_Result)()
-        _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
+        for any caller (what the Go shim would receive) and then freed. The ctypes
+        argument objects are built once per (blocks, pipeline, limit, flags)."""
+        key = (self.h.value, pipeline.query_addr, limit, flags) + tuple(b.h.value for b in blocks)
+        call = _cache.get(key)
+        if call is None:
+            L = _raw_lib()  # its own function objects: no argtypes, arguments are prebuilt ctypes objects
+            fn, free = L.tsg_search, L.tsg_result_free
+            arr = (C.c_void_p * max(len(blocks), 1))(*[b.h.value for b in blocks])
+            opts = _SearchOpts(limit=limit, flags=flags)
+            rp = C.POINTER(_Result)()
+            args = (C.c_void_p(self.h.value), arr, C.c_size_t(len(blocks)), C.c_void_p(pipeline.query_addr),
+                    C.byref(opts), C.byref(rp))
+            call = _cache[key] = (fn, free, args, rp, arr, opts, blocks)
+        fn, free, args, rp = call[0], call[1], call[2], call[3]
+        rc = fn(*args)
+        if rc:
+            _check(rc)
         r = rp.contents
         n, m = r.n, r.metrics
         met = SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,
                             m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
-        lib().tsg_result_free(rp)
+        free(rp)
         return n, met
 
     def kernel_times(self, cap: int = 65536) -> List[int]:
