@@ -66,6 +66,19 @@ def pct(xs):
     return {"p10": at(0.1), "p50": at(0.5), "p90": at(0.9)}
 
 
+def node_cpus(node):
+    """CPUs of a NUMA node (sysfs cpulist)."""
+    try:
+        lst = open(f"/sys/devices/system/node/node{node}/cpulist").read().strip()
+    except OSError:
+        return set()
+    out = set()
+    for part in lst.split(","):
+        a, _, b = part.partition("-")
+        out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -80,6 +93,8 @@ def parse():
                          "the average over those launches); 0 = off")
     ap.add_argument("--limit-steps", type=int, default=20,
                     help="extra timed searches with limit=20 (early exit, config-3 mode); 0 = skip")
+    ap.add_argument("--pin", default="auto", choices=["auto", "none"],
+                    help="auto: keep this process on the CPUs of its GPU's NUMA node (tsg_device_numa_node)")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--keep", action="store_true")
     return ap.parse_args()
@@ -161,6 +176,19 @@ def main():
     log(f"rank {rank}: loaded {entries} entries ({fb_bytes / 1e9:.2f} GB flatbuffer) in {load_s:.1f}s, "
         f"{dev_bytes / 1e9:.2f} GB resident")
 
+    all_cpus = os.sched_getaffinity(0)
+    if args.pin == "auto":
+        # the step polls a completion word and copies its records from pinned host memory:
+        # both are served faster from the GPU's own socket (profiles/r01_host).
+        # After loading (which uses many threads): 8 CPUs of that node, a slice per local rank.
+        node = eng.numa_node(0)
+        cpus = sorted(node_cpus(node) & os.sched_getaffinity(0)) if node >= 0 else []
+        if cpus:
+            k = (local * 8) % len(cpus)
+            mine = set(cpus[k:k + 8]) or set(cpus[:8])
+            os.sched_setaffinity(0, mine)
+        log(f"rank {rank}: GPU NUMA node {node}, search thread on CPUs {sorted(mine)}" if cpus else
+            f"rank {rank}: GPU NUMA node unknown, not pinned")
     req = T.SearchRequest(tags=QUERY["tags"], min_duration_ms=QUERY["min_duration_ms"],
                           max_duration_ms=QUERY["max_duration_ms"], start=QUERY["start"], end=QUERY["end"])
     pipe = T.Pipeline(req)
@@ -250,6 +278,7 @@ def main():
                           "entries_per_s": entries / (sum(ls) / len(ls))}
 
     if rank == 0 and world == 1 and args.cpu_baseline:
+        os.sched_setaffinity(0, all_cpus)  # (the CPU baseline gets the whole host share back)
         from oracle import oracle as O
         nb = min(args.cpu_blocks, len(paths))
         oblocks = [O.Block(p) for p in paths[:nb]]

@@ -151,6 +151,10 @@ typedef struct tsg_search_opts {
 int tsg_init(const tsg_options *opts, tsg_ctx **out);
 void tsg_shutdown(tsg_ctx *ctx);
 int tsg_device_count(tsg_ctx *ctx);
+/* NUMA node of device `dev`'s PCI function (sysfs), -1 if unknown. The search path
+ * polls a completion word and reads its records in pinned host memory: a caller that
+ * keeps its search threads on this node's CPUs sees both sooner. */
+int tsg_device_numa_node(tsg_ctx *ctx, int dev);
 const char *tsg_last_error(void);
 int tsg_abi_version(void);
 int tsg_cancel(tsg_ctx *ctx, uint64_t query_id);

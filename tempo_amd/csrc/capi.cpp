@@ -195,6 +195,10 @@ void tsg_shutdown(tsg_ctx *ctx) {
   delete ctx;
 }
 int tsg_device_count(tsg_ctx *ctx) { return ctx ? int(ctx->c.devs.size()) : 0; }
+int tsg_device_numa_node(tsg_ctx *ctx, int dev) {
+  if (!ctx || dev < 0 || size_t(dev) >= ctx->c.devs.size()) return -1;
+  return device_numa_node(*ctx->c.devs[size_t(dev)]);
+}
 int tsg_cancel(tsg_ctx *, uint64_t) { return TSG_OK; }  // searches are short and non-preemptible
 
 int tsg_pipeline_new(const tsg_request *req, tsg_pipeline **out) {

@@ -1,5 +1,8 @@
 // devctx.hip — device contexts, HBM residency of search blocks (host code using the
 // HIP runtime; the search kernels are in search.hip, the lookup kernels in lookup.hip).
+#include <cctype>
+#include <cstdio>
+#include <string>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -209,4 +212,18 @@ void block_free(Block &b) {
   b.dc = nullptr;
 }
 
+}  // namespace tsg
+
+namespace tsg {
+int device_numa_node(const DeviceCtx &dc) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, dc.ordinal) != hipSuccess) return -1;
+  for (char *c = bus; *c; c++) *c = char(std::tolower(uint8_t(*c)));
+  std::FILE *f = std::fopen((std::string("/sys/bus/pci/devices/") + bus + "/numa_node").c_str(), "r");
+  if (!f) return -1;
+  int node = -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
+}
 }  // namespace tsg

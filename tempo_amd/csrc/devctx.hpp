@@ -120,4 +120,5 @@ struct DeviceCtx {
 
 
 
+int device_numa_node(const DeviceCtx &dc);
 }  // namespace tsg

@@ -102,6 +102,7 @@ struct SearchOut {
 };
 // Runs the device pipeline for a set of (block index, block) pairs that share
 // one device. limit 0 = every match; limit L = each block's first L matches.
+int device_numa_node(const DeviceCtx &dc);
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
                    uint32_t limit, uint32_t flags, SearchOut &out);
 

@@ -111,7 +111,7 @@ class _LookupResult(C.Structure):
 
 # Every symbol include/tsg.h declares (checked by tests/test_abi.py).
 EXPORTED = [
-    "tsg_init", "tsg_shutdown", "tsg_device_count", "tsg_last_error", "tsg_abi_version", "tsg_cancel",
+    "tsg_init", "tsg_shutdown", "tsg_device_count", "tsg_device_numa_node", "tsg_last_error", "tsg_abi_version", "tsg_cancel",
     "tsg_pipeline_new", "tsg_pipeline_query", "tsg_pipeline_free", "tsg_pipeline_matches_header",
     "tsg_block_open", "tsg_block_open_mem", "tsg_wal_block_open", "tsg_wal_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
     "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_kernel_times", "tsg_results_combine",
@@ -135,6 +135,7 @@ def lib():
         L.tsg_init.argtypes = [C.POINTER(_Options), C.POINTER(vp)]
         L.tsg_shutdown.argtypes = [vp]
         L.tsg_device_count.argtypes = [vp]
+        L.tsg_device_numa_node.argtypes = [vp, C.c_int]
         L.tsg_pipeline_new.argtypes = [C.POINTER(_Request), C.POINTER(vp)]
         L.tsg_pipeline_query.argtypes = [vp]
         L.tsg_pipeline_query.restype = C.POINTER(_Query)
@@ -310,6 +311,10 @@ class Engine:
     @property
     def device_count(self):
         return lib().tsg_device_count(self.h)
+
+    def numa_node(self, dev: int = 0) -> int:
+        """NUMA node of the device (tsg_device_numa_node), -1 if unknown."""
+        return lib().tsg_device_numa_node(self.h, dev)
 
     def open_wal_block(self, path: str, device: int = 0) -> "StreamingSearchBlock":
         """Replay a search WAL file (<blockID>:<tenant>:v2:<encoding>[:...]) onto a device."""
