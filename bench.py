@@ -88,7 +88,7 @@ def parse():
     ap.add_argument("--entries", type=int, default=1_000_000, help="entries per block")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-blocks", type=int, default=4, help="blocks in the CPU baseline sample")
-    ap.add_argument("--events", type=int, default=4,
+    ap.add_argument("--events", type=int, default=8,
                     help="HIP events around the search kernel of every N-th timed step (roofline.achieved: "
                          "the average over those launches); 0 = off")
     ap.add_argument("--limit-steps", type=int, default=20,

@@ -59,14 +59,13 @@ struct DeviceCtx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, es0 = nullptr, es1 = nullptr;
   hipEvent_t mk0 = nullptr, mk1 = nullptr;  // untimed markers around a launch
-  // TSG_MARK (default 1): bit 0 = an untimed marker event recorded right before each
-  // search launch, bit 1 = one right after it. Measured on MI355X (tools/gpu_hostsweep.sh,
-  // profiles/r01_host): a marker in front of the launch cuts the config-2 step from
-  // ~80 to ~64 us (launch-to-flag 47.6 -> 38.5 us, result copy 12.5 -> 7.7 us); one
-  // behind it does not help. A timed event pair (SEARCH_TIME_*) has the same effect.
+  // TSG_MARK (default 0, experiment): bit 0 = an untimed marker event recorded right
+  // before each search launch, bit 1 = one right after it. An apparent 16 us/step gain
+  // was NUMA placement of the polling thread (profiles/r01_host); with the thread on the
+  // GPU's node a marker costs ~2-3 us per step.
   int mark_mode = [] {
     const char *e = std::getenv("TSG_MARK");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 0;
   }();
   std::mutex mu;
   // search scratch: descriptors, dictionary matches, value-set bitmaps, match
