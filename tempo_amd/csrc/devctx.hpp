@@ -63,6 +63,10 @@ struct DeviceCtx {
   // before each search launch, bit 1 = one right after it. An apparent 16 us/step gain
   // was NUMA placement of the polling thread (profiles/r01_host); with the thread on the
   // GPU's node a marker costs ~2-3 us per step.
+  bool stage_first = [] {  // TSG_STAGE_FIRST=0/1: dictionary words before the tile stream
+    const char *e = std::getenv("TSG_STAGE_FIRST");
+    return e ? std::atoi(e) != 0 : false;
+  }();
   int mark_mode = [] {
     const char *e = std::getenv("TSG_MARK");
     return e ? std::atoi(e) : 0;

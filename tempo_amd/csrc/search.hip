@@ -479,6 +479,7 @@ __device__ __forceinline__ void emit_tile(const ScanSeg &S, uint32_t mask, uint6
 //   fails the query loudly). Only workgroups with matches (and the last one, which
 //   writes the header) look back.
 // Phase 3 (emit): records in scan order straight into the pinned host buffer.
+constexpr uint32_t kStampSlots = 8;     // TSG_STAMPS: start setup scan lookback end | desc staged inlds
 constexpr uint32_t kLdsTiles = 16;      // tiles per workgroup whose masks stay in LDS
 constexpr uint32_t kMaxTpw = 2048;      // tiles per workgroup (per-tile counts in LDS)
 constexpr uint32_t kSpinMax = 1u << 22; // look-back poll bound (~seconds): never reached unless broken
@@ -524,9 +525,9 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
   __shared__ unsigned long long s_wsum[kThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   auto stamp = [&](int k) {
-    if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * 5 + k] = __builtin_amdgcn_s_memrealtime();
+    if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * kStampSlots + k] = __builtin_amdgcn_s_memrealtime();
   };
-  if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * 5] = t_start;
+  if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * kStampSlots] = t_start;
 
   // ---- phase 1: scan, one tile of loads in flight ahead of the tile evaluated
   const uint32_t lw = wg - S.first_wg;  // units split evenly over the block's workgroups (+-1 unit)
@@ -750,6 +751,7 @@ struct QArgs {
   uint32_t bm_words, stage_words;
   uint32_t mask_words;      // LDS words between the bitmaps and the block sums: tile masks / self-match stage
   uint32_t self_dict;       // 1: every scan workgroup matches its block's (small) dictionaries itself, njobs = 0
+  uint32_t stage_first;     // self_dict: the dictionary words land before the first tile loads issue
   unsigned long long *gbm;  // njobs x gstride granules
   ScanParams P;             // thresholds, outputs (segs/terms/wg_seg unused)
 };
@@ -922,6 +924,8 @@ __device__ __forceinline__ void self_finish(SelfStage<NTA> &X, const QArgs &A, c
     }
   }
   __syncthreads();
+  if (A.P.stamps && tid == 0)  // TSG_STAMPS slot 7: dictionary words in LDS
+    A.P.stamps[uint64_t(blockIdx.x - A.njobs) * kStampSlots + 7] = __builtin_amdgcn_s_memrealtime();
   bool sets = false;
 #pragma unroll
   for (int q = 0; q < NTA; q++) {
@@ -1039,7 +1043,18 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   // tile's loads are in flight
   SelfStage<NTA> X;
   auto issue_stage = [&] {
-    if (NT > 0 && A.self_dict) self_issue<NTA>(X, KD);
+    if (A.P.stamps && threadIdx.x == 0)  // (waits for the descriptor scalar loads: lgkmcnt)
+      A.P.stamps[uint64_t(wg) * kStampSlots + 5] = __builtin_amdgcn_s_memrealtime();
+    if (NT > 0 && A.self_dict) {
+      self_issue<NTA>(X, KD);
+      // stage_first: wait for the (few, L2-shared) dictionary words before this
+      // workgroup's tile stream is issued. Issued together, they queue behind every
+      // CU's opening burst of tile loads (~60 MB chip-wide) and gate the scan for
+      // ~10 us; alone they land in ~1-2 us and the matching then hides under the tiles.
+      if (A.stage_first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (A.P.stamps && threadIdx.x == 0)
+      A.P.stamps[uint64_t(wg) * kStampSlots + 6] = __builtin_amdgcn_s_memrealtime();
   };
   auto wait_bitmaps = [&] {
     if (NT > 0 && A.self_dict) {  // (self_finish ends with a barrier)
@@ -1180,16 +1195,17 @@ struct Tracer {
 
 // TSG_STAMPS: where a launch's time goes (us from the first workgroup start; 100 MHz clock)
 static void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast) {
-  std::vector<unsigned long long> st(size_t(nwg) * 5);
+  std::vector<unsigned long long> st(size_t(nwg) * kStampSlots);
   HIP_OK(hipMemcpy(st.data(), dc.stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
   unsigned long long t0 = ~0ull;
-  for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, st[size_t(w) * 5]);
-  const char *names[5] = {"start", "setup", "scan", "lookback", "end"};
+  for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, st[size_t(w) * kStampSlots]);
+  const char *names[8] = {"start", "setup", "scan", "lookback", "end", "desc", "staged", "inlds"};
   std::fprintf(stderr, "[tsg] stamps (%s, %u wg) us avg/max:", fast ? "one-launch" : "general", nwg);
-  for (int k = 0; k < 5; k++) {
+  for (int k = 0; k < 8; k++) {
     double sum = 0, mx = 0;
     for (uint32_t w = 0; w < nwg; w++) {
-      const double v = double(st[size_t(w) * 5 + k] - t0) / 100.0;
+      const unsigned long long x = st[size_t(w) * kStampSlots + k];
+      const double v = x ? double(x - t0) / 100.0 : 0.0;  // (unwritten slot: 0)
       sum += v;
       mx = std::max(mx, v);
     }
@@ -1201,8 +1217,8 @@ static void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast) {
   double gsum[8] = {}, gmax[8] = {};
   uint32_t gn[8] = {};
   for (uint32_t w = 0; w < nwg; w++) {
-    se[w] = double(st[size_t(w) * 5 + 2] - t0) / 100.0;
-    su[w] = double(st[size_t(w) * 5 + 1] - t0) / 100.0;
+    se[w] = double(st[size_t(w) * kStampSlots + 2] - t0) / 100.0;
+    su[w] = double(st[size_t(w) * kStampSlots + 1] - t0) / 100.0;
     gsum[w & 7] += se[w];
     gmax[w & 7] = std::max(gmax[w & 7], se[w]);
     gn[w & 7]++;
@@ -1477,8 +1493,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   configure(seg, seg ? 0 : lb_cap());
   static const bool want_stamps = std::getenv("TSG_STAMPS") != nullptr;
   if (want_stamps) {
-    dc.stamps.ensure(size_t(nwg) * 5 * 8);
-    HIP_OK(hipMemsetAsync(dc.stamps.p, 0, size_t(nwg) * 5 * 8, s));
+    dc.stamps.ensure(size_t(nwg) * kStampSlots * 8);
+    HIP_OK(hipMemsetAsync(dc.stamps.p, 0, size_t(nwg) * kStampSlots * 8, s));
     P.stamps = static_cast<unsigned long long *>(dc.stamps.p);
   }
   QArgs A;
@@ -1498,6 +1514,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     A.nterms = q.nterms;
     A.njobs = njobs_fast;
     A.self_dict = self_dict ? 1u : 0u;
+    A.stage_first = dc.stage_first ? 1u : 0u;
     A.mask_words = fast_mask_words;
     A.gstride = fast_words;
     A.bm_words = fast_bm_words;
