@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <list>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -379,7 +380,6 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     std::memset(&m, 0, sizeof m);
     // block filter on the host (header), device work grouped per device
     std::vector<int> state(nblocks, 0);  // 0 no meta, 1 skipped, 2 inspected
-    std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, Block *>>> per_dev;
     for (size_t i = 0; i < nblocks; i++) {
       Block &b = blocks[i]->b;
       if (!b.host.has_meta) continue;
@@ -387,20 +387,28 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
                     ? pipeline_matches_stream_header(*q, b.host.min_dur, b.host.max_dur, b.host.stream_tags)
                     : pipeline_matches_block(*q, b.host.header.data(), b.host.header.size());
       state[i] = ok ? 2 : 1;
-      if (ok && b.dc) per_dev[b.dc].push_back({uint32_t(i), &b});
     }
-    std::vector<std::pair<DeviceCtx *, SearchOut>> outs;
-    outs.reserve(per_dev.size());
-    for (auto &kv : per_dev) outs.push_back({kv.first, SearchOut()});
-    {
+    // Blocks [b0, b1) on their devices, one device_search per device (concurrently).
+    std::list<std::pair<DeviceCtx *, SearchOut>> outs;  // (stable: per_block points into recs)
+    std::vector<std::pair<const SearchOut::Rec *, size_t>> per_block(nblocks, {nullptr, 0});
+    size_t nrec = 0;
+    auto search_range = [&](size_t b0, size_t b1) {
+      std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, Block *>>> per_dev;
+      for (size_t i = b0; i < b1; i++)
+        if (state[i] == 2 && blocks[i]->b.dc) per_dev[blocks[i]->b.dc].push_back({uint32_t(i), &blocks[i]->b});
+      std::vector<SearchOut *> slots;
+      for (auto &kv : per_dev) {
+        outs.push_back({kv.first, SearchOut()});
+        slots.push_back(&outs.back().second);
+      }
       std::vector<std::thread> th;
-      std::vector<std::exception_ptr> errs(outs.size());
+      std::vector<std::exception_ptr> errs(slots.size());
       size_t k = 0;
       for (auto &kv : per_dev) {
-        size_t slot = k++;
-        auto work = [&, slot, &list = kv.second]() {
+        const size_t slot = k++;
+        auto work = [&, slot, dc = kv.first, &list = kv.second]() {
           try {
-            device_search(*outs[slot].first, list, *q, limit, flags, outs[slot].second);
+            device_search(*dc, list, *q, limit, flags, *slots[slot]);
           } catch (...) {
             errs[slot] = std::current_exception();
           }
@@ -411,26 +419,55 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       for (auto &t : th) t.join();
       for (auto &e : errs)
         if (e) std::rethrow_exception(e);
+      // per block match lists in scan order (each device's records are grouped by block already)
+      uint64_t wave_k = 0, wave_s = 0;  // devices run concurrently: a wave takes its slowest
+      for (SearchOut *o : slots) {
+        m.device_bytes_read += o->device_bytes;
+        wave_k = std::max<uint64_t>(wave_k, o->kernel_ns);
+        wave_s = std::max<uint64_t>(wave_s, o->scan_ns);
+        m.scan_bytes += o->scan_bytes;
+        const auto &recs = o->recs;
+        for (size_t r = 0; r < recs.size();) {
+          const uint32_t bi = recs[r].block_il & 0xffffffu;
+          size_t e = r;
+          while (e < recs.size() && (recs[e].block_il & 0xffffffu) == bi) e++;
+          per_block[bi] = {&recs[r], e - r};
+          r = e;
+        }
+        nrec += recs.size();
+      }
+      m.kernel_ns += wave_k;
+      m.scan_kernel_ns += wave_s;
+    };
+    // Early exit (limit > 0): the consumer stops at the L-th distinct
+    // id in block order, so the blocks behind that point are never needed. A first wave
+    // searches the leading blocks (>= 1/8 of the entries); only if the consumer has not
+    // stopped inside them does a second wave search the rest. Each block's matches do
+    // not depend on which other blocks share its launch, so the result is the one-wave
+    // result. limit 0, or a single block: one wave.
+    size_t b1 = nblocks;
+    if (limit && nblocks > 1) {
+      uint64_t total = 0, acc = 0;
+      for (size_t i = 0; i < nblocks; i++)
+        if (state[i] == 2) total += blocks[i]->b.host.n;
+      b1 = 0;
+      while (b1 < nblocks && (acc * 8 < total || acc == 0)) {
+        if (state[b1] == 2) acc += blocks[b1]->b.host.n;
+        b1++;
+      }
+    }
+    search_range(0, b1);
+    if (b1 < nblocks) {
+      std::unordered_set<std::string> seen;
+      bool stop = false;
+      for (size_t i = 0; i < b1 && !stop; i++)
+        for (size_t ri = 0; ri < per_block[i].second && !stop; ri++) {
+          seen.insert(std::string(reinterpret_cast<const char *>(per_block[i].first[ri].id), 16));
+          stop = seen.size() >= limit;
+        }
+      if (!stop) search_range(b1, nblocks);
     }
     const clk::time_point t_dev = trace ? clk::now() : clk::time_point();
-    // per block match lists in scan order (each device's records are grouped by block already)
-    std::vector<std::pair<const SearchOut::Rec *, size_t>> per_block(nblocks, {nullptr, 0});
-    size_t nrec = 0;
-    for (auto &o : outs) {
-      m.device_bytes_read += o.second.device_bytes;
-      m.kernel_ns = std::max<uint64_t>(m.kernel_ns, o.second.kernel_ns);
-      m.scan_kernel_ns = std::max<uint64_t>(m.scan_kernel_ns, o.second.scan_ns);
-      m.scan_bytes += o.second.scan_bytes;
-      const auto &recs = o.second.recs;
-      for (size_t r = 0; r < recs.size();) {
-        const uint32_t bi = recs[r].block_il & 0xffffffu;
-        size_t e = r;
-        while (e < recs.size() && (recs[e].block_il & 0xffffffu) == bi) e++;
-        per_block[bi] = {&recs[r], e - r};
-        r = e;
-      }
-      nrec += recs.size();
-    }
     res->reserve(nrec);
     res->resize(nrec);
     size_t nout = 0;

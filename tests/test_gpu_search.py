@@ -312,3 +312,21 @@ def test_high_cardinality_config4(engine, tmp_path):
         got, met, exp, omet = both(engine, [p], **q)
         assert_parity(got, met, exp, omet)
         assert len(exp) > 0
+
+
+@pytest.mark.parametrize("limit", [1, 20, 300, 5000])
+def test_limit_early_exit_waves(engine, tmp_path, limit):
+    """limit > 0 over many blocks: the leading blocks are searched first and the rest
+    only when the consumer has not stopped inside them (tsg_search's two waves). Dense
+    queries stop in the first wave, sparse ones need the second; both must equal the
+    oracle's single sequential pass, metrics included."""
+    rng = random.Random(100 + limit)
+    paths = []
+    for b in range(10):
+        ents = random_entries(rng, 2000 + 300 * b, nkeys=3, nvals=4)
+        paths.append(write_block(str(tmp_path), "w%d" % b, ents, page_size=16384))
+    for q in [dict(tags={"k0": "v"}),            # dense: stops in block 0
+              dict(tags={"k1": "v1-x"}),         # medium
+              dict(tags={"k2": "v3-z", "k0": "v2"}, min_ms=50)]:  # sparse: all blocks
+        got, met, exp, omet = both(engine, paths, limit=limit, **q)
+        assert_parity(got, met, exp, omet)
