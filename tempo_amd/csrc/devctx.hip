@@ -51,7 +51,7 @@ void ctx_shutdown(Ctx &c) {
     (void)hipSetDevice(dc->ordinal);
     (void)hipStreamSynchronize(dc->stream);
     for (DevBuf *b : {&dc->desc, &dc->vmatch, &dc->bitmaps, &dc->gran, &dc->ticket, &dc->out, &dc->regions,
-                      &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps, &dc->gbm,
+                      &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps, &dc->gbm, &dc->lkhits,
                       &dc->done})
       b->release();
     for (hipEvent_t e : dc->tring) (void)hipEventDestroy(e);

@@ -76,7 +76,7 @@ struct DeviceCtx {
   // bitmasks (one bit per entry of tiles that matched), per-tile / per-workgroup
   // counts, [header | records] output. lookup reuses desc/gran/ticket/out/hdr/err.
   DevBuf desc, vmatch, bitmaps, gran, ticket, out, regions, seg_counts, hdr, err;
-  DevBuf maskbits, agg, stamps, gbm;
+  DevBuf maskbits, agg, stamps, gbm, lkhits;
   HostBuf hdesc, hout;
   // search results, written by the emit kernel directly (coherent: the kernel's
   // stores go over the fabric, visible to the host once the stream is synchronised)

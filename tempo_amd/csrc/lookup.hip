@@ -43,6 +43,10 @@ struct LkParams {
   uint64_t *offsets;  // per id: first output slot
   uint64_t *total;
   uint32_t *err;
+  // the count pass keeps each id's first kHitK hits (block ordinal, record): the write
+  // pass copies them instead of probing every block again (more hits: it re-probes)
+  uint32_t *hit_cnt, *hit_b;
+  int32_t *hit_r;
   // write pass
   uint32_t *o_id, *o_block;
   int32_t *o_rec;
@@ -133,6 +137,7 @@ __device__ __forceinline__ int32_t d_probe(const LkBlock &B, const uint8_t *id, 
 }
 
 constexpr int kLkThreads = 256;
+constexpr uint32_t kHitK = 4;
 constexpr unsigned long long kGAgg = 1, kGInc = 2;
 
 __device__ __forceinline__ void d_id_hash(const uint8_t *id, uint32_t &fnv, uint64_t h[4]) {
@@ -160,8 +165,16 @@ extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_count_kernel(LkP
     uint32_t fnv;
     uint64_t h[4];
     d_id_hash(id, fnv, h);
-    for (uint32_t b = 0; b < P.nblocks; b++)
-      if (d_probe(P.blocks[b], id, fnv, h) >= 0) cnt++;
+    for (uint32_t b = 0; b < P.nblocks; b++) {
+      const int32_t r = d_probe(P.blocks[b], id, fnv, h);
+      if (r < 0) continue;
+      if (cnt < kHitK) {
+        P.hit_b[i * kHitK + cnt] = b;
+        P.hit_r[i * kHitK + cnt] = r;
+      }
+      cnt++;
+    }
+    P.hit_cnt[i] = cnt;
   }
   // block scan of counts
   unsigned long long v = cnt;
@@ -229,6 +242,20 @@ extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_count_kernel(LkP
 extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_write_kernel(LkParams P) {
   const uint64_t i = uint64_t(blockIdx.x) * kLkThreads + threadIdx.x;
   if (i >= P.nids) return;
+  const uint32_t cnt = P.hit_cnt[i];
+  if (cnt <= kHitK) {  // every hit was kept by the count pass, in block order
+    uint64_t o = P.offsets[i];
+    for (uint32_t j = 0; j < cnt; j++, o++) {
+      const LkBlock &B = P.blocks[P.hit_b[i * kHitK + j]];
+      const int32_t r = P.hit_r[i * kHitK + j];
+      P.o_id[o] = uint32_t(i);
+      P.o_block[o] = B.block_idx;
+      P.o_rec[o] = r;
+      P.o_start[o] = B.rec_start[r];
+      P.o_len[o] = B.rec_len[r];
+    }
+    return;
+  }
   uint8_t id[16];
   memcpy(id, P.ids + i * 16, 16);
   uint32_t fnv;
@@ -458,6 +485,10 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
   P.offsets = static_cast<uint64_t *>(dc.vmatch.p);
   P.total = static_cast<uint64_t *>(dc.hdr.p);
   P.err = static_cast<uint32_t *>(dc.err.p);
+  dc.lkhits.ensure(std::max<uint64_t>(nids, 1) * (4 + kHitK * 8));
+  P.hit_cnt = static_cast<uint32_t *>(dc.lkhits.p);
+  P.hit_b = P.hit_cnt + nids;
+  P.hit_r = reinterpret_cast<int32_t *>(P.hit_b + nids * kHitK);
   HIP_OK(hipEventRecord(dc.ev0, s));
   lookup_count_kernel<<<tiles, kLkThreads, 0, s>>>(P);
   HIP_OK(hipGetLastError());

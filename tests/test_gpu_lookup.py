@@ -62,3 +62,23 @@ def test_time_and_block_range(engine, tmp_path):
     lo, hi = bytes(16), bytes([0x80] + [0] * 15)
     got, _ = engine.lookup(blocks, ids, block_start=lo, block_end=hi)
     np.testing.assert_array_equal(got, oracle_hits(paths, ids, bstart=lo, bend=hi))
+
+
+def test_ids_in_many_blocks(engine, tmp_path):
+    """The same block set opened 7 times: every present id hits 7 blocks, more than
+    the count pass keeps per id (4), so the write pass re-probes those ids; ids with
+    <= 4 hits are copied. Both must give the oracle's (id, block) order."""
+    paths = []
+    for b in range(2):
+        p = os.path.join(str(tmp_path), "m%d" % b)
+        T.synth_v2_block(p, 8000, seed=40 + b)
+        paths.append(p)
+    stored = [T.synth_v2_block(os.path.join(str(tmp_path), "s"), 8000, seed=40)]
+    rng = np.random.default_rng(3)
+    ids = np.concatenate([stored[0][rng.integers(0, len(stored[0]), 2000)],
+                          rng.integers(0, 256, size=(3000, 16), dtype=np.uint8)])
+    order = [paths[0]] * 5 + [paths[1]] * 2  # id of block m0: 5 hits; duplicates of m1 ids: 2
+    blocks = [engine.open_v2block(p) for p in order]
+    got, _ = engine.lookup(blocks, ids)
+    np.testing.assert_array_equal(got, oracle_hits(order, ids))
+    assert np.bincount(got[:, 0]).max() >= 5
