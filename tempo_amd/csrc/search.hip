@@ -484,6 +484,7 @@ constexpr uint32_t kLdsTiles = 16;      // tiles per workgroup whose masks stay 
 constexpr uint32_t kMaxTpw = 2048;      // tiles per workgroup (per-tile counts in LDS)
 constexpr uint32_t kSpinMax = 1u << 22; // look-back poll bound (~seconds): never reached unless broken
 constexpr uint32_t kMaxSegs = 2048;
+constexpr uint32_t kCountPending = 0xffffffffu;  // segment mode: a workgroup count not stored yet (host sentinel)
 
 // workgroup -> block and per-block record caps, from the device descriptors
 struct DescSegs {
@@ -584,7 +585,9 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
     // segment mode: the first min(seg_cap, cap) matches of this workgroup go to its
     // own segment of the pinned buffer, its count to counts[wg]; the host concatenates
     // the segments in workgroup order (= scan order). No workgroup waits on another.
-    if (tid == 0) host_store(P.counts + wg, wsum);
+    // The count is stored after the records have completed: the host reads a count
+    // that is no longer the sentinel it wrote before the launch as "this segment is
+    // final" and pulls it into its caches while later workgroups are still scanning.
     stamp(3);
     if (wsum) {
       // records are gathered into LDS first (no gather load waits behind a host store:
@@ -609,7 +612,10 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
       const uint32_t nw = uint32_t(umin64(wsum, keep)) * 6;
       auto *dst = reinterpret_cast<unsigned long long *>(P.out + P.hdr_bytes) + (unsigned long long)wg * P.seg_cap * 6;
       for (uint32_t i = tid; i < nw; i += kThreads) host_store(dst + i, lds_rec[i]);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
     }
+    if (tid == 0) host_store(P.counts + wg, wsum);
     stamp(4);
     return;
   }
@@ -1592,6 +1598,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     h[0] = 0;
     h[1] = 0;  // look-back / granule poll error flag
     h[2] = 0;  // completion flag (one-launch path)
+    if (fast && P.seg_cap) std::fill_n(P.counts, nwg, kCountPending);  // (each workgroup stores its count last)
     if (fast) {
       uint32_t ng = 0;
       for (uint32_t g = 0; g < 8; g++) {
@@ -1637,8 +1644,28 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       return;
     }
     const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(P.out);
+    // while the tail of the launch runs, pull the record segments of workgroups that
+    // have finished into this core's caches (the copy after the flag then reads cached
+    // lines instead of missing on every one)
+    const volatile uint32_t *cnt = P.counts;
+    const uint8_t *rec = P.out + P.hdr_bytes;
+    thread_local std::vector<uint8_t> seen;
+    seen.assign(nwg, 0);
+    uint32_t lo = 0;  // every workgroup below lo has been seen
     for (uint32_t it = 1;; it++) {
       if (h[2] == P.epoch) return;
+      for (uint32_t w = lo; w < nwg; w++) {
+        if (seen[w]) {
+          if (w == lo) lo++;
+          continue;
+        }
+        const uint32_t c = cnt[w];
+        if (c == kCountPending) continue;
+        seen[w] = 1;
+        if (w == lo) lo++;
+        const uint8_t *p0 = rec + uint64_t(w) * P.seg_cap * sizeof(MatchRec);
+        for (uint64_t o = 0; o < uint64_t(std::min(c, P.seg_cap)) * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
+      }
       if ((it & 255u) == 0) {
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) {
