@@ -63,7 +63,7 @@ if has pmc; then
   export TMPDIR=/tmp
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 900 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv -- \
-      python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err
+      python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 --limit-steps 0 ${BENCH_ARGS:-} > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err
     rc=$?; echo "pmc $c rc=$rc"
     [ $rc -eq 0 ] || exit $rc
   done
