@@ -61,19 +61,33 @@ struct ResultHolder {
   std::vector<uint64_t> start, end, entry;
   std::vector<uint32_t> dur, block, svc_len, name_len;
   std::vector<uint64_t> svc_off, name_off;  // into `arena` (one allocation for every name)
-  std::vector<char> arena;
+  char *arena = nullptr;  // (grown by hand: no zero-fill, no per-name insert)
+  size_t arena_size = 0, arena_cap = 0;
+  ResultHolder() = default;
+  ResultHolder(const ResultHolder &) = delete;
+  ResultHolder &operator=(const ResultHolder &) = delete;
+  ~ResultHolder() { std::free(arena); }
+  void arena_grow(size_t need) {
+    const size_t cap = std::max<size_t>({need, 2 * arena_cap, 4096});
+    char *p = static_cast<char *>(std::realloc(arena, cap));
+    if (!p) throw std::bad_alloc();
+    arena = p;
+    arena_cap = cap;
+  }
   std::vector<const char *> svc_p, name_p;
   void reserve(size_t n) {
     ids.reserve(16 * n);
     for (auto *v : {&start, &end, &entry, &svc_off, &name_off}) v->reserve(n);
     for (auto *v : {&dur, &block, &svc_len, &name_len}) v->reserve(n);
     id_len.reserve(n);
-    arena.reserve(24 * n);
+    if (24 * n > arena_cap) arena_grow(24 * n);
   }
   void set_str(std::vector<uint64_t> &off, std::vector<uint32_t> &len, size_t i, const char *p, size_t l) {
-    off[i] = arena.size();
+    off[i] = arena_size;
     len[i] = uint32_t(l);
-    arena.insert(arena.end(), p, p + l);
+    if (arena_size + l > arena_cap) arena_grow(arena_size + l);
+    if (l) std::memcpy(arena + arena_size, p, l);
+    arena_size += l;
   }
   size_t size() const { return start.size(); }
   void resize(size_t n) {
@@ -100,8 +114,8 @@ struct ResultHolder {
     resize(i + 1);
     set(i, id, il, s, e, b, en, sv, svl, nm, nml);
   }
-  const char *svc(size_t i) const { return arena.data() + svc_off[i]; }
-  const char *name(size_t i) const { return arena.data() + name_off[i]; }
+  const char *svc(size_t i) const { return arena + svc_off[i]; }
+  const char *name(size_t i) const { return arena + name_off[i]; }
   void finalize() {
     const size_t n = start.size();
     svc_p.resize(n);
