@@ -56,7 +56,7 @@ fi
 if has prof; then
   export TMPDIR=/tmp
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-    python3 bench.py --steps 20 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
+    python3 bench.py --steps 20 --warmup 3 --cpu-baseline 0 --limit-steps 0 ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
   rc=$?; echo "rocprof rc=$rc"; cat gpurun_out/prof/run_kernel_stats.csv
 fi
 if has pmc; then
