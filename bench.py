@@ -1,12 +1,18 @@
 #!/usr/bin/env python3
 """Benchmark: Tempo backend search on MI355X (BASELINE.json configs[1], "config 2").
 
-One step = one full search (tsg_search) of the resident block set with the
+One step = one full search (tsg_search) of a resident 10 M-entry block set with the
 config-2 query: {service.name: svc-07, http.method: get, status.code: error}
 + MinDurationMs=10 + MaxDurationMs=1000 + Start/End over the middle 50 % of
 the one-hour window, limit 0 (every match, ordered). Inputs are resident in HBM
-before the timed region; each step includes the dictionary pass, the scan +
-compaction kernels, the result D2H and host result assembly.
+before the timed region; each step includes the dictionary match, the scan +
+compaction kernel, the records landing in pinned host memory and host result
+assembly (names resolved), i.e. what the Go shim receives.
+
+HBM regime: the set is resident --sets (4) times as disjoint copies (tsg_block_clone)
+and step i searches copy i % 4, so 4 x 150 MB of filter columns rotate through the
+256 MiB Infinity Cache and every step streams from HBM (roofline.regime "hbm").
+The same-copy-every-step number (round 1's, MALL-resident) is reported as "mall".
 
 Multi-GPU: one process per GPU (torchrun); blocks are sharded by block, each
 rank holds its own 10 M entries (weak scaling). Rank timings are bracketed by a
@@ -79,15 +85,32 @@ def node_cpus(node):
     return out
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--blocks", type=int, default=10, help="blocks per GPU")
+    ap.add_argument("--blocks", type=int, default=10, help="blocks per GPU (one config-2 set)")
     ap.add_argument("--entries", type=int, default=1_000_000, help="entries per block")
+    ap.add_argument("--sets", type=int, default=4,
+                    help="disjoint resident copies of the block set (tsg_block_clone), searched in rotation: "
+                         "4 x 150 MB of filter columns >> the 256 MiB Infinity Cache, so every step streams "
+                         "from HBM (roofline.regime 'hbm'); 1 = the same set every step ('mall')")
+    ap.add_argument("--mall-steps", type=int, default=100,
+                    help="extra timed steps on one set (the MALL-resident regime), reported beside; 0 = skip")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
-    ap.add_argument("--cpu-blocks", type=int, default=4, help="blocks in the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the columnar CPU baseline (0 = this process's CPU share, at most 16)")
     ap.add_argument("--events", type=int, default=8,
                     help="HIP events around the search kernel of every N-th timed step (roofline.achieved: "
                          "the average over those launches); 0 = off")
@@ -134,6 +157,80 @@ def gen_blocks(workdir, rank, nblocks, n, threads):
     return paths
 
 
+def parallel(fn, items):
+    out = [None] * len(items)
+    errs = []
+
+    def run(i):
+        try:
+            out[i] = fn(items[i])
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(items))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    if errs:
+        raise errs[0]
+    return out
+
+
+def cpu_baselines(paths, got, threads):
+    """The reference's scan restated (oracle: snappy decode + flatbuffer walk + ContainsTag,
+    one thread per block like instance.searchLocalBlocks) and the CPU columnar variant
+    (the same predicates over host-decoded columns, `threads` threads), both on every
+    block of this rank's set. Returns the cpu_baseline object."""
+    from oracle import oracle as O
+    q = dict(tags=QUERY["tags"], min_ms=QUERY["min_duration_ms"], max_ms=QUERY["max_duration_ms"],
+             start=QUERY["start"], end=QUERY["end"])
+    oblocks = [O.Block(p) for p in paths]
+    nb = len(oblocks)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        exp, omet, st = O.search(oblocks, nthreads=nb, **q)
+        reps += 1
+        if time.perf_counter() - t0 > 10 or reps >= 5:
+            break
+    cpu_s = (time.perf_counter() - t0) / reps
+    entries = omet["traces_inspected"]
+    # parity of the GPU's full result against it: every field of every match, in order
+    gk = [(m.block_idx, m.entry_idx, m.trace_id, m.start_time_unix_nano, m.end_time_unix_nano, m.duration_ms,
+           m.root_service_name.encode(), m.root_trace_name.encode()) for m in got]
+    ek = [(m["block_idx"], m["entry_idx"], m["id"], m["start_ns"], m["end_ns"], m["duration_ms"], m["root_service"],
+           m["root_name"]) for m in exp]
+    out = {
+        "value": entries / cpu_s, "unit": "entries/s", "cores": nb, "kind": "port",
+        "sample": f"oracle BackendSearchBlock.Search restatement (snappy decode + flatbuffer walk + ContainsTag "
+                  f"included), all {nb} blocks ({entries} entries) of the GPU's set, one thread per block "
+                  f"(instance.searchLocalBlocks), {reps} rep(s)",
+        "decompression_included": True,
+        "nproc": os.cpu_count(), "cpu_share": len(os.sched_getaffinity(0)), "cpu_model": cpu_model(),
+        "parity": gk == ek and omet["blocks_inspected"] == nb,
+    }
+    # columnar: decode once (not timed, like the GPU's resident columns), then time the scan
+    t0 = time.perf_counter()
+    cols = parallel(O.ColumnarBlock, oblocks)
+    build_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        cm, ch = O.columnar_search(cols, nthreads=threads, **q)
+        reps += 1
+        if time.perf_counter() - t0 > 5 or reps >= 50:
+            break
+    col_s = (time.perf_counter() - t0) / reps
+    out["columnar"] = {
+        "value": entries / col_s, "unit": "entries/s", "cores": threads,
+        "sample": f"the same {entries} entries decoded once into host columns ({build_s:.1f}s, untimed), "
+                  f"Pipeline predicates over the columns on {threads} threads, {reps} rep(s)",
+        "parity": cm == len(got) and ch == O.match_hash([(m.block_idx, m.entry_idx) for m in got]),
+    }
+    return out
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -158,25 +255,21 @@ def main():
 
     eng = T.Engine(devices=[local])
     t0 = time.time()
-    blocks = [None] * len(paths)
-
-    def opener(i):
-        blocks[i] = eng.open_block(paths[i])
-
-    ths = [threading.Thread(target=opener, args=(i,)) for i in range(len(paths))]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
+    base = parallel(eng.open_block, paths)
     load_s = time.time() - t0
-    infos = [b.info() for b in blocks]
+    infos = [b.info() for b in base]
     entries = sum(i["entries"] for i in infos)
     fb_bytes = sum(i["fb_bytes"] for i in infos)
     dev_bytes = sum(i["device_bytes"] for i in infos)
     log(f"rank {rank}: loaded {entries} entries ({fb_bytes / 1e9:.2f} GB flatbuffer) in {load_s:.1f}s, "
         f"{dev_bytes / 1e9:.2f} GB resident")
+    # disjoint resident copies of the set: the rotation's working set is sets x the set
+    sets = [base] + [[b.clone(eng) for b in base] for _ in range(max(1, args.sets) - 1)]
+    if len(sets) > 1:
+        log(f"rank {rank}: {len(sets)} resident copies of the set ({len(sets) * dev_bytes / 1e9:.2f} GB)")
 
     all_cpus = os.sched_getaffinity(0)
+    cpu_threads = args.cpu_threads or max(1, min(16, len(all_cpus)))
     if args.pin == "auto":
         # the step polls a completion word and copies its records from pinned host memory:
         # both are served faster from the GPU's own socket (profiles/r01_host).
@@ -192,26 +285,33 @@ def main():
     req = T.SearchRequest(tags=QUERY["tags"], min_duration_ms=QUERY["min_duration_ms"],
                           max_duration_ms=QUERY["max_duration_ms"], start=QUERY["start"], end=QUERY["end"])
     pipe = T.Pipeline(req)
-    got, met = eng.search(blocks, pipe)  # full result once (parity spot check below)
+    got, met = eng.search(base, pipe)  # full result once (parity check against the oracle below)
+    for s in sets[1:]:
+        g2, _ = eng.search(s, pipe)
+        assert [(m.block_idx, m.entry_idx, m.trace_id) for m in g2] == [(m.block_idx, m.entry_idx, m.trace_id)
+                                                                        for m in got], "clone differs"
     # HIP events around the search kernel of every --events-th timed step, on the
     # library's stream; read after the timed region (the search does not wait for them).
     # A pair of event records costs the host ~10 us, so not every step carries one.
     sflags = T.SEARCH_TIME_DEFER if args.events else 0
-    for _ in range(args.warmup):
-        eng.search_raw(blocks, pipe, flags=0)
+    for i in range(max(args.warmup, len(sets))):
+        eng.search_raw(sets[i % len(sets)], pipe, flags=0)
     eng.kernel_times()  # (drain)
+
+    def timed(nsteps, rot):
+        step_s = []
+        t0 = time.perf_counter()
+        for i in range(nsteps):  # (tsg_search is synchronous: results are on the host when it returns)
+            ts = time.perf_counter()
+            eng.search_raw(sets[i % rot], pipe, flags=sflags if args.events and i % args.events == 0 else 0)
+            step_s.append(time.perf_counter() - ts)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, step_s
 
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    step_s = []
-    t0 = time.perf_counter()
-    for i in range(args.steps):  # (tsg_search is synchronous: results are on the host when it returns)
-        ts = time.perf_counter()
-        nm, met = eng.search_raw(blocks, pipe, flags=sflags if args.events and i % args.events == 0 else 0)
-        step_s.append(time.perf_counter() - ts)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed, step_s = timed(args.steps, len(sets))
     scan_ns = eng.kernel_times() if args.events else []
     if dist:
         dist.barrier()
@@ -229,7 +329,8 @@ def main():
     scan_avg_ns = sum(scan_ns) / len(scan_ns) if scan_ns else 0
     scan_bytes = met.scan_bytes
     achieved = scan_bytes / scan_avg_ns if scan_avg_ns else None  # bytes/ns == GB/s
-    traffic, traffic_src = pmc_traffic(f"blocks={args.blocks},entries={args.entries}")
+    regime = "hbm" if len(sets) * scan_bytes > 256 * 2**20 * 1.5 else "mall"
+    traffic, traffic_src = pmc_traffic(f"blocks={args.blocks},entries={args.entries},sets={len(sets)}")
     out = {
         "metric": METRIC,
         "value": value,
@@ -247,30 +348,48 @@ def main():
             "workload": "cfg2: 10M-entry block set per GPU, 3-tag AND + min/max duration + time range, "
                         "full scan (limit 0), ordered match list",
             "blocks_per_gpu": args.blocks, "entries_per_block": args.entries, "entries_per_gpu": entries,
-            "query": QUERY, "limit": 0, "matches_per_gpu": len(got), "parallelism": f"block-sharded x{world}",
+            "resident_sets": len(sets), "query": QUERY, "limit": 0, "matches_per_gpu": len(got),
+            "parallelism": f"block-sharded x{world}",
         },
         "achieved_hbm_gbps": achieved,
         "roofline": {
             "bound": "hbm", "kernel": KERNEL, "achieved": achieved, "peak": PEAK_HBM_GBPS,
-            "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS if achieved else None, "traffic": traffic,
+            "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS if achieved else None,
+            "regime": regime,
+            "regime_note": (f"each step searches the next of {len(sets)} disjoint resident copies of the set "
+                            f"({len(sets)} x {scan_bytes / 1e6:.0f} MB of filter columns per rotation > the "
+                            f"256 MiB Infinity Cache)" if len(sets) > 1 else
+                            "the same set every step: its filter columns stay in the 256 MiB Infinity Cache"),
+            "traffic": traffic, "traffic_measured_in_run": False,
             "traffic_source": traffic_src, "bytes_per_launch": scan_bytes, "avg_launch_us": scan_avg_ns / 1e3,
             "bytes_per_entry": 15,
         },
         "load_s": load_s,
+        "load_gb_per_s": fb_bytes / load_s / 1e9 if load_s else None,
         "flatbuffer_gb_per_gpu": fb_bytes / 1e9,
     }
-
     out["latency_us"] = {"step": pct([x * 1e6 for x in step_s]), "kernel": pct([x / 1e3 for x in scan_ns])}
+
+    if args.mall_steps and len(sets) > 1:
+        # the same set every step: its columns stay in the Infinity Cache (round 1's regime)
+        e2, s2 = timed(args.mall_steps, 1)
+        k2 = eng.kernel_times() if args.events else []
+        a2 = scan_bytes / (sum(k2) / len(k2)) if k2 else None
+        out["mall"] = {"steps": args.mall_steps, "entries_per_s": entries * args.mall_steps / e2,
+                       "step_us": pct([x * 1e6 for x in s2]), "kernel_us": pct([x / 1e3 for x in k2]),
+                       "achieved_gbps": a2, "frac": a2 / PEAK_HBM_GBPS if a2 else None}
+
     if args.limit_steps:
         # SURVEY.md §8(d) config-3 mode on this rank's set: limit=20 (ingester default),
         # the deterministic early-exit rule, same query; reported beside the full scan
         for _ in range(3):
-            eng.search_raw(blocks, pipe, limit=20)
+            eng.search_raw(base, pipe, limit=20)
         eng.kernel_times()
         ls = []
         for i in range(args.limit_steps):
             ts = time.perf_counter()
-            nl, metl = eng.search_raw(blocks, pipe, limit=20, flags=sflags if args.events and i % args.events == 0 else 0)
+            nl, metl = eng.search_raw(sets[i % len(sets)], pipe, limit=20,
+                                      flags=sflags if args.events and i % args.events == 0 else 0)
             ls.append(time.perf_counter() - ts)
         lk = eng.kernel_times() if args.events else []
         out["limit20"] = {"steps": args.limit_steps, "matches": nl, "traces_inspected": metl.inspected_traces,
@@ -278,37 +397,14 @@ def main():
                           "entries_per_s": entries / (sum(ls) / len(ls))}
 
     if rank == 0 and world == 1 and args.cpu_baseline:
-        os.sched_setaffinity(0, all_cpus)  # (the CPU baseline gets the whole host share back)
-        from oracle import oracle as O
-        nb = min(args.cpu_blocks, len(paths))
-        oblocks = [O.Block(p) for p in paths[:nb]]
-        cores = min(nb, 16)
-        q = dict(tags=QUERY["tags"], min_ms=QUERY["min_duration_ms"], max_ms=QUERY["max_duration_ms"],
-                 start=QUERY["start"], end=QUERY["end"])
-        t0 = time.perf_counter()
-        reps = 0
-        while True:
-            exp, omet, st = O.search(oblocks, nthreads=cores, **q)
-            reps += 1
-            if time.perf_counter() - t0 > 10 or reps >= 5:
-                break
-        cpu_s = (time.perf_counter() - t0) / reps
-        cpu_entries = sum(i["entries"] for i in infos[:nb])
-        out["cpu_baseline"] = {
-            "value": cpu_entries / cpu_s, "unit": "entries/s", "cores": cores, "kind": "port",
-            "sample": f"oracle BackendSearchBlock.Search restatement (snappy decode + flatbuffer walk), "
-                      f"{nb} of the {len(paths)} blocks ({cpu_entries} entries), one thread per block, "
-                      f"{reps} rep(s)",
-        }
-        # parity spot check on the sample (same ordered matches for those blocks)
-        g = [(m.block_idx, m.entry_idx, m.trace_id) for m in got if m.block_idx < nb]
-        e = [(m["block_idx"], m["entry_idx"], m["id"]) for m in exp]
-        out["cpu_baseline"]["parity"] = g == e
+        os.sched_setaffinity(0, all_cpus)  # (the CPU baselines get the whole host share back)
+        out["cpu_baseline"] = cpu_baselines(paths, got, cpu_threads)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
-    for b in blocks:
-        b.close()
+    for s in sets:
+        for b in s:
+            b.close()
     eng.close()
     if not args.keep and not args.workdir:
         shutil.rmtree(workdir, ignore_errors=True)

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define TSG_ABI_VERSION 2
+#define TSG_ABI_VERSION 3
 
 /* Status codes. */
 #define TSG_OK 0
@@ -134,6 +134,15 @@ typedef struct tsg_result {
   const char *const *root_name;
   const uint32_t *root_name_len;
   tsg_metrics metrics;
+  /* Per caller block (nblocks entries): TSG_OK, or the error the reference's
+   * BackendSearchBlock.Search returns for that block AFTER the matches listed above
+   * (a damaged data page, backend_search_block.go:258-266; the ingester logs it and
+   * keeps the other blocks' results, instance_search.go:179-182). block_error[i] is
+   * the message (NULL when OK). A damaged index ends a block silently instead
+   * (`record, _ := ir.At(ctx, i)`, :252-255): no error, fewer pages. */
+  uint64_t nblocks;
+  const int32_t *block_status;
+  const char *const *block_error;
 } tsg_result;
 
 /* Options for tsg_search. */
@@ -178,6 +187,11 @@ int tsg_block_open_mem(tsg_ctx *ctx, const uint8_t *meta_json, size_t meta_len,
                        size_t index_len, const uint8_t *data, size_t data_len, int device_hint,
                        tsg_block **out);
 void tsg_block_close(tsg_block *b);
+/* A second resident copy of an open block (backend or WAL) on device_hint's device:
+ * device-to-device copies of its columns and dictionaries. Replicates a block onto
+ * another GPU without re-reading and re-decoding its files (block-sharded serving with
+ * replicas), or makes disjoint copies of one data set (bench.py's HBM-regime rotation). */
+int tsg_block_clone(tsg_ctx *ctx, const tsg_block *src, int device_hint, tsg_block **out);
 
 /* ---- WAL search blocks (StreamingSearchBlock) -------------------------------------- */
 /* Replaces search.RescanBlocks' per-file replay + StreamingSearchBlock.Search's
@@ -207,6 +221,10 @@ typedef struct tsg_block_info {
   int32_t encoding;        /* backend.Encoding numeric value */
   int32_t streaming;       /* 1: a WAL (StreamingSearchBlock) replay */
   int32_t partial;         /* 1: the WAL replay stopped at a damaged page (the reference's warning) */
+  int32_t stop_status;     /* backend block with a damaged data page: the error its Search returns
+                              after the pages before it (0 = none) */
+  int32_t index_truncated; /* 1: an index record failed (checksum, framing, zero record): the block
+                              ends silently before it, as the reference's Search does */
 } tsg_block_info;
 int tsg_block_info_get(const tsg_block *b, tsg_block_info *out);
 

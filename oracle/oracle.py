@@ -39,7 +39,8 @@ class Metrics(C.Structure):
 
 class Result(C.Structure):
     _fields_ = [("n", C.c_uint64), ("m", C.POINTER(Match)), ("strings", C.POINTER(C.c_char)),
-                ("strings_len", C.c_uint64), ("metrics", Metrics), ("status", C.c_int32), ("pad", C.c_int32)]
+                ("strings_len", C.c_uint64), ("metrics", Metrics), ("status", C.c_int32), ("pad", C.c_int32),
+                ("nblocks", C.c_uint64), ("block_status", C.POINTER(C.c_int32))]
 
 
 class Hit(C.Structure):
@@ -95,6 +96,12 @@ def lib():
         L.orc_lookup_ids.argtypes = [C.POINTER(vp), C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
                                      C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.POINTER(Hit)),
                                      C.POINTER(C.c_uint64)]
+        L.orc_colblock_build.argtypes = [vp, C.POINTER(vp)]
+        L.orc_colblock_free.argtypes = [vp]
+        L.orc_colblock_entries.argtypes = [vp]
+        L.orc_colblock_entries.restype = C.c_uint64
+        L.orc_columnar_search.argtypes = [C.POINTER(vp), C.c_uint32, C.POINTER(Request), C.c_int,
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.orc_v2_shard_count.argtypes = [vp]
         L.orc_v2_shard_count.restype = C.c_uint32
         _lib = L
@@ -149,7 +156,8 @@ def _unpack(res):
             "root_name": strings[m.name_off:m.name_off + m.name_len],
         })
     met = {"traces_inspected": r.metrics.traces_inspected, "blocks_inspected": r.metrics.blocks_inspected,
-           "blocks_skipped": r.metrics.blocks_skipped, "bytes_inspected": r.metrics.bytes_inspected}
+           "blocks_skipped": r.metrics.blocks_skipped, "bytes_inspected": r.metrics.bytes_inspected,
+           "block_status": [r.block_status[i] for i in range(r.nblocks)]}
     return out, met, r.status
 
 
@@ -268,3 +276,36 @@ def pipeline_matches_entry(fb, **req):
 def pipeline_matches_block(fb, **req):
     r = make_request(**req)
     return bool(lib().orc_pipeline_matches_block(C.byref(r), fb, len(fb)))
+
+
+class ColumnarBlock:
+    """CPU columnar baseline: a backend search block decoded once into host columns
+    (orc_colblock_build); searched by columnar_search over nthreads threads."""
+
+    def __init__(self, block):
+        self.h = C.c_void_p()
+        rc = lib().orc_colblock_build(block.h, C.byref(self.h))
+        if rc != 0:
+            raise OSError(f"orc_colblock_build -> {rc}")
+
+    def entries(self):
+        return lib().orc_colblock_entries(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_colblock_free(self.h)
+            self.h = None
+
+
+def columnar_search(cblocks, tags=None, min_ms=0, max_ms=0, start=0, end=0, nthreads=1):
+    """(match count, order-independent hash of the (block, scan position) matches)."""
+    req = make_request(tags, min_ms, max_ms, start, end)
+    arr = (C.c_void_p * max(len(cblocks), 1))(*[b.h for b in cblocks])
+    m, h = C.c_uint64(), C.c_uint64()
+    lib().orc_columnar_search(arr, len(cblocks), C.byref(req), nthreads, C.byref(m), C.byref(h))
+    return m.value, h.value
+
+
+def match_hash(matches):
+    """The columnar_search hash of a match list [(block_idx, entry_idx), ...]."""
+    return sum(((b << 32) | e) * 0x9E3779B97F4A7C15 for b, e in matches) % (1 << 64)

@@ -894,6 +894,8 @@ typedef struct mlist {
   uint64_t sl, scap;
   orc_metrics met;
   int status;
+  int32_t *bstat; /* per block (orc_search) */
+  uint64_t nb;
 } mlist;
 static uint32_t ml_str(mlist *l, const uint8_t *p, uint32_t n) {
   if (l->sl + n + 1 > l->scap) {
@@ -1102,6 +1104,8 @@ static void finish(mlist *l, orc_result **out) {
   r->strings_len = l->sl;
   r->metrics = l->met;
   r->status = l->status;
+  r->nblocks = l->nb;
+  r->block_status = l->bstat;
   *out = r;
 }
 
@@ -1111,6 +1115,8 @@ int orc_search(orc_block *const *blocks, uint32_t nblocks, const orc_request *re
   pipeline_new(req, &p);
   mlist all;
   memset(&all, 0, sizeof all);
+  all.nb = nblocks;
+  all.bstat = (int32_t *)calloc(nblocks + 1, sizeof(int32_t));
   if (limit == 0 && nthreads > 1 && nblocks > 1) {
     /* one thread per block (instance.searchLocalBlocks: a goroutine per block),
      * at most nthreads in flight; concatenated in block order. */
@@ -1139,6 +1145,7 @@ int orc_search(orc_block *const *blocks, uint32_t nblocks, const orc_request *re
       all.met.blocks_skipped += l->met.blocks_skipped;
       all.met.bytes_inspected += l->met.bytes_inspected;
       if (ta[i].rc && !all.status) all.status = ta[i].rc;
+      all.bstat[i] = ta[i].rc;
       free(l->m);
       free(l->s);
     }
@@ -1152,6 +1159,7 @@ int orc_search(orc_block *const *blocks, uint32_t nblocks, const orc_request *re
     for (uint32_t i = 0; i < nblocks && !quit; i++) {
       int rc = block_search(blocks[i], i, &p, &all, limit ? limit_consume : NULL, &lc, &quit);
       if (rc && !all.status) all.status = rc; /* searchLocalBlocks logs and continues */
+      all.bstat[i] = rc;
     }
     free(lc.ids.k);
     free(lc.ids.used);
@@ -1211,6 +1219,7 @@ void orc_result_free(orc_result *r) {
   if (!r) return;
   free(r->m);
   free(r->strings);
+  free(r->block_status);
   free(r);
 }
 
@@ -1971,5 +1980,282 @@ int orc_entry_to_bytes(const uint8_t *id, size_t idl, uint64_t st, uint64_t en, 
   for (uint32_t i = 0; i < npairs; i++) kvset_add(&tags, k[i], kl[i], v[i], vl[i]);
   *out = combined_to_bytes(id, idl, &tags, st, en, out_len);
   kvset_free(&tags);
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* CPU columnar baseline (see tsg_oracle.h)                                    */
+typedef struct ctab { /* interned byte strings -> dense ids (open addressing on xxhash64) */
+  uint64_t *slot_h;
+  uint32_t *slot_id; /* UINT32_MAX = empty */
+  uint64_t cap, n;
+  uint8_t *bytes;
+  uint64_t blen, bcap;
+  uint64_t *off; /* n + 1 */
+  uint64_t ocap;
+} ctab;
+static void ctab_init(ctab *t) {
+  memset(t, 0, sizeof *t);
+  t->cap = 64;
+  t->slot_h = (uint64_t *)calloc(t->cap, 8);
+  t->slot_id = (uint32_t *)malloc(t->cap * 4);
+  memset(t->slot_id, 0xff, t->cap * 4);
+  t->ocap = 64;
+  t->off = (uint64_t *)calloc(t->ocap, 8);
+}
+static void ctab_free(ctab *t) {
+  free(t->slot_h);
+  free(t->slot_id);
+  free(t->bytes);
+  free(t->off);
+}
+static uint32_t ctab_id(ctab *t, const uint8_t *s, size_t l) {
+  if (t->n * 2 + 2 > t->cap) { /* grow */
+    uint64_t nc = t->cap * 2;
+    uint64_t *nh = (uint64_t *)calloc(nc, 8);
+    uint32_t *ni = (uint32_t *)malloc(nc * 4);
+    memset(ni, 0xff, nc * 4);
+    for (uint64_t i = 0; i < t->cap; i++) {
+      if (t->slot_id[i] == UINT32_MAX) continue;
+      uint64_t j = t->slot_h[i] & (nc - 1);
+      while (ni[j] != UINT32_MAX) j = (j + 1) & (nc - 1);
+      nh[j] = t->slot_h[i];
+      ni[j] = t->slot_id[i];
+    }
+    free(t->slot_h);
+    free(t->slot_id);
+    t->slot_h = nh;
+    t->slot_id = ni;
+    t->cap = nc;
+  }
+  uint64_t h = orc_xxhash64(s, l), j = h & (t->cap - 1);
+  while (t->slot_id[j] != UINT32_MAX) {
+    uint32_t id = t->slot_id[j];
+    if (t->slot_h[j] == h && t->off[id + 1] - t->off[id] == l && memcmp(t->bytes + t->off[id], s, l) == 0) return id;
+    j = (j + 1) & (t->cap - 1);
+  }
+  uint32_t id = (uint32_t)t->n++;
+  if (t->blen + l > t->bcap) {
+    while (t->blen + l > t->bcap) t->bcap = t->bcap ? 2 * t->bcap : 4096;
+    t->bytes = (uint8_t *)realloc(t->bytes, t->bcap);
+  }
+  if (l) memcpy(t->bytes + t->blen, s, l);
+  t->blen += l;
+  if (t->n + 1 > t->ocap) {
+    t->ocap *= 2;
+    t->off = (uint64_t *)realloc(t->off, t->ocap * 8);
+  }
+  t->off[id + 1] = t->blen;
+  t->slot_h[j] = h;
+  t->slot_id[j] = id;
+  return id;
+}
+
+typedef struct ckey {
+  ctab sets;     /* value sets: values joined as [u32 len][bytes]... */
+  uint32_t *col; /* per entry: set id or UINT32_MAX (key absent) */
+} ckey;
+struct orc_colblock {
+  uint64_t n, cap;
+  uint64_t *start, *end;
+  ctab keys;
+  ckey *k;
+  uint32_t nk, kcap;
+};
+
+static void cb_grow(orc_colblock *c, uint64_t need) {
+  if (need <= c->cap) return;
+  uint64_t nc = c->cap ? c->cap : 4096;
+  while (nc < need) nc *= 2;
+  c->start = (uint64_t *)realloc(c->start, nc * 8);
+  c->end = (uint64_t *)realloc(c->end, nc * 8);
+  for (uint32_t i = 0; i < c->nk; i++) {
+    c->k[i].col = (uint32_t *)realloc(c->k[i].col, nc * 4);
+    memset(c->k[i].col + c->cap, 0xff, (nc - c->cap) * 4);
+  }
+  c->cap = nc;
+}
+
+int orc_colblock_build(const orc_block *b, orc_colblock **out) {
+  orc_colblock *c = (orc_colblock *)calloc(1, sizeof *c);
+  ctab_init(&c->keys);
+  *out = c;
+  if (b->wal || !b->has_meta || b->enc < 0) return b->wal ? ORC_INVALID : ORC_OK;
+  orc_index ix;
+  index_init(&ix, b->index, b->index_len, b->index_page_size, b->index_records);
+  uint8_t *joined = NULL;
+  size_t jcap = 0;
+  int rc = ORC_OK;
+  for (int64_t i = 0;; i++) {
+    const uint8_t *rec;
+    if (index_at(&ix, i, &rec) <= 0) break;
+    uint8_t *page;
+    size_t pl;
+    rc = data_read_page(b->data, b->data_len, b->enc, le64(rec + 16), le32(rec + 24), &page, &pl);
+    if (rc) break;
+    const uint8_t *cur = page, *id, *obj;
+    size_t cl = pl, objl;
+    uint32_t idl;
+    if (unmarshal_advance(&cur, &cl, &id, &idl, &obj, &objl) != 0) { free(page); rc = ORC_CORRUPT; break; }
+    fbt pg = fb_root(obj, objl);
+    uint16_t eo = fb_offset(&pg, VT_PAGE_ENTRIES);
+    uint32_t ne = eo ? fb_vector_len(&pg, eo) : 0;
+    cb_grow(c, c->n + ne);
+    for (uint32_t j = 0; j < ne; j++) {
+      fbt e = pg;
+      e.pos = fb_indirect(&pg, fb_vector(&pg, eo) + j * 4);
+      const uint64_t ei = c->n++;
+      c->start[ei] = fb_u64(&e, VT_ENTRY_START);
+      c->end[ei] = fb_u64(&e, VT_ENTRY_END);
+      uint16_t to = fb_offset(&e, VT_ENTRY_TAGS);
+      uint32_t nt = to ? fb_vector_len(&e, to) : 0;
+      for (uint32_t t = 0; t < nt; t++) {
+        fbt kv = e;
+        kv.pos = fb_indirect(&e, fb_vector(&e, to) + t * 4);
+        uint32_t kl = 0;
+        uint16_t ko = fb_offset(&kv, 4);
+        const uint8_t *kp = ko ? fb_byte_vector(&kv, kv.pos + ko, &kl) : NULL;
+        uint32_t kid = ctab_id(&c->keys, kp ? kp : (const uint8_t *)"", kl);
+        if (kid >= c->nk) { /* new key: a column of its own */
+          if (kid >= c->kcap) {
+            c->kcap = c->kcap ? 2 * c->kcap : 32;
+            c->k = (ckey *)realloc(c->k, c->kcap * sizeof(ckey));
+          }
+          ctab_init(&c->k[kid].sets);
+          c->k[kid].col = (uint32_t *)malloc(c->cap * 4);
+          memset(c->k[kid].col, 0xff, c->cap * 4);
+          c->nk = kid + 1;
+        }
+        if (c->k[kid].col[ei] != UINT32_MAX) continue; /* first table of the key (unique keys) */
+        uint16_t vo = fb_offset(&kv, 6);
+        uint32_t vn = vo ? fb_vector_len(&kv, vo) : 0;
+        size_t jl = 0;
+        for (uint32_t q = 0; q < vn; q++) {
+          uint32_t vl = 0;
+          const uint8_t *vp = fb_byte_vector(&kv, fb_vector(&kv, vo) + q * 4, &vl);
+          if (jl + 4 + vl > jcap) {
+            jcap = (jl + 4 + vl) * 2;
+            joined = (uint8_t *)realloc(joined, jcap);
+          }
+          memcpy(joined + jl, &vl, 4);
+          if (vl) memcpy(joined + jl + 4, vp, vl);
+          jl += 4 + vl;
+        }
+        c->k[kid].col[ei] = ctab_id(&c->k[kid].sets, joined, jl);
+      }
+    }
+    free(page);
+  }
+  free(joined);
+  index_free(&ix);
+  return rc;
+}
+void orc_colblock_free(orc_colblock *c) {
+  if (!c) return;
+  for (uint32_t i = 0; i < c->nk; i++) {
+    ctab_free(&c->k[i].sets);
+    free(c->k[i].col);
+  }
+  free(c->k);
+  ctab_free(&c->keys);
+  free(c->start);
+  free(c->end);
+  free(c);
+}
+uint64_t orc_colblock_entries(const orc_colblock *c) { return c->n; }
+
+typedef struct cscan {
+  const orc_colblock *c;
+  const orc_pipeline *p;
+  const uint32_t *const *col; /* per term */
+  uint8_t *const *bm;         /* per term: set id -> match */
+  uint64_t lo, hi, bidx, matches, hash;
+} cscan;
+static void *cscan_main(void *a) {
+  cscan *s = (cscan *)a;
+  const orc_pipeline *p = s->p;
+  uint64_t m = 0, h = 0;
+  for (uint64_t e = s->lo; e < s->hi; e++) {
+    const uint64_t st = s->c->start[e], et = s->c->end[e];
+    if (p->has_min && !((et - st) >= p->min_ns)) continue;
+    if (p->has_max && !((et - st) <= p->max_ns)) continue;
+    if (p->has_range) {
+      uint32_t ss = (uint32_t)(st / 1000000000ULL), es = (uint32_t)(et / 1000000000ULL);
+      if (!(p->start <= es && p->end >= ss)) continue;
+    }
+    uint32_t t = 0;
+    for (; t < p->nterms; t++) {
+      uint32_t x = s->col[t][e];
+      if (x == UINT32_MAX || !s->bm[t][x]) break;
+    }
+    if (t < p->nterms) continue;
+    m++;
+    h += ((s->bidx << 32) | e) * 0x9E3779B97F4A7C15ULL;
+  }
+  s->matches = m;
+  s->hash = h;
+  return NULL;
+}
+
+int orc_columnar_search(orc_colblock *const *cbs, uint32_t n, const orc_request *req, int nthreads,
+                        uint64_t *matches, uint64_t *hash) {
+  orc_pipeline p;
+  pipeline_new(req, &p);
+  if (nthreads < 1) nthreads = 1;
+  uint64_t m = 0, h = 0;
+  for (uint32_t b = 0; b < n && !p.exhaustive; b++) {
+    const orc_colblock *c = cbs[b];
+    const uint32_t **col = (const uint32_t **)calloc(p.nterms + 1, sizeof(void *));
+    uint8_t **bm = (uint8_t **)calloc(p.nterms + 1, sizeof(void *));
+    int dead = 0;
+    for (uint32_t t = 0; t < p.nterms && !dead; t++) { /* dictionary pass: value sets matching term t */
+      uint32_t kid = UINT32_MAX;
+      for (uint32_t k = 0; k < c->nk; k++)
+        if (c->keys.off[k + 1] - c->keys.off[k] == p.kl[t] && memcmp(c->keys.bytes + c->keys.off[k], p.k[t], p.kl[t]) == 0)
+          kid = k;
+      if (kid == UINT32_MAX) { dead = 1; break; }
+      const ctab *sets = &c->k[kid].sets;
+      bm[t] = (uint8_t *)calloc(sets->n + 1, 1);
+      for (uint64_t sidx = 0; sidx < sets->n; sidx++) {
+        const uint8_t *q = sets->bytes + sets->off[sidx], *qe = sets->bytes + sets->off[sidx + 1];
+        while (q < qe && !bm[t][sidx]) {
+          uint32_t vl;
+          memcpy(&vl, q, 4);
+          bm[t][sidx] = (uint8_t)bytes_contains(q + 4, vl, p.v[t], p.vl[t]);
+          q += 4 + vl;
+        }
+      }
+      col[t] = c->k[kid].col;
+    }
+    if (!dead && c->n) {
+      int nt = nthreads;
+      if ((uint64_t)nt > c->n) nt = (int)c->n;
+      cscan *sc = (cscan *)calloc((size_t)nt, sizeof *sc);
+      pthread_t *th = (pthread_t *)calloc((size_t)nt, sizeof *th);
+      for (int i = 0; i < nt; i++) {
+        sc[i].c = c;
+        sc[i].p = &p;
+        sc[i].col = col;
+        sc[i].bm = bm;
+        sc[i].bidx = b;
+        sc[i].lo = c->n * (uint64_t)i / (uint64_t)nt;
+        sc[i].hi = c->n * (uint64_t)(i + 1) / (uint64_t)nt;
+        pthread_create(&th[i], NULL, cscan_main, &sc[i]);
+      }
+      for (int i = 0; i < nt; i++) {
+        pthread_join(th[i], NULL);
+        m += sc[i].matches;
+        h += sc[i].hash;
+      }
+      free(sc);
+      free(th);
+    }
+    for (uint32_t t = 0; t < p.nterms; t++) free(bm[t]);
+    free(bm);
+    free(col);
+  }
+  pipeline_free(&p);
+  *matches = m;
+  *hash = h;
   return ORC_OK;
 }

@@ -58,6 +58,8 @@ typedef struct orc_result {
   orc_metrics metrics;
   int32_t status; /* first per-block error, 0 ok */
   int32_t pad;
+  uint64_t nblocks;      /* orc_search: one status per block (the error its Search returned, 0 ok) */
+  int32_t *block_status;
 } orc_result;
 
 typedef struct orc_block orc_block; /* search block files held in memory */
@@ -127,6 +129,21 @@ int orc_lookup_ids(orc_v2block *const *blocks, uint32_t nblocks, const uint8_t (
 uint32_t orc_v2_shard_count(const orc_v2block *b);
 
 void orc_free(void *p);
+
+/* CPU columnar baseline (bench.py cpu_baseline.columnar; SURVEY.md §8(d) "CPU columnar"
+ * variant): a backend search block decoded once into host columns (start/end ns, and
+ * per key the KeyValues value-set id of every entry), then the Pipeline predicates
+ * evaluated over the columns, multi-threaded over entries. Same match set as the
+ * reference's scan for backend blocks (unique keys per entry); it is a baseline to time,
+ * not a restatement. */
+typedef struct orc_colblock orc_colblock;
+int orc_colblock_build(const orc_block *b, orc_colblock **out);
+void orc_colblock_free(orc_colblock *c);
+uint64_t orc_colblock_entries(const orc_colblock *c);
+/* matches of req over the blocks (limit ignored: full scan); *hash = sum over matches of
+ * (block index << 32 | scan position) * golden-ratio constant (order independent) */
+int orc_columnar_search(orc_colblock *const *cbs, uint32_t n, const orc_request *req, int nthreads,
+                        uint64_t *matches, uint64_t *hash);
 /* SearchEntryMutable.ToBytes (Go flatbuffers builder restatement); *out malloc'd */
 int orc_entry_to_bytes(const uint8_t *id, size_t idl, uint64_t st, uint64_t en, uint32_t npairs,
                        const uint8_t *const *k, const uint32_t *kl, const uint8_t *const *v, const uint32_t *vl,

@@ -8,4 +8,6 @@ from .tsg import (  # noqa: F401
     BackendSearchBlock, Engine, StreamingSearchBlock, Pipeline, SearchMetrics, SearchRequest, TraceSearchMetadata, TsgError, V2Block,
     ENC_NONE, ENC_SNAPPY, SEARCH_TIME_ALL, SEARCH_TIME_DEFER, SEARCH_TIME_SCAN, fb_search_entry, fb_search_header, lib, synth_search_block, synth_v2_block,
     write_search_block, write_wal_search, wal_filename,
+    TSG_OK, TSG_E_NOT_FOUND, TSG_E_CORRUPT, TSG_E_UNSUPPORTED_ENCODING, TSG_E_DEVICE, TSG_E_CANCELLED, TSG_E_OOM,
+    TSG_E_INVALID, TSG_E_UNSUPPORTED, TSG_E_IO,
 )

@@ -90,31 +90,38 @@ static void unmarshal_page(const uint8_t *b, size_t n, size_t hdr_len, const uin
   dlen = n - 6 - hl;
 }
 
-std::vector<IndexRecord> read_index(const uint8_t *p, size_t n, uint32_t page_size, uint32_t total) {
+std::vector<IndexRecord> read_index(const uint8_t *p, size_t n, uint32_t page_size, uint32_t total, bool *prefix) {
   std::vector<IndexRecord> out;
+  if (prefix) *prefix = false;
   if (total == 0) return out;
-  if (page_size < 14 + 28) fail(TSG_E_CORRUPT, "index page too small for one record");
-  uint32_t rpp = (page_size - 8 - 6) / 28;  // objectsPerPage (page.go:175-182)
-  out.reserve(total);
-  for (uint32_t pidx = 0; uint64_t(pidx) * rpp < total; pidx++) {
-    uint64_t off = uint64_t(pidx) * page_size;
-    if (off + page_size > n) fail(TSG_E_CORRUPT, "index truncated");
-    const uint8_t *hdr, *data;
-    size_t dlen;
-    unmarshal_page(p + off, page_size, 8, hdr, data, dlen);
-    if (le64(hdr) != xxhash64(data, dlen)) fail(TSG_E_CORRUPT, "mismatched index page checksum");
-    for (uint32_t r = 0; r < rpp && uint64_t(pidx) * rpp + r < total; r++) {
-      if ((r + 1) * 28 > dlen) fail(TSG_E_CORRUPT, "index record out of bounds");
-      const uint8_t *rec = data + r * 28;
-      bool zero = true;
-      for (int k = 0; k < 28 && zero; k++) zero = rec[k] == 0;
-      if (zero) fail(TSG_E_CORRUPT, "unexpected zero value index record");
-      IndexRecord ir;
-      std::memcpy(ir.id, rec, 16);
-      ir.start = le64(rec + 16);
-      ir.length = le32(rec + 24);
-      out.push_back(ir);
+  try {
+    if (page_size < 14 + 28) fail(TSG_E_CORRUPT, "index page too small for one record");
+    uint32_t rpp = (page_size - 8 - 6) / 28;  // objectsPerPage (page.go:175-182)
+    out.reserve(total);
+    for (uint32_t pidx = 0; uint64_t(pidx) * rpp < total; pidx++) {
+      // getPage: ReadAt of one whole page (a short read is an error), framing, checksum
+      uint64_t off = uint64_t(pidx) * page_size;
+      if (off + page_size > n) fail(TSG_E_CORRUPT, "index truncated");
+      const uint8_t *hdr, *data;
+      size_t dlen;
+      unmarshal_page(p + off, page_size, 8, hdr, data, dlen);
+      if (le64(hdr) != xxhash64(data, dlen)) fail(TSG_E_CORRUPT, "mismatched index page checksum");
+      for (uint32_t r = 0; r < rpp && uint64_t(pidx) * rpp + r < total; r++) {
+        if ((r + 1) * 28 > dlen) fail(TSG_E_CORRUPT, "index record out of bounds");
+        const uint8_t *rec = data + r * 28;
+        bool zero = true;
+        for (int k = 0; k < 28 && zero; k++) zero = rec[k] == 0;
+        if (zero) fail(TSG_E_CORRUPT, "unexpected zero value index record");
+        IndexRecord ir;
+        std::memcpy(ir.id, rec, 16);
+        ir.start = le64(rec + 16);
+        ir.length = le32(rec + 24);
+        out.push_back(ir);
+      }
     }
+  } catch (const Error &) {
+    if (!prefix) throw;
+    *prefix = true;  // At(i) failed: the records before i are what Search visits
   }
   return out;
 }
@@ -364,14 +371,16 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
     hb.min_dur = h.u64(kHdrMin);
     hb.max_dur = h.u64(kHdrMax);
   }
-  std::vector<IndexRecord> recs = read_index(index, index_len, hb.meta.index_page_size, hb.meta.index_records);
+  std::vector<IndexRecord> recs =
+      read_index(index, index_len, hb.meta.index_page_size, hb.meta.index_records, &hb.index_truncated);
   if (nthreads <= 0) nthreads = int(std::max(1u, std::thread::hardware_concurrency()));
   nthreads = std::min<int>(nthreads, 64);
 
   std::vector<KeyBuild> kb;
   size_t batch = size_t(nthreads) * 4;
   std::vector<PageParse> pages;
-  for (size_t b0 = 0; b0 < recs.size(); b0 += batch) {
+  bool stopped = false;
+  for (size_t b0 = 0; b0 < recs.size() && !stopped; b0 += batch) {
     size_t b1 = std::min(recs.size(), b0 + batch);
     pages.clear();
     pages.resize(b1 - b0);
@@ -394,9 +403,16 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
     for (int t = 1; t < nt; t++) th.emplace_back(work);
     work();
     for (auto &t : th) t.join();
-    // merge pages in order (scan order = pages ascending, entry index ascending)
+    // merge pages in order (scan order = pages ascending, entry index ascending); the
+    // first damaged page ends the block: the pages before it stay, and its error is
+    // what Search returns once it gets there (backend_search_block.go:258-266)
     for (auto &pp : pages) {
-      if (pp.err) fail(pp.err, pp.msg);
+      if (pp.err) {
+        hb.stop_status = pp.err;
+        hb.stop_msg = pp.msg;
+        stopped = true;
+        break;
+      }
       merge_page(hb, kb, pp);
     }
   }

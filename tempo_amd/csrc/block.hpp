@@ -93,8 +93,14 @@ struct IndexRecord {
   uint64_t start;
   uint32_t length;
 };
-// Reads every record: page checksum (xxhash64) verified, all-zero record rejected.
-std::vector<IndexRecord> read_index(const uint8_t *p, size_t n, uint32_t page_size, uint32_t total);
+// indexReader.At for i = 0, 1, ... (index_reader.go:42-82,116-143): page checksum
+// (xxhash64) verified, all-zero record rejected. prefix == nullptr: any failure throws
+// TSG_E_CORRUPT (the trace-ID lookup path, where Find returns the error). Otherwise the
+// records before the first failing At(i) are returned and *prefix is set to true when
+// one failed: BackendSearchBlock.Search drops At's error (`record, _ := ir.At(ctx, i)`,
+// backend_search_block.go:252-255) and ends the block there without an error.
+std::vector<IndexRecord> read_index(const uint8_t *p, size_t n, uint32_t page_size, uint32_t total,
+                                    bool *prefix = nullptr);
 // dataReader.Read of one record + decompression (data_reader.go:45-125).
 void read_data_page(const uint8_t *file, size_t flen, const IndexRecord &r, int enc, std::vector<uint8_t> &out);
 
@@ -122,6 +128,14 @@ struct HostBlock {
   // header is the SearchBlockHeaderMutable rebuilt during replay (exact-value Contains)
   bool streaming = false;
   bool partial = false;  // replay stopped at a damaged page (the reference's warning)
+  // Backend blocks with damage: a failing index record ends the block silently (its
+  // pages are not resident; index_truncated = true). A damaged data page k (read, page
+  // framing, decompression, object framing, flatbuffer bounds) keeps pages [0, k)
+  // resident and stop_status / stop_msg is the error the reference's Search returns
+  // after their matches (backend_search_block.go:258-266); 0 = none.
+  bool index_truncated = false;
+  int stop_status = 0;
+  std::string stop_msg;
   std::map<std::string, std::set<std::string>> stream_tags;
   SearchMeta meta;
   std::vector<uint8_t> header;  // raw search-header flatbuffer (kept for MatchesBlock/Tags)

@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
 #include <list>
 #include <thread>
 #include <unordered_map>
@@ -19,6 +20,22 @@
 
 struct tsg_ctx {
   tsg::Ctx c;
+  // tsg_cancel: query ids cancelled and not yet seen finishing (bounded, FIFO eviction).
+  // A search with that id checks the set between device chunks and waves
+  // (cooperative, like BackendSearchBlock.Search's per-page sr.Quit()).
+  std::mutex cmu;
+  std::unordered_set<uint64_t> cancelled;
+  std::deque<uint64_t> corder;
+  bool is_cancelled(uint64_t qid) {
+    if (!qid) return false;
+    std::lock_guard<std::mutex> lk(cmu);
+    return cancelled.count(qid) != 0;
+  }
+  void forget(uint64_t qid) {
+    if (!qid) return;
+    std::lock_guard<std::mutex> lk(cmu);
+    if (cancelled.erase(qid)) corder.erase(std::remove(corder.begin(), corder.end(), qid), corder.end());
+  }
 };
 struct tsg_block {
   tsg::Block b;
@@ -75,6 +92,13 @@ struct ResultHolder {
     arena_cap = cap;
   }
   std::vector<const char *> svc_p, name_p;
+  std::vector<int32_t> bstatus;      // per caller block
+  std::vector<std::string> berr_s;
+  std::vector<const char *> berr;
+  void set_blocks(size_t nb) {
+    bstatus.assign(nb, TSG_OK);
+    berr_s.assign(nb, std::string());
+  }
   void reserve(size_t n) {
     ids.reserve(16 * n);
     for (auto *v : {&start, &end, &entry, &svc_off, &name_off}) v->reserve(n);
@@ -136,6 +160,11 @@ struct ResultHolder {
     pub.root_service_len = svc_len.data();
     pub.root_name = name_p.data();
     pub.root_name_len = name_len.data();
+    berr.resize(bstatus.size());
+    for (size_t i = 0; i < bstatus.size(); i++) berr[i] = bstatus[i] ? berr_s[i].c_str() : nullptr;
+    pub.nblocks = bstatus.size();
+    pub.block_status = bstatus.data();
+    pub.block_error = berr.data();
   }
 };
 static_assert(offsetof(ResultHolder, pub) == 0, "pub first");
@@ -214,7 +243,18 @@ int tsg_device_numa_node(tsg_ctx *ctx, int dev) {
   if (!ctx || dev < 0 || size_t(dev) >= ctx->c.devs.size()) return -1;
   return device_numa_node(*ctx->c.devs[size_t(dev)]);
 }
-int tsg_cancel(tsg_ctx *, uint64_t) { return TSG_OK; }  // searches are short and non-preemptible
+int tsg_cancel(tsg_ctx *ctx, uint64_t qid) {
+  if (!ctx || !qid) return TSG_E_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->cmu);
+  if (ctx->cancelled.insert(qid).second) {
+    ctx->corder.push_back(qid);
+    if (ctx->corder.size() > 4096) {  // ids cancelled but never searched: keep the newest
+      ctx->cancelled.erase(ctx->corder.front());
+      ctx->corder.pop_front();
+    }
+  }
+  return TSG_OK;
+}
 
 int tsg_pipeline_new(const tsg_request *req, tsg_pipeline **out) {
   if (!req || !out) return TSG_E_INVALID;
@@ -271,6 +311,22 @@ int tsg_wal_block_open_mem(tsg_ctx *ctx, const uint8_t *data, size_t len, int en
     open_common(ctx, [&](HostBlock &h) { decode_wal_search_block(data, len, encoding, h); }, device_hint, out);
   });
 }
+int tsg_block_clone(tsg_ctx *ctx, const tsg_block *src, int device_hint, tsg_block **out) {
+  if (!ctx || !src || !out) return TSG_E_INVALID;
+  return guard([&] {
+    auto *b = new tsg_block();
+    b->ctx = ctx;
+    try {
+      if (src->b.host.has_meta) block_clone(ctx->c, src->b, b->b, device_hint);
+      else b->b.host = src->b.host;
+    } catch (...) {
+      block_free(b->b);
+      delete b;
+      throw;
+    }
+    *out = b;
+  });
+}
 void tsg_block_close(tsg_block *b) {
   if (!b) return;
   block_free(b->b);
@@ -291,6 +347,8 @@ int tsg_block_info_get(const tsg_block *b, tsg_block_info *o) {
   o->encoding = h.meta.encoding;
   o->streaming = h.streaming ? 1 : 0;
   o->partial = h.partial ? 1 : 0;
+  o->stop_status = h.stop_status;
+  o->index_truncated = h.index_truncated ? 1 : 0;
   return TSG_OK;
 }
 
@@ -382,16 +440,33 @@ int tsg_block_tag_values(const tsg_block *b, const uint8_t *key, size_t klen, ui
 int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
                const tsg_search_opts *opts, tsg_result **out) {
   if (!ctx || !q || !out || (nblocks && !blocks)) return TSG_E_INVALID;
+  // TSG_CHUNK_BLOCKS: blocks per device launch (default 32 = the one-launch path's
+  // kernel-argument capacity; 0 = one launch for all, the descriptor path beyond 32)
+  static const size_t kChunk = [] {
+    const char *e = std::getenv("TSG_CHUNK_BLOCKS");
+    return e ? size_t(std::atoll(e)) : size_t(32);
+  }();
   static const bool trace = std::getenv("TSG_TRACE") != nullptr || prof_on();
   using clk = std::chrono::steady_clock;
   const clk::time_point t_in = trace ? clk::now() : clk::time_point();
+  const uint64_t qid = opts ? opts->query_id : 0;
+  struct Forget {  // the id is done with once this search returns, cancelled or not
+    tsg_ctx *c;
+    uint64_t q;
+    ~Forget() { c->forget(q); }
+  } forget_qid{ctx, qid};
+  auto check_cancel = [&] {
+    if (ctx->is_cancelled(qid)) fail(TSG_E_CANCELLED, "search cancelled (tsg_cancel)");
+  };
   return guard([&] {
+    check_cancel();
     const uint32_t limit = opts ? opts->limit : 0;
     const uint32_t flags = opts ? opts->flags : 0;
     auto *res = new ResultHolder();
     std::unique_ptr<ResultHolder> guard_res(res);
     tsg_metrics &m = res->pub.metrics;
     std::memset(&m, 0, sizeof m);
+    res->set_blocks(nblocks);
     // block filter on the host (header), device work grouped per device
     std::vector<int> state(nblocks, 0);  // 0 no meta, 1 skipped, 2 inspected
     for (size_t i = 0; i < nblocks; i++) {
@@ -422,7 +497,27 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         const size_t slot = k++;
         auto work = [&, slot, dc = kv.first, &list = kv.second]() {
           try {
-            device_search(*dc, list, *q, limit, flags, *slots[slot]);
+            // chunks of at most kChunk blocks, one launch each (the one-launch path
+            // carries 32 blocks in its kernel arguments); cancellation is checked
+            // before every chunk
+            const size_t nl = list.size(), step = kChunk ? kChunk : nl;
+            SearchOut &o = *slots[slot];
+            for (size_t c0 = 0; c0 < nl; c0 += step) {
+              check_cancel();
+              const std::vector<std::pair<uint32_t, Block *>> part(list.begin() + c0,
+                                                                   list.begin() + std::min(nl, c0 + step));
+              if (c0 == 0) {
+                device_search(*dc, part, *q, limit, flags, o);
+                continue;
+              }
+              SearchOut more;
+              device_search(*dc, part, *q, limit, flags, more);
+              o.recs.insert(o.recs.end(), more.recs.begin(), more.recs.end());
+              o.device_bytes += more.device_bytes;
+              o.kernel_ns += more.kernel_ns;
+              o.scan_ns += more.scan_ns;
+              o.scan_bytes += more.scan_bytes;
+            }
           } catch (...) {
             errs[slot] = std::current_exception();
           }
@@ -471,6 +566,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       }
     }
     search_range(0, b1);
+    check_cancel();
     if (b1 < nblocks) {
       std::unordered_set<std::string> seen;
       bool stop = false;
@@ -480,6 +576,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
           stop = seen.size() >= limit;
         }
       if (!stop) search_range(b1, nblocks);
+      check_cancel();
     }
     const clk::time_point t_dev = trace ? clk::now() : clk::time_point();
     res->reserve(nrec);
@@ -517,6 +614,10 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       if (!stopped) {
         m.traces_inspected += uint32_t(h.n);
         m.bytes_inspected += h.fb_bytes;
+        if (h.stop_status) {  // the damaged page is reached: Search returns its error
+          res->bstatus[i] = h.stop_status;
+          res->berr_s[i] = h.stop_msg;
+        }
       } else {
         // pages up to and including the stop page; entries up to and including the match
         m.traces_inspected += uint32_t(stop_entry + 1);
@@ -604,6 +705,11 @@ int tsg_results_combine(const tsg_result *in, uint32_t max_results, tsg_result *
       fin->dur.back() = res->dur[e];
     }
     fin->pub.metrics = in->metrics;
+    fin->set_blocks(size_t(in->nblocks));
+    for (uint64_t i = 0; i < in->nblocks; i++) {
+      fin->bstatus[i] = in->block_status[i];
+      if (in->block_error[i]) fin->berr_s[i] = in->block_error[i];
+    }
     fin->finalize();
     *out = &gf.release()->pub;
   });

@@ -80,12 +80,15 @@ static T *dev_upload(DevBlock &b, const T *src, size_t count, hipStream_t s, siz
   size_t bytes = std::max<size_t>((elems * sizeof(T) + 15) / 16 * 16, 16);
   HIP_OK(hipMalloc(&p, bytes));
   b.allocs.push_back(p);
+  b.alloc_bytes.push_back(bytes);
   b.bytes += bytes;
   if (count) HIP_OK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
   if (bytes > count * sizeof(T))
     HIP_OK(hipMemsetAsync(static_cast<uint8_t *>(p) + count * sizeof(T), 0, bytes - count * sizeof(T), s));
   return static_cast<T *>(p);
 }
+
+static void upload_desc(DevBlock &d, hipStream_t s);
 
 void block_upload(Ctx &c, Block &b, int device_hint) {
   if (c.devs.empty()) fail(TSG_E_DEVICE, "no device");
@@ -169,7 +172,12 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     }
     d.keys.push_back(k);
   }
-  // resident descriptor (one-launch search path)
+  upload_desc(d, s);
+}
+
+// resident descriptor (one-launch search path): the block's column and dictionary pointers
+static void upload_desc(DevBlock &d, hipStream_t s) {
+  const uint64_t n = d.n;
   std::vector<uint8_t> desc(sizeof(DevBlockDesc) + d.keys.size() * sizeof(DevKeyDesc));
   auto *bd = reinterpret_cast<DevBlockDesc *>(desc.data());
   bd->n = n;
@@ -200,6 +208,60 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
   }
   d.desc = reinterpret_cast<const DevBlockDesc *>(dev_upload(d, desc.data(), desc.size(), s));
   HIP_OK(hipStreamSynchronize(s));
+}
+
+void block_clone(Ctx &c, const Block &src, Block &dst, int device_hint) {
+  if (c.devs.empty()) fail(TSG_E_DEVICE, "no device");
+  if (!src.dc) fail(TSG_E_INVALID, "block_clone: source block is not resident");
+  DeviceCtx &dc = *c.devs[size_t(std::max(device_hint, 0)) % c.devs.size()];
+  dst.host = src.host;
+  dst.dc = &dc;
+  DevBlock &d = dst.dev;
+  const DevBlock &o = src.dev;
+  d = DevBlock();
+  d.device = dc.ordinal;
+  d.n = o.n;
+  std::lock_guard<std::mutex> lk(dc.mu);
+  HIP_OK(hipSetDevice(dc.ordinal));
+  // the descriptor allocation (last) is rebuilt, every other one copied
+  const size_t ncopy = o.allocs.empty() ? 0 : o.allocs.size() - 1;
+  for (size_t i = 0; i < ncopy; i++) {
+    void *p = nullptr;
+    HIP_OK(hipMalloc(&p, o.alloc_bytes[i]));
+    d.allocs.push_back(p);
+    d.alloc_bytes.push_back(o.alloc_bytes[i]);
+    d.bytes += o.alloc_bytes[i];
+    // (hipMemcpyPeer semantics: a plain device-to-device copy works across devices too)
+    HIP_OK(hipMemcpyAsync(p, o.allocs[i], o.alloc_bytes[i], hipMemcpyDeviceToDevice, dc.stream));
+  }
+  auto xl = [&](const void *q) -> void * {  // source pointer -> the same byte of the copy
+    if (!q) return nullptr;
+    for (size_t i = 0; i < ncopy; i++) {
+      const uint8_t *a = static_cast<const uint8_t *>(o.allocs[i]);
+      if (static_cast<const uint8_t *>(q) >= a && static_cast<const uint8_t *>(q) < a + o.alloc_bytes[i])
+        return static_cast<uint8_t *>(d.allocs[i]) + (static_cast<const uint8_t *>(q) - a);
+    }
+    fail(TSG_E_INVALID, "block_clone: pointer outside the block's allocations");
+  };
+  d.dur32 = static_cast<uint32_t *>(xl(o.dur32));
+  d.dur64 = static_cast<uint64_t *>(xl(o.dur64));
+  d.start_s = static_cast<uint32_t *>(xl(o.start_s));
+  d.end_s = static_cast<uint32_t *>(xl(o.end_s));
+  d.ids = static_cast<uint8_t *>(xl(o.ids));
+  d.start_ns = static_cast<uint64_t *>(xl(o.start_ns));
+  d.end_ns = static_cast<uint64_t *>(xl(o.end_ns));
+  d.names = static_cast<uint32_t *>(xl(o.names));
+  d.id_len = static_cast<uint8_t *>(xl(o.id_len));
+  for (const DevKey &k0 : o.keys) {
+    DevKey k = k0;
+    k.col = xl(k0.col);
+    k.dict_off = static_cast<uint32_t *>(xl(k0.dict_off));
+    k.dict_bytes = static_cast<uint8_t *>(xl(k0.dict_bytes));
+    k.set_off = static_cast<uint32_t *>(xl(k0.set_off));
+    k.set_vals = static_cast<uint32_t *>(xl(k0.set_vals));
+    d.keys.push_back(k);
+  }
+  upload_desc(d, dc.stream);
 }
 
 void block_free(Block &b) {

@@ -67,6 +67,7 @@ struct DevBlock {
   std::vector<DevKey> keys;
   uint64_t bytes = 0;
   std::vector<void *> allocs;
+  std::vector<size_t> alloc_bytes;  // (same order as allocs)
 };
 
 struct DeviceCtx;
@@ -85,6 +86,10 @@ struct Ctx {
 void ctx_init(Ctx &c, const tsg_options *opts);
 void ctx_shutdown(Ctx &c);
 void block_upload(Ctx &c, Block &b, int device_hint);
+// A second resident copy of an open block on device_hint's device (device-to-device
+// copies of every column and dictionary, a descriptor of its own; host metadata shared
+// by value): replicas for load balancing across GPUs, or disjoint copies of one data set.
+void block_clone(Ctx &c, const Block &src, Block &dst, int device_hint);
 void block_free(Block &b);
 
 struct SearchOut {

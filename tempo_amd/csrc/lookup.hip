@@ -440,7 +440,7 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
     k.m = b.bloom_m;
     k.k = b.bloom_k;
     k.bitlen = b.bloom_bitlen;
-    k.m_magic = k.m > 1 ? uint64_t(~0ULL / k.m) : 0;  // floor((2^64-1)/m)
+    k.m_magic = uint64_t(~0ULL / k.m);  // floor((2^64-1)/m), m >= 1 (v2block_open): d_mod corrects by <= 2 steps
     k.rec_ids = b.d_rec_ids;
     k.rec_start = b.d_rec_start;
     k.rec_len = b.d_rec_len;

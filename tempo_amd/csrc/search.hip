@@ -97,6 +97,12 @@ struct ScanParams {
   uint32_t seg_cap;          // segment mode (> 0): records per tile segment; 0 = look-back mode
   uint32_t done_top;         // top counter value once every XCD group has finished
   uint32_t done_target[8];   // group counter values once every scan workgroup of the group has finished
+  // use_ticket: workgroup order from a device-wide ticket counter (ticket - ticket_base),
+  // for the protocols that wait on lower-numbered workgroups (look-back, dictionary
+  // granules): HIP promises no dispatch order, a ticket holder has started by definition
+  unsigned long long *ticket;
+  unsigned long long ticket_base;
+  uint32_t use_ticket, pad3;
 };
 
 constexpr int kThreads = 256;
@@ -403,6 +409,19 @@ __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsig
   return a < b ? a : b;
 }
 
+// The launch-order index of this workgroup: blockIdx.x, or with use_ticket a ticket
+// claimed from one device counter, so that every workgroup this one waits for (a lower
+// index) is already running whatever order the dispatcher chose.
+__device__ __forceinline__ uint32_t wg_order(const ScanParams &P) {
+  if (!P.use_ticket) return blockIdx.x;
+  __shared__ uint32_t s_ticket;
+  if (threadIdx.x == 0)
+    s_ticket = uint32_t(__hip_atomic_fetch_add(P.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                        P.ticket_base);
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(s_ticket);
+}
+
 // Stores to pinned host memory (records, counts, header): relaxed system-scope
 // stores, i.e. write-through, no cache maintenance. A workgroup makes them complete
 // with one s_waitcnt before it arrives at the completion counter; no L2 writeback /
@@ -612,7 +631,7 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
       const uint32_t nw = uint32_t(umin64(wsum, keep)) * 6;
       auto *dst = reinterpret_cast<unsigned long long *>(P.out + P.hdr_bytes) + (unsigned long long)wg * P.seg_cap * 6;
       for (uint32_t i = tid; i < nw; i += kThreads) host_store(dst + i, lds_rec[i]);
-      __builtin_amdgcn_s_waitcnt(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (memory clobber: no store moves below it)
       __syncthreads();
     }
     if (tid == 0) host_store(P.counts + wg, wsum);
@@ -712,7 +731,8 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
   uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + P.lds_bm_words);  // [kLdsTiles][kThreads]
   uint32_t *lds_seg = lds + P.lds_bm_words + kLdsTiles * kThreads / 2;      // [nsegs]
   const int tid = threadIdx.x;
-  const uint32_t si = P.wg_seg[blockIdx.x];
+  const uint32_t vb = wg_order(P);
+  const uint32_t si = P.wg_seg[vb];
   const ScanSeg S = P.segs[si];
   constexpr int NTA = NT > 0 ? NT : 1;
   ScanTerm T[NTA];
@@ -720,7 +740,7 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
 #pragma unroll
     for (int q = 0; q < NTA; q++) T[q] = P.terms[S.term0 + q];
   scan_emit<NT, DUR, RANGE, W1, false>(P, S, T, si, DescSegs{P.wg_seg, P.segs}, lds_bm, lds_mask, lds_seg, nullptr, t_start,
-                                blockIdx.x, [] {}, [&] {
+                                vb, [] {}, [&] {
                                   for (uint32_t q = 0; q < S.nterms; q++) {  // stage the small bitmaps in LDS
                                     const ScanTerm &Tq = P.terms[S.term0 + q];
                                     if (Tq.lds_off != kNoLds)
@@ -907,7 +927,7 @@ __device__ __forceinline__ void self_issue(SelfStage<NTA> &X, const DevKeyDesc *
 
 template <int NTA>
 __device__ __forceinline__ void self_finish(SelfStage<NTA> &X, const QArgs &A, const ScanTerm *T, uint32_t *lds_bm,
-                                            uint32_t *scratch) {
+                                            uint32_t *scratch, uint32_t wg) {
   __shared__ __attribute__((aligned(16))) uint32_t s_nd2w[kArgNeedle / 4];
   const uint8_t *s_nd2 = reinterpret_cast<const uint8_t *>(s_nd2w);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -931,7 +951,7 @@ __device__ __forceinline__ void self_finish(SelfStage<NTA> &X, const QArgs &A, c
   }
   __syncthreads();
   if (A.P.stamps && tid == 0)  // TSG_STAMPS slot 7: dictionary words in LDS
-    A.P.stamps[uint64_t(blockIdx.x - A.njobs) * kStampSlots + 7] = __builtin_amdgcn_s_memrealtime();
+    A.P.stamps[uint64_t(wg) * kStampSlots + 7] = __builtin_amdgcn_s_memrealtime();
   bool sets = false;
 #pragma unroll
   for (int q = 0; q < NTA; q++) {
@@ -981,19 +1001,20 @@ template <int NT, bool DUR, bool RANGE, bool W1, bool SEG>
 __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   const unsigned long long t_start = A.P.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  if (blockIdx.x < A.njobs) {  // dictionary workgroup: [value bits | stage]
-    dict_job(A, blockIdx.x, lds + A.bm_words, lds);
+  const uint32_t vb = wg_order(A.P);  // (a ticket when dictionary or look-back waits exist)
+  if (vb < A.njobs) {  // dictionary workgroup: [value bits | stage]
+    dict_job(A, vb, lds + A.bm_words, lds);
     return;
   }
   // scan workgroup: [bitmaps bm_words | kLdsTiles masks | seg sums nsegs | first_wg nsegs+1 | caps]
   uint32_t *lds_bm = lds;
   uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + A.bm_words);
   uint32_t *lds_seg = lds + A.bm_words + A.mask_words;
-  uint32_t *lds_fw = lds_seg + A.nsegs;
+  uint32_t *lds_fw = lds_seg + ((A.nsegs + 1) & ~1u);  // (even: lds_cap below is 8-byte aligned)
   unsigned long long *lds_cap = reinterpret_cast<unsigned long long *>(lds_fw + ((A.nsegs + 2) & ~1u));
   unsigned long long *lds_rec = lds_cap + A.nsegs;  // segment mode: kSegMax staged records
   const int tid = threadIdx.x;
-  const uint32_t wg = blockIdx.x - A.njobs;
+  const uint32_t wg = vb - A.njobs;
   uint32_t si = 0;  // (fixed trip count: every first_wg load issues in one round trip)
 #pragma unroll
   for (int s2 = 1; s2 < kArgSegs; s2++) si += (uint32_t(s2) < A.nsegs && A.first_wg[s2] <= wg) ? 1u : 0u;
@@ -1064,7 +1085,7 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   };
   auto wait_bitmaps = [&] {
     if (NT > 0 && A.self_dict) {  // (self_finish ends with a barrier)
-      self_finish<NTA>(X, A, T, lds_bm, lds + A.bm_words);
+      self_finish<NTA>(X, A, T, lds_bm, lds + A.bm_words, wg);
       return;
     }
     if (NT > 0) {
@@ -1109,10 +1130,10 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   // only) and the last of each group arrives at the top counter, so no single word
   // takes a thousand atomics at the end of the launch. Every workgroup's record and
   // count stores (system-scope write-through) have completed before it arrives.
-  __builtin_amdgcn_s_waitcnt(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    const uint32_t g = blockIdx.x & 7u;
+    const uint32_t g = vb & 7u;
     // (relaxed: the only data behind the flag is host memory written through at system
     // scope, already complete; an acquire/release here would write back / invalidate L2)
     const unsigned prev = __hip_atomic_fetch_add(A.P.done + 32 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1407,7 +1428,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       uint32_t(align_up(std::max(all_w1 ? fast_bm8 : fast_bm, self_dict ? 0u : fast_vbits), 2));
   const uint32_t fast_mask_words =
       std::max<uint32_t>(kLdsTiles * kThreads / 2, self_dict ? uint32_t(align_up(fast_self, 4)) : 0u);
-  const uint32_t fast_scan_words = fast_mask_words + nsegs + ((nsegs + 2) & ~1u) + 2 * nsegs +
+  const uint32_t fast_scan_words = fast_mask_words + ((nsegs + 1) & ~1u) + ((nsegs + 2) & ~1u) + 2 * nsegs +
                                    (seg ? kSegMax * uint32_t(sizeof(MatchRec) / 4) : 0u);
   const uint32_t lds_words = fast ? fast_bm_words + std::max<uint32_t>(fast_scan_words, uint32_t(align_up(fast_stage, 4)))
                                   : max_lds_words + kLdsTiles * kThreads / 2 + nsegs;
@@ -1607,6 +1628,10 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       }
       P.done_top = dc.done_base[8] + ng;
     }
+    // workgroups that wait on lower-numbered ones take their order from a ticket
+    P.ticket = static_cast<unsigned long long *>(dc.ticket.p);
+    P.ticket_base = dc.ticket_base;
+    P.use_ticket = (!fast || !P.seg_cap || A.njobs) ? 1u : 0u;
     hipEvent_t e0 = dc.es0, e1 = dc.es1;
     const bool timed = first && time_scan;
     const bool defer = first && !timed && time_defer && dc.defer_slot(e0, e1);
@@ -1633,6 +1658,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       for (uint32_t g = 0; g < 8; g++) dc.done_base[g] = P.done_target[g];
       dc.done_base[8] = P.done_top;
     }
+    if (P.use_ticket) dc.ticket_base += grid;
   };
   // segment mode: poll the completion flag the last workgroup raises in the pinned
   // header instead of waiting for the stream (the end-of-kernel signal comes later);
@@ -1643,7 +1669,13 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       HIP_OK(hipStreamSynchronize(s));
       return;
     }
-    const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(P.out);
+    // The flag is read with acquire semantics: the record and count loads after it
+    // cannot be satisfied before it. On the device side every workgroup's record and
+    // count stores (system-scope write-through) complete (s_waitcnt vmcnt(0), memory
+    // clobber) before its arrival at the completion counters, and the flag store is
+    // issued by the last arrival, so the flag is the last of the launch's host writes.
+    const uint64_t *flag = reinterpret_cast<const uint64_t *>(P.out) + 2;
+    auto flag_up = [&] { return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == P.epoch; };
     // while the tail of the launch runs, pull the record segments of workgroups that
     // have finished into this core's caches (the copy after the flag then reads cached
     // lines instead of missing on every one)
@@ -1653,7 +1685,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     seen.assign(nwg, 0);
     uint32_t lo = 0;  // every workgroup below lo has been seen
     for (uint32_t it = 1;; it++) {
-      if (h[2] == P.epoch) return;
+      if (flag_up()) return;
       for (uint32_t w = lo; w < nwg; w++) {
         if (seen[w]) {
           if (w == lo) lo++;
@@ -1669,7 +1701,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       if ((it & 255u) == 0) {
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) {
-          if (h[2] == P.epoch) return;
+          if (flag_up()) return;
           fail(TSG_E_DEVICE, "search kernel completed without raising its completion flag");
         }
         if (e != hipErrorNotReady) HIP_OK(e);

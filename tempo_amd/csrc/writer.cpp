@@ -20,6 +20,7 @@
 #include <ctime>
 #include <map>
 #include <set>
+#include <type_traits>
 #include <unordered_map>
 
 #include "common.hpp"
@@ -28,7 +29,8 @@
 namespace tsg {
 
 // ---- SearchDataMap / writeKeyValues -------------------------------------------
-static uint32_t write_key_values(FBBuilder &b, const std::string &key_in, const std::set<std::string> &vals_in,
+template <class Values>
+static uint32_t write_key_values(FBBuilder &b, const std::string &key_in, const Values &vals_in,
                                  std::unordered_map<uint64_t, uint32_t> *cache) {
   if (vals_in.empty()) return 0;  // searchdatamap.go:104-106
   std::string key = go_to_lower(key_in);
@@ -63,11 +65,17 @@ static uint32_t write_key_values(FBBuilder &b, const std::string &key_in, const 
   return off;
 }
 
-static uint32_t write_search_data_map(FBBuilder &b, const TagMap &d, std::unordered_map<uint64_t, uint32_t> *cache) {
-  // keys sorted (std::map is ordered bytewise like sort.Strings)
+template <class Map>
+static uint32_t write_search_data_map(FBBuilder &b, const Map &d, std::unordered_map<uint64_t, uint32_t> *cache) {
+  // keys sorted bytewise like sort.Strings (a std::map already is; a rollup is sorted here)
+  std::vector<const typename Map::value_type *> kvs;
+  kvs.reserve(d.size());
+  for (auto &kv : d) kvs.push_back(&kv);
+  if (!std::is_same<Map, TagMap>::value)
+    std::sort(kvs.begin(), kvs.end(), [](auto *a, auto *b) { return a->first < b->first; });
   std::vector<uint32_t> offs;
   offs.reserve(d.size());
-  for (auto &kv : d) offs.push_back(write_key_values(b, kv.first, kv.second, cache));
+  for (auto *kv : kvs) offs.push_back(write_key_values(b, kv->first, kv->second, cache));
   b.start_vector(4, offs.size(), 4);  // SearchEntryStartTagsVector
   for (uint32_t o : offs) b.prepend_uoffset(o);
   return b.end_vector(offs.size());
@@ -195,7 +203,7 @@ struct SearchBlockWriter::Impl {
   uint32_t page_size;
   HeaderBuilder header;
   FBBuilder b{1024};
-  TagMap all_tags;
+  TagRollup all_tags;
   std::vector<uint32_t> page_entries;
   std::unordered_map<uint64_t, uint32_t> kvcache;
   std::vector<uint8_t> file;

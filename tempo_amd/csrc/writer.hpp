@@ -4,12 +4,17 @@
 #include <map>
 #include <set>
 #include <string>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace tsg {
 
 // SearchDataMap: key -> set of values (pkg/tempofb/searchdatamap.go:13)
 using TagMap = std::map<std::string, std::set<std::string>>;
+// The same map accumulated over many entries (page and block-header rollups): hashed,
+// sorted once when written (write_search_data_map orders keys and values as Go does).
+using TagRollup = std::unordered_map<std::string, std::unordered_set<std::string>>;
 
 struct SearchEntryIn {
   std::vector<uint8_t> id;
@@ -18,7 +23,7 @@ struct SearchEntryIn {
 };
 
 struct HeaderBuilder {  // SearchBlockHeaderMutable
-  TagMap tags;
+  TagRollup tags;
   uint64_t min_dur = 0, max_dur = 0;
   void add_entry(const SearchEntryIn &e);
   std::vector<uint8_t> to_bytes() const;

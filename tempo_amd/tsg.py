@@ -84,7 +84,8 @@ class _Result(C.Structure):
                 ("entry_idx", C.POINTER(C.c_uint64)),
                 ("root_service", C.POINTER(C.c_char_p)), ("root_service_len", C.POINTER(C.c_uint32)),
                 ("root_name", C.POINTER(C.c_char_p)), ("root_name_len", C.POINTER(C.c_uint32)),
-                ("metrics", _Metrics)]
+                ("metrics", _Metrics), ("nblocks", C.c_uint64), ("block_status", C.POINTER(C.c_int32)),
+                ("block_error", C.POINTER(C.c_char_p))]
 
 
 class _SearchOpts(C.Structure):
@@ -95,7 +96,8 @@ class _BlockInfo(C.Structure):
     _fields_ = [("entries", C.c_uint64), ("pages", C.c_uint64), ("keys", C.c_uint64),
                 ("header_bytes", C.c_uint64), ("fb_bytes", C.c_uint64), ("device_bytes", C.c_uint64),
                 ("min_dur_ns", C.c_uint64), ("max_dur_ns", C.c_uint64), ("device", C.c_int32),
-                ("encoding", C.c_int32), ("streaming", C.c_int32), ("partial", C.c_int32)]
+                ("encoding", C.c_int32), ("streaming", C.c_int32), ("partial", C.c_int32),
+                ("stop_status", C.c_int32), ("index_truncated", C.c_int32)]
 
 
 class _LookupOpts(C.Structure):
@@ -113,7 +115,7 @@ class _LookupResult(C.Structure):
 EXPORTED = [
     "tsg_init", "tsg_shutdown", "tsg_device_count", "tsg_device_numa_node", "tsg_last_error", "tsg_abi_version", "tsg_cancel",
     "tsg_pipeline_new", "tsg_pipeline_query", "tsg_pipeline_free", "tsg_pipeline_matches_header",
-    "tsg_block_open", "tsg_block_open_mem", "tsg_wal_block_open", "tsg_wal_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
+    "tsg_block_open", "tsg_block_open_mem", "tsg_block_clone", "tsg_wal_block_open", "tsg_wal_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
     "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_kernel_times", "tsg_results_combine",
     "tsg_v2block_open", "tsg_v2block_close", "tsg_lookup_ids", "tsg_lookup_result_free",
     "tsg_write_search_block", "tsg_write_wal_search", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
@@ -136,6 +138,7 @@ def lib():
         L.tsg_shutdown.argtypes = [vp]
         L.tsg_device_count.argtypes = [vp]
         L.tsg_device_numa_node.argtypes = [vp, C.c_int]
+        L.tsg_cancel.argtypes = [vp, C.c_uint64]
         L.tsg_pipeline_new.argtypes = [C.POINTER(_Request), C.POINTER(vp)]
         L.tsg_pipeline_query.argtypes = [vp]
         L.tsg_pipeline_query.restype = C.POINTER(_Query)
@@ -143,6 +146,7 @@ def lib():
         L.tsg_pipeline_matches_header.argtypes = [C.POINTER(_Query), C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
         L.tsg_block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
         L.tsg_block_close.argtypes = [vp]
+        L.tsg_block_clone.argtypes = [vp, vp, C.c_int, C.POINTER(vp)]
         L.tsg_wal_block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
         L.tsg_wal_block_open_mem.argtypes = [vp, C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(vp)]
         L.tsg_write_wal_search.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int]
@@ -274,6 +278,10 @@ class SearchMetrics:
     kernel_ns: int = 0
     scan_kernel_ns: int = 0
     scan_bytes: int = 0
+    # per block: TSG_OK or the error the reference's Search returns for it after its
+    # matches (a damaged data page), with the message
+    block_status: List[int] = field(default_factory=list)
+    block_errors: List[Optional[str]] = field(default_factory=list)
 
 
 def _unpack(rp) -> (List[TraceSearchMetadata], SearchMetrics):
@@ -290,8 +298,10 @@ def _unpack(rp) -> (List[TraceSearchMetadata], SearchMetrics):
                 start_time_unix_nano=r.start_ns[i], duration_ms=r.duration_ms[i], end_time_unix_nano=r.end_ns[i],
                 block_idx=r.block_idx[i], entry_idx=r.entry_idx[i]))
     m = r.metrics
+    st = [r.block_status[i] for i in range(r.nblocks)]
+    errs = [r.block_error[i].decode(errors="replace") if st[i] else None for i in range(r.nblocks)]
     return out, SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,
-                              m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
+                              m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes, st, errs)
 
 
 # ---------------------------------------------------------------------------
@@ -306,6 +316,7 @@ class Engine:
             self._devs = (C.c_int32 * len(devices))(*devices)
             o.num_devices, o.devices = len(devices), self._devs
         self.h = C.c_void_p()
+        self._raw_calls = {}  # search_raw: prebuilt ctypes arguments (handle values only)
         _check(lib().tsg_init(C.byref(o), C.byref(self.h)))
 
     @property
@@ -323,10 +334,12 @@ class Engine:
     def open_block(self, path: str, device: int = 0) -> "BackendSearchBlock":
         return BackendSearchBlock(self, path, device)
 
-    def search(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0, flags: int = 0):
-        """Ordered match sequence + metrics (tsg_search). flags: SEARCH_TIME_*."""
+    def search(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0, flags: int = 0,
+               query_id: int = 0):
+        """Ordered match sequence + metrics (tsg_search). flags: SEARCH_TIME_*; query_id
+        (non-zero) makes the search cancellable with Engine.cancel(query_id)."""
         arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
-        opts = _SearchOpts(limit=limit, flags=flags)
+        opts = _SearchOpts(limit=limit, flags=flags, query_id=query_id)
         rp = C.POINTER(_Result)()
         _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
         try:
@@ -335,14 +348,18 @@ class Engine:
             lib().tsg_result_free(rp)
 
     def search_raw(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0,
-                   flags: int = 0, _cache={}):
+                   flags: int = 0):
         """tsg_search without unpacking the matches into Python objects: returns
         (match count, SearchMetrics). The result arrays are assembled by libtsg as
         for any caller (what the Go shim would receive) and then freed. The ctypes
-        argument objects are built once per (blocks, pipeline, limit, flags)."""
-        key = (self.h.value, pipeline.query_addr, limit, flags) + tuple(b.h.value for b in blocks)
+        argument objects are built once per (blocks, pipeline, limit, flags) and kept on
+        this Engine (bounded; they hold handle values, not the block objects)."""
+        key = (pipeline.query_addr, limit, flags) + tuple(b.h.value for b in blocks)
+        _cache = self._raw_calls
         call = _cache.get(key)
         if call is None:
+            if len(_cache) >= 64:
+                _cache.clear()
             L = _raw_lib()  # its own function objects: no argtypes, arguments are prebuilt ctypes objects
             fn, free = L.tsg_search, L.tsg_result_free
             arr = (C.c_void_p * max(len(blocks), 1))(*[b.h.value for b in blocks])
@@ -350,7 +367,7 @@ class Engine:
             rp = C.POINTER(_Result)()
             args = (C.c_void_p(self.h.value), arr, C.c_size_t(len(blocks)), C.c_void_p(pipeline.query_addr),
                     C.byref(opts), C.byref(rp))
-            call = _cache[key] = (fn, free, args, rp, arr, opts, blocks)
+            call = _cache[key] = (fn, free, args, rp, arr, opts)
         fn, free, args, rp = call[0], call[1], call[2], call[3]
         rc = fn(*args)
         if rc:
@@ -361,6 +378,11 @@ class Engine:
                             m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
         free(rp)
         return n, met
+
+    def cancel(self, query_id: int):
+        """tsg_cancel: the search running (or about to run) with this id stops at its next
+        chunk boundary with TSG_E_CANCELLED (the Go shim maps ctx.Done() to this)."""
+        _check(lib().tsg_cancel(self.h, query_id))
 
     def kernel_times(self, cap: int = 65536) -> List[int]:
         """Durations (ns) of the searches run with SEARCH_TIME_DEFER since the last
@@ -415,6 +437,7 @@ class Engine:
             lib().tsg_lookup_result_free(rp)
 
     def close(self):
+        self._raw_calls = {}
         if getattr(self, "h", None):
             lib().tsg_shutdown(self.h)
             self.h = None
@@ -423,11 +446,18 @@ class Engine:
 class BackendSearchBlock:
     """A backend search block resident on one device (tsg_block)."""
 
-    def __init__(self, eng: Engine, path: str, device: int = 0, _wal: bool = False):
+    def __init__(self, eng: Engine, path: str, device: int = 0, _wal: bool = False, _clone_of=None):
         self.path = path
         self.h = C.c_void_p()
+        if _clone_of is not None:
+            _check(lib().tsg_block_clone(eng.h, _clone_of.h, device, C.byref(self.h)))
+            return
         opener = lib().tsg_wal_block_open if _wal else lib().tsg_block_open
         _check(opener(eng.h, path.encode(), device, C.byref(self.h)))
+
+    def clone(self, eng: Engine, device: int = 0) -> "BackendSearchBlock":
+        """tsg_block_clone: a second resident copy (device-to-device), e.g. on another GPU."""
+        return BackendSearchBlock(eng, self.path, device, _clone_of=self)
 
     def info(self):
         i = _BlockInfo()

@@ -8,7 +8,7 @@ has() { [[ ",$STAGES," == *",$1,"* ]]; }
 ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 0 pass, 1 test failures (no crash)
 
 if has test; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
   ok_rc $rc || exit $rc
   # the general (prep kernel + descriptor) search path, forced
@@ -18,6 +18,10 @@ if has test; then
   # the one-launch path with dictionary workgroups (granule hand-off) instead of per-workgroup matching
   TSG_NO_SELF_DICT=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_noself.log 2>&1
   rc=$?; echo "pytest gpu (TSG_NO_SELF_DICT) rc=$rc"; tail -5 gpurun_out/pytest_gpu_noself.log
+  ok_rc $rc || exit $rc
+  # one descriptor-path launch for blocks beyond 32 (no chunking)
+  TSG_CHUNK_BLOCKS=0 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider -k "many_blocks or cancel or limit" > gpurun_out/pytest_gpu_nochunk.log 2>&1
+  rc=$?; echo "pytest gpu (TSG_CHUNK_BLOCKS=0) rc=$rc"; tail -5 gpurun_out/pytest_gpu_nochunk.log
   ok_rc $rc || exit $rc
   # the one-launch path in look-back mode only (no per-tile segments)
   TSG_NO_SEG=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_noseg.log 2>&1
