@@ -284,6 +284,28 @@ int tsg_lookup_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks,
                    tsg_lookup_result **out);
 void tsg_lookup_result_free(tsg_lookup_result *r);
 
+/* tempodb.Find's per-block step for a batch of ids, whole on the device: the lookup above,
+ * then PagedFinder.findOne (tempodb/encoding/v2/finder_paged.go:79-110) for every hit: the
+ * data page its index record names (resident in HBM since tsg_v2block_open) is decompressed
+ * (encodings none and snappy; others -> TSG_E_UNSUPPORTED_ENCODING for that hit) and its
+ * objects are scanned for the exact id. One entry per lookup hit, sorted (id_idx,
+ * block_idx): status TSG_OK with the object's bytes (what findOne returns), TSG_E_NOT_FOUND
+ * (a bloom false positive: findOne returns nil), or the error findOne returns for that
+ * page (read, framing, decompression, object framing). */
+typedef struct tsg_find_result {
+  uint64_t n;
+  const uint32_t *id_idx;
+  const uint32_t *block_idx;
+  const int32_t *status;
+  const uint64_t *obj_off; /* into obj_bytes (status TSG_OK) */
+  const uint32_t *obj_len;
+  const uint8_t *obj_bytes;
+  uint64_t kernel_ns;
+} tsg_find_result;
+int tsg_find_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, const uint8_t (*ids)[16],
+                 size_t nids, const tsg_lookup_opts *opts, tsg_find_result **out);
+void tsg_find_result_free(tsg_find_result *r);
+
 /* ---- block writer (tooling: synthetic data and test fixtures) ----------------- */
 /* Entry list wire format (little endian), one record per trace:
  *   u32 id_len, id bytes, u64 start_ns, u64 end_ns, u32 ntags,

@@ -353,6 +353,59 @@ static void merge_page(HostBlock &hb, std::vector<KeyBuild> &kb, PageParse &pp) 
   hb.n = n1;
 }
 
+// Narrow keys (fewer than 255 value sets: one-byte columns) get a canonical numbering:
+// values in byte order, value sets in order of their (renumbered) value lists. Blocks
+// holding the same values for a key then hold byte-identical dictionaries, which the
+// engine interns once per context and matches once per query on the host (the one-launch
+// search path takes the resulting 256-bit set bitmaps in its kernel arguments).
+// Ids are internal; scan order, set membership and Value(0) are unchanged.
+static void canonicalize_narrow_keys(HostBlock &hb) {
+  for (size_t k = 0; k < hb.keys.size(); k++) {
+    KeyColumn &kc = hb.keys[k];
+    if (kc.width() != 1) continue;
+    const uint32_t nv = kc.nvals(), ns = kc.nsets();
+    std::vector<uint32_t> vord(nv);
+    for (uint32_t i = 0; i < nv; i++) vord[i] = i;
+    std::sort(vord.begin(), vord.end(), [&](uint32_t a, uint32_t b) {
+      std::string_view x = hb.dict_value(int(k), a), y = hb.dict_value(int(k), b);
+      return x < y;
+    });
+    std::vector<uint32_t> vnew(nv);
+    for (uint32_t i = 0; i < nv; i++) vnew[vord[i]] = i;
+    std::vector<uint8_t> bytes;
+    std::vector<uint32_t> off(1, 0);
+    for (uint32_t i = 0; i < nv; i++) {
+      std::string_view v = hb.dict_value(int(k), vord[i]);
+      bytes.insert(bytes.end(), v.begin(), v.end());
+      off.push_back(uint32_t(bytes.size()));
+    }
+    std::vector<std::vector<uint32_t>> sets(ns);
+    for (uint32_t sidx = 0; sidx < ns; sidx++)
+      for (uint32_t i = kc.set_off[sidx]; i < kc.set_off[sidx + 1]; i++) sets[sidx].push_back(vnew[kc.set_vals[i]]);
+    std::vector<uint32_t> sord(ns);
+    for (uint32_t i = 0; i < ns; i++) sord[i] = i;
+    std::sort(sord.begin(), sord.end(), [&](uint32_t a, uint32_t b) { return sets[a] < sets[b]; });
+    std::vector<uint32_t> snew(ns), set_off(1, 0), set_vals;
+    for (uint32_t i = 0; i < ns; i++) {
+      snew[sord[i]] = i;
+      set_vals.insert(set_vals.end(), sets[sord[i]].begin(), sets[sord[i]].end());
+      set_off.push_back(uint32_t(set_vals.size()));
+    }
+    kc.dict_bytes.swap(bytes);
+    kc.dict_off.swap(off);
+    kc.set_off.swap(set_off);
+    kc.set_vals.swap(set_vals);
+    for (auto &c : kc.col)
+      if (c != kNone) c = snew[c];
+    if (int(k) == hb.svc_key)
+      for (auto &v : hb.svc_vid)
+        if (v != kNone) v = vnew[v];
+    if (int(k) == hb.name_key)
+      for (auto &v : hb.name_vid)
+        if (v != kNone) v = vnew[v];
+  }
+}
+
 void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
                          const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
                          HostBlock &hb) {
@@ -417,6 +470,7 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
     }
   }
   for (auto &kc : hb.keys) kc.col.resize(hb.n, kNone);
+  canonicalize_narrow_keys(hb);
 }
 
 }  // namespace tsg
@@ -558,6 +612,7 @@ void decode_wal_search_block(const uint8_t *file, size_t len, int enc, HostBlock
     i = j;
   }
   for (auto &kc : hb.keys) kc.col.resize(hb.n, kNone);
+  canonicalize_narrow_keys(hb);
 }
 
 }  // namespace tsg

@@ -174,6 +174,11 @@ struct LookupHolder {
   LookupOut o;
 };
 static_assert(offsetof(LookupHolder, pub) == 0, "pub first");
+struct FindHolder {
+  tsg_find_result pub{};
+  FindOut o;
+};
+static_assert(offsetof(FindHolder, pub) == 0, "pub first");
 
 static std::string join(const char *dir, const char *name) { return std::string(dir) + "/" + name; }
 
@@ -756,6 +761,29 @@ int tsg_lookup_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, con
   });
 }
 void tsg_lookup_result_free(tsg_lookup_result *r) { delete reinterpret_cast<LookupHolder *>(r); }
+
+int tsg_find_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, const uint8_t (*ids)[16], size_t nids,
+                 const tsg_lookup_opts *opts, tsg_find_result **out) {
+  if (!ctx || !out || (nblocks && !blocks) || (nids && !ids)) return TSG_E_INVALID;
+  return guard([&] {
+    auto *h = new FindHolder();
+    std::unique_ptr<FindHolder> g(h);
+    std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, V2Block *>>> per_dev;
+    for (size_t i = 0; i < nblocks; i++) per_dev[blocks[i]->b.dc].push_back({uint32_t(i), &blocks[i]->b});
+    if (per_dev.size() > 1) fail(TSG_E_INVALID, "tsg_find_ids: blocks must share one device (shard ids instead)");
+    if (!per_dev.empty()) device_find(*per_dev.begin()->first, per_dev.begin()->second, ids, nids, opts, h->o);
+    h->pub.n = h->o.id_idx.size();
+    h->pub.id_idx = h->o.id_idx.data();
+    h->pub.block_idx = h->o.block_idx.data();
+    h->pub.status = h->o.status.data();
+    h->pub.obj_off = h->o.obj_off.data();
+    h->pub.obj_len = h->o.obj_len.data();
+    h->pub.obj_bytes = h->o.bytes.data();
+    h->pub.kernel_ns = h->o.kernel_ns;
+    *out = &g.release()->pub;
+  });
+}
+void tsg_find_result_free(tsg_find_result *r) { delete reinterpret_cast<FindHolder *>(r); }
 
 // ---- writer ---------------------------------------------------------------------------
 int tsg_write_search_block(const char *dir, const uint8_t *entries, size_t len, int encoding, uint32_t page_size) {

@@ -52,7 +52,7 @@ void ctx_shutdown(Ctx &c) {
     (void)hipStreamSynchronize(dc->stream);
     for (DevBuf *b : {&dc->desc, &dc->vmatch, &dc->bitmaps, &dc->gran, &dc->ticket, &dc->out, &dc->regions,
                       &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps, &dc->gbm, &dc->lkhits,
-                      &dc->done})
+                      &dc->done, &dc->fpages, &dc->fhits, &dc->fres, &dc->farena, &dc->fcrc, &dc->fdst, &dc->foff})
       b->release();
     for (hipEvent_t e : dc->tring) (void)hipEventDestroy(e);
     dc->hdesc.release();
@@ -90,6 +90,22 @@ static T *dev_upload(DevBlock &b, const T *src, size_t count, hipStream_t s, siz
 
 static void upload_desc(DevBlock &d, hipStream_t s);
 
+// One interned copy per distinct narrow dictionary (content-equal dictionaries of
+// different blocks share it; entries of closed blocks expire).
+static std::shared_ptr<const NarrowDict> intern_narrow(Ctx &c, NarrowDict &&nd) {
+  auto hv = [](const auto &v) { return xxhash64(reinterpret_cast<const uint8_t *>(v.data()), v.size() * sizeof(v[0])); };
+  const uint64_t h = hv(nd.bytes) ^ (hv(nd.off) * 31) ^ (hv(nd.set_off) * 131) ^ (hv(nd.set_vals) * 1313);
+  std::lock_guard<std::mutex> lk(c.dmu);
+  auto &vec = c.dicts[h];
+  vec.erase(std::remove_if(vec.begin(), vec.end(), [](const auto &w) { return w.expired(); }), vec.end());
+  for (auto &w : vec)
+    if (auto p = w.lock())
+      if (*p == nd) return p;
+  auto p = std::make_shared<const NarrowDict>(std::move(nd));
+  vec.push_back(p);
+  return p;
+}
+
 void block_upload(Ctx &c, Block &b, int device_hint) {
   if (c.devs.empty()) fail(TSG_E_DEVICE, "no device");
   DeviceCtx &dc = *c.devs[size_t(std::max(device_hint, 0)) % c.devs.size()];
@@ -102,19 +118,50 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
   HIP_OK(hipSetDevice(dc.ordinal));
   hipStream_t s = dc.stream;
   size_t n = h.n;
-  std::vector<uint32_t> dur32(n), ss(n), es(n);
+  // [dur32 | start_s | end_s], npad entries each (whole tiles: kColPad), one allocation
+  const size_t npad = (std::max<size_t>(n, 1) + kColPad - 1) / kColPad * kColPad;
+  d.npad = npad;
+  std::vector<uint32_t> scan(3 * npad, 0);
   std::vector<uint64_t> dur64(n);
   for (size_t i = 0; i < n; i++) {
     uint64_t dd = h.end[i] - h.start[i];  // uint64 wrap (pitfall P2)
     dur64[i] = dd;
-    dur32[i] = dd >= 0xffffffffULL ? 0xffffffffu : uint32_t(dd);
-    ss[i] = uint32_t(h.start[i] / 1000000000ULL);
-    es[i] = uint32_t(h.end[i] / 1000000000ULL);
+    scan[i] = dd >= 0xffffffffULL ? 0xffffffffu : uint32_t(dd);
+    scan[npad + i] = uint32_t(h.start[i] / 1000000000ULL);
+    scan[2 * npad + i] = uint32_t(h.end[i] / 1000000000ULL);
   }
-  d.dur32 = dev_upload(d, dur32.data(), n, s, kColPad);
+  d.dur32 = dev_upload(d, scan.data(), scan.size(), s);
+  d.start_s = d.dur32 + npad;
+  d.end_s = d.dur32 + 2 * npad;
   d.dur64 = dev_upload(d, dur64.data(), n, s);
-  d.start_s = dev_upload(d, ss.data(), n, s, kColPad);
-  d.end_s = dev_upload(d, es.data(), n, s, kColPad);
+  // one-byte key columns: one allocation, npad bytes per narrow key
+  {
+    d.narrow_slot.assign(h.keys.size(), -1);
+    int nn = 0;
+    for (size_t k = 0; k < h.keys.size(); k++)
+      if (h.keys[k].width() == 1) d.narrow_slot[k] = nn++;
+    std::vector<uint8_t> ncol(std::max<size_t>(size_t(nn), 1) * npad, 0xff);
+    for (size_t k = 0; k < h.keys.size(); k++) {
+      if (d.narrow_slot[k] < 0) continue;
+      uint8_t *dst = ncol.data() + size_t(d.narrow_slot[k]) * npad;
+      const auto &col = h.keys[k].col;
+      for (size_t i = 0; i < n; i++) dst[i] = col[i] == kNone ? 0xff : uint8_t(col[i]);
+    }
+    d.narrow_base = dev_upload(d, ncol.data(), ncol.size(), s);
+    HIP_OK(hipStreamSynchronize(s));  // (ncol is a temporary)
+  }
+  b.narrow.assign(h.keys.size(), nullptr);
+  for (size_t k = 0; k < h.keys.size(); k++) {
+    if (d.narrow_slot[k] < 0) continue;
+    const KeyColumn &kc = h.keys[k];
+    NarrowDict nd;
+    nd.bytes = kc.dict_bytes;
+    nd.off = kc.dict_off;
+    nd.set_off = kc.set_off;
+    nd.set_vals = kc.set_vals;
+    nd.identity = kc.identity;
+    b.narrow[k] = intern_narrow(c, std::move(nd));
+  }
   d.ids = dev_upload(d, h.ids.data(), n * 16, s);
   d.start_ns = dev_upload(d, h.start.data(), n, s);
   d.end_ns = dev_upload(d, h.end.data(), n, s);
@@ -135,10 +182,7 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     k.nsets = kc.nsets();
     k.identity = kc.identity;
     if (k.width == 1) {
-      std::vector<uint8_t> col(n);
-      for (size_t i = 0; i < n; i++) col[i] = kc.col[i] == kNone ? 0xff : uint8_t(kc.col[i]);
-      k.col = dev_upload(d, col.data(), n, s, kColPad);
-      HIP_OK(hipStreamSynchronize(s));
+      k.col = const_cast<uint8_t *>(d.narrow_base) + size_t(d.narrow_slot[size_t(&kc - h.keys.data())]) * npad;
     } else if (k.width == 2) {
       std::vector<uint16_t> col(n);
       for (size_t i = 0; i < n; i++) col[i] = kc.col[i] == kNone ? 0xffff : uint16_t(kc.col[i]);
@@ -252,6 +296,10 @@ void block_clone(Ctx &c, const Block &src, Block &dst, int device_hint) {
   d.end_ns = static_cast<uint64_t *>(xl(o.end_ns));
   d.names = static_cast<uint32_t *>(xl(o.names));
   d.id_len = static_cast<uint8_t *>(xl(o.id_len));
+  d.npad = o.npad;
+  d.narrow_base = static_cast<const uint8_t *>(xl(o.narrow_base));
+  d.narrow_slot = o.narrow_slot;
+  dst.narrow = src.narrow;
   for (const DevKey &k0 : o.keys) {
     DevKey k = k0;
     k.col = xl(k0.col);

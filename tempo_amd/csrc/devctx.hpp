@@ -77,6 +77,7 @@ struct DeviceCtx {
   // counts, [header | records] output. lookup reuses desc/gran/ticket/out/hdr/err.
   DevBuf desc, vmatch, bitmaps, gran, ticket, out, regions, seg_counts, hdr, err;
   DevBuf maskbits, agg, stamps, gbm, lkhits;
+  DevBuf fpages, fhits, fres, farena, fcrc, fdst, foff;  // device findOne (find.hip)
   HostBuf hdesc, hout;
   // search results, written by the emit kernel directly (coherent: the kernel's
   // stores go over the fabric, visible to the host once the stream is synchronised)
@@ -85,6 +86,7 @@ struct DeviceCtx {
   uint32_t search_epoch = 0;
   bool fast_off = std::getenv("TSG_NO_FAST") != nullptr;  // force the general (prep + search) path
   bool self_off = std::getenv("TSG_NO_SELF_DICT") != nullptr;  // one-launch path: always use dictionary workgroups
+  bool narrow_off = std::getenv("TSG_NO_NARROW") != nullptr;  // one-launch path: never host-matched narrow dictionaries
   std::map<std::pair<const void *, size_t>, int> occupancy;  // (kernel, dynamic LDS) -> blocks per CU  // search launches: tag of the published workgroup counts
   size_t gran_tiles = 0;
   // one-launch search path: per-XCD-group completion counters + top counter, 128 B

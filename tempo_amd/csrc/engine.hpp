@@ -4,6 +4,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "block.hpp"
@@ -51,6 +52,22 @@ struct DevBlockDesc {  // 128 B, followed by nkeys DevKeyDesc
 };
 static_assert(sizeof(DevKeyDesc) == 64 && sizeof(DevBlockDesc) == 128, "descriptor layout");
 
+// The dictionary of a narrow key (< 255 value sets, one-byte column) in canonical form
+// (block.cpp canonicalize_narrow_keys), interned per context: blocks with the same
+// values share one. A query matches it on the host once and hands the one-launch kernel
+// the 256-bit value-set bitmap.
+struct NarrowDict {
+  std::vector<uint8_t> bytes;
+  std::vector<uint32_t> off;                // nvals + 1
+  std::vector<uint32_t> set_off, set_vals;  // value sets (CSR over value ids)
+  bool identity = true;
+  uint32_t nvals() const { return uint32_t(off.size() - 1); }
+  uint32_t nsets() const { return uint32_t(set_off.size() - 1); }
+  bool operator==(const NarrowDict &o) const {
+    return bytes == o.bytes && off == o.off && set_off == o.set_off && set_vals == o.set_vals && identity == o.identity;
+  }
+};
+
 // One backend search block resident in HBM (DESIGN.md "Data layout in HBM").
 struct DevBlock {
   int device = 0;
@@ -64,6 +81,11 @@ struct DevBlock {
   uint32_t *names = nullptr;   // n x {svc vid, name vid}: record fields resolved on the host
   uint8_t *id_len = nullptr;
   const DevBlockDesc *desc = nullptr;
+  // dur32 | start_s | end_s share one allocation, `npad` entries each; the one-byte key
+  // columns share another, `npad` bytes per slot (narrow_slot[k], -1 for wider keys)
+  uint64_t npad = 0;
+  const uint8_t *narrow_base = nullptr;
+  std::vector<int> narrow_slot;
   std::vector<DevKey> keys;
   uint64_t bytes = 0;
   std::vector<void *> allocs;
@@ -76,11 +98,14 @@ struct Block {
   HostBlock host;     // dictionaries/metadata kept on the host (names, header, page table)
   DevBlock dev;
   DeviceCtx *dc = nullptr;
+  std::vector<std::shared_ptr<const NarrowDict>> narrow;  // per key: interned dictionary (narrow keys)
 };
 
 struct Ctx {
   std::vector<DeviceCtx *> devs;  // owned; freed by ctx_shutdown
   std::mutex mu;
+  std::mutex dmu;  // narrow-dictionary intern table (content hash -> live dictionaries)
+  std::unordered_map<uint64_t, std::vector<std::weak_ptr<const NarrowDict>>> dicts;
 };
 
 void ctx_init(Ctx &c, const tsg_options *opts);
@@ -130,6 +155,11 @@ struct V2Block {
   uint64_t *d_rec_start = nullptr;
   uint32_t *d_rec_len = nullptr;
   uint64_t *d_shard_m = nullptr, *d_shard_k = nullptr, *d_shard_bitlen = nullptr, *d_shard_woff = nullptr;
+  // the data file (compressed pages) resident for findOne on the device; enc = meta.json
+  // "encoding" (backend.Encoding)
+  const uint8_t *d_data = nullptr;
+  uint64_t data_len = 0;
+  int enc = -1;
   std::vector<void *> allocs;
 };
 void v2block_open(Ctx &c, V2Block &b, const std::string &dir, int device_hint);
@@ -143,6 +173,17 @@ struct LookupOut {
 };
 void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>> &blocks, const uint8_t (*ids)[16],
                    size_t nids, const tsg_lookup_opts *opts, LookupOut &out);
+// tempodb.Find per (id, block): the lookup, then findOne on the device (find.hip)
+struct FindOut {
+  std::vector<uint32_t> id_idx, block_idx;
+  std::vector<int32_t> status;      // TSG_OK found, TSG_E_NOT_FOUND, or the page's error
+  std::vector<uint64_t> obj_off;    // into bytes
+  std::vector<uint32_t> obj_len;
+  std::vector<uint8_t> bytes;
+  uint64_t kernel_ns = 0;
+};
+void device_find(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>> &blocks, const uint8_t (*ids)[16],
+                 size_t nids, const tsg_lookup_opts *opts, FindOut &out);
 
 int device_ordinal(const DeviceCtx &dc);
 // Durations of the TSG_SEARCH_TIME_DEFER launches since the last call (waits for the stream).

@@ -408,6 +408,13 @@ void v2block_open(Ctx &c, V2Block &b, const std::string &dir, int device_hint) {
   b.d_rec_ids = static_cast<uint8_t *>(up(rid.data(), rid.size()));
   b.d_rec_start = static_cast<uint64_t *>(up(rs.data(), rs.size() * 8));
   b.d_rec_len = static_cast<uint32_t *>(up(rl.data(), rl.size() * 4));
+  // the data file for findOne on the device (pages stay compressed in HBM)
+  b.enc = enc.empty() ? -1 : parse_encoding(enc);
+  std::vector<uint8_t> data;
+  if (!std::getenv("TSG_V2_NO_DATA") && read_file(dir + "/data", data)) {
+    b.d_data = static_cast<const uint8_t *>(up(data.data(), data.size()));
+    b.data_len = data.size();
+  }
 }
 
 void v2block_free(V2Block &b) {

@@ -763,7 +763,7 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
 // (agent-scope stores: untorn, no fences needed). The scan workgroups behind them
 // poll the granules of their block's terms, then scan. Dispatch is in index
 // order, so the producers are resident or done; polls are bounded.
-constexpr int kArgSegs = 32, kArgTerms = 8, kArgNeedle = 256;
+constexpr int kArgSegs = 32, kArgTerms = 4, kArgNeedle = 256, kArgBms = 16;
 constexpr uint32_t kFastStageWords = 6144;  // 24 KiB: one dictionary's offsets + bytes + value bits + set CSR
 struct QArgs {
   const DevBlockDesc *blk[kArgSegs];
@@ -779,6 +779,16 @@ struct QArgs {
   uint32_t self_dict;       // 1: every scan workgroup matches its block's (small) dictionaries itself, njobs = 0
   uint32_t stage_first;     // self_dict: the dictionary words land before the first tile loads issue
   unsigned long long *gbm;  // njobs x gstride granules
+  // narrow mode: every term column of every block is one byte wide and its dictionary
+  // was matched on the host (interned canonical dictionaries): the scan columns and the
+  // 256-bit value-set bitmaps travel here, so a workgroup's first tile load waits for
+  // nothing but these arguments (no descriptor chain, no dictionary staging)
+  uint32_t narrow;
+  const uint32_t *scan[kArgSegs];   // [dur32 | start_s | end_s], npad entries each
+  const uint8_t *ncol[kArgSegs];    // one-byte key columns, npad bytes per slot
+  uint32_t npad[kArgSegs], nent[kArgSegs];
+  uint8_t slot[kArgSegs][kArgTerms], bmi[kArgSegs][kArgTerms], nsets8[kArgSegs][kArgTerms];
+  uint32_t bms[kArgBms][8];
   ScanParams P;             // thresholds, outputs (segs/terms/wg_seg unused)
 };
 static_assert(sizeof(QArgs) <= 4096, "kernel arguments");
@@ -1022,23 +1032,41 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   si = __builtin_amdgcn_readfirstlane(si);
   const DevBlockDesc *B = A.blk[si];
   constexpr int NTA = NT > 0 ? NT : 1;
+  const bool narrow = A.narrow != 0;
   DevKeyDesc KD[NTA];  // scalar loads, all issued together (one-launch kernels: NT == nterms)
-  if (NT > 0)
+  if (NT > 0 && !narrow)
 #pragma unroll
     for (int q = 0; q < NTA; q++) KD[q] = key_desc(B, A.key_of[si][q]);
   ScanSeg S;
-  {
-    const auto *Bc = K4(B);
-    S.n = Bc->n;
-    S.dur32 = Bc->dur32;
+  // the record columns (ids, times, names) are read only to emit matches; in narrow mode
+  // their descriptor loads are issued after the scan: scalar loads complete out of order,
+  // so any earlier use of a kernel argument would wait for them (s_waitcnt lgkmcnt(0))
+  auto cold = [&](const DevBlockDesc *Bd) {
+    const auto *Bc = K4(Bd);
     S.dur64 = Bc->dur64;
-    S.start_s = Bc->start_s;
-    S.end_s = Bc->end_s;
     S.ids = Bc->ids;
     S.start_ns = Bc->start_ns;
     S.end_ns = Bc->end_ns;
     S.names = Bc->names;
     S.id_len = Bc->id_len;
+  };
+  if (narrow) {
+    S.n = A.nent[si];
+    S.dur32 = A.scan[si];
+    S.start_s = A.scan[si] + A.npad[si];
+    S.end_s = A.scan[si] + 2ull * A.npad[si];
+    S.dur64 = nullptr;  // (narrow mode: no threshold >= 2^32-1 ns)
+    S.ids = nullptr;
+    S.start_ns = S.end_ns = nullptr;
+    S.names = nullptr;
+    S.id_len = nullptr;
+  } else {
+    const auto *Bc = K4(B);
+    S.n = Bc->n;
+    S.dur32 = Bc->dur32;
+    S.start_s = Bc->start_s;
+    S.end_s = Bc->end_s;
+    cold(B);
   }
   S.nunits = uint32_t((S.n + kUnit - 1) / kUnit);
   S.first_wg = A.first_wg[si];
@@ -1057,10 +1085,16 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   for (int q = 0; q < NTA; q++) {
     if (NT <= 0) break;
     const DevKeyDesc &K = KD[q];
-    T[q].col = K.col;
+    if (narrow) {
+      T[q].col = A.ncol[si] + uint64_t(A.slot[si][q]) * A.npad[si];
+      T[q].width = 1;
+      T[q].nsets = A.nsets8[si][q];
+    } else {
+      T[q].col = K.col;
+      T[q].width = K.width;
+      T[q].nsets = K.nsets;
+    }
     T[q].bm = nullptr;
-    T[q].width = K.width;
-    T[q].nsets = K.nsets;
     T[q].lds_off = bmo;
     T[q].bm_words = (K.nsets + 31) / 32;
     bmo += W1 ? 8u : T[q].bm_words;
@@ -1084,6 +1118,15 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
       A.P.stamps[uint64_t(wg) * kStampSlots + 6] = __builtin_amdgcn_s_memrealtime();
   };
   auto wait_bitmaps = [&] {
+    if (narrow) {  // the host's bitmaps, from the kernel arguments (uniform: scalar loads)
+      if (NT > 0 && tid == 0)
+#pragma unroll
+        for (int q = 0; q < NTA; q++)
+#pragma unroll
+          for (int w = 0; w < 8; w++) lds_bm[T[q].lds_off + w] = A.bms[A.bmi[si][q]][w];
+      __syncthreads();
+      return;
+    }
     if (NT > 0 && A.self_dict) {  // (self_finish ends with a barrier)
       self_finish<NTA>(X, A, T, lds_bm, lds + A.bm_words, wg);
       return;
@@ -1116,6 +1159,11 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   };
   scan_emit<NT, DUR, RANGE, W1, SEG>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, A.nsegs}, lds_bm, lds_mask, lds_seg,
                                      lds_rec, t_start, wg, issue_stage, wait_bitmaps, [&] {
+                                       if (narrow) {  // (the asm keeps the loads below the scan loop)
+                                         const DevBlockDesc *Bd = B;
+                                         asm volatile("" : "+s"(Bd));
+                                         cold(Bd);
+                                       }
                                        if constexpr (!SEG) {
                                          for (uint32_t i = tid; i < A.nsegs; i += kThreads) {
                                            lds_seg[i] = 0;
@@ -1291,6 +1339,17 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // workgroups need to match the dictionaries themselves
   std::vector<std::array<uint16_t, kArgTerms>> seg_keys;
   std::vector<const DevBlockDesc *> seg_desc;
+  // narrow mode: per block its scan / one-byte column bases and per term the column slot
+  // and interned dictionary
+  struct NarrowSeg {
+    const uint32_t *scan;
+    const uint8_t *ncol;
+    uint32_t npad;
+    std::array<uint8_t, kArgTerms> slot, nsets;
+    std::array<const NarrowDict *, kArgTerms> dict;
+  };
+  std::vector<NarrowSeg> nsegv;
+  bool all_narrow = q.nterms <= uint32_t(kArgTerms);
   uint32_t fast_stage = 0, fast_bm = 0, fast_bm8 = 0, fast_vbits = 0, fast_words = 1, fast_self = 0;
   for (auto &bp : blocks) {
     Block &b = *bp.second;
@@ -1363,6 +1422,24 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     }
     max_lds_words = std::max(max_lds_words, sg.lds_words);
     {
+      NarrowSeg ns{};
+      ns.scan = d.dur32;
+      ns.ncol = d.narrow_base;
+      ns.npad = uint32_t(d.npad);
+      for (uint32_t t = 0; t < q.nterms && all_narrow; t++) {
+        const size_t k = size_t(kidx[t]);
+        if (d.narrow_slot.size() <= k || d.narrow_slot[k] < 0 || d.narrow_slot[k] > 255 || !b.narrow[k]) {
+          all_narrow = false;
+          break;
+        }
+        ns.slot[t] = uint8_t(d.narrow_slot[k]);
+        ns.nsets[t] = uint8_t(d.keys[k].nsets);
+        ns.dict[t] = b.narrow[k].get();
+      }
+      if (d.npad >= (1ull << 32)) all_narrow = false;
+      nsegv.push_back(ns);
+    }
+    {
       std::array<uint16_t, kArgTerms> ks{};
       uint32_t bmw = 0, bmw8 = 0, selfw = 0;
       for (uint32_t t = 0; t < q.nterms && t < kArgTerms; t++) {
@@ -1401,8 +1478,49 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   const uint32_t nsegs = uint32_t(segs.size());
   // one launch when the whole query fits the kernel arguments and every block's
   // dictionaries for it can be matched in LDS by the scanning workgroups
+  // narrow mode: the value-set bitmap of every (dictionary, term) pair, matched here on
+  // the host (bytes.Contains per value, a set matches when one of its values does);
+  // identical dictionaries of different blocks are matched once
+  std::vector<std::array<uint32_t, 8>> nbms;
+  std::vector<std::array<uint8_t, kArgTerms>> nbmi(segs.size());
+  const bool need64 = (q.has_min && q.min_ns >= 0xffffffffULL) || (q.has_max && q.max_ns >= 0xffffffffULL);
+  bool narrow = all_narrow && !need64 && !dc.narrow_off && nsegs <= uint32_t(kArgSegs) &&
+                needles.size() <= size_t(kArgNeedle);
+  if (narrow) {
+    std::pair<const NarrowDict *, uint32_t> memo[kArgBms];  // (dictionary, term) of each bitmap
+    thread_local std::vector<uint8_t> vm;
+    for (size_t i = 0; i < segs.size() && narrow; i++)
+      for (uint32_t t = 0; t < q.nterms && narrow; t++) {
+        const NarrowDict *nd = nsegv[i].dict[t];
+        size_t j = 0;
+        while (j < nbms.size() && !(memo[j].first == nd && memo[j].second == t)) j++;
+        if (j < nbms.size()) {
+          nbmi[i][t] = uint8_t(j);
+          continue;
+        }
+        if (nbms.size() == size_t(kArgBms)) {
+          narrow = false;
+          break;
+        }
+        const std::string_view needle(reinterpret_cast<const char *>(q.values[t]), q.value_lens[t]);
+        vm.assign(nd->nvals(), 0);
+        for (uint32_t v = 0; v < nd->nvals(); v++) {
+          const std::string_view val(reinterpret_cast<const char *>(nd->bytes.data() + nd->off[v]), nd->off[v + 1] - nd->off[v]);
+          vm[v] = needle.empty() || val.find(needle) != std::string_view::npos;  // bytes.Contains (P7)
+        }
+        std::array<uint32_t, 8> bm{};
+        for (uint32_t st = 0; st < nd->nsets(); st++) {
+          bool m = false;
+          for (uint32_t j = nd->set_off[st]; j < nd->set_off[st + 1] && !m; j++) m = vm[nd->set_vals[j]] != 0;
+          if (m) bm[st >> 5] |= 1u << (st & 31);
+        }
+        nbmi[i][t] = uint8_t(nbms.size());
+        memo[nbms.size()] = {nd, t};
+        nbms.push_back(bm);
+      }
+  }
   const bool fast = !dc.fast_off && nsegs <= uint32_t(kArgSegs) && q.nterms <= 4 && needles.size() <= size_t(kArgNeedle) &&
-                    fast_stage <= kFastStageWords;
+                    (fast_stage <= kFastStageWords || narrow);
   // workgroups: about one resident wave of them (occupancy x CUs), each owning a
   // contiguous tile range of one block
   const ScanFn scan_fn = fast ? nullptr : pick_scan(q.nterms, has_dur, q.has_range, all_w1);
@@ -1423,7 +1541,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // workgroups [value bits | stage]; the launch takes the larger
   // self-match: every block's dictionaries for this query fit one workgroup's LDS
   // stage, so no dictionary workgroups and no cross-workgroup wait
-  const bool self_dict = fast && !dc.self_off && q.nterms > 0 && fast_self <= kSelfWords;
+  const bool self_dict = fast && !narrow && !dc.self_off && q.nterms > 0 && fast_self <= kSelfWords;
   const uint32_t fast_bm_words =
       uint32_t(align_up(std::max(all_w1 ? fast_bm8 : fast_bm, self_dict ? 0u : fast_vbits), 2));
   const uint32_t fast_mask_words =
@@ -1441,7 +1559,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // when another retires starts a full scan slice late and the in-order look-back
   // waits for it. The one-launch grid also holds the dictionary workgroups.
   const uint32_t slots = uint32_t(dc.num_cu) * uint32_t(dc.per_cu_override ? dc.per_cu_override : per_cu);
-  const uint32_t njobs_fast = fast && !self_dict ? nsegs * q.nterms : 0;
+  const uint32_t njobs_fast = fast && !self_dict && !narrow ? nsegs * q.nterms : 0;
   const uint32_t target_wg = slots > njobs_fast + uint32_t(dc.num_cu) ? slots - njobs_fast : uint32_t(dc.num_cu);
   // workgroups per block in proportion to its units, the units of a block split
   // evenly over its workgroups: every CU gets the same load (+-1 unit of 1024 entries)
@@ -1535,6 +1653,22 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       for (int t = 0; t < kArgTerms; t++) A.key_of[i][t] = seg_keys[i][size_t(t)];
     }
     A.first_wg[nsegs] = nwg;
+    A.narrow = narrow ? 1u : 0u;
+    if (narrow) {
+      for (uint32_t i = 0; i < nsegs; i++) {
+        A.scan[i] = nsegv[i].scan;
+        A.ncol[i] = nsegv[i].ncol;
+        A.npad[i] = nsegv[i].npad;
+        A.nent[i] = uint32_t(segs[i].n);
+        for (uint32_t t = 0; t < q.nterms; t++) {
+          A.slot[i][t] = nsegv[i].slot[t];
+          A.nsets8[i][t] = nsegv[i].nsets[t];
+          A.bmi[i][t] = nbmi[i][t];
+        }
+      }
+      for (size_t j = 0; j < nbms.size(); j++)
+        for (int w = 0; w < 8; w++) A.bms[j][w] = nbms[j][size_t(w)];
+    }
     for (uint32_t t = 0; t <= q.nterms; t++) A.nd_off[t] = uint16_t(t < q.nterms ? needle_off[t] : needles.size());
     if (!needles.empty()) std::memcpy(A.needles, needles.data(), needles.size());
     A.nsegs = nsegs;

@@ -105,6 +105,12 @@ class _LookupOpts(C.Structure):
                 ("block_start", C.c_char_p), ("block_end", C.c_char_p)]
 
 
+class _FindResult(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("id_idx", C.POINTER(C.c_uint32)), ("block_idx", C.POINTER(C.c_uint32)),
+                ("status", C.POINTER(C.c_int32)), ("obj_off", C.POINTER(C.c_uint64)),
+                ("obj_len", C.POINTER(C.c_uint32)), ("obj_bytes", C.POINTER(C.c_uint8)), ("kernel_ns", C.c_uint64)]
+
+
 class _LookupResult(C.Structure):
     _fields_ = [("n", C.c_uint64), ("id_idx", C.POINTER(C.c_uint32)), ("block_idx", C.POINTER(C.c_uint32)),
                 ("record_idx", C.POINTER(C.c_int32)), ("record_start", C.POINTER(C.c_uint64)),
@@ -117,7 +123,8 @@ EXPORTED = [
     "tsg_pipeline_new", "tsg_pipeline_query", "tsg_pipeline_free", "tsg_pipeline_matches_header",
     "tsg_block_open", "tsg_block_open_mem", "tsg_block_clone", "tsg_wal_block_open", "tsg_wal_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
     "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_kernel_times", "tsg_results_combine",
-    "tsg_v2block_open", "tsg_v2block_close", "tsg_lookup_ids", "tsg_lookup_result_free",
+    "tsg_v2block_open", "tsg_v2block_close", "tsg_lookup_ids", "tsg_lookup_result_free", "tsg_find_ids",
+    "tsg_find_result_free",
     "tsg_write_search_block", "tsg_write_wal_search", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
     "tsg_synth_v2_block",
 ]
@@ -165,6 +172,9 @@ def lib():
         L.tsg_lookup_ids.argtypes = [vp, C.POINTER(vp), C.c_size_t, vp, C.c_size_t, C.POINTER(_LookupOpts),
                                      C.POINTER(C.POINTER(_LookupResult))]
         L.tsg_lookup_result_free.argtypes = [C.POINTER(_LookupResult)]
+        L.tsg_find_ids.argtypes = [vp, C.POINTER(vp), C.c_size_t, vp, C.c_size_t, C.POINTER(_LookupOpts),
+                                   C.POINTER(C.POINTER(_FindResult))]
+        L.tsg_find_result_free.argtypes = [C.POINTER(_FindResult)]
         L.tsg_write_search_block.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int, C.c_uint32]
         L.tsg_fb_search_entry.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]
         L.tsg_fb_search_header.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]
@@ -435,6 +445,30 @@ class Engine:
             return np.stack(cols, axis=1), r.kernel_ns
         finally:
             lib().tsg_lookup_result_free(rp)
+
+    def find(self, blocks: Sequence["V2Block"], ids, time_start=0, time_end=0, block_start=None, block_end=None):
+        """tempodb.Find's per-block step on the device (tsg_find_ids): for every lookup hit
+        (id_idx, block_idx) the findOne outcome: (id_idx, block_idx, status, object bytes or
+        None). status TSG_OK = found, TSG_E_NOT_FOUND = bloom false positive."""
+        import numpy as np
+        ids = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1, 16)
+        arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+        o = _LookupOpts(time_start, time_end, block_start, block_end)
+        rp = C.POINTER(_FindResult)()
+        _check(lib().tsg_find_ids(self.h, arr, len(blocks), ids.ctypes.data, ids.shape[0], C.byref(o), C.byref(rp)))
+        try:
+            r = rp.contents
+            n = r.n
+            total = sum(r.obj_len[i] for i in range(n)) if n else 0
+            blob = C.string_at(r.obj_bytes, total) if total else b""
+            out = []
+            for i in range(n):
+                st = r.status[i]
+                obj = blob[r.obj_off[i]:r.obj_off[i] + r.obj_len[i]] if st == TSG_OK else None
+                out.append((r.id_idx[i], r.block_idx[i], st, obj))
+            return out, r.kernel_ns
+        finally:
+            lib().tsg_find_result_free(rp)
 
     def close(self):
         self._raw_calls = {}

@@ -16,8 +16,12 @@ if has test; then
   rc=$?; echo "pytest gpu (TSG_NO_FAST) rc=$rc"; tail -5 gpurun_out/pytest_gpu_nofast.log
   ok_rc $rc || exit $rc
   # the one-launch path with dictionary workgroups (granule hand-off) instead of per-workgroup matching
-  TSG_NO_SELF_DICT=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_noself.log 2>&1
+  TSG_NO_NARROW=1 TSG_NO_SELF_DICT=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_noself.log 2>&1
   rc=$?; echo "pytest gpu (TSG_NO_SELF_DICT) rc=$rc"; tail -5 gpurun_out/pytest_gpu_noself.log
+  ok_rc $rc || exit $rc
+  # the one-launch path without host-matched narrow dictionaries (self-matching workgroups)
+  TSG_NO_NARROW=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py tests/test_gpu_wal.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_nonarrow.log 2>&1
+  rc=$?; echo "pytest gpu (TSG_NO_NARROW) rc=$rc"; tail -5 gpurun_out/pytest_gpu_nonarrow.log
   ok_rc $rc || exit $rc
   # one descriptor-path launch for blocks beyond 32 (no chunking)
   TSG_CHUNK_BLOCKS=0 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider -k "many_blocks or cancel or limit" > gpurun_out/pytest_gpu_nochunk.log 2>&1
