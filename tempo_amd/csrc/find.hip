@@ -18,8 +18,8 @@
 // one wave per page walks the objects through 64 KiB LDS windows and the lanes compare
 // each object id against the page's pending ids (first exact match, as findOne);
 // (5) the found objects are gathered into one arena for the copy back.
-// Encodings: none and snappy; zstd / lz4 / gzip / s2 report TSG_E_UNSUPPORTED_ENCODING
-// per hit (the caller's CPU path takes those blocks).
+// Encodings: none, snappy and zstd (zstd_dev.hpp: one lane per page); lz4 / gzip / s2
+// report TSG_E_UNSUPPORTED_ENCODING per hit (the caller's CPU path takes those blocks).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,6 +27,7 @@
 #include <numeric>
 
 #include "devctx.hpp"
+#include "zstd_dev.hpp"
 
 namespace tsg {
 
@@ -63,6 +64,12 @@ extern "C" __global__ void __launch_bounds__(256) find_size_kernel(FindPage *pag
   if (P.enc == 0) {  // EncNone
     P.out_len = n;
     P.status = TSG_OK;
+    return;
+  }
+  if (P.enc == 7) {  // zstd: frame content sizes (or block bounds)
+    uint64_t sz = 0;
+    P.status = zdev::zstd_size(b, n, sz);
+    P.out_len = P.status == TSG_OK ? uint32_t(sz) : 0;
     return;
   }
   if (P.enc != 6) {
@@ -148,7 +155,7 @@ extern "C" __global__ void __launch_bounds__(kFindThreads) find_decode_kernel(Fi
   __shared__ uint32_t lane_crc[kFindThreads];
   const int lane = threadIdx.x;
   FindPage &P = pages[blockIdx.x];
-  if (P.status != TSG_OK) return;
+  if (P.status != TSG_OK || P.enc == 7) return;  // (zstd pages: find_decode_zstd_kernel)
   for (int i = lane; i < 256; i += kFindThreads) tab[i] = crc->table[i];
   const uint8_t *b = P.src + 6;
   const uint32_t n = P.len - 6;
@@ -274,6 +281,17 @@ extern "C" __global__ void __launch_bounds__(kFindThreads) find_decode_kernel(Fi
     __syncthreads();
   }
   if (lane == 0 && (status != TSG_OK || pos != P.out_len)) P.status = status != TSG_OK ? status : TSG_E_CORRUPT;
+}
+
+// (3') zstd pages: one lane decodes the page (tables and literals in LDS)
+extern "C" __global__ void __launch_bounds__(64) find_decode_zstd_kernel(FindPage *pages, uint8_t *arena) {
+  __shared__ zdev::Work W;
+  FindPage &P = pages[blockIdx.x];
+  if (P.status != TSG_OK || P.enc != 7 || threadIdx.x != 0) return;
+  uint64_t len = 0;
+  const int st = zdev::zstd_decode(P.src + 6, P.len - 6, arena + P.out_off, P.out_len, len, W);
+  if (st != TSG_OK) P.status = st;
+  else P.out_len = uint32_t(len);  // (the size pass may hold an upper bound)
 }
 
 // (4) the page's objects against its pending ids (hit_ids[hit0 .. hit0 + nhit), 16 bytes
@@ -478,6 +496,12 @@ void device_find(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>
   find_decode_kernel<<<np, kFindThreads, 0, s>>>(static_cast<FindPage *>(dpages.p), static_cast<uint8_t *>(darena.p),
                                                static_cast<const CrcArgs *>(dc.fcrc.p));
   HIP_OK(hipGetLastError());
+  bool any_zstd = false;
+  for (auto &pg : pages) any_zstd = any_zstd || (pg.enc == 7 && pg.status == TSG_OK);
+  if (any_zstd) {
+    find_decode_zstd_kernel<<<np, 64, 0, s>>>(static_cast<FindPage *>(dpages.p), static_cast<uint8_t *>(darena.p));
+    HIP_OK(hipGetLastError());
+  }
   // (4) objects
   dhid.ensure(hid.size());
   HIP_OK(hipMemcpyAsync(dhid.p, hid.data(), hid.size(), hipMemcpyHostToDevice, s));

@@ -134,3 +134,46 @@ def test_find_synthetic_blocks(engine, tmp_path):
     rng.shuffle(ids)
     got = check_find(engine, paths, ids)
     assert sum(g[2] == T.TSG_OK for g in got) >= 1200
+
+
+def _py_find_pages(data_path):
+    """Every object of a zstd v2 data file, decoded with libzstd (pyarrow): {id: object}
+    (first occurrence per id, as findOne's linear scan returns)."""
+    import struct
+    pa = pytest.importorskip("pyarrow")
+    from tests.test_zstd_host import fcs, pages_of
+    codec = pa.Codec("zstd")
+    objs = {}
+    for f in pages_of(open(data_path, "rb").read()):
+        page = bytes(codec.decompress(f, decompressed_size=fcs(f)))
+        o = 0
+        while o + 8 <= len(page):
+            total, il = struct.unpack_from("<II", page, o)
+            oid, obj = page[o + 8:o + 8 + il], page[o + 8 + il:o + total]
+            objs.setdefault(oid, obj)
+            o += total
+    return objs
+
+
+def test_find_zstd_reference_block(engine):
+    """The reference's zstd v2 block (cmd/tempo-cli/test-data: 611 pages, 621 objects,
+    64-bit ids zero-padded to 16 bytes): every object comes back byte-exact through the
+    device zstd decoder; absent ids find nothing."""
+    path = os.path.join(GOLD, "tempo_cli")
+    objs = _py_find_pages(os.path.join(path, "data"))
+    assert len(objs) >= 611
+    ids = np.array([list(k) for k in objs if len(k) == 16], dtype=np.uint8)
+    rng = np.random.default_rng(4)
+    absent = rng.integers(0, 256, size=(500, 16), dtype=np.uint8)
+    absent[:, :8] = 0  # same 64-bit-id shape: passes the block's id range more often
+    allids = np.concatenate([ids, absent])
+    blk = engine.open_v2block(path)
+    try:
+        got, _ = engine.find([blk], allids)
+    finally:
+        blk.close()
+    found = {i: obj for i, b, st, obj in got if st == T.TSG_OK}
+    for i in range(len(ids)):
+        assert found.get(i) == objs[bytes(ids[i])], i
+    assert all(i < len(ids) for i in found)
+    assert all(st in (T.TSG_OK, T.TSG_E_NOT_FOUND) for _, _, st, _ in got)
