@@ -85,6 +85,26 @@ def node_cpus(node):
     return out
 
 
+def idlest(cpus, k, window=0.3):
+    """The k CPUs of `cpus` with the most idle time over `window` seconds (/proc/stat):
+    the GPU box shares its host with other jobs, and a search thread that lands on a
+    busy core loses tens of microseconds per step to preemption."""
+    def snap():
+        out = {}
+        try:
+            for line in open("/proc/stat"):
+                if line.startswith("cpu") and line[3:4].isdigit():
+                    f = line.split()
+                    out[int(f[0][3:])] = int(f[4]) + int(f[5])  # idle + iowait
+        except OSError:
+            pass
+        return out
+    a = snap()
+    time.sleep(window)
+    b = snap()
+    return sorted(sorted(cpus, key=lambda c: -(b.get(c, 0) - a.get(c, 0)))[:k])
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -277,8 +297,11 @@ def main():
         node = eng.numa_node(0)
         cpus = sorted(node_cpus(node) & os.sched_getaffinity(0)) if node >= 0 else []
         if cpus:
-            k = (local * 8) % len(cpus)
-            mine = set(cpus[k:k + 8]) or set(cpus[:8])
+            # a slice of the node per local rank, then its 8 idlest CPUs
+            lws = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+            per = max(8, len(cpus) // max(1, lws))
+            k = (local * per) % len(cpus)
+            mine = set(idlest(cpus[k:k + per] or cpus, 8))
             os.sched_setaffinity(0, mine)
         log(f"rank {rank}: GPU NUMA node {node}, search thread on CPUs {sorted(mine)}" if cpus else
             f"rank {rank}: GPU NUMA node unknown, not pinned")

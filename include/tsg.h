@@ -267,6 +267,8 @@ typedef struct tsg_lookup_opts {
 
 /* One hit per (id, block) pair where includeBlock passes, bloom.Test is true
  * and the index lower_bound is < TotalRecords, sorted by (id_idx, block_idx).
+ * Blocks may live on different devices: every device probes all ids against its own
+ * blocks concurrently (tempodb.Find's per-block fan-out) and the lists are merged.
  * Exactly the (record, i) pairs the reference hands to findOne
  * (tempodb/encoding/v2/finder_paged.go:37-48); bloom false positives included. */
 typedef struct tsg_lookup_result {

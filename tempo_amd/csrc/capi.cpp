@@ -740,16 +740,85 @@ void tsg_v2block_close(tsg_v2block *b) {
   v2block_free(b->b);
   delete b;
 }
+// Blocks on several devices: each device probes every id against its own blocks (the
+// block fan-out of tempodb.Find, tempodb/tempodb.go:335-350), concurrently, and the
+// per-device hit lists (each sorted by (id, block)) are merged into one (id, block) order.
+extern "C++" {
+template <class Out, class Run>
+static void per_device_merge(tsg_v2block *const *blocks, size_t nblocks, Out &out, Run &&run,
+                             void (*append)(Out &, const Out &, size_t)) {
+  std::vector<DeviceCtx *> order;
+  std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, V2Block *>>> per_dev;
+  for (size_t i = 0; i < nblocks; i++) {
+    DeviceCtx *dc = blocks[i]->b.dc;
+    if (!per_dev.count(dc)) order.push_back(dc);
+    per_dev[dc].push_back({uint32_t(i), &blocks[i]->b});
+  }
+  if (order.size() <= 1) {
+    if (!order.empty()) run(*order[0], per_dev[order[0]], out);
+    return;
+  }
+  std::vector<Out> parts(order.size());
+  std::vector<std::exception_ptr> errs(order.size());
+  std::vector<std::thread> th;
+  for (size_t d = 0; d < order.size(); d++)
+    th.emplace_back([&, d] {
+      try {
+        run(*order[d], per_dev[order[d]], parts[d]);
+      } catch (...) {
+        errs[d] = std::current_exception();
+      }
+    });
+  for (auto &t : th) t.join();
+  for (auto &e : errs)
+    if (e) std::rethrow_exception(e);
+  // k-way merge by (id_idx, block_idx)
+  std::vector<size_t> pos(parts.size(), 0);
+  out = Out();
+  out.kernel_ns = 0;
+  for (auto &p : parts) out.kernel_ns = std::max(out.kernel_ns, p.kernel_ns);
+  for (;;) {
+    size_t best = parts.size();
+    for (size_t d = 0; d < parts.size(); d++) {
+      if (pos[d] >= parts[d].id_idx.size()) continue;
+      if (best == parts.size() ||
+          std::make_pair(parts[d].id_idx[pos[d]], parts[d].block_idx[pos[d]]) <
+              std::make_pair(parts[best].id_idx[pos[best]], parts[best].block_idx[pos[best]]))
+        best = d;
+    }
+    if (best == parts.size()) break;
+    append(out, parts[best], pos[best]++);
+  }
+}
+static void lk_append(LookupOut &o, const LookupOut &p, size_t i) {
+  o.id_idx.push_back(p.id_idx[i]);
+  o.block_idx.push_back(p.block_idx[i]);
+  o.rec.push_back(p.rec[i]);
+  o.start.push_back(p.start[i]);
+  o.len.push_back(p.len[i]);
+}
+static void find_append(FindOut &o, const FindOut &p, size_t i) {
+  o.id_idx.push_back(p.id_idx[i]);
+  o.block_idx.push_back(p.block_idx[i]);
+  o.status.push_back(p.status[i]);
+  o.obj_off.push_back(o.bytes.size());
+  o.obj_len.push_back(p.obj_len[i]);
+  if (p.status[i] == TSG_OK)
+    o.bytes.insert(o.bytes.end(), p.bytes.begin() + long(p.obj_off[i]), p.bytes.begin() + long(p.obj_off[i] + p.obj_len[i]));
+}
+}  // extern "C++"
+
 int tsg_lookup_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, const uint8_t (*ids)[16], size_t nids,
                    const tsg_lookup_opts *opts, tsg_lookup_result **out) {
   if (!ctx || !out || (nblocks && !blocks) || (nids && !ids)) return TSG_E_INVALID;
   return guard([&] {
     auto *h = new LookupHolder();
     std::unique_ptr<LookupHolder> g(h);
-    std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, V2Block *>>> per_dev;
-    for (size_t i = 0; i < nblocks; i++) per_dev[blocks[i]->b.dc].push_back({uint32_t(i), &blocks[i]->b});
-    if (per_dev.size() > 1) fail(TSG_E_INVALID, "tsg_lookup_ids: blocks must share one device (shard ids instead)");
-    if (!per_dev.empty()) device_lookup(*per_dev.begin()->first, per_dev.begin()->second, ids, nids, opts, h->o);
+    per_device_merge(blocks, nblocks, h->o,
+                     [&](DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>> &list, LookupOut &o) {
+                       device_lookup(dc, list, ids, nids, opts, o);
+                     },
+                     lk_append);
     h->pub.n = h->o.id_idx.size();
     h->pub.id_idx = h->o.id_idx.data();
     h->pub.block_idx = h->o.block_idx.data();
@@ -768,10 +837,11 @@ int tsg_find_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, const
   return guard([&] {
     auto *h = new FindHolder();
     std::unique_ptr<FindHolder> g(h);
-    std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, V2Block *>>> per_dev;
-    for (size_t i = 0; i < nblocks; i++) per_dev[blocks[i]->b.dc].push_back({uint32_t(i), &blocks[i]->b});
-    if (per_dev.size() > 1) fail(TSG_E_INVALID, "tsg_find_ids: blocks must share one device (shard ids instead)");
-    if (!per_dev.empty()) device_find(*per_dev.begin()->first, per_dev.begin()->second, ids, nids, opts, h->o);
+    per_device_merge(blocks, nblocks, h->o,
+                     [&](DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>> &list, FindOut &o) {
+                       device_find(dc, list, ids, nids, opts, o);
+                     },
+                     find_append);
     h->pub.n = h->o.id_idx.size();
     h->pub.id_idx = h->o.id_idx.data();
     h->pub.block_idx = h->o.block_idx.data();

@@ -52,7 +52,7 @@ void ctx_shutdown(Ctx &c) {
     (void)hipStreamSynchronize(dc->stream);
     for (DevBuf *b : {&dc->desc, &dc->vmatch, &dc->bitmaps, &dc->gran, &dc->ticket, &dc->out, &dc->regions,
                       &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps, &dc->gbm, &dc->lkhits,
-                      &dc->done, &dc->fpages, &dc->fhits, &dc->fres, &dc->farena, &dc->fcrc, &dc->fdst, &dc->foff})
+                      &dc->done, &dc->steal, &dc->fpages, &dc->fhits, &dc->fres, &dc->farena, &dc->fcrc, &dc->fdst, &dc->foff})
       b->release();
     for (hipEvent_t e : dc->tring) (void)hipEventDestroy(e);
     dc->hdesc.release();

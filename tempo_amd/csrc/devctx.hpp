@@ -94,6 +94,12 @@ struct DeviceCtx {
   // in done_base
   DevBuf done;
   uint32_t done_base[9] = {};
+  // segment-mode work stealing: per block slot claim counters (128 B apart), monotonic;
+  // steal_base mirrors each one's value at the next launch. Opt-in (TSG_STEAL=1): on
+  // MI355X the static split's kernel p50 was equal or better (profiles/r02_steal)
+  DevBuf steal;
+  uint32_t steal_base[32] = {};
+  bool steal_off = std::getenv("TSG_STEAL") == nullptr;
   uint32_t seg_cap = 16;                                  // segment-mode records per workgroup (limit 0), adaptive
   bool seg_off = std::getenv("TSG_NO_SEG") != nullptr;    // one-launch path: always look-back mode
   // TSG_PER_CU=k (1..16): scan workgroups per CU in the grid plan instead of the

@@ -59,10 +59,11 @@ struct ScanSeg {
   const uint64_t *start_ns, *end_ns;
   const uint32_t *names;
   const uint8_t *id_len;
-  uint32_t pad1, nunits;        // scan units (kUnit entries) in the block
+  uint32_t tail, nunits;        // scan units (kUnit entries) in the block; the last `tail` tiles of
+                                // them are claimed dynamically (segment mode: work stealing)
   uint32_t first_wg, nwg, tpw;  // workgroups owning this block (units split evenly), max tiles per workgroup
   uint32_t term0, nterms, lds_words;
-  uint32_t block_idx, pad;
+  uint32_t block_idx, steal_base;  // claim counter value at launch start (tail tiles)
   uint64_t cap;  // limit mode: records kept from this block
 };
 struct MatchRec {  // == SearchOut::Rec
@@ -103,6 +104,7 @@ struct ScanParams {
   unsigned long long *ticket;
   unsigned long long ticket_base;
   uint32_t use_ticket, pad3;
+  unsigned *steal;  // tail claim counters, one per block slot (128 B apart), monotonic
 };
 
 constexpr int kThreads = 256;
@@ -412,8 +414,8 @@ __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsig
 // The launch-order index of this workgroup: blockIdx.x, or with use_ticket a ticket
 // claimed from one device counter, so that every workgroup this one waits for (a lower
 // index) is already running whatever order the dispatcher chose.
-__device__ __forceinline__ uint32_t wg_order(const ScanParams &P) {
-  if (!P.use_ticket) return blockIdx.x;
+__device__ __forceinline__ uint32_t wg_order(const ScanParams &P, bool use_ticket) {
+  if (!use_ticket) return blockIdx.x;
   __shared__ uint32_t s_ticket;
   if (threadIdx.x == 0)
     s_ticket = uint32_t(__hip_atomic_fetch_add(P.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
@@ -550,9 +552,10 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
   if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * kStampSlots] = t_start;
 
   // ---- phase 1: scan, one tile of loads in flight ahead of the tile evaluated
-  const uint32_t lw = wg - S.first_wg;  // units split evenly over the block's workgroups (+-1 unit)
-  const uint32_t u0 = uint32_t(uint64_t(lw) * S.nunits / S.nwg);
-  const uint32_t u1 = uint32_t(uint64_t(lw + 1) * S.nunits / S.nwg);
+  const uint32_t lw = wg - S.first_wg;  // static units split evenly over the block's workgroups (+-1 unit)
+  const uint32_t us = S.nunits - min(S.nunits, 2 * S.tail);  // static units: all but the tail tiles
+  const uint32_t u0 = uint32_t(uint64_t(lw) * us / S.nwg);
+  const uint32_t u1 = uint32_t(uint64_t(lw + 1) * us / S.nwg);
   const uint32_t ntl = (u1 - u0 + kSteps - 1) / kSteps;
   const uint64_t tbase = uint64_t(u0) * kUnit;
   const uint64_t lim = min(uint64_t(u1) * kUnit, S.n);
@@ -608,25 +611,63 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
     // that is no longer the sentinel it wrote before the launch as "this segment is
     // final" and pulls it into its caches while later workgroups are still scanning.
     stamp(3);
+    // records are gathered into LDS first (no gather load waits behind a host store:
+    // loads and stores share vmcnt), then copied out in one burst of write-through
+    // stores, the only host traffic the completion protocol waits for
+    const unsigned long long keep = umin64(P.seg_cap, S.cap);
+    unsigned long long run = 0;
+    auto to_lds = [&](unsigned long long slot, const unsigned long long *w) {
+#pragma unroll
+      for (int i = 0; i < 6; i++) lds_rec[slot * 6 + i] = w[i];
+    };
+    auto kept = [&](unsigned long long r) { return r < keep ? r : ~0ull; };
     if (wsum) {
-      // records are gathered into LDS first (no gather load waits behind a host store:
-      // loads and stores share vmcnt), then copied out in one burst of write-through
-      // stores, the only host traffic the completion protocol waits for
-      const unsigned long long keep = umin64(P.seg_cap, S.cap);
-      unsigned long long run = 0;
       for (uint32_t t = 0; t < ntl; t++) {
         const uint32_t tc = s_tc[t];
         if (tc == 0) continue;
         const uint32_t mask = t < kLdsTiles ? lds_mask[t * kThreads + tid]
                                             : G(P.mask)[(uint64_t(wg) * P.mask_tpw + t) * kThreads + tid];
-        emit_tile(S, mask, tbase + uint64_t(t) * kTile, run, s_wsum,
-                  [&](unsigned long long r) { return r < keep ? r : ~0ull; },
-                  [&](unsigned long long slot, const unsigned long long *w) {
-#pragma unroll
-                    for (int i = 0; i < 6; i++) lds_rec[slot * 6 + i] = w[i];
-                  });
+        emit_tile(S, mask, tbase + uint64_t(t) * kTile, run, s_wsum, kept, to_lds);
         run += tc;
       }
+    }
+    // tail: the block's last S.tail tiles, one per claim from the block's counter, by
+    // whichever of its workgroups is free first (per-CU bandwidth is uneven: the early
+    // finishers absorb the slow ones' share). The records of a workgroup stay in its own
+    // segment in claim order, after its static ones; the host orders each block's
+    // records by scan position (tail positions follow every static one).
+    if (S.tail) {
+      __shared__ uint32_t s_claim;
+      auto claim = [&]() -> uint32_t {
+        __syncthreads();
+        if (tid == 0)
+          s_claim = __hip_atomic_fetch_add(P.steal + 32 * si, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                    S.steal_base;
+        __syncthreads();
+        return s_claim;
+      };
+      uint32_t c = claim();
+      while (c < S.tail) {
+        const uint64_t t0 = uint64_t(us + 2 * c) * kUnit;
+        const uint64_t tl = min(uint64_t(us + 2 * c + 2) * kUnit, S.n);
+        load_tile<NT, DUR, RANGE, W1>(ra, S, T, t0, tl, tid);
+        const uint32_t next = claim();  // (its return waits for the tile loads anyway)
+        const uint32_t mask = eval_tile<NT, DUR, RANGE, W1>(ra, P, S, T, lds_bm, t0, tl, tid);
+        uint32_t cnt = __popc(mask);
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+        if (lane == 0) s_wcnt[0][wid] = cnt;
+        __syncthreads();
+        uint32_t tc = 0;
+#pragma unroll
+        for (int w = 0; w < kThreads / 64; w++) tc += s_wcnt[0][w];
+        if (tc) emit_tile(S, mask, t0, run, s_wsum, kept, to_lds);
+        run += tc;
+        wsum += tc;
+        c = next;
+      }
+    }
+    if (wsum) {
       __syncthreads();
       const uint32_t nw = uint32_t(umin64(wsum, keep)) * 6;
       auto *dst = reinterpret_cast<unsigned long long *>(P.out + P.hdr_bytes) + (unsigned long long)wg * P.seg_cap * 6;
@@ -731,7 +772,7 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
   uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + P.lds_bm_words);  // [kLdsTiles][kThreads]
   uint32_t *lds_seg = lds + P.lds_bm_words + kLdsTiles * kThreads / 2;      // [nsegs]
   const int tid = threadIdx.x;
-  const uint32_t vb = wg_order(P);
+  const uint32_t vb = wg_order(P, P.use_ticket);
   const uint32_t si = P.wg_seg[vb];
   const ScanSeg S = P.segs[si];
   constexpr int NTA = NT > 0 ? NT : 1;
@@ -789,6 +830,9 @@ struct QArgs {
   uint32_t npad[kArgSegs], nent[kArgSegs];
   uint8_t slot[kArgSegs][kArgTerms], bmi[kArgSegs][kArgTerms], nsets8[kArgSegs][kArgTerms];
   uint32_t bms[kArgBms][8];
+  // segment mode work stealing: tail tiles per block and its claim counter's value at launch
+  uint16_t tail[kArgSegs];
+  uint32_t steal_base[kArgSegs];
   ScanParams P;             // thresholds, outputs (segs/terms/wg_seg unused)
 };
 static_assert(sizeof(QArgs) <= 4096, "kernel arguments");
@@ -1009,10 +1053,22 @@ __device__ __forceinline__ void self_finish(SelfStage<NTA> &X, const QArgs &A, c
 
 template <int NT, bool DUR, bool RANGE, bool W1, bool SEG>
 __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
-  const unsigned long long t_start = A.P.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t vb = wg_order(A.P);  // (a ticket when dictionary or look-back waits exist)
-  if (vb < A.njobs) {  // dictionary workgroup: [value bits | stage]
+  // Every kernel argument the prologue branches on arrives in ONE round trip: scalar
+  // loads return out of order, so each s_waitcnt lgkmcnt waits for every load issued,
+  // and loads issued behind a branch would each add a round trip before the first tile
+  // load (the empty asm statements pin them all in front of the first use)
+  uint32_t use_ticket = A.P.use_ticket, njobs = A.njobs, nsegs = A.nsegs, narrow_arg = A.narrow;
+  unsigned long long *stamps = A.P.stamps;
+  uint32_t fw[kArgSegs];
+#pragma unroll
+  for (int s2 = 0; s2 < kArgSegs; s2++) fw[s2] = A.first_wg[s2];
+  asm volatile("" : "+s"(use_ticket), "+s"(njobs), "+s"(nsegs), "+s"(narrow_arg), "+s"(stamps));
+#pragma unroll
+  for (int s2 = 0; s2 < kArgSegs; s2++) asm volatile("" : "+s"(fw[s2]));
+  const uint32_t vb = wg_order(A.P, use_ticket != 0);  // (a ticket when dictionary or look-back waits exist)
+  if (vb < njobs) {  // dictionary workgroup: [value bits | stage]
     dict_job(A, vb, lds + A.bm_words, lds);
     return;
   }
@@ -1024,15 +1080,28 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   unsigned long long *lds_cap = reinterpret_cast<unsigned long long *>(lds_fw + ((A.nsegs + 2) & ~1u));
   unsigned long long *lds_rec = lds_cap + A.nsegs;  // segment mode: kSegMax staged records
   const int tid = threadIdx.x;
-  const uint32_t wg = vb - A.njobs;
-  uint32_t si = 0;  // (fixed trip count: every first_wg load issues in one round trip)
+  const uint32_t wg = vb - njobs;
+  uint32_t si = 0;
 #pragma unroll
-  for (int s2 = 1; s2 < kArgSegs; s2++) si += (uint32_t(s2) < A.nsegs && A.first_wg[s2] <= wg) ? 1u : 0u;
+  for (int s2 = 1; s2 < kArgSegs; s2++) si += (uint32_t(s2) < nsegs && fw[s2] <= wg) ? 1u : 0u;
   // wave-uniform: descriptor reads become scalar loads (one round trip, not vmcnt-serialised)
   si = __builtin_amdgcn_readfirstlane(si);
   const DevBlockDesc *B = A.blk[si];
   constexpr int NTA = NT > 0 ? NT : 1;
-  const bool narrow = A.narrow != 0;
+  const bool narrow = narrow_arg != 0;
+  // narrow mode: this block's scan arguments, again in one round trip
+  const uint32_t *n_scan = A.scan[si];
+  const uint8_t *n_col = A.ncol[si];
+  uint32_t n_npad = A.npad[si], n_ent = A.nent[si];
+  uint32_t n_slot[NTA], n_sets[NTA];
+#pragma unroll
+  for (int q = 0; q < NTA; q++) {
+    n_slot[q] = A.slot[si][q];
+    n_sets[q] = A.nsets8[si][q];
+  }
+  asm volatile("" : "+s"(n_scan), "+s"(n_col), "+s"(n_npad), "+s"(n_ent));
+#pragma unroll
+  for (int q = 0; q < NTA; q++) asm volatile("" : "+s"(n_slot[q]), "+s"(n_sets[q]));
   DevKeyDesc KD[NTA];  // scalar loads, all issued together (one-launch kernels: NT == nterms)
   if (NT > 0 && !narrow)
 #pragma unroll
@@ -1051,10 +1120,10 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
     S.id_len = Bc->id_len;
   };
   if (narrow) {
-    S.n = A.nent[si];
-    S.dur32 = A.scan[si];
-    S.start_s = A.scan[si] + A.npad[si];
-    S.end_s = A.scan[si] + 2ull * A.npad[si];
+    S.n = n_ent;
+    S.dur32 = n_scan;
+    S.start_s = n_scan + n_npad;
+    S.end_s = n_scan + 2ull * n_npad;
     S.dur64 = nullptr;  // (narrow mode: no threshold >= 2^32-1 ns)
     S.ids = nullptr;
     S.start_ns = S.end_ns = nullptr;
@@ -1070,13 +1139,15 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   }
   S.nunits = uint32_t((S.n + kUnit - 1) / kUnit);
   S.first_wg = A.first_wg[si];
-  S.nwg = A.first_wg[si + 1] - S.first_wg;
+  S.nwg = A.first_wg[si + 1] - S.first_wg;  // (first_wg[nsegs] = the grid's scan workgroups)
   S.tpw = 0;
   S.term0 = 0;
   S.nterms = A.nterms;
   S.lds_words = A.bm_words;
   S.block_idx = A.block_idx[si];
   S.cap = A.cap[si];
+  S.tail = SEG ? A.tail[si] : 0u;
+  S.steal_base = A.steal_base[si];
   ScanTerm T[NTA];
   uint32_t gw[NTA + 1];  // granule prefix over this block's terms
   gw[0] = 0;
@@ -1086,9 +1157,9 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
     if (NT <= 0) break;
     const DevKeyDesc &K = KD[q];
     if (narrow) {
-      T[q].col = A.ncol[si] + uint64_t(A.slot[si][q]) * A.npad[si];
+      T[q].col = n_col + uint64_t(n_slot[q]) * n_npad;
       T[q].width = 1;
-      T[q].nsets = A.nsets8[si][q];
+      T[q].nsets = n_sets[q];
     } else {
       T[q].col = K.col;
       T[q].width = K.width;
@@ -1104,8 +1175,8 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   // tile's loads are in flight
   SelfStage<NTA> X;
   auto issue_stage = [&] {
-    if (A.P.stamps && threadIdx.x == 0)  // (waits for the descriptor scalar loads: lgkmcnt)
-      A.P.stamps[uint64_t(wg) * kStampSlots + 5] = __builtin_amdgcn_s_memrealtime();
+    if (stamps && threadIdx.x == 0)  // (waits for the descriptor scalar loads: lgkmcnt)
+      stamps[uint64_t(wg) * kStampSlots + 5] = __builtin_amdgcn_s_memrealtime();
     if (NT > 0 && A.self_dict) {
       self_issue<NTA>(X, KD);
       // stage_first: wait for the (few, L2-shared) dictionary words before this
@@ -1114,8 +1185,8 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
       // ~10 us; alone they land in ~1-2 us and the matching then hides under the tiles.
       if (A.stage_first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (A.P.stamps && threadIdx.x == 0)
-      A.P.stamps[uint64_t(wg) * kStampSlots + 6] = __builtin_amdgcn_s_memrealtime();
+    if (stamps && threadIdx.x == 0)
+      stamps[uint64_t(wg) * kStampSlots + 6] = __builtin_amdgcn_s_memrealtime();
   };
   auto wait_bitmaps = [&] {
     if (narrow) {  // the host's bitmaps, from the kernel arguments (uniform: scalar loads)
@@ -1576,6 +1647,13 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     sg.first_wg = nwg;
     sg.nwg = uint32_t(w);
     sg.tpw = uint32_t(((sg.nunits + w - 1) / w + kSteps - 1) / kSteps);
+    // work stealing (segment mode): the block's last quarter of tiles is claimed at run time
+    // (static tiles stay >= one per workgroup)
+    {
+      const uint32_t tiles = (sg.nunits + kSteps - 1) / kSteps;
+      sg.tail = dc.steal_off ? 0u : std::min<uint32_t>(tiles / 4, tiles - uint32_t(w));
+      if (sg.tail > 0xffffu) sg.tail = 0xffffu;
+    }
     tpw = std::max(tpw, sg.tpw);
     nwg += sg.nwg;
   }
@@ -1653,6 +1731,12 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       for (int t = 0; t < kArgTerms; t++) A.key_of[i][t] = seg_keys[i][size_t(t)];
     }
     A.first_wg[nsegs] = nwg;
+    for (uint32_t i = 0; i < nsegs; i++) A.tail[i] = uint16_t(segs[i].tail);
+    if (dc.steal.ensure(kArgSegs * 128)) {  // claim counters: zeroed once, then monotonic
+      HIP_OK(hipMemsetAsync(dc.steal.p, 0, dc.steal.cap, s));
+      std::fill(std::begin(dc.steal_base), std::end(dc.steal_base), 0u);
+    }
+    P.steal = static_cast<unsigned *>(dc.steal.p);
     A.narrow = narrow ? 1u : 0u;
     if (narrow) {
       for (uint32_t i = 0; i < nsegs; i++) {
@@ -1704,6 +1788,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     dc.hdesc.ensure(total_desc);
     dc.desc.ensure(total_desc);
     auto *hd = static_cast<uint8_t *>(dc.hdesc.p);
+    for (auto &sg : segs) sg.tail = 0;  // (the descriptor path splits every tile statically)
     std::memcpy(hd + o_segs, segs.data(), segs.size() * sizeof(ScanSeg));
     std::memcpy(hd + o_terms, terms.data(), terms.size() * sizeof(ScanTerm));
     std::memcpy(hd + o_jobs, jobs.data(), jobs.size() * sizeof(DictJob));
@@ -1755,6 +1840,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     h[2] = 0;  // completion flag (one-launch path)
     if (fast && P.seg_cap) std::fill_n(P.counts, nwg, kCountPending);  // (each workgroup stores its count last)
     if (fast) {
+      for (uint32_t i = 0; i < nsegs; i++) A.steal_base[i] = dc.steal_base[i];
       uint32_t ng = 0;
       for (uint32_t g = 0; g < 8; g++) {
         P.done_target[g] = dc.done_base[g] + group_n[g];
@@ -1793,6 +1879,9 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       dc.done_base[8] = P.done_top;
     }
     if (P.use_ticket) dc.ticket_base += grid;
+    if (fast && P.seg_cap)  // every workgroup of a block with a tail ends with one failed claim
+      for (uint32_t i = 0; i < nsegs; i++)
+        if (segs[i].tail) dc.steal_base[i] += segs[i].tail + segs[i].nwg;
   };
   // segment mode: poll the completion flag the last workgroup raises in the pinned
   // header instead of waiting for the stream (the end-of-kernel signal comes later);
@@ -1908,12 +1997,23 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     out.recs.resize(upper);
     for (size_t i = 0; i < segs.size(); i++) {
       uint64_t kept = 0;
-      for (uint32_t w = segs[i].first_wg; w < segs[i].first_wg + segs[i].nwg && kept < segs[i].cap; w++) {
-        const uint64_t c = std::min<uint64_t>(std::min(cnt[w], P.seg_cap), segs[i].cap - kept);
+      const bool stole = fast && segs[i].tail;  // tail records sit in their claimers' segments
+      const size_t b0 = nrec;
+      for (uint32_t w = segs[i].first_wg; w < segs[i].first_wg + segs[i].nwg && (stole || kept < segs[i].cap); w++) {
+        const uint64_t c = stole ? std::min(cnt[w], P.seg_cap)
+                                 : std::min<uint64_t>(std::min(cnt[w], P.seg_cap), segs[i].cap - kept);
         if (!c) continue;
         std::memcpy(&out.recs[nrec], rec + uint64_t(w) * P.seg_cap * sizeof(MatchRec), c * sizeof(MatchRec));
         nrec += c;
         kept += c;
+      }
+      if (stole && nrec - b0 > 1) {  // scan order = scan position within the block; then the cap
+        std::sort(out.recs.begin() + b0, out.recs.begin() + nrec,
+                  [](const SearchOut::Rec &a, const SearchOut::Rec &b) { return a.entry < b.entry; });
+      }
+      if (stole && kept > segs[i].cap) {
+        nrec = b0 + segs[i].cap;
+        kept = segs[i].cap;
       }
       for (size_t bi = 0; bi < blocks.size(); bi++)
         if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = kept;

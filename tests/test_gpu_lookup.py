@@ -177,3 +177,33 @@ def test_find_zstd_reference_block(engine):
         assert found.get(i) == objs[bytes(ids[i])], i
     assert all(i < len(ids) for i in found)
     assert all(st in (T.TSG_OK, T.TSG_E_NOT_FOUND) for _, _, st, _ in got)
+
+
+def test_lookup_and_find_across_devices(tmp_path):
+    """Blocks spread over two device contexts (both on ordinal 0 here, so the one-GPU
+    box exercises the per-device fan-out, the concurrent probes and the (id, block)
+    merge) give the same hits and objects as the single-device call."""
+    paths, stored = [], []
+    for b in range(5):
+        p = os.path.join(str(tmp_path), "d%d" % b)
+        stored.append(T.synth_v2_block(p, 6000 + 900 * b, seed=90 + b))
+        paths.append(p)
+    rng = np.random.default_rng(11)
+    ids = np.concatenate([s[rng.integers(0, len(s), 300)] for s in stored] +
+                         [rng.integers(0, 256, size=(1000, 16), dtype=np.uint8)])
+    rng.shuffle(ids)
+    eng = T.Engine(devices=[0, 0])
+    assert eng.device_count == 2
+    blocks = [eng.open_v2block(p, device=b % 2) for b, p in enumerate(paths)]
+    try:
+        got, _ = eng.lookup(blocks, ids)
+        np.testing.assert_array_equal(got, oracle_hits(paths, ids))
+        fgot, _ = eng.find(blocks, ids)
+    finally:
+        for b in blocks:
+            b.close()
+    assert [(g[0], g[1]) for g in fgot] == [(int(r[0]), int(r[1])) for r in got]
+    exp = oracle_find(paths, ids)
+    for i, b, st, obj in fgot:
+        assert obj == exp[(i, b)]
+    assert sum(g[2] == T.TSG_OK for g in fgot) >= 1500

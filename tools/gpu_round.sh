@@ -23,6 +23,10 @@ if has test; then
   TSG_NO_NARROW=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py tests/test_gpu_wal.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_nonarrow.log 2>&1
   rc=$?; echo "pytest gpu (TSG_NO_NARROW) rc=$rc"; tail -5 gpurun_out/pytest_gpu_nonarrow.log
   ok_rc $rc || exit $rc
+  # segment mode without tail work stealing (static tile split only)
+  TSG_STEAL=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_steal.log 2>&1
+  rc=$?; echo "pytest gpu (TSG_STEAL) rc=$rc"; tail -5 gpurun_out/pytest_gpu_steal.log
+  ok_rc $rc || exit $rc
   # one descriptor-path launch for blocks beyond 32 (no chunking)
   TSG_CHUNK_BLOCKS=0 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider -k "many_blocks or cancel or limit" > gpurun_out/pytest_gpu_nochunk.log 2>&1
   rc=$?; echo "pytest gpu (TSG_CHUNK_BLOCKS=0) rc=$rc"; tail -5 gpurun_out/pytest_gpu_nochunk.log
