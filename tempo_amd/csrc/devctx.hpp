@@ -77,6 +77,7 @@ struct DeviceCtx {
   // counts, [header | records] output. lookup reuses desc/gran/ticket/out/hdr/err.
   DevBuf desc, vmatch, bitmaps, gran, ticket, out, regions, seg_counts, hdr, err;
   DevBuf maskbits, agg, stamps, gbm, lkhits;
+  DevBuf lkslab, lkslabdesc;  // lookup: transposed bloom slabs + their member tables
   DevBuf fpages, fhits, fres, farena, fcrc, fdst, foff;  // device findOne (find.hip)
   HostBuf hdesc, hout;
   // search results, written by the emit kernel directly (coherent: the kernel's

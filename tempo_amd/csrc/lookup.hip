@@ -10,6 +10,15 @@
 // The id's hashes are computed once and reused across all blocks. Hits are
 // emitted sorted by (id, block) with a count pass + decoupled look-back offsets
 // and a write pass (the write pass recomputes: ALU is cheap, HBM is not).
+//
+// Bloom slabs. The k probe positions of an id depend only on (m, k) and its hashes,
+// not on the block, so blocks whose blooms share (m, k, bitlen, shards) — every
+// block a given config writes for a given object estimate — are probed together:
+// per call their blooms are transposed into one table, slab[shard][bit] = a J-bit
+// vector (bit j = block j's bloom bit). An id then costs k loads of J/8 bytes for
+// the whole slab (J <= 256 blocks: 7 x 32 B for the default k), AND-ed, instead of
+// up to k random loads per block; the surviving bits are the bloom-positive blocks.
+// 200 blocks x 1 M probes: ~0.45 GB of slab reads instead of ~19 GB of bloom reads.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,9 +42,19 @@ struct LkBlock {
   uint32_t block_idx, pad;
 };
 
+struct LkSlab {
+  const uint32_t *T;               // [shards][bitlen][W] u32
+  uint64_t m, k, bitlen, m_magic;  // shared bloom parameters of the members
+  uint32_t shards, W, J, first;    // W u32 per position; J members at slab_blk[first..]
+};
+
 struct LkParams {
   const LkBlock *blocks;
   uint32_t nblocks;
+  const LkSlab *slabs;       // slab-probed blocks
+  uint32_t nslabs, ndirect;
+  const uint32_t *slab_blk;  // member block ordinals of every slab, in block order
+  const uint32_t *direct;    // block ordinals probed one by one (ascending)
   const uint8_t *ids;
   uint64_t nids;
   unsigned long long epoch, ticket_base;
@@ -112,17 +131,10 @@ __device__ __forceinline__ int d_cmp16(const uint8_t *a, const uint8_t *b, uint3
   return 16 == bl ? 0 : (16 < bl ? -1 : 1);
 }
 
-// evaluates one (id, block): returns record index (>= 0) on a hit, -1 otherwise
-__device__ __forceinline__ int32_t d_probe(const LkBlock &B, const uint8_t *id, uint32_t fnv, const uint64_t h[4]) {
+// includeBlock's id range + index lower_bound: first record with
+// bytes.Compare(rec.ID, id) >= 0 (pkg/sort/search.go:5-24), a hit if < TotalRecords
+__device__ __forceinline__ int32_t d_post(const LkBlock &B, const uint8_t *id) {
   if (d_cmp16(id, B.min_id, B.min_len) < 0 || d_cmp16(id, B.max_id, B.max_len) > 0) return -1;
-  uint32_t shard = fnv % B.shards;
-  const uint64_t *w = B.bloom + uint64_t(shard) * B.words;
-  for (uint64_t i = 0; i < B.k; i++) {
-    uint64_t loc = d_mod(h[i % 2] + i * h[2 + (((i + (i % 2)) % 4) / 2)], B.m, B.m_magic);
-    if (loc >= B.bitlen) return -1;
-    if (!((w[loc >> 6] >> (loc & 63)) & 1ULL)) return -1;
-  }
-  // lower_bound: first record with bytes.Compare(rec.ID, id) >= 0 (pkg/sort/search.go:5-24)
   uint32_t lo = 0, hi = B.records;
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
@@ -134,6 +146,109 @@ __device__ __forceinline__ int32_t d_probe(const LkBlock &B, const uint8_t *id, 
     else hi = mid;
   }
   return lo < B.records ? int32_t(lo) : -1;
+}
+
+// evaluates one (id, block) against the block's own bloom: record index (>= 0) on a
+// hit, -1 otherwise (the range check and the bloom are both required: order is free)
+__device__ __forceinline__ int32_t d_probe(const LkBlock &B, const uint8_t *id, uint32_t fnv, const uint64_t h[4]) {
+  uint32_t shard = fnv % B.shards;
+  const uint64_t *w = B.bloom + uint64_t(shard) * B.words;
+  for (uint64_t i = 0; i < B.k; i++) {
+    uint64_t loc = d_mod(h[i % 2] + i * h[2 + (((i + (i % 2)) % 4) / 2)], B.m, B.m_magic);
+    if (loc >= B.bitlen) return -1;
+    if (!((w[loc >> 6] >> (loc & 63)) & 1ULL)) return -1;
+  }
+  return d_post(B, id);
+}
+
+// Calls f(block ordinal, record) for every hit of one id: slab members first (each
+// slab in block order), then the directly probed blocks. Not globally block-ordered
+// when several sources interleave: the write pass sorts each id's range.
+template <class F>
+__device__ __forceinline__ void for_each_hit(const LkParams &P, const uint8_t *id, uint32_t fnv, const uint64_t h[4], F &&f) {
+  for (uint32_t si = 0; si < P.nslabs; si++) {
+    const LkSlab &S = P.slabs[si];
+    const uint32_t W = S.W;
+    const uint32_t *base = S.T + uint64_t(fnv % S.shards) * S.bitlen * W;
+    uint32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++)  // (columns past J are zero in the table too)
+      v[q] = uint32_t(q) * 32 >= S.J ? 0u : uint32_t(q + 1) * 32 <= S.J ? ~0u : (1u << (S.J % 32)) - 1u;
+    // (probes stay a chain with an early exit: issuing all k loads up front needs ~130
+    // VGPRs, and at 3 waves/SIMD the count pass measured 2.35 ms vs 1.74 ms, config 5)
+    for (uint64_t i = 0; i < S.k; i++) {
+      uint64_t loc = d_mod(h[i % 2] + i * h[2 + (((i + (i % 2)) % 4) / 2)], S.m, S.m_magic);
+      if (loc >= S.bitlen) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[q] = 0;
+        break;
+      }
+      const uint32_t *p = base + loc * W;
+      if (W == 8) {
+        uint4 a = *reinterpret_cast<const uint4 *>(p), b = *reinterpret_cast<const uint4 *>(p + 4);
+        v[0] &= a.x; v[1] &= a.y; v[2] &= a.z; v[3] &= a.w;
+        v[4] &= b.x; v[5] &= b.y; v[6] &= b.z; v[7] &= b.w;
+      } else if (W == 4) {
+        uint4 a = *reinterpret_cast<const uint4 *>(p);
+        v[0] &= a.x; v[1] &= a.y; v[2] &= a.z; v[3] &= a.w;
+      } else if (W == 2) {
+        uint2 a = *reinterpret_cast<const uint2 *>(p);
+        v[0] &= a.x; v[1] &= a.y;
+      } else {
+        v[0] &= p[0];
+      }
+      uint32_t any = 0;
+#pragma unroll
+      for (int q = 0; q < 8; q++) any |= v[q];
+      if (!any) break;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      uint32_t x = v[q];
+      while (x) {
+        const uint32_t j = uint32_t(q) * 32 + uint32_t(__builtin_ctz(x));
+        x &= x - 1;
+        const uint32_t b = P.slab_blk[S.first + j];
+        const int32_t r = d_post(P.blocks[b], id);
+        if (r >= 0) f(b, r);
+      }
+    }
+  }
+  for (uint32_t di = 0; di < P.ndirect; di++) {
+    const uint32_t b = P.direct[di];
+    const int32_t r = d_probe(P.blocks[b], id, fnv, h);
+    if (r >= 0) f(b, r);
+  }
+}
+
+// slab[s][pos][jc] bit j = bloom bit pos of shard s of member jc*32+j. One thread per
+// (shard, 64-bit word, 32-member column): 32 words in registers, 64 positions out.
+struct TrParams {
+  const uint64_t *const *bloom;  // member bloom words (shards x words), J entries
+  uint32_t *T;
+  uint64_t words, bitlen;
+  uint32_t shards, W, J;
+};
+extern "C" __global__ void __launch_bounds__(256) lookup_transpose_kernel(TrParams P) {
+  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint32_t jc = uint32_t(g % P.W);
+  const uint64_t rest = g / P.W;
+  const uint64_t w = rest % P.words, s = rest / P.words;
+  if (s >= P.shards) return;
+  uint64_t x[32];
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const uint32_t mj = jc * 32 + uint32_t(j);
+    x[j] = mj < P.J ? P.bloom[mj][s * P.words + w] : 0ULL;
+  }
+  uint32_t *out = P.T + (s * P.bitlen + w * 64) * P.W + jc;
+  const uint32_t nq = uint32_t(min<uint64_t>(64, P.bitlen - w * 64));
+  for (uint32_t q = 0; q < nq; q++) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < 32; j++) o |= uint32_t((x[j] >> q) & 1ULL) << j;
+    out[uint64_t(q) * P.W] = o;
+  }
 }
 
 constexpr int kLkThreads = 256;
@@ -165,15 +280,13 @@ extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_count_kernel(LkP
     uint32_t fnv;
     uint64_t h[4];
     d_id_hash(id, fnv, h);
-    for (uint32_t b = 0; b < P.nblocks; b++) {
-      const int32_t r = d_probe(P.blocks[b], id, fnv, h);
-      if (r < 0) continue;
+    for_each_hit(P, id, fnv, h, [&](uint32_t b, int32_t r) {
       if (cnt < kHitK) {
         P.hit_b[i * kHitK + cnt] = b;
         P.hit_r[i * kHitK + cnt] = r;
       }
       cnt++;
-    }
+    });
     P.hit_cnt[i] = cnt;
   }
   // block scan of counts
@@ -243,16 +356,26 @@ extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_write_kernel(LkP
   const uint64_t i = uint64_t(blockIdx.x) * kLkThreads + threadIdx.x;
   if (i >= P.nids) return;
   const uint32_t cnt = P.hit_cnt[i];
-  if (cnt <= kHitK) {  // every hit was kept by the count pass, in block order
-    uint64_t o = P.offsets[i];
-    for (uint32_t j = 0; j < cnt; j++, o++) {
-      const LkBlock &B = P.blocks[P.hit_b[i * kHitK + j]];
-      const int32_t r = P.hit_r[i * kHitK + j];
-      P.o_id[o] = uint32_t(i);
-      P.o_block[o] = B.block_idx;
-      P.o_rec[o] = r;
-      P.o_start[o] = B.rec_start[r];
-      P.o_len[o] = B.rec_len[r];
+  const uint64_t o0 = P.offsets[i];
+  if (cnt <= kHitK) {  // every hit was kept by the count pass: sort by block, copy
+    uint32_t hb[kHitK];
+    int32_t hr[kHitK];
+    for (uint32_t j = 0; j < cnt; j++) {
+      hb[j] = P.hit_b[i * kHitK + j];
+      hr[j] = P.hit_r[i * kHitK + j];
+      for (uint32_t q = j; q > 0 && hb[q - 1] > hb[q]; q--) {
+        uint32_t tb = hb[q]; hb[q] = hb[q - 1]; hb[q - 1] = tb;
+        int32_t tr = hr[q]; hr[q] = hr[q - 1]; hr[q - 1] = tr;
+      }
+    }
+    for (uint32_t j = 0; j < cnt; j++) {
+      const LkBlock &B = P.blocks[hb[j]];
+      const int32_t r = hr[j];
+      P.o_id[o0 + j] = uint32_t(i);
+      P.o_block[o0 + j] = B.block_idx;
+      P.o_rec[o0 + j] = r;
+      P.o_start[o0 + j] = B.rec_start[r];
+      P.o_len[o0 + j] = B.rec_len[r];
     }
     return;
   }
@@ -261,17 +384,33 @@ extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_write_kernel(LkP
   uint32_t fnv;
   uint64_t h[4];
   d_id_hash(id, fnv, h);
-  uint64_t o = P.offsets[i];
-  for (uint32_t b = 0; b < P.nblocks; b++) {
+  uint64_t o = o0;
+  for_each_hit(P, id, fnv, h, [&](uint32_t b, int32_t r) {
     const LkBlock &B = P.blocks[b];
-    int32_t r = d_probe(B, id, fnv, h);
-    if (r < 0) continue;
     P.o_id[o] = uint32_t(i);
     P.o_block[o] = B.block_idx;
     P.o_rec[o] = r;
     P.o_start[o] = B.rec_start[r];
     P.o_len[o] = B.rec_len[r];
     o++;
+  });
+  // sources interleave in block order: insertion sort of this id's range by block
+  for (uint64_t a = o0 + 1; a < o; a++) {
+    const uint32_t kb = P.o_block[a];
+    const int32_t kr = P.o_rec[a];
+    const uint64_t ks = P.o_start[a];
+    const uint32_t kl = P.o_len[a];
+    uint64_t q = a;
+    for (; q > o0 && P.o_block[q - 1] > kb; q--) {
+      P.o_block[q] = P.o_block[q - 1];
+      P.o_rec[q] = P.o_rec[q - 1];
+      P.o_start[q] = P.o_start[q - 1];
+      P.o_len[q] = P.o_len[q - 1];
+    }
+    P.o_block[q] = kb;
+    P.o_rec[q] = kr;
+    P.o_start[q] = ks;
+    P.o_len[q] = kl;
   }
 }
 
@@ -463,12 +602,83 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
   out = LookupOut();
   if (nids == 0 || lb.empty()) return;
   uint32_t tiles = uint32_t((nids + kLkThreads - 1) / kLkThreads);
-  size_t desc_bytes = (lb.size() * sizeof(LkBlock) + 15) & ~size_t(15);
+
+  // ---- slabs: blocks with identical bloom parameters, up to 256 per slab, when the
+  // probes they save outweigh building the table (TSG_LK_SLAB=0/1 forces it off/on)
+  const char *slab_env = std::getenv("TSG_LK_SLAB");
+  const int slab_mode = slab_env ? std::atoi(slab_env) : -1;
+  std::vector<LkSlab> slabs;
+  std::vector<uint32_t> slab_blk, direct;
+  std::vector<std::vector<uint32_t>> members;  // per slab: lb ordinals
+  {
+    std::vector<bool> used(lb.size(), false);
+    for (size_t a = 0; a < lb.size(); a++) {
+      if (used[a]) continue;
+      std::vector<uint32_t> grp;
+      for (size_t b = a; b < lb.size(); b++)
+        if (!used[b] && lb[b].m == lb[a].m && lb[b].k == lb[a].k && lb[b].bitlen == lb[a].bitlen &&
+            lb[b].shards == lb[a].shards && lb[b].words == lb[a].words) {
+          grp.push_back(uint32_t(b));
+          used[b] = true;
+        }
+      for (size_t g0 = 0; g0 < grp.size(); g0 += 256) {
+        std::vector<uint32_t> part(grp.begin() + long(g0), grp.begin() + long(std::min(grp.size(), g0 + 256)));
+        const uint64_t J = part.size();
+        const uint32_t W = J <= 32 ? 1 : J <= 64 ? 2 : J <= 128 ? 4 : 8;
+        const double table = double(lb[a].shards) * double(lb[a].bitlen) * W * 4;
+        const double blooms = double(J) * lb[a].shards * lb[a].words * 8;
+        const bool use = slab_mode == 1 ? true : slab_mode == 0 ? false
+                                                : (J >= 2 && double(nids) * double(J) * 96.0 >= 2.0 * (table + blooms));
+        if (!use) {
+          for (uint32_t b : part) direct.push_back(b);
+          continue;
+        }
+        LkSlab sl{};
+        sl.m = lb[a].m;
+        sl.k = lb[a].k;
+        sl.bitlen = lb[a].bitlen;
+        sl.m_magic = lb[a].m_magic;
+        sl.shards = lb[a].shards;
+        sl.W = W;
+        sl.J = uint32_t(J);
+        sl.first = uint32_t(slab_blk.size());
+        for (uint32_t b : part) slab_blk.push_back(b);
+        slabs.push_back(sl);
+        members.push_back(part);
+      }
+    }
+    std::sort(direct.begin(), direct.end());
+  }
+  std::vector<size_t> slab_off(slabs.size());
+  size_t slab_bytes = 0;
+  for (size_t i = 0; i < slabs.size(); i++) {
+    slab_off[i] = slab_bytes;
+    slab_bytes += (size_t(slabs[i].shards) * slabs[i].bitlen * slabs[i].W * 4 + 255) & ~size_t(255);
+  }
+  if (slab_bytes) dc.lkslab.ensure(slab_bytes);
+  for (size_t i = 0; i < slabs.size(); i++)
+    slabs[i].T = reinterpret_cast<const uint32_t *>(static_cast<uint8_t *>(dc.lkslab.p) + slab_off[i]);
+
+  // descriptor area: LkBlock[] | LkSlab[] | slab_blk[] | direct[] | member bloom ptrs | ids
+  auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
+  const size_t o_slab = al(lb.size() * sizeof(LkBlock));
+  const size_t o_sblk = o_slab + al(slabs.size() * sizeof(LkSlab));
+  const size_t o_dir = o_sblk + al(slab_blk.size() * 4);
+  const size_t o_bptr = o_dir + al(direct.size() * 4);
+  const size_t desc_bytes = o_bptr + al(slab_blk.size() * 8);
   dc.desc.ensure(desc_bytes + nids * 16);
   dc.hdesc.ensure(desc_bytes);
-  std::memcpy(dc.hdesc.p, lb.data(), lb.size() * sizeof(LkBlock));
+  auto *hd = static_cast<uint8_t *>(dc.hdesc.p);
+  std::memcpy(hd, lb.data(), lb.size() * sizeof(LkBlock));
+  if (!slabs.empty()) std::memcpy(hd + o_slab, slabs.data(), slabs.size() * sizeof(LkSlab));
+  if (!slab_blk.empty()) std::memcpy(hd + o_sblk, slab_blk.data(), slab_blk.size() * 4);
+  if (!direct.empty()) std::memcpy(hd + o_dir, direct.data(), direct.size() * 4);
+  for (size_t i = 0; i < slab_blk.size(); i++) {
+    const uint64_t *bp = lb[slab_blk[i]].bloom;
+    std::memcpy(hd + o_bptr + i * 8, &bp, 8);
+  }
   auto *dd = static_cast<uint8_t *>(dc.desc.p);
-  HIP_OK(hipMemcpyAsync(dd, dc.hdesc.p, lb.size() * sizeof(LkBlock), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(dd, hd, desc_bytes, hipMemcpyHostToDevice, s));
   HIP_OK(hipMemcpyAsync(dd + desc_bytes, ids, nids * 16, hipMemcpyHostToDevice, s));
   if (dc.gran_tiles < tiles) {
     HIP_OK(hipStreamSynchronize(s));
@@ -483,6 +693,11 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
   LkParams P{};
   P.blocks = reinterpret_cast<const LkBlock *>(dd);
   P.nblocks = uint32_t(lb.size());
+  P.slabs = reinterpret_cast<const LkSlab *>(dd + o_slab);
+  P.nslabs = uint32_t(slabs.size());
+  P.slab_blk = reinterpret_cast<const uint32_t *>(dd + o_sblk);
+  P.direct = reinterpret_cast<const uint32_t *>(dd + o_dir);
+  P.ndirect = uint32_t(direct.size());
   P.ids = dd + desc_bytes;
   P.nids = nids;
   P.epoch = dc.epoch;
@@ -497,6 +712,20 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
   P.hit_b = P.hit_cnt + nids;
   P.hit_r = reinterpret_cast<int32_t *>(P.hit_b + nids * kHitK);
   HIP_OK(hipEventRecord(dc.ev0, s));
+  for (size_t i = 0; i < slabs.size(); i++) {  // (inside the timed region: built per call)
+    TrParams tp{};
+    tp.bloom = reinterpret_cast<const uint64_t *const *>(dd + o_bptr + size_t(slabs[i].first) * 8);
+    tp.T = const_cast<uint32_t *>(slabs[i].T);
+    tp.words = lb[members[i][0]].words;
+    tp.bitlen = slabs[i].bitlen;
+    tp.shards = slabs[i].shards;
+    tp.W = slabs[i].W;
+    tp.J = slabs[i].J;
+    if (tp.words * 64 < tp.bitlen) fail(TSG_E_CORRUPT, "bloom shorter than its bit length");
+    const uint64_t threads = uint64_t(tp.shards) * tp.words * tp.W;
+    lookup_transpose_kernel<<<uint32_t((threads + 255) / 256), 256, 0, s>>>(tp);
+    HIP_OK(hipGetLastError());
+  }
   lookup_count_kernel<<<tiles, kLkThreads, 0, s>>>(P);
   HIP_OK(hipGetLastError());
   dc.ticket_base += tiles;
