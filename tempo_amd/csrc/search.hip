@@ -500,7 +500,7 @@ __device__ __forceinline__ void emit_tile(const ScanSeg &S, uint32_t mask, uint6
 //   fails the query loudly). Only workgroups with matches (and the last one, which
 //   writes the header) look back.
 // Phase 3 (emit): records in scan order straight into the pinned host buffer.
-constexpr uint32_t kStampSlots = 8;     // TSG_STAMPS: start setup scan lookback end | desc staged inlds
+constexpr uint32_t kStampSlots = 9;     // TSG_STAMPS: start setup scan lookback end | desc staged inlds | hw id
 constexpr uint32_t kLdsTiles = 16;      // tiles per workgroup whose masks stay in LDS
 constexpr uint32_t kMaxTpw = 2048;      // tiles per workgroup (per-tile counts in LDS)
 constexpr uint32_t kSpinMax = 1u << 22; // look-back poll bound (~seconds): never reached unless broken
@@ -540,16 +540,25 @@ template <int NT, bool DUR, bool RANGE, bool W1, bool SEG, class Segs, class Iss
 __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S, const ScanTerm *T, uint32_t si,
                                           const Segs &segs, const uint32_t *lds_bm, uint16_t *lds_mask,
                                           uint32_t *lds_seg, unsigned long long *lds_rec, unsigned long long t_start,
-                                          uint32_t wg, Issue &&issue_stage, Wait &&wait_bitmaps, Init &&init_segs) {
+                                          unsigned long long *stamps, uint32_t wg, Issue &&issue_stage,
+                                          Wait &&wait_bitmaps, Init &&init_segs) {
   __shared__ uint16_t s_tc[kMaxTpw];
   __shared__ uint32_t s_wcnt[2][kThreads / 64];
   __shared__ unsigned long long s_red[kThreads / 64];
   __shared__ unsigned long long s_wsum[kThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // (`stamps` = P.stamps, passed in already loaded: a kernel-argument load here would
+  // add a scalar round trip in front of the first tile load)
   auto stamp = [&](int k) {
-    if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * kStampSlots + k] = __builtin_amdgcn_s_memrealtime();
+    if (stamps && tid == 0) stamps[uint64_t(wg) * kStampSlots + k] = __builtin_amdgcn_s_memrealtime();
   };
-  if (P.stamps && tid == 0) P.stamps[uint64_t(wg) * kStampSlots] = t_start;
+  if (stamps && tid == 0) {
+    stamps[uint64_t(wg) * kStampSlots] = t_start;
+    // where the workgroup ran: XCC_ID (hwreg 20) << 32 | HW_ID (hwreg 4: wave, SIMD, CU, SH, SE)
+    const unsigned long long hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+    const unsigned long long xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+    stamps[uint64_t(wg) * kStampSlots + 8] = (xcc << 32) | hw;
+  }
 
   // ---- phase 1: scan, one tile of loads in flight ahead of the tile evaluated
   const uint32_t lw = wg - S.first_wg;  // static units split evenly over the block's workgroups (+-1 unit)
@@ -781,7 +790,7 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
 #pragma unroll
     for (int q = 0; q < NTA; q++) T[q] = P.terms[S.term0 + q];
   scan_emit<NT, DUR, RANGE, W1, false>(P, S, T, si, DescSegs{P.wg_seg, P.segs}, lds_bm, lds_mask, lds_seg, nullptr, t_start,
-                                vb, [] {}, [&] {
+                                P.stamps, vb, [] {}, [&] {
                                   for (uint32_t q = 0; q < S.nterms; q++) {  // stage the small bitmaps in LDS
                                     const ScanTerm &Tq = P.terms[S.term0 + q];
                                     if (Tq.lds_off != kNoLds)
@@ -819,6 +828,7 @@ struct QArgs {
   uint32_t mask_words;      // LDS words between the bitmaps and the block sums: tile masks / self-match stage
   uint32_t self_dict;       // 1: every scan workgroup matches its block's (small) dictionaries itself, njobs = 0
   uint32_t stage_first;     // self_dict: the dictionary words land before the first tile loads issue
+  uint32_t bm_first;        // narrow: the bitmap words land before the first tile loads issue
   unsigned long long *gbm;  // njobs x gstride granules
   // narrow mode: every term column of every block is one byte wide and its dictionary
   // was matched on the host (interned canonical dictionaries): the scan columns and the
@@ -831,7 +841,7 @@ struct QArgs {
   uint8_t slot[kArgSegs][kArgTerms], bmi[kArgSegs][kArgTerms], nsets8[kArgSegs][kArgTerms];
   uint32_t bms[kArgBms][8];
   // segment mode work stealing: tail tiles per block and its claim counter's value at launch
-  uint16_t tail[kArgSegs];
+  uint32_t tail[kArgSegs];  // (u32: one scalar load; u16 kernel arguments become vector loads)
   uint32_t steal_base[kArgSegs];
   ScanParams P;             // thresholds, outputs (segs/terms/wg_seg unused)
 };
@@ -1060,22 +1070,25 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   // and loads issued behind a branch would each add a round trip before the first tile
   // load (the empty asm statements pin them all in front of the first use)
   uint32_t use_ticket = A.P.use_ticket, njobs = A.njobs, nsegs = A.nsegs, narrow_arg = A.narrow;
+  uint32_t bm_words = A.bm_words, mask_words = A.mask_words, nterms = A.nterms, bm_first = A.bm_first,
+           self_dict = A.self_dict;
   unsigned long long *stamps = A.P.stamps;
   uint32_t fw[kArgSegs];
 #pragma unroll
   for (int s2 = 0; s2 < kArgSegs; s2++) fw[s2] = A.first_wg[s2];
   asm volatile("" : "+s"(use_ticket), "+s"(njobs), "+s"(nsegs), "+s"(narrow_arg), "+s"(stamps));
+  asm volatile("" : "+s"(bm_words), "+s"(mask_words), "+s"(nterms), "+s"(bm_first), "+s"(self_dict));
 #pragma unroll
   for (int s2 = 0; s2 < kArgSegs; s2++) asm volatile("" : "+s"(fw[s2]));
   const uint32_t vb = wg_order(A.P, use_ticket != 0);  // (a ticket when dictionary or look-back waits exist)
   if (vb < njobs) {  // dictionary workgroup: [value bits | stage]
-    dict_job(A, vb, lds + A.bm_words, lds);
+    dict_job(A, vb, lds + bm_words, lds);
     return;
   }
   // scan workgroup: [bitmaps bm_words | kLdsTiles masks | seg sums nsegs | first_wg nsegs+1 | caps]
   uint32_t *lds_bm = lds;
-  uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + A.bm_words);
-  uint32_t *lds_seg = lds + A.bm_words + A.mask_words;
+  uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + bm_words);
+  uint32_t *lds_seg = lds + bm_words + mask_words;
   uint32_t *lds_fw = lds_seg + ((A.nsegs + 1) & ~1u);  // (even: lds_cap below is 8-byte aligned)
   unsigned long long *lds_cap = reinterpret_cast<unsigned long long *>(lds_fw + ((A.nsegs + 2) & ~1u));
   unsigned long long *lds_rec = lds_cap + A.nsegs;  // segment mode: kSegMax staged records
@@ -1093,15 +1106,37 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   const uint32_t *n_scan = A.scan[si];
   const uint8_t *n_col = A.ncol[si];
   uint32_t n_npad = A.npad[si], n_ent = A.nent[si];
-  uint32_t n_slot[NTA], n_sets[NTA];
+  // (the per-term bytes as raw dwords, and one pin for everything: the compiler then
+  // issues every load before a single wait instead of unpacking between batches)
+  static_assert(kArgTerms == 4, "slot/bmi/nsets8 rows are one dword");
+  uint32_t r_slot = *reinterpret_cast<const uint32_t *>(A.slot[si]);
+  uint32_t r_sets = *reinterpret_cast<const uint32_t *>(A.nsets8[si]);
+  uint32_t r_bmi = *reinterpret_cast<const uint32_t *>(A.bmi[si]);
+  // the rest of this block's arguments, in the same round trip
+  uint32_t b_fw0 = A.first_wg[si], b_fw1 = A.first_wg[si + 1], b_idx = A.block_idx[si], b_tail = A.tail[si],
+           b_sbase = A.steal_base[si];
+  unsigned long long b_cap = A.cap[si];
+  asm volatile(""
+               : "+s"(n_scan), "+s"(n_col), "+s"(n_npad), "+s"(n_ent), "+s"(r_slot), "+s"(r_sets), "+s"(r_bmi),
+                 "+s"(b_fw0), "+s"(b_fw1), "+s"(b_idx), "+s"(b_tail), "+s"(b_sbase), "+s"(b_cap), "+s"(B));
+  uint32_t n_slot[NTA], n_sets[NTA], n_bmi[NTA];
 #pragma unroll
   for (int q = 0; q < NTA; q++) {
-    n_slot[q] = A.slot[si][q];
-    n_sets[q] = A.nsets8[si][q];
+    n_slot[q] = (r_slot >> (8 * q)) & 0xffu;
+    n_sets[q] = (r_sets >> (8 * q)) & 0xffu;
+    n_bmi[q] = (r_bmi >> (8 * q)) & 0xffu;
   }
-  asm volatile("" : "+s"(n_scan), "+s"(n_col), "+s"(n_npad), "+s"(n_ent));
+  // narrow: the query's bitmap words for this block's terms, requested now (before the
+  // tile burst: issued behind it, the scalar round trip queues behind ~30 MB of tile
+  // loads chip-wide and gates the first evaluation by ~10 us)
+  uint32_t bw[NTA][8];
+  if (NT > 0 && narrow_arg) {
 #pragma unroll
-  for (int q = 0; q < NTA; q++) asm volatile("" : "+s"(n_slot[q]), "+s"(n_sets[q]));
+    for (int q = 0; q < NTA; q++)
+#pragma unroll
+      for (int w = 0; w < 8; w++) bw[q][w] = A.bms[n_bmi[q]][w];
+    if (bm_first) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   DevKeyDesc KD[NTA];  // scalar loads, all issued together (one-launch kernels: NT == nterms)
   if (NT > 0 && !narrow)
 #pragma unroll
@@ -1138,16 +1173,16 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
     cold(B);
   }
   S.nunits = uint32_t((S.n + kUnit - 1) / kUnit);
-  S.first_wg = A.first_wg[si];
-  S.nwg = A.first_wg[si + 1] - S.first_wg;  // (first_wg[nsegs] = the grid's scan workgroups)
+  S.first_wg = b_fw0;
+  S.nwg = b_fw1 - b_fw0;  // (first_wg[nsegs] = the grid's scan workgroups)
   S.tpw = 0;
   S.term0 = 0;
-  S.nterms = A.nterms;
-  S.lds_words = A.bm_words;
-  S.block_idx = A.block_idx[si];
-  S.cap = A.cap[si];
-  S.tail = SEG ? A.tail[si] : 0u;
-  S.steal_base = A.steal_base[si];
+  S.nterms = nterms;
+  S.lds_words = bm_words;
+  S.block_idx = b_idx;
+  S.cap = b_cap;
+  S.tail = SEG ? b_tail : 0u;
+  S.steal_base = b_sbase;
   ScanTerm T[NTA];
   uint32_t gw[NTA + 1];  // granule prefix over this block's terms
   gw[0] = 0;
@@ -1177,7 +1212,7 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   auto issue_stage = [&] {
     if (stamps && threadIdx.x == 0)  // (waits for the descriptor scalar loads: lgkmcnt)
       stamps[uint64_t(wg) * kStampSlots + 5] = __builtin_amdgcn_s_memrealtime();
-    if (NT > 0 && A.self_dict) {
+    if (NT > 0 && self_dict) {
       self_issue<NTA>(X, KD);
       // stage_first: wait for the (few, L2-shared) dictionary words before this
       // workgroup's tile stream is issued. Issued together, they queue behind every
@@ -1189,16 +1224,16 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
       stamps[uint64_t(wg) * kStampSlots + 6] = __builtin_amdgcn_s_memrealtime();
   };
   auto wait_bitmaps = [&] {
-    if (narrow) {  // the host's bitmaps, from the kernel arguments (uniform: scalar loads)
+    if (narrow) {  // the host's bitmaps, from the kernel arguments (loaded in the prologue)
       if (NT > 0 && tid == 0)
 #pragma unroll
         for (int q = 0; q < NTA; q++)
 #pragma unroll
-          for (int w = 0; w < 8; w++) lds_bm[T[q].lds_off + w] = A.bms[A.bmi[si][q]][w];
+          for (int w = 0; w < 8; w++) lds_bm[T[q].lds_off + w] = bw[q][w];
       __syncthreads();
       return;
     }
-    if (NT > 0 && A.self_dict) {  // (self_finish ends with a barrier)
+    if (NT > 0 && self_dict) {  // (self_finish ends with a barrier)
       self_finish<NTA>(X, A, T, lds_bm, lds + A.bm_words, wg);
       return;
     }
@@ -1229,7 +1264,7 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
     __syncthreads();
   };
   scan_emit<NT, DUR, RANGE, W1, SEG>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, A.nsegs}, lds_bm, lds_mask, lds_seg,
-                                     lds_rec, t_start, wg, issue_stage, wait_bitmaps, [&] {
+                                     lds_rec, t_start, stamps, wg, issue_stage, wait_bitmaps, [&] {
                                        if (narrow) {  // (the asm keeps the loads below the scan loop)
                                          const DevBlockDesc *Bd = B;
                                          asm volatile("" : "+s"(Bd));
@@ -1346,6 +1381,22 @@ static void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast) {
   unsigned long long t0 = ~0ull;
   for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, st[size_t(w) * kStampSlots]);
   const char *names[8] = {"start", "setup", "scan", "lookback", "end", "desc", "staged", "inlds"};
+  if (const char *f = std::getenv("TSG_STAMPS_FILE")) {  // raw rows: wg, 8 stamps (us), xcc, se, sh, cu
+    static int launch = 0;
+    if (FILE *o = std::fopen(f, "a")) {
+      for (uint32_t w = 0; w < nwg; w++) {
+        std::fprintf(o, "%d,%u", launch, w);
+        for (int k = 0; k < 8; k++) {
+          const unsigned long long x = st[size_t(w) * kStampSlots + k];
+          std::fprintf(o, ",%.2f", x ? double(x - t0) / 100.0 : -1.0);
+        }
+        const unsigned long long hw = st[size_t(w) * kStampSlots + 8];
+        std::fprintf(o, ",%llu,%llu,%llu,%llu\n", hw >> 32, (hw >> 13) & 3, (hw >> 12) & 1, (hw >> 8) & 15);
+      }
+      std::fclose(o);
+    }
+    launch++;
+  }
   std::fprintf(stderr, "[tsg] stamps (%s, %u wg) us avg/max:", fast ? "one-launch" : "general", nwg);
   for (int k = 0; k < 8; k++) {
     double sum = 0, mx = 0;
@@ -1731,7 +1782,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       for (int t = 0; t < kArgTerms; t++) A.key_of[i][t] = seg_keys[i][size_t(t)];
     }
     A.first_wg[nsegs] = nwg;
-    for (uint32_t i = 0; i < nsegs; i++) A.tail[i] = uint16_t(segs[i].tail);
+    for (uint32_t i = 0; i < nsegs; i++) A.tail[i] = segs[i].tail;
     if (dc.steal.ensure(kArgSegs * 128)) {  // claim counters: zeroed once, then monotonic
       HIP_OK(hipMemsetAsync(dc.steal.p, 0, dc.steal.cap, s));
       std::fill(std::begin(dc.steal_base), std::end(dc.steal_base), 0u);
@@ -1760,6 +1811,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     A.njobs = njobs_fast;
     A.self_dict = self_dict ? 1u : 0u;
     A.stage_first = dc.stage_first ? 1u : 0u;
+    A.bm_first = dc.bm_first ? 1u : 0u;
     A.mask_words = fast_mask_words;
     A.gstride = fast_words;
     A.bm_words = fast_bm_words;

@@ -1,12 +1,13 @@
 #!/bin/bash
 # Config-2 bench (HBM rotation) under env variants: value, step p50, kernel p50, roofline frac.
-# usage: tools/gpu_envsweep.sh "NO_STEAL=1 NO_STEAL=1,PER_CU=8 ..."   (TSG_ prefix implied)
+# usage: tools/gpu_envsweep.sh "default PER_CU=3 HIP_FORCE_DEV_KERNARG=1 ..."   (TSG_ prefix implied
+# unless HIP_; a trailing @tag makes repeated names distinct)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for st in $1; do
   envs=()
-  [ "$st" != "default" ] && for kv in ${st//,/ }; do envs+=("TSG_$kv"); done
+  [ "${st%%@*}" != "default" ] && for kv in ${st//,/ }; do case $kv in HIP_*) envs+=("$kv");; *) envs+=("TSG_${kv%%@*}");; esac; done
   env "${envs[@]}" timeout -k 10 300 python bench.py --steps ${STEPS:-200} --warmup 10 --cpu-baseline 0 --limit-steps 0 \
     --mall-steps ${MALL:-0} --workdir /tmp/tsgw > gpurun_out/env_$st.json 2> gpurun_out/env_$st.err || { echo "$st failed"; tail -3 gpurun_out/env_$st.err; exit 1; }
   python3 -c "
