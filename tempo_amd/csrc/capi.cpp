@@ -187,30 +187,30 @@ static void open_common(tsg_ctx *ctx, Decode &&decode, int device_hint, tsg_bloc
   auto *b = new tsg_block();
   b->ctx = ctx;
   try {
-    decode(b->b.host);
-    if (b->b.host.has_meta) block_upload(ctx->c, b->b, device_hint);
+    decode(*b->b.host);
+    if (b->b.host->has_meta) block_upload(ctx->c, b->b, device_hint);
   } catch (...) {
     block_free(b->b);
     delete b;
     throw;
   }
   // the device holds the columns now; keep only what the host needs (names, header, pages)
-  for (size_t k = 0; k < b->b.host.keys.size(); k++) {
-    auto &kc = b->b.host.keys[k];
+  for (size_t k = 0; k < b->b.host->keys.size(); k++) {
+    auto &kc = b->b.host->keys[k];
     std::vector<uint32_t>().swap(kc.col);
-    if (int(k) != b->b.host.svc_key && int(k) != b->b.host.name_key) {
+    if (int(k) != b->b.host->svc_key && int(k) != b->b.host->name_key) {
       std::vector<uint8_t>().swap(kc.dict_bytes);
       std::vector<uint32_t>().swap(kc.dict_off);
       std::vector<uint32_t>().swap(kc.set_vals);
       kc.set_off.resize(1);
     }
   }
-  std::vector<uint8_t>().swap(b->b.host.ids);
-  std::vector<uint8_t>().swap(b->b.host.id_len);
-  std::vector<uint64_t>().swap(b->b.host.start);
-  std::vector<uint64_t>().swap(b->b.host.end);
-  std::vector<uint32_t>().swap(b->b.host.svc_vid);
-  std::vector<uint32_t>().swap(b->b.host.name_vid);
+  std::vector<uint8_t>().swap(b->b.host->ids);
+  std::vector<uint8_t>().swap(b->b.host->id_len);
+  std::vector<uint64_t>().swap(b->b.host->start);
+  std::vector<uint64_t>().swap(b->b.host->end);
+  std::vector<uint32_t>().swap(b->b.host->svc_vid);
+  std::vector<uint32_t>().swap(b->b.host->name_vid);
   *out = b;
 }
 
@@ -322,7 +322,7 @@ int tsg_block_clone(tsg_ctx *ctx, const tsg_block *src, int device_hint, tsg_blo
     auto *b = new tsg_block();
     b->ctx = ctx;
     try {
-      if (src->b.host.has_meta) block_clone(ctx->c, src->b, b->b, device_hint);
+      if (src->b.host->has_meta) block_clone(ctx->c, src->b, b->b, device_hint);
       else b->b.host = src->b.host;
     } catch (...) {
       block_free(b->b);
@@ -339,7 +339,7 @@ void tsg_block_close(tsg_block *b) {
 }
 int tsg_block_info_get(const tsg_block *b, tsg_block_info *o) {
   if (!b || !o) return TSG_E_INVALID;
-  const HostBlock &h = b->b.host;
+  const HostBlock &h = *b->b.host;
   o->entries = h.n;
   o->pages = h.page_entries.size();
   o->keys = h.keys.size();
@@ -378,10 +378,10 @@ int tsg_block_tags(const tsg_block *b, uint8_t **out, size_t *len, size_t *n) {
   if (!b || !out || !len || !n) return TSG_E_INVALID;
   return guard([&] {
     std::vector<std::string> keys;
-    const auto &hb = b->b.host.header;
-    if (b->b.host.streaming) {  // StreamingSearchBlock.Tags: the mutable header's keys
-      for (auto &kv : b->b.host.stream_tags) keys.push_back(kv.first);
-    } else if (b->b.host.has_meta) {
+    const auto &hb = b->b.host->header;
+    if (b->b.host->streaming) {  // StreamingSearchBlock.Tags: the mutable header's keys
+      for (auto &kv : b->b.host->stream_tags) keys.push_back(kv.first);
+    } else if (b->b.host->has_meta) {
       FbTable h = FbTable::root(hb.data(), hb.size());
       uint16_t o = h.field(kHdrTags);
       uint32_t cnt = o ? h.vector_len(o) : 0, st = o ? h.vector_start(o) : 0;
@@ -402,11 +402,11 @@ int tsg_block_tag_values(const tsg_block *b, const uint8_t *key, size_t klen, ui
   if (!b || !out || !len || !n) return TSG_E_INVALID;
   return guard([&] {
     std::vector<std::string> vals;
-    const auto &hb = b->b.host.header;
-    if (b->b.host.streaming) {  // StreamingSearchBlock.TagValues
-      auto it = b->b.host.stream_tags.find(std::string(reinterpret_cast<const char *>(key), klen));
-      if (it != b->b.host.stream_tags.end()) vals.assign(it->second.begin(), it->second.end());
-    } else if (b->b.host.has_meta) {
+    const auto &hb = b->b.host->header;
+    if (b->b.host->streaming) {  // StreamingSearchBlock.TagValues
+      auto it = b->b.host->stream_tags.find(std::string(reinterpret_cast<const char *>(key), klen));
+      if (it != b->b.host->stream_tags.end()) vals.assign(it->second.begin(), it->second.end());
+    } else if (b->b.host->has_meta) {
       FbTable h = FbTable::root(hb.data(), hb.size());
       uint16_t o = h.field(kHdrTags);
       uint32_t cnt = o ? h.vector_len(o) : 0, st = o ? h.vector_start(o) : 0;
@@ -476,10 +476,10 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     std::vector<int> state(nblocks, 0);  // 0 no meta, 1 skipped, 2 inspected
     for (size_t i = 0; i < nblocks; i++) {
       Block &b = blocks[i]->b;
-      if (!b.host.has_meta) continue;
-      bool ok = b.host.streaming
-                    ? pipeline_matches_stream_header(*q, b.host.min_dur, b.host.max_dur, b.host.stream_tags)
-                    : pipeline_matches_block(*q, b.host.header.data(), b.host.header.size());
+      if (!b.host->has_meta) continue;
+      bool ok = b.host->streaming
+                    ? pipeline_matches_stream_header(*q, b.host->min_dur, b.host->max_dur, b.host->stream_tags)
+                    : pipeline_matches_block(*q, b.host->header.data(), b.host->header.size());
       state[i] = ok ? 2 : 1;
     }
     // Blocks [b0, b1) on their devices, one device_search per device (concurrently).
@@ -563,10 +563,10 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     if (limit && nblocks > 1) {
       uint64_t total = 0, acc = 0;
       for (size_t i = 0; i < nblocks; i++)
-        if (state[i] == 2) total += blocks[i]->b.host.n;
+        if (state[i] == 2) total += blocks[i]->b.host->n;
       b1 = 0;
       while (b1 < nblocks && (acc * 8 < total || acc == 0)) {
-        if (state[b1] == 2) acc += blocks[b1]->b.host.n;
+        if (state[b1] == 2) acc += blocks[b1]->b.host->n;
         b1++;
       }
     }
@@ -591,7 +591,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     std::unordered_set<std::string> distinct;
     bool stopped = false;
     for (size_t i = 0; i < nblocks && !stopped; i++) {
-      const HostBlock &h = blocks[i]->b.host;
+      const HostBlock &h = *blocks[i]->b.host;
       if (state[i] == 0) continue;  // meta missing: no-op (backend_search_block.go:191-203)
       m.bytes_inspected += h.header.size();
       if (state[i] == 1) {

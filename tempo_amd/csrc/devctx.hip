@@ -111,7 +111,7 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
   DeviceCtx &dc = *c.devs[size_t(std::max(device_hint, 0)) % c.devs.size()];
   b.dc = &dc;
   DevBlock &d = b.dev;
-  const HostBlock &h = b.host;
+  const HostBlock &h = *b.host;
   d.device = dc.ordinal;
   d.n = h.n;
   std::lock_guard<std::mutex> lk(dc.mu);
@@ -258,7 +258,7 @@ void block_clone(Ctx &c, const Block &src, Block &dst, int device_hint) {
   if (c.devs.empty()) fail(TSG_E_DEVICE, "no device");
   if (!src.dc) fail(TSG_E_INVALID, "block_clone: source block is not resident");
   DeviceCtx &dc = *c.devs[size_t(std::max(device_hint, 0)) % c.devs.size()];
-  dst.host = src.host;
+  dst.host = src.host;  // (shared: the host side is immutable after open)
   dst.dc = &dc;
   DevBlock &d = dst.dev;
   const DevBlock &o = src.dev;

@@ -67,6 +67,10 @@ struct DeviceCtx {
     const char *e = std::getenv("TSG_STAGE_FIRST");
     return e ? std::atoi(e) != 0 : false;
   }();
+  bool prio = [] {  // TSG_PRIO=1: progress-ordered wave priority in the scan loop (default off)
+    const char *e = std::getenv("TSG_PRIO");
+    return e ? std::atoi(e) != 0 : false;
+  }();
   bool bm_first = [] {  // TSG_BM_FIRST=0/1: narrow bitmap words before the tile stream
     const char *e = std::getenv("TSG_BM_FIRST");
     return e ? std::atoi(e) != 0 : false;

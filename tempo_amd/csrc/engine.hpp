@@ -95,7 +95,9 @@ struct DevBlock {
 struct DeviceCtx;
 
 struct Block {
-  HostBlock host;     // dictionaries/metadata kept on the host (names, header, page table)
+  // dictionaries/metadata kept on the host (names, header, page table); immutable after
+  // open, shared by clones (tsg_block_clone copies only the device side)
+  std::shared_ptr<HostBlock> host = std::make_shared<HostBlock>();
   DevBlock dev;
   DeviceCtx *dc = nullptr;
   std::vector<std::shared_ptr<const NarrowDict>> narrow;  // per key: interned dictionary (narrow keys)

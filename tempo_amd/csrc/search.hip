@@ -103,7 +103,13 @@ struct ScanParams {
   // granules): HIP promises no dispatch order, a ticket holder has started by definition
   unsigned long long *ticket;
   unsigned long long ticket_base;
-  uint32_t use_ticket, pad3;
+  uint32_t use_ticket;
+  // TSG_PRIO=1: scan loop wave priority from progress (s_setprio 3 -> 0 over the
+  // workgroup's tiles). The co-resident workgroups of a CU progress in dispatch order
+  // (issue is arbitrated by priority, then age: the 4th one ends ~10 us after the 1st);
+  // this evens a CU out, but the kernel's end is set by the chip-wide tail, which it
+  // does not move (profiles/r02_prio: kernel p50 38.7-39.8 vs 38.5-38.6 us off)
+  uint32_t prio;
   unsigned *steal;  // tail claim counters, one per block slot (128 B apart), monotonic
 };
 
@@ -592,12 +598,22 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
   // tile re-reads the last tile (cache hit) so the load sequence stays
   // unconditional and hipcc's vmcnt counting stays exact.
   auto tile0 = [&](uint32_t t) { return tbase + uint64_t(min(t, ntl - 1)) * kTile; };
+  const uint32_t prio = P.prio;
+  auto set_prio = [&](uint32_t t) {  // (s_setprio takes an immediate)
+    if (!prio) return;
+    const uint32_t lvl = min(3u, (t * 4) / max(ntl, 1u));
+    if (lvl == 0) __builtin_amdgcn_s_setprio(3);
+    else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+    else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  };
   issue_stage();
   load_tile<NT, DUR, RANGE, W1>(ra, S, T, tile0(0), lim, tid);  // (ntl >= 1: never more workgroups than units)
   load_tile<NT, DUR, RANGE, W1>(rb, S, T, tile0(1), lim, tid);
   wait_bitmaps();
   stamp(1);
   for (uint32_t t = 0;; t += 2) {
+    set_prio(t);
     finish(t, eval_tile<NT, DUR, RANGE, W1>(ra, P, S, T, lds_bm, tile0(t), lim, tid));
     if (t + 1 >= ntl) break;
     load_tile<NT, DUR, RANGE, W1>(ra, S, T, tile0(t + 2), lim, tid);
@@ -606,6 +622,7 @@ __device__ __forceinline__ void scan_emit(const ScanParams &P, const ScanSeg &S,
     load_tile<NT, DUR, RANGE, W1>(rb, S, T, tile0(t + 3), lim, tid);
   }
 
+  if (prio) __builtin_amdgcn_s_setprio(0);
   // ---- phase 2: publish, look back
   // (the per-block tables the look-back needs are staged only now: their loads
   // would otherwise sit in front of the dictionary and tile loads)
@@ -1480,8 +1497,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     std::vector<int> kidx(q.nterms);
     bool dead = false;  // a key absent from the block: FindTag fails for every entry
     for (uint32_t t = 0; t < q.nterms && !dead; t++) {
-      auto it = b.host.key_index.find(std::string(reinterpret_cast<const char *>(q.keys[t]), q.key_lens[t]));
-      if (it == b.host.key_index.end()) dead = true;
+      auto it = b.host->key_index.find(std::string(reinterpret_cast<const char *>(q.keys[t]), q.key_lens[t]));
+      if (it == b.host->key_index.end()) dead = true;
       else kidx[t] = it->second;
     }
     if (dead) continue;
@@ -1741,6 +1758,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   const bool time_defer = flags & TSG_SEARCH_TIME_DEFER;
 
   ScanParams P{};
+  P.prio = dc.prio ? 1u : 0u;
   P.nsegs = nsegs;
   P.nwg = nwg;
   P.has_min = q.has_min;
