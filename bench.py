@@ -136,6 +136,13 @@ def parse():
                          "the average over those launches); 0 = off")
     ap.add_argument("--limit-steps", type=int, default=20,
                     help="extra timed searches with limit=20 (early exit, config-3 mode); 0 = skip")
+    ap.add_argument("--cfg3", type=int, default=1,
+                    help="config-3 leg on this GPU's share: --cfg3-blocks resident blocks of --cfg3-entries "
+                         "(one generated block + device clones), full scan x --cfg3-steps back-to-back queries "
+                         "and limit=20 (time to the first 20); 0 = skip")
+    ap.add_argument("--cfg3-blocks", type=int, default=25)
+    ap.add_argument("--cfg3-entries", type=int, default=5_000_000)
+    ap.add_argument("--cfg3-steps", type=int, default=64)
     ap.add_argument("--pin", default="auto", choices=["auto", "none"],
                     help="auto: keep this process on the CPUs of its GPU's NUMA node (tsg_device_numa_node)")
     ap.add_argument("--workdir", default=None)
@@ -249,6 +256,74 @@ def cpu_baselines(paths, got, threads):
         "parity": cm == len(got) and ch == O.match_hash([(m.block_idx, m.entry_idx) for m in got]),
     }
     return out
+
+
+def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags):
+    """BASELINE config 3 on this GPU's share (200 blocks x 5 M over 8 GPUs = 25 x 5 M per
+    GPU): one generated 5 M-entry block and device clones of it (tsg_block_clone: the
+    clones share the host side), 125 M entries resident. Full scan: --cfg3-steps
+    back-to-back queries (SURVEY.md 8(d)'s batched mode over a >= 100 M-entry resident
+    set), kernel HIP events on every 8th; limit=20: the deterministic early exit."""
+    import torch
+    import tempo_amd as T
+    t0 = time.time()
+    p = os.path.join(workdir, f"r{rank}cfg3")
+    if not os.path.exists(os.path.join(p, "search.meta.json")):
+        T.synth_search_block(p, args.cfg3_entries, seed=7000 + rank, profile=0, encoding=T.ENC_SNAPPY,
+                             page_size=1024 * 1024)
+    gen_s = time.time() - t0
+    t0 = time.time()
+    b0 = eng.open_block(p)
+    blocks = [b0] + [b0.clone(eng) for _ in range(args.cfg3_blocks - 1)]
+    load_s = time.time() - t0
+    entries = sum(b.info()["entries"] for b in blocks)
+    log(f"rank {rank}: cfg3 {len(blocks)} x {args.cfg3_entries} entries resident (gen {gen_s:.1f}s, "
+        f"load+clone {load_s:.1f}s)")
+    got, met = eng.search(blocks, pipe)
+    for _ in range(2):
+        eng.search_raw(blocks, pipe, flags=0)
+    eng.kernel_times()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step = []
+    for i in range(args.cfg3_steps):
+        ts = time.perf_counter()
+        eng.search_raw(blocks, pipe, flags=sflags if i % 8 == 0 else 0)
+        step.append(time.perf_counter() - ts)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kns = eng.kernel_times() if sflags else []
+    if dist:
+        dist.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    scan_bytes = met.scan_bytes
+    kavg = sum(kns) / len(kns) if kns else 0
+    ach = scan_bytes / kavg if kavg else None
+    lim = []
+    for i in range(23):
+        ts = time.perf_counter()
+        nl, metl = eng.search_raw(blocks, pipe, limit=20)
+        if i >= 3:
+            lim.append(time.perf_counter() - ts)
+    res = {
+        "workload": f"config 3 per-GPU share: {len(blocks)} blocks x {args.cfg3_entries} entries "
+                    f"(1 generated + {len(blocks) - 1} device clones), config-2 query",
+        "entries_per_gpu": entries, "matches_full": len(got),
+        "full_scan": {"queries": args.cfg3_steps, "entries_per_s": entries * args.cfg3_steps * world / elapsed,
+                      "step_us": pct([x * 1e6 for x in step]), "kernel_us": pct([x / 1e3 for x in kns]),
+                      "scan_bytes": scan_bytes, "achieved_gbps": ach,
+                      "frac": ach / PEAK_HBM_GBPS if ach else None,
+                      "regime": "hbm" if scan_bytes > 256 * 2**20 * 1.5 else "mall"},
+        "limit20": {"matches": nl, "traces_inspected": metl.inspected_traces, "blocks_inspected": metl.inspected_blocks,
+                    "time_to_first_20_us": pct([x * 1e6 for x in lim])},
+    }
+    for b in blocks:
+        b.close()
+    return res
 
 
 def main():
@@ -418,6 +493,9 @@ def main():
         out["limit20"] = {"steps": args.limit_steps, "matches": nl, "traces_inspected": metl.inspected_traces,
                           "step_us": pct([x * 1e6 for x in ls]), "kernel_us": pct([x / 1e3 for x in lk]),
                           "entries_per_s": entries / (sum(ls) / len(ls))}
+
+    if args.cfg3:
+        out["cfg3"] = cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags)
 
     if rank == 0 and world == 1 and args.cpu_baseline:
         os.sched_setaffinity(0, all_cpus)  # (the CPU baselines get the whole host share back)
