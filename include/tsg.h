@@ -289,7 +289,7 @@ void tsg_lookup_result_free(tsg_lookup_result *r);
 /* tempodb.Find's per-block step for a batch of ids, whole on the device: the lookup above,
  * then PagedFinder.findOne (tempodb/encoding/v2/finder_paged.go:79-110) for every hit: the
  * data page its index record names (resident in HBM since tsg_v2block_open) is decompressed
- * (encodings none and snappy; others -> TSG_E_UNSUPPORTED_ENCODING for that hit) and its
+ * (encodings none, snappy and zstd; others -> TSG_E_UNSUPPORTED_ENCODING for that hit) and its
  * objects are scanned for the exact id. One entry per lookup hit, sorted (id_idx,
  * block_idx): status TSG_OK with the object's bytes (what findOne returns), TSG_E_NOT_FOUND
  * (a bloom false positive: findOne returns nil), or the error findOne returns for that
@@ -308,7 +308,65 @@ int tsg_find_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, const
                  size_t nids, const tsg_lookup_opts *opts, tsg_find_result **out);
 void tsg_find_result_free(tsg_find_result *r);
 
+/* ---- proto-object backend search ---------------------------
+ * tempodb.Search over one v2 block whose objects are trace protos: what querier and
+ * serverless SearchBlock jobs run (modules/querier/querier.go:420-452 ->
+ * tempodb/tempodb.go:368-375 -> v2.BackendBlock.Search, tempodb/encoding/v2/
+ * backend_block.go:159-231 -> ObjectDecoder.Matches -> trace.MatchesProto,
+ * pkg/model/trace/matches.go:33-184). meta.json dataEncoding "v1" (objects are
+ * tempopb.TraceBytes) or "v2" (u32 start, u32 end seconds + TraceBytes, with the FastRange
+ * and duration prefilter, pkg/model/v2/object_decoder.go:57-89). tsg_proto_block_open
+ * decodes every data page (none, snappy, zstd) and every object once into per-object
+ * columns and per-attribute-key value-set columns resident on the device; a search is one
+ * kernel over the page range plus the host replay of Search's loop. */
+typedef struct tsg_proto_block tsg_proto_block;
+typedef struct tsg_proto_request {
+  uint32_t ntags; /* SearchRequest.Tags (map: a repeated key keeps its last value) */
+  const char *const *keys;
+  const uint32_t *key_lens;
+  const char *const *values;
+  const uint32_t *value_lens;
+  uint32_t min_duration_ms, max_duration_ms; /* 0 = unset */
+  uint32_t start, end;                       /* unix seconds (compared even when 0, as the reference) */
+  uint32_t limit;                            /* Search breaks once len(Traces) >= Limit (0: after one object) */
+  uint32_t start_page, total_pages;          /* SearchOptions: total_pages > 0 = partial iterator */
+  uint32_t max_bytes;                        /* SearchOptions.MaxBytes: larger objects are SkippedTraces */
+  uint32_t chunk_size_bytes;                 /* SearchOptions.ChunkSizeBytes (0 = 1 000 000) */
+} tsg_proto_request;
+typedef struct tsg_proto_result {
+  uint32_t n; /* TraceSearchMetadata, in object order */
+  const uint8_t *trace_ids;     /* object ids, trace_id_off / trace_id_len into this */
+  const uint32_t *trace_id_off;
+  const uint8_t *trace_id_len;
+  const char *const *root_service_name;
+  const char *const *root_trace_name;
+  const uint64_t *start_time_unix_nano;
+  const uint32_t *duration_ms;
+  const uint32_t *object_idx;   /* position of the object in the block's iterator order */
+  uint64_t inspected_traces, inspected_bytes, skipped_traces; /* SearchMetrics */
+  uint64_t kernel_ns;
+} tsg_proto_result;
+int tsg_proto_block_open(tsg_ctx *ctx, const char *block_dir, int device_hint, tsg_proto_block **out);
+void tsg_proto_block_close(tsg_proto_block *b);
+/* out[0] objects, out[1] pages (index records read), out[2] attribute keys, out[3] device bytes */
+int tsg_proto_block_info(const tsg_proto_block *b, uint64_t out[4]);
+/* TSG_E_CORRUPT (message in tsg_last_error) where Search returns an error: a trace that
+ * fails to decode, an index/page/object framing error, reached before the limit break. */
+int tsg_proto_search(tsg_ctx *ctx, tsg_proto_block *b, const tsg_proto_request *req, tsg_proto_result **out);
+void tsg_proto_result_free(tsg_proto_result *r);
+
+/* Go strconv semantics used by matchAttributes (tooling / tests): kind 0 ParseInt(s, 10, 64)
+ * -> *i, 1 ParseFloat(s, 64) -> *f, 2 ParseBool -> *i. Returns 1 when Go returns err == nil. */
+int tsg_go_parse(int kind, const char *s, size_t n, double *f, int64_t *i);
+
 /* ---- block writer (tooling: synthetic data and test fixtures) ----------------- */
+/* A v2 block from caller objects (ids ascending): data pages cut at
+ * index_downsample_bytes (0 = 1 MiB), index, bloom, meta.json with the given page
+ * encoding (0 none, 6 snappy) and dataEncoding ("v1" / "v2"). objs: concatenated object
+ * bytes, obj_off: n + 1 offsets. */
+int tsg_write_v2_block(const char *block_dir, const uint8_t (*ids)[16], const uint8_t *objs,
+                       const uint64_t *obj_off, size_t n, int encoding, const char *data_encoding,
+                       uint32_t index_downsample_bytes);
 /* Entry list wire format (little endian), one record per trace:
  *   u32 id_len, id bytes, u64 start_ns, u64 end_ns, u32 ntags,
  *   ntags x (u32 klen, key, u32 vlen, value)

@@ -246,6 +246,17 @@ def entry_to_bytes(entry):
     return b
 
 
+def snappy_framed_decode(b):
+    """The C oracle's snappy framing-format decoder (golang/snappy Reader restated)."""
+    out, n = C.POINTER(C.c_uint8)(), C.c_size_t()
+    rc = lib().orc_snappy_framed_decode(b, len(b), C.byref(out), C.byref(n))
+    if rc != 0:
+        raise ValueError("snappy decode failed (%d)" % rc)
+    r = C.string_at(out, n.value)
+    lib().orc_free(out)
+    return r
+
+
 def xxhash64(b):
     return lib().orc_xxhash64(b, len(b))
 

@@ -133,7 +133,10 @@ void read_data_page(const uint8_t *file, size_t flen, const IndexRecord &r, int 
   unmarshal_page(file + r.start, r.length, 0, hdr, payload, pl);
   if (enc == 0) out.assign(payload, payload + pl);
   else if (enc == 6) snappy_framed_decode(payload, pl, out);
-  else fail(TSG_E_UNSUPPORTED_ENCODING, std::string("unsupported search encoding ") + encoding_name(enc));
+  else if (enc == 7) {
+    const int st = zstd_host_decode(payload, pl, out);
+    if (st != TSG_OK) fail(st, "zstd page decode failed");
+  } else fail(TSG_E_UNSUPPORTED_ENCODING, std::string("unsupported page encoding ") + encoding_name(enc));
 }
 
 // ---- page parse ---------------------------------------------------------------------------

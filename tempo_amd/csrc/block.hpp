@@ -103,6 +103,7 @@ std::vector<IndexRecord> read_index(const uint8_t *p, size_t n, uint32_t page_si
                                     bool *prefix = nullptr);
 // dataReader.Read of one record + decompression (data_reader.go:45-125).
 void read_data_page(const uint8_t *file, size_t flen, const IndexRecord &r, int enc, std::vector<uint8_t> &out);
+int zstd_host_decode(const uint8_t *src, size_t n, std::vector<uint8_t> &out);  // zstd_host.cpp
 
 // ---- the decoded block ------------------------------------------------------------
 static constexpr uint32_t kNone = 0xFFFFFFFFu;

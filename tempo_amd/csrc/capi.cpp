@@ -16,6 +16,7 @@
 #include "block.hpp"
 #include "common.hpp"
 #include "engine.hpp"
+#include "proto.hpp"
 #include "writer.hpp"
 
 struct tsg_ctx {
@@ -40,6 +41,10 @@ struct tsg_ctx {
 struct tsg_block {
   tsg::Block b;
   tsg_ctx *ctx = nullptr;
+};
+struct tsg_proto_block {
+  tsg_ctx *ctx = nullptr;
+  tsg::ProtoBlock b;
 };
 struct tsg_v2block {
   tsg::V2Block b;
@@ -179,6 +184,17 @@ struct FindHolder {
   FindOut o;
 };
 static_assert(offsetof(FindHolder, pub) == 0, "pub first");
+
+struct ProtoHolder {
+  tsg_proto_result pub{};
+  std::vector<uint8_t> ids;
+  std::vector<uint32_t> id_off, dur, obj;
+  std::vector<uint8_t> id_len;
+  std::vector<uint64_t> start;
+  std::vector<std::string> svc, root;
+  std::vector<const char *> svc_p, root_p;
+};
+static_assert(offsetof(ProtoHolder, pub) == 0, "pub first");
 
 static std::string join(const char *dir, const char *name) { return std::string(dir) + "/" + name; }
 
@@ -894,6 +910,120 @@ int tsg_synth_search_block(const char *dir, uint64_t n, uint64_t seed, int profi
 int tsg_synth_v2_block(const char *dir, uint64_t n, uint64_t seed, uint8_t (*ids_out)[16]) {
   if (!dir) return TSG_E_INVALID;
   return guard([&] { synth_v2_block(dir, n, seed, ids_out); });
+}
+
+int tsg_write_v2_block(const char *dir, const uint8_t (*ids)[16], const uint8_t *objs, const uint64_t *obj_off,
+                       size_t n, int encoding, const char *data_encoding, uint32_t index_downsample_bytes) {
+  if (!dir || (n && (!ids || !objs || !obj_off))) return TSG_E_INVALID;
+  return guard([&] {
+    for (size_t i = 1; i < n; i++)
+      if (bytes_compare(ids[i - 1], 16, ids[i], 16) >= 0) fail(TSG_E_INVALID, "ids must be strictly ascending");
+    std::vector<std::vector<uint8_t>> o(n ? n : 1);
+    for (size_t i = 0; i < n; i++) o[i].assign(objs + obj_off[i], objs + obj_off[i + 1]);
+    V2Params prm;
+    prm.encoding = encoding;
+    prm.data_encoding = data_encoding ? data_encoding : "v2";
+    if (index_downsample_bytes) prm.index_downsample_bytes = index_downsample_bytes;
+    for (int k = 0; k < 16; k++) prm.block_id[k] = uint8_t(0x11 * (k + 1));
+    prm.block_id[6] = (prm.block_id[6] & 0x0f) | 0x40;
+    write_v2_block(dir, ids, o, n, prm);
+  });
+}
+
+int tsg_proto_block_open(tsg_ctx *ctx, const char *dir, int device_hint, tsg_proto_block **out) {
+  if (!ctx || !dir || !out) return TSG_E_INVALID;
+  return guard([&] {
+    auto *b = new tsg_proto_block();
+    b->ctx = ctx;
+    try {
+      proto_block_open(ctx->c, b->b, dir, device_hint);
+    } catch (...) {
+      proto_block_free(b->b);
+      delete b;
+      throw;
+    }
+    *out = b;
+  });
+}
+void tsg_proto_block_close(tsg_proto_block *b) {
+  if (!b) return;
+  proto_block_free(b->b);
+  delete b;
+}
+int tsg_proto_block_info(const tsg_proto_block *b, uint64_t out[4]) {
+  if (!b || !out) return TSG_E_INVALID;
+  out[0] = b->b.n;
+  out[1] = b->b.page_len.size();
+  out[2] = b->b.keys.size();
+  out[3] = b->b.device_bytes;
+  return TSG_OK;
+}
+int tsg_proto_search(tsg_ctx *ctx, tsg_proto_block *b, const tsg_proto_request *req, tsg_proto_result **out) {
+  if (!ctx || !b || !req || !out || (req->ntags && (!req->keys || !req->key_lens || !req->values || !req->value_lens)))
+    return TSG_E_INVALID;
+  *out = nullptr;
+  return guard([&] {
+    ProtoOut o;
+    proto_search(b->b, *req, o);
+    if (o.status != TSG_OK) fail(o.status, o.error);
+    auto *h = new ProtoHolder();
+    std::unique_ptr<ProtoHolder> g(h);
+    const ProtoBlock &pb = b->b;
+    for (uint32_t i : o.traces) {
+      h->id_off.push_back(uint32_t(h->ids.size()));
+      h->id_len.push_back(pb.id_len[i]);
+      h->ids.insert(h->ids.end(), pb.ids.begin() + pb.id_off[i], pb.ids.begin() + pb.id_off[i] + pb.id_len[i]);
+      h->svc.emplace_back(pb.names, pb.svc_off[i], pb.svc_len[i]);
+      h->root.emplace_back(pb.names, pb.root_off[i], pb.root_len[i]);
+      h->start.push_back(pb.start_ns[i]);
+      h->dur.push_back(pb.dur_ms[i]);
+      h->obj.push_back(i);
+    }
+    for (size_t i = 0; i < h->svc.size(); i++) {
+      h->svc_p.push_back(h->svc[i].c_str());
+      h->root_p.push_back(h->root[i].c_str());
+    }
+    tsg_proto_result &r = h->pub;
+    r.n = uint32_t(o.traces.size());
+    r.trace_ids = h->ids.data();
+    r.trace_id_off = h->id_off.data();
+    r.trace_id_len = h->id_len.data();
+    r.root_service_name = h->svc_p.data();
+    r.root_trace_name = h->root_p.data();
+    r.start_time_unix_nano = h->start.data();
+    r.duration_ms = h->dur.data();
+    r.object_idx = h->obj.data();
+    r.inspected_traces = o.inspected_traces;
+    r.inspected_bytes = o.inspected_bytes;
+    r.skipped_traces = o.skipped_traces;
+    r.kernel_ns = o.kernel_ns;
+    *out = &g.release()->pub;
+  });
+}
+void tsg_proto_result_free(tsg_proto_result *r) { delete reinterpret_cast<ProtoHolder *>(r); }
+
+int tsg_go_parse(int kind, const char *s, size_t n, double *f, int64_t *i) {
+  if (!s && n) return TSG_E_INVALID;
+  std::string_view v(s ? s : "", n);
+  if (kind == 0) {
+    int64_t x = 0;
+    const bool ok = go_parse_int(v, x);
+    if (ok && i) *i = x;
+    return ok;
+  }
+  if (kind == 1) {
+    double x = 0;
+    const bool ok = go_parse_float(v, x);
+    if (ok && f) *f = x;
+    return ok;
+  }
+  if (kind == 2) {
+    bool x = false;
+    const bool ok = go_parse_bool(v, x);
+    if (ok && i) *i = x;
+    return ok;
+  }
+  return TSG_E_INVALID;
 }
 
 }  // extern "C"

@@ -86,6 +86,7 @@ struct DeviceCtx {
   DevBuf desc, vmatch, bitmaps, gran, ticket, out, regions, seg_counts, hdr, err;
   DevBuf maskbits, agg, stamps, gbm, lkhits;
   DevBuf lkslab, lkslabdesc;  // lookup: transposed bloom slabs + their member tables
+  DevBuf pbm, pout;  // proto search: term bitmaps, per-object match/error bits
   DevBuf fpages, fhits, fres, farena, fcrc, fdst, foff;  // device findOne (find.hip)
   HostBuf hdesc, hout;
   // search results, written by the emit kernel directly (coherent: the kernel's

@@ -471,7 +471,7 @@ void write_v2_block(const std::string &dir, const uint8_t (*ids)[16], const std:
                      ",\"compactionLevel\":0,\"encoding\":\"" + encoding_name(prm.encoding) +
                      "\",\"indexPageSize\":" + std::to_string(prm.index_page_bytes) +
                      ",\"totalRecords\":" + std::to_string(records.size()) +
-                     ",\"dataEncoding\":\"v2\",\"bloomShards\":" + std::to_string(shards) + "}";
+                     ",\"dataEncoding\":\"" + prm.data_encoding + "\",\"bloomShards\":" + std::to_string(shards) + "}";
   write_file(dir + "/meta.json", reinterpret_cast<const uint8_t *>(meta.data()), meta.size());
 }
 

@@ -56,6 +56,7 @@ struct V2Params {
   int encoding = 0;
   uint8_t block_id[16] = {0};
   int64_t start_unix = 1700000000, end_unix = 1700003600;
+  std::string data_encoding = "v2";  // meta dataEncoding: the object format (pkg/model/{v1,v2})
 };
 void bloom_estimate(uint64_t n, double fp, uint64_t &m, uint64_t &k);
 uint32_t bloom_shard_count(double fp, uint64_t shard_size, uint64_t n);

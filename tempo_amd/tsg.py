@@ -17,6 +17,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import struct
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence
 
@@ -111,6 +112,23 @@ class _FindResult(C.Structure):
                 ("obj_len", C.POINTER(C.c_uint32)), ("obj_bytes", C.POINTER(C.c_uint8)), ("kernel_ns", C.c_uint64)]
 
 
+class _ProtoRequest(C.Structure):
+    _fields_ = [("ntags", C.c_uint32), ("keys", C.POINTER(C.c_char_p)), ("key_lens", C.POINTER(C.c_uint32)),
+                ("values", C.POINTER(C.c_char_p)), ("value_lens", C.POINTER(C.c_uint32)),
+                ("min_duration_ms", C.c_uint32), ("max_duration_ms", C.c_uint32), ("start", C.c_uint32),
+                ("end", C.c_uint32), ("limit", C.c_uint32), ("start_page", C.c_uint32), ("total_pages", C.c_uint32),
+                ("max_bytes", C.c_uint32), ("chunk_size_bytes", C.c_uint32)]
+
+
+class _ProtoResult(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("trace_ids", C.POINTER(C.c_uint8)), ("trace_id_off", C.POINTER(C.c_uint32)),
+                ("trace_id_len", C.POINTER(C.c_uint8)), ("root_service_name", C.POINTER(C.c_char_p)),
+                ("root_trace_name", C.POINTER(C.c_char_p)), ("start_time_unix_nano", C.POINTER(C.c_uint64)),
+                ("duration_ms", C.POINTER(C.c_uint32)), ("object_idx", C.POINTER(C.c_uint32)),
+                ("inspected_traces", C.c_uint64), ("inspected_bytes", C.c_uint64), ("skipped_traces", C.c_uint64),
+                ("kernel_ns", C.c_uint64)]
+
+
 class _LookupResult(C.Structure):
     _fields_ = [("n", C.c_uint64), ("id_idx", C.POINTER(C.c_uint32)), ("block_idx", C.POINTER(C.c_uint32)),
                 ("record_idx", C.POINTER(C.c_int32)), ("record_start", C.POINTER(C.c_uint64)),
@@ -124,7 +142,8 @@ EXPORTED = [
     "tsg_block_open", "tsg_block_open_mem", "tsg_block_clone", "tsg_wal_block_open", "tsg_wal_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
     "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_kernel_times", "tsg_results_combine",
     "tsg_v2block_open", "tsg_v2block_close", "tsg_lookup_ids", "tsg_lookup_result_free", "tsg_find_ids",
-    "tsg_find_result_free",
+    "tsg_find_result_free", "tsg_proto_block_open", "tsg_proto_block_close", "tsg_proto_block_info",
+    "tsg_proto_search", "tsg_proto_result_free", "tsg_go_parse", "tsg_write_v2_block",
     "tsg_write_search_block", "tsg_write_wal_search", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
     "tsg_synth_v2_block",
 ]
@@ -175,6 +194,14 @@ def lib():
         L.tsg_find_ids.argtypes = [vp, C.POINTER(vp), C.c_size_t, vp, C.c_size_t, C.POINTER(_LookupOpts),
                                    C.POINTER(C.POINTER(_FindResult))]
         L.tsg_find_result_free.argtypes = [C.POINTER(_FindResult)]
+        L.tsg_proto_block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
+        L.tsg_proto_block_close.argtypes = [vp]
+        L.tsg_proto_block_info.argtypes = [vp, C.POINTER(C.c_uint64)]
+        L.tsg_proto_search.argtypes = [vp, vp, C.POINTER(_ProtoRequest), C.POINTER(C.POINTER(_ProtoResult))]
+        L.tsg_proto_result_free.argtypes = [C.POINTER(_ProtoResult)]
+        L.tsg_go_parse.argtypes = [C.c_int, C.c_char_p, C.c_size_t, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+        L.tsg_write_v2_block.argtypes = [C.c_char_p, vp, C.c_char_p, C.POINTER(C.c_uint64), C.c_size_t, C.c_int,
+                                         C.c_char_p, C.c_uint32]
         L.tsg_write_search_block.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int, C.c_uint32]
         L.tsg_fb_search_entry.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]
         L.tsg_fb_search_header.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]
@@ -327,6 +354,8 @@ class Engine:
             o.num_devices, o.devices = len(devices), self._devs
         self.h = C.c_void_p()
         self._raw_calls = {}  # search_raw: prebuilt ctypes arguments (handle values only)
+        # open blocks (weak): closed before tsg_shutdown frees the device contexts they use
+        self._open = weakref.WeakSet()
         _check(lib().tsg_init(C.byref(o), C.byref(self.h)))
 
     @property
@@ -470,8 +499,46 @@ class Engine:
         finally:
             lib().tsg_find_result_free(rp)
 
+    def open_proto_block(self, path: str, device: int = 0) -> "ProtoBlock":
+        return ProtoBlock(self, path, device)
+
+    def proto_search(self, block: "ProtoBlock", tags: Optional[dict] = None, min_ms: int = 0,
+                     max_ms: int = 0, start: int = 0, end: int = 0, limit: int = 20,
+                     start_page: int = 0, total_pages: int = 0, max_bytes: int = 0,
+                     chunk_size_bytes: int = 0) -> ProtoSearchResponse:
+        """v2.BackendBlock.Search of one block (tsg_proto_search); raises TsgError where the
+        reference's Search returns an error."""
+        items = [(k.encode() if isinstance(k, str) else k, v.encode() if isinstance(v, str) else v)
+                 for k, v in (tags or {}).items()]
+        n = len(items)
+        keys = (C.c_char_p * max(n, 1))(*[k for k, _ in items])
+        vals = (C.c_char_p * max(n, 1))(*[v for _, v in items])
+        kl = (C.c_uint32 * max(n, 1))(*[len(k) for k, _ in items])
+        vl = (C.c_uint32 * max(n, 1))(*[len(v) for _, v in items])
+        req = _ProtoRequest(n, keys, kl, vals, vl, min_ms, max_ms, start, end, limit, start_page,
+                            total_pages, max_bytes, chunk_size_bytes)
+        rp = C.POINTER(_ProtoResult)()
+        _check(lib().tsg_proto_search(self.h, block.h, C.byref(req), C.byref(rp)))
+        try:
+            r = rp.contents
+            traces, objs = [], []
+            for i in range(r.n):
+                tl = r.trace_id_len[i]
+                tid = C.string_at(C.addressof(r.trace_ids.contents) + r.trace_id_off[i], tl) if tl else b""
+                traces.append(TraceSearchMetadata(
+                    trace_id=tid, trace_id_len=tl, root_service_name=r.root_service_name[i].decode("utf-8", "surrogateescape"),
+                    root_trace_name=r.root_trace_name[i].decode("utf-8", "surrogateescape"),
+                    start_time_unix_nano=r.start_time_unix_nano[i], duration_ms=r.duration_ms[i]))
+                objs.append(r.object_idx[i])
+            return ProtoSearchResponse(traces, r.inspected_traces, r.inspected_bytes, r.skipped_traces, objs,
+                                       r.kernel_ns)
+        finally:
+            lib().tsg_proto_result_free(rp)
+
     def close(self):
         self._raw_calls = {}
+        for b in list(getattr(self, "_open", ())):
+            b.close()
         if getattr(self, "h", None):
             lib().tsg_shutdown(self.h)
             self.h = None
@@ -485,9 +552,10 @@ class BackendSearchBlock:
         self.h = C.c_void_p()
         if _clone_of is not None:
             _check(lib().tsg_block_clone(eng.h, _clone_of.h, device, C.byref(self.h)))
-            return
-        opener = lib().tsg_wal_block_open if _wal else lib().tsg_block_open
-        _check(opener(eng.h, path.encode(), device, C.byref(self.h)))
+        else:
+            opener = lib().tsg_wal_block_open if _wal else lib().tsg_block_open
+            _check(opener(eng.h, path.encode(), device, C.byref(self.h)))
+        eng._open.add(self)
 
     def clone(self, eng: Engine, device: int = 0) -> "BackendSearchBlock":
         """tsg_block_clone: a second resident copy (device-to-device), e.g. on another GPU."""
@@ -532,10 +600,45 @@ class StreamingSearchBlock(BackendSearchBlock):
         super().__init__(eng, path, device, _wal=True)
 
 
+@dataclass
+class ProtoSearchResponse:
+    """tempopb.SearchResponse of one v2.BackendBlock.Search (traces in object order)."""
+    traces: List[TraceSearchMetadata]
+    inspected_traces: int
+    inspected_bytes: int
+    skipped_traces: int
+    object_idx: List[int]
+    kernel_ns: int = 0
+
+
+class ProtoBlock:
+    """A v2 trace block whose objects are trace protos (tsg_proto_block), resident on one
+    device: the querier's SearchBlock path (tempodb.Search -> BackendBlock.Search)."""
+
+    def __init__(self, eng: Engine, path: str, device: int = 0):
+        self.path = path
+        self.h = C.c_void_p()
+        _check(lib().tsg_proto_block_open(eng.h, path.encode(), device, C.byref(self.h)))
+        eng._open.add(self)
+
+    def info(self) -> dict:
+        o = (C.c_uint64 * 4)()
+        _check(lib().tsg_proto_block_info(self.h, o))
+        return {"objects": o[0], "pages": o[1], "keys": o[2], "device_bytes": o[3]}
+
+    def close(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.tsg_proto_block_close(self.h)
+            self.h = None
+
+    __del__ = close
+
+
 class V2Block:
     def __init__(self, eng: Engine, path: str, device: int = 0):
         self.h = C.c_void_p()
         _check(lib().tsg_v2block_open(eng.h, path.encode(), device, C.byref(self.h)))
+        eng._open.add(self)
 
     def close(self):
         if getattr(self, "h", None) and _lib is not None:
@@ -608,6 +711,31 @@ def fb_search_header(entries: Iterable[dict]) -> bytes:
 def synth_search_block(path: str, n: int, seed: int = 0, profile: int = 0, encoding: int = ENC_SNAPPY,
                        page_size: int = 1024 * 1024):
     _check(lib().tsg_synth_search_block(path.encode(), n, seed, profile, encoding, page_size))
+
+
+def write_v2_block(path: str, ids, objects: Sequence[bytes], encoding: int = 0, data_encoding: str = "v2",
+                   index_downsample_bytes: int = 0):
+    """tsg_write_v2_block: a v2 block of the given objects (ids: (n, 16) uint8, ascending)."""
+    import numpy as np
+    ids = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1, 16)
+    blob = b"".join(objects)
+    off = [0]
+    for o in objects:
+        off.append(off[-1] + len(o))
+    offs = (C.c_uint64 * len(off))(*off)
+    _check(lib().tsg_write_v2_block(path.encode(), ids.ctypes.data, blob, offs, ids.shape[0], encoding,
+                                    data_encoding.encode(), index_downsample_bytes))
+
+
+def go_parse(kind: str, s) -> tuple:
+    """Go strconv as the engine implements it: kind "int" | "float" | "bool" -> (ok, value)."""
+    b = s.encode() if isinstance(s, str) else s
+    f, i = C.c_double(), C.c_int64()
+    k = {"int": 0, "float": 1, "bool": 2}[kind]
+    ok = lib().tsg_go_parse(k, b, len(b), C.byref(f), C.byref(i))
+    if ok < 0:
+        raise ValueError(kind)
+    return bool(ok), (f.value if kind == "float" else (bool(i.value) if kind == "bool" else i.value))
 
 
 def synth_v2_block(path: str, n: int, seed: int = 0):
