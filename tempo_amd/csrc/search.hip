@@ -110,6 +110,10 @@ struct ScanParams {
   // this evens a CU out, but the kernel's end is set by the chip-wide tail, which it
   // does not move (profiles/r02_prio: kernel p50 38.7-39.8 vs 38.5-38.6 us off)
   uint32_t prio;
+  // 1: the last workgroup raises header word 2 through the completion counters; 0 (segment
+  // mode): the host completes on the per-workgroup counts alone (each stored after its
+  // records), so no counter round trips sit at the end of the launch
+  uint32_t flag_done, pad4;
   unsigned *steal;  // tail claim counters, one per block slot (128 B apart), monotonic
 };
 
@@ -1301,6 +1305,7 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   // only) and the last of each group arrives at the top counter, so no single word
   // takes a thousand atomics at the end of the launch. Every workgroup's record and
   // count stores (system-scope write-through) have completed before it arrives.
+  if (!A.P.flag_done) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -1909,6 +1914,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     h[1] = 0;  // look-back / granule poll error flag
     h[2] = 0;  // completion flag (one-launch path)
     if (fast && P.seg_cap) std::fill_n(P.counts, nwg, kCountPending);  // (each workgroup stores its count last)
+    static const bool flag_env = std::getenv("TSG_FLAG_DONE") != nullptr;
+    P.flag_done = fast && (!P.seg_cap || flag_env) ? 1u : 0u;
     if (fast) {
       for (uint32_t i = 0; i < nsegs; i++) A.steal_base[i] = dc.steal_base[i];
       uint32_t ng = 0;
@@ -1944,7 +1951,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       if (timed || defer) HIP_OK(hipEventRecord(e1, s));
       else if (dc.mark_mode & 2) HIP_OK(hipEventRecord(dc.mk1, s));
     }
-    if (fast) {  // the launch advances every counter by a known amount
+    if (fast && P.flag_done) {  // the launch advances every counter by a known amount
       for (uint32_t g = 0; g < 8; g++) dc.done_base[g] = P.done_target[g];
       dc.done_base[8] = P.done_top;
     }
@@ -1967,12 +1974,15 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     // count stores (system-scope write-through) complete (s_waitcnt vmcnt(0), memory
     // clobber) before its arrival at the completion counters, and the flag store is
     // issued by the last arrival, so the flag is the last of the launch's host writes.
+    // Without the flag (P.flag_done 0): done once every workgroup's count has been seen —
+    // each count is stored after that workgroup's records completed, and the counts are
+    // read with acquire loads, so the copy below reads complete records.
     const uint64_t *flag = reinterpret_cast<const uint64_t *>(P.out) + 2;
-    auto flag_up = [&] { return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == P.epoch; };
+    auto flag_up = [&] { return P.flag_done && __atomic_load_n(flag, __ATOMIC_ACQUIRE) == P.epoch; };
     // while the tail of the launch runs, pull the record segments of workgroups that
     // have finished into this core's caches (the copy after the flag then reads cached
     // lines instead of missing on every one)
-    const volatile uint32_t *cnt = P.counts;
+    const uint32_t *cnt = P.counts;
     const uint8_t *rec = P.out + P.hdr_bytes;
     thread_local std::vector<uint8_t> seen;
     seen.assign(nwg, 0);
@@ -1984,18 +1994,22 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
           if (w == lo) lo++;
           continue;
         }
-        const uint32_t c = cnt[w];
+        const uint32_t c = __atomic_load_n(cnt + w, __ATOMIC_ACQUIRE);
         if (c == kCountPending) continue;
         seen[w] = 1;
         if (w == lo) lo++;
         const uint8_t *p0 = rec + uint64_t(w) * P.seg_cap * sizeof(MatchRec);
         for (uint64_t o = 0; o < uint64_t(std::min(c, P.seg_cap)) * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
       }
+      if (!P.flag_done && lo == nwg) return;
       if ((it & 255u) == 0) {
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) {
-          if (flag_up()) return;
-          fail(TSG_E_DEVICE, "search kernel completed without raising its completion flag");
+          if (flag_up() || lo == nwg) return;
+          bool all = true;
+          for (uint32_t w = 0; w < nwg && all; w++) all = __atomic_load_n(cnt + w, __ATOMIC_ACQUIRE) != kCountPending;
+          if (all) return;
+          fail(TSG_E_DEVICE, "search kernel completed without storing every workgroup count");
         }
         if (e != hipErrorNotReady) HIP_OK(e);
       }
