@@ -136,10 +136,11 @@ def parse():
                          "the average over those launches); 0 = off")
     ap.add_argument("--limit-steps", type=int, default=20,
                     help="extra timed searches with limit=20 (early exit, config-3 mode); 0 = skip")
-    ap.add_argument("--cfg3", type=int, default=1,
+    ap.add_argument("--cfg3", type=int, default=None,
                     help="config-3 leg on this GPU's share: --cfg3-blocks resident blocks of --cfg3-entries "
                          "(one generated block + device clones), full scan x --cfg3-steps back-to-back queries "
-                         "and limit=20 (time to the first 20); 0 = skip")
+                         "and limit=20 (time to the first 20); 0 = skip (default: on at N=1 only — the "
+                         "multi-GPU runs keep to the config-2 line and its disk/HBM footprint)")
     ap.add_argument("--cfg3-blocks", type=int, default=25)
     ap.add_argument("--cfg3-entries", type=int, default=5_000_000)
     ap.add_argument("--cfg3-steps", type=int, default=64)
@@ -258,7 +259,21 @@ def cpu_baselines(paths, got, threads):
     return out
 
 
-def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags):
+def cfg3_path(workdir, rank):
+    return os.path.join(workdir, f"r{rank}cfg3")
+
+
+def cfg3_generate(args, workdir, rank):
+    """The config-3 block (one 5 M-entry block; the single-threaded writer takes ~1 min),
+    started in a thread at bench start so it overlaps the config-2 legs."""
+    import tempo_amd as T
+    p = cfg3_path(workdir, rank)
+    if not os.path.exists(os.path.join(p, "search.meta.json")):
+        T.synth_search_block(p, args.cfg3_entries, seed=7000 + rank, profile=0, encoding=T.ENC_SNAPPY,
+                             page_size=1024 * 1024)
+
+
+def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, gen_thread=None):
     """BASELINE config 3 on this GPU's share (200 blocks x 5 M over 8 GPUs = 25 x 5 M per
     GPU): one generated 5 M-entry block and device clones of it (tsg_block_clone: the
     clones share the host side), 125 M entries resident. Full scan: --cfg3-steps
@@ -267,11 +282,11 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags):
     import torch
     import tempo_amd as T
     t0 = time.time()
-    p = os.path.join(workdir, f"r{rank}cfg3")
-    if not os.path.exists(os.path.join(p, "search.meta.json")):
-        T.synth_search_block(p, args.cfg3_entries, seed=7000 + rank, profile=0, encoding=T.ENC_SNAPPY,
-                             page_size=1024 * 1024)
-    gen_s = time.time() - t0
+    p = cfg3_path(workdir, rank)
+    if gen_thread is not None:
+        gen_thread.join()
+    cfg3_generate(args, workdir, rank)  # (no-op when the thread wrote it)
+    gen_s = time.time() - t0  # (time still waited for the generator here)
     t0 = time.time()
     b0 = eng.open_block(p)
     blocks = [b0] + [b0.clone(eng) for _ in range(args.cfg3_blocks - 1)]
@@ -312,7 +327,7 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags):
     res = {
         "workload": f"config 3 per-GPU share: {len(blocks)} blocks x {args.cfg3_entries} entries "
                     f"(1 generated + {len(blocks) - 1} device clones), config-2 query",
-        "entries_per_gpu": entries, "matches_full": len(got),
+        "entries_per_gpu": entries, "matches_full": len(got), "wait_for_generator_s": gen_s,
         "full_scan": {"queries": args.cfg3_steps, "entries_per_s": entries * args.cfg3_steps * world / elapsed,
                       "step_us": pct([x * 1e6 for x in step]), "kernel_us": pct([x / 1e3 for x in kns]),
                       "scan_bytes": scan_bytes, "achieved_gbps": ach,
@@ -331,6 +346,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cfg3 is None:
+        args.cfg3 = 1 if world == 1 else 0
     import torch
     dist = None
     if world > 1:
@@ -344,6 +361,10 @@ def main():
     workdir = args.workdir or tempfile.mkdtemp(prefix="tsg_bench_", dir="/tmp")
     os.makedirs(workdir, exist_ok=True)
     threads = min(args.blocks, max(1, min(16, (os.cpu_count() or 8)) // max(1, min(world, 8))))
+    cfg3_thread = None
+    if args.cfg3:
+        cfg3_thread = threading.Thread(target=cfg3_generate, args=(args, workdir, rank), daemon=True)
+        cfg3_thread.start()
     t0 = time.time()
     paths = gen_blocks(workdir, rank, args.blocks, args.entries, threads)
     log(f"rank {rank}: generated {args.blocks} x {args.entries} entries in {time.time() - t0:.1f}s")
@@ -495,7 +516,7 @@ def main():
                           "entries_per_s": entries / (sum(ls) / len(ls))}
 
     if args.cfg3:
-        out["cfg3"] = cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags)
+        out["cfg3"] = cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, cfg3_thread)
 
     if rank == 0 and world == 1 and args.cpu_baseline:
         os.sched_setaffinity(0, all_cpus)  # (the CPU baselines get the whole host share back)
