@@ -141,6 +141,11 @@ def parse():
                          "(one generated block + device clones), full scan x --cfg3-steps back-to-back queries "
                          "and limit=20 (time to the first 20); 0 = skip (default: on at N=1 only — the "
                          "multi-GPU runs keep to the config-2 line and its disk/HBM footprint)")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="concurrent leg: query streams (device contexts on this GPU, each with its own HIP "
+                         "stream, pinned output and resident copy of the set) driven by as many host threads")
+    ap.add_argument("--concurrent-steps", type=int, default=64,
+                    help="queries per stream in the concurrent leg (0 = skip)")
     ap.add_argument("--cfg3-blocks", type=int, default=25)
     ap.add_argument("--cfg3-entries", type=int, default=5_000_000)
     ap.add_argument("--cfg3-steps", type=int, default=64)
@@ -259,6 +264,62 @@ def cpu_baselines(paths, got, threads):
     return out
 
 
+def concurrent_leg(args, base, pipe, streams, entries, dist, world, local):
+    """Serving throughput: `streams` query streams on this GPU, each a device context of
+    its own (HIP stream, pinned result buffers) searching its own resident copy of the
+    config-2 set, one host thread each, --concurrent-steps full-scan queries per stream.
+    One query's host work (plan, launch, result assembly) overlaps other streams'
+    kernels, so the rate approaches the kernel's; the per-query work is the same as the
+    main line's (SURVEY.md 8(d) batched mode: back-to-back queries)."""
+    import torch
+    import tempo_amd as T
+    # (its own engine, created after the main legs: they run with one device context)
+    eng = T.Engine(devices=[local] * streams)
+    csets = [[b.clone(eng, device=i) for b in base] for i in range(streams)]
+    for i, cs in enumerate(csets):  # warm every stream (plans, pinned buffers)
+        for _ in range(3):
+            eng.search_raw(cs, pipe)
+    errs = []
+    n = args.concurrent_steps
+    go = threading.Barrier(streams + 1)
+
+    def worker(i):
+        try:
+            go.wait()
+            for _ in range(n):
+                eng.search_raw(csets[i], pipe)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(streams)]
+    for t in ths:
+        t.start()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    go.wait()
+    for t in ths:
+        t.join()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    if dist:
+        dist.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    for cs in csets:
+        for b in cs:
+            b.close()
+    eng.close()
+    return {"streams": streams, "queries_per_stream": n,
+            "entries_per_s": entries * n * streams * world / elapsed,
+            "queries_per_s": n * streams * world / elapsed,
+            "note": "one resident copy of the config-2 set per stream; full scans, same query as the main line"}
+
+
 def cfg3_path(workdir, rank):
     return os.path.join(workdir, f"r{rank}cfg3")
 
@@ -369,6 +430,7 @@ def main():
     paths = gen_blocks(workdir, rank, args.blocks, args.entries, threads)
     log(f"rank {rank}: generated {args.blocks} x {args.entries} entries in {time.time() - t0:.1f}s")
 
+    streams = max(1, args.streams) if args.concurrent_steps else 1
     eng = T.Engine(devices=[local])
     t0 = time.time()
     base = parallel(eng.open_block, paths)
@@ -514,6 +576,9 @@ def main():
         out["limit20"] = {"steps": args.limit_steps, "matches": nl, "traces_inspected": metl.inspected_traces,
                           "step_us": pct([x * 1e6 for x in ls]), "kernel_us": pct([x / 1e3 for x in lk]),
                           "entries_per_s": entries / (sum(ls) / len(ls))}
+
+    if args.concurrent_steps and streams > 1:
+        out["concurrent"] = concurrent_leg(args, base, pipe, streams, entries, dist, world, local)
 
     if args.cfg3:
         out["cfg3"] = cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, cfg3_thread)

@@ -1082,25 +1082,28 @@ __device__ __forceinline__ void self_finish(SelfStage<NTA> &X, const QArgs &A, c
   __syncthreads();
 }
 
+// Leading scalar arguments: the first kernel-argument dwords are preloaded into SGPRs at
+// wave launch (-mllvm -amdgpu-kernarg-preload-count, gfx950; firmware without preload
+// runs the compiler's compatibility prologue instead). With a uniform block split
+// (kPreUniform) a workgroup finds its block from these alone, so its first memory round
+// trip already fetches the block's arguments.
+enum : uint32_t { kPreTicket = 1, kPreNarrow = 2, kPreBmFirst = 4, kPreSelf = 8, kPreUniform = 16, kPreStamps = 32 };
 template <int NT, bool DUR, bool RANGE, bool W1, bool SEG>
-__global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+__global__ void __launch_bounds__(kThreads, 3)
+    search_fast_kernel(uint32_t k_flags, uint32_t k_nsegs, uint32_t k_njobs, uint32_t k_wgs, uint32_t k_half,
+                       uint32_t k_bm_words, uint32_t k_mask_words, uint32_t k_nterms,
+                       unsigned long long *k_stamps, QArgs A) {
+  // (stamps only: s_memrealtime is a scalar memory operation)
+  const unsigned long long t_start = k_stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   // Every kernel argument the prologue branches on arrives in ONE round trip: scalar
   // loads return out of order, so each s_waitcnt lgkmcnt waits for every load issued,
   // and loads issued behind a branch would each add a round trip before the first tile
   // load (the empty asm statements pin them all in front of the first use)
-  uint32_t use_ticket = A.P.use_ticket, njobs = A.njobs, nsegs = A.nsegs, narrow_arg = A.narrow;
-  uint32_t bm_words = A.bm_words, mask_words = A.mask_words, nterms = A.nterms, bm_first = A.bm_first,
-           self_dict = A.self_dict;
-  unsigned long long *stamps = A.P.stamps;
-  uint32_t fw[kArgSegs];
-#pragma unroll
-  for (int s2 = 0; s2 < kArgSegs; s2++) fw[s2] = A.first_wg[s2];
-  asm volatile("" : "+s"(use_ticket), "+s"(njobs), "+s"(nsegs), "+s"(narrow_arg), "+s"(stamps));
-  asm volatile("" : "+s"(bm_words), "+s"(mask_words), "+s"(nterms), "+s"(bm_first), "+s"(self_dict));
-#pragma unroll
-  for (int s2 = 0; s2 < kArgSegs; s2++) asm volatile("" : "+s"(fw[s2]));
+  const uint32_t use_ticket = k_flags & kPreTicket, njobs = k_njobs, nsegs = k_nsegs,
+                 narrow_arg = k_flags & kPreNarrow, bm_words = k_bm_words, mask_words = k_mask_words,
+                 nterms = k_nterms, bm_first = k_flags & kPreBmFirst, self_dict = k_flags & kPreSelf;
+  unsigned long long *const stamps = k_stamps;
   const uint32_t vb = wg_order(A.P, use_ticket != 0);  // (a ticket when dictionary or look-back waits exist)
   if (vb < njobs) {  // dictionary workgroup: [value bits | stage]
     dict_job(A, vb, lds + bm_words, lds);
@@ -1110,14 +1113,24 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
   uint32_t *lds_bm = lds;
   uint16_t *lds_mask = reinterpret_cast<uint16_t *>(lds + bm_words);
   uint32_t *lds_seg = lds + bm_words + mask_words;
-  uint32_t *lds_fw = lds_seg + ((A.nsegs + 1) & ~1u);  // (even: lds_cap below is 8-byte aligned)
-  unsigned long long *lds_cap = reinterpret_cast<unsigned long long *>(lds_fw + ((A.nsegs + 2) & ~1u));
-  unsigned long long *lds_rec = lds_cap + A.nsegs;  // segment mode: kSegMax staged records
+  uint32_t *lds_fw = lds_seg + ((nsegs + 1) & ~1u);  // (even: lds_cap below is 8-byte aligned)
+  unsigned long long *lds_cap = reinterpret_cast<unsigned long long *>(lds_fw + ((nsegs + 2) & ~1u));
+  unsigned long long *lds_rec = lds_cap + nsegs;  // segment mode: kSegMax staged records
   const int tid = threadIdx.x;
   const uint32_t wg = vb - njobs;
   uint32_t si = 0;
+  if (k_flags & kPreUniform) {
+    // first_wg[s] = (k_wgs * s + k_half) / nsegs: the block whose range holds wg
+    si = min(nsegs - 1, ((wg + 1) * nsegs - k_half - 1) / k_wgs);
+  } else {
+    uint32_t fw[kArgSegs];
 #pragma unroll
-  for (int s2 = 1; s2 < kArgSegs; s2++) si += (uint32_t(s2) < nsegs && fw[s2] <= wg) ? 1u : 0u;
+    for (int s2 = 0; s2 < kArgSegs; s2++) fw[s2] = A.first_wg[s2];
+#pragma unroll
+    for (int s2 = 0; s2 < kArgSegs; s2++) asm volatile("" : "+s"(fw[s2]));
+#pragma unroll
+    for (int s2 = 1; s2 < kArgSegs; s2++) si += (uint32_t(s2) < nsegs && fw[s2] <= wg) ? 1u : 0u;
+  }
   // wave-uniform: descriptor reads become scalar loads (one round trip, not vmcnt-serialised)
   si = __builtin_amdgcn_readfirstlane(si);
   const DevBlockDesc *B = A.blk[si];
@@ -1255,17 +1268,17 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
       return;
     }
     if (NT > 0 && self_dict) {  // (self_finish ends with a barrier)
-      self_finish<NTA>(X, A, T, lds_bm, lds + A.bm_words, wg);
+      self_finish<NTA>(X, A, T, lds_bm, lds + bm_words, wg);
       return;
     }
     if (NT > 0) {
       const unsigned long long tag = (unsigned long long)A.P.epoch << 32;
-      for (uint32_t i = tid; i < gw[A.nterms]; i += kThreads) {
+      for (uint32_t i = tid; i < gw[nterms]; i += kThreads) {
         uint32_t q = 0;
 #pragma unroll
         for (int q2 = 1; q2 < NTA; q2++)
           if (i >= gw[q2]) q = q2;
-        const unsigned long long *g = A.gbm + uint64_t(si * A.nterms + q) * A.gstride + (i - gw[q]);
+        const unsigned long long *g = A.gbm + uint64_t(si * nterms + q) * A.gstride + (i - gw[q]);
         unsigned long long v;
         uint32_t spins = 0;
         while (((v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~0xffffffffull) != tag) {
@@ -1284,7 +1297,7 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
     }
     __syncthreads();
   };
-  scan_emit<NT, DUR, RANGE, W1, SEG>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, A.nsegs}, lds_bm, lds_mask, lds_seg,
+  scan_emit<NT, DUR, RANGE, W1, SEG>(A.P, S, T, si, ArgSegs{lds_fw, lds_cap, nsegs}, lds_bm, lds_mask, lds_seg,
                                      lds_rec, t_start, stamps, wg, issue_stage, wait_bitmaps, [&] {
                                        if (narrow) {  // (the asm keeps the loads below the scan loop)
                                          const DevBlockDesc *Bd = B;
@@ -1292,12 +1305,12 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
                                          cold(Bd);
                                        }
                                        if constexpr (!SEG) {
-                                         for (uint32_t i = tid; i < A.nsegs; i += kThreads) {
+                                         for (uint32_t i = tid; i < nsegs; i += kThreads) {
                                            lds_seg[i] = 0;
                                            lds_fw[i] = A.first_wg[i];
                                            lds_cap[i] = A.cap[i];
                                          }
-                                         if (tid == 0) lds_fw[A.nsegs] = A.first_wg[A.nsegs];
+                                         if (tid == 0) lds_fw[nsegs] = A.first_wg[nsegs];
                                        }
                                      });
   // completion: the last scan workgroup raises the flag the host polls (header word 2 =
@@ -1328,7 +1341,8 @@ __global__ void __launch_bounds__(kThreads, 3) search_fast_kernel(QArgs A) {
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 using ScanFn = void (*)(ScanParams);
-using FastFn = void (*)(QArgs);
+using FastFn = void (*)(uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
+                        unsigned long long *, QArgs);
 template <int NT, bool W1, bool SEG>
 static FastFn pick3_fast(bool dur, bool range) {
   if (dur && range) return search_fast_kernel<NT, true, true, W1, SEG>;
@@ -1929,13 +1943,31 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     P.ticket = static_cast<unsigned long long *>(dc.ticket.p);
     P.ticket_base = dc.ticket_base;
     P.use_ticket = (!fast || !P.seg_cap || A.njobs) ? 1u : 0u;
+    // the fast kernel's preloaded scalar arguments (search_fast_kernel)
+    uint32_t pre[8] = {};
+    if (fast) {
+      const uint32_t n = A.nsegs, W = A.first_wg[A.nsegs], h = n / 2;
+      bool uniform = n > 0 && W > 0 && uint64_t(W + 1) * n < (1ull << 32);
+      for (uint32_t i = 0; i <= n && uniform; i++) uniform = A.first_wg[i] == uint32_t((uint64_t(W) * i + h) / n);
+      pre[0] = (P.use_ticket ? kPreTicket : 0u) | (A.narrow ? kPreNarrow : 0u) | (A.bm_first ? kPreBmFirst : 0u) |
+               (A.self_dict ? kPreSelf : 0u) | (uniform ? kPreUniform : 0u) | (P.stamps ? kPreStamps : 0u);
+      pre[1] = n;
+      pre[2] = A.njobs;
+      pre[3] = W;
+      pre[4] = h;
+      pre[5] = A.bm_words;
+      pre[6] = A.mask_words;
+      pre[7] = A.nterms;
+    }
     hipEvent_t e0 = dc.es0, e1 = dc.es1;
     const bool timed = first && time_scan;
     const bool defer = first && !timed && time_defer && dc.defer_slot(e0, e1);
     static const bool ext_events = std::getenv("TSG_EXT_EVENTS") != nullptr;
     if ((timed || defer) && ext_events) {  // events stamped from the dispatch packet (hipExtLaunchKernel)
       if (fast) A.P = P;
-      void *args[] = {fast ? static_cast<void *>(&A) : static_cast<void *>(&P)};
+      void *fargs[] = {&pre[0], &pre[1], &pre[2], &pre[3], &pre[4], &pre[5], &pre[6], &pre[7], &P.stamps, &A};
+      void *sargs[] = {&P};
+      void **args = fast ? fargs : sargs;
       const void *f = fast ? reinterpret_cast<const void *>(P.seg_cap ? fast_seg : fast_lb) : kfn;
       HIP_OK(hipExtLaunchKernel(f, dim3(grid), dim3(kThreads), args, size_t(lds_words) * 4, s, e0, e1, 0));
     } else {
@@ -1943,7 +1975,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       else if (dc.mark_mode & 1) HIP_OK(hipEventRecord(dc.mk0, s));
       if (fast) {
         A.P = P;
-        (P.seg_cap ? fast_seg : fast_lb)<<<grid, kThreads, size_t(lds_words) * 4, s>>>(A);
+        (P.seg_cap ? fast_seg : fast_lb)<<<grid, kThreads, size_t(lds_words) * 4, s>>>(
+            pre[0], pre[1], pre[2], pre[3], pre[4], pre[5], pre[6], pre[7], P.stamps, A);
       } else {
         scan_fn<<<grid, kThreads, size_t(lds_words) * 4, s>>>(P);
       }
