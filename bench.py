@@ -22,6 +22,7 @@ collective: the ranks' ordered match lists are independent per block.
 Prints ONE JSON line (rank 0).
 """
 import argparse
+import gc
 import json
 import os
 import shutil
@@ -69,7 +70,7 @@ def pct(xs):
         return None
     v = sorted(xs)
     at = lambda q: v[min(len(v) - 1, int(q * (len(v) - 1) + 0.5))]  # noqa: E731
-    return {"p10": at(0.1), "p50": at(0.5), "p90": at(0.9)}
+    return {"p10": at(0.1), "p50": at(0.5), "p90": at(0.9), "p99": at(0.99), "mean": sum(v) / len(v), "max": v[-1]}
 
 
 def node_cpus(node):
@@ -489,6 +490,11 @@ def main():
         torch.cuda.synchronize()
         return time.perf_counter() - t0, step_s
 
+    # Python's cyclic GC stays off through the timed legs (re-enabled before the CPU
+    # baselines): a collection pass over this process's heap is host noise that the
+    # library's real caller, a Go querier, does not have
+    gc.collect()
+    gc.disable()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -583,6 +589,7 @@ def main():
     if args.cfg3:
         out["cfg3"] = cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, cfg3_thread)
 
+    gc.enable()
     if rank == 0 and world == 1 and args.cpu_baseline:
         os.sched_setaffinity(0, all_cpus)  # (the CPU baselines get the whole host share back)
         out["cpu_baseline"] = cpu_baselines(paths, got, cpu_threads)
