@@ -288,7 +288,7 @@ def concurrent_leg(args, base, pipe, streams, entries, dist, world, local):
         try:
             go.wait()
             for _ in range(n):
-                eng.search_raw(csets[i], pipe)
+                eng.search_raw(csets[i], pipe, metrics=False)
         except Exception as e:  # noqa: BLE001
             errs.append(e)
 
@@ -485,7 +485,8 @@ def main():
         t0 = time.perf_counter()
         for i in range(nsteps):  # (tsg_search is synchronous: results are on the host when it returns)
             ts = time.perf_counter()
-            eng.search_raw(sets[i % rot], pipe, flags=sflags if args.events and i % args.events == 0 else 0)
+            eng.search_raw(sets[i % rot], pipe, flags=sflags if args.events and i % args.events == 0 else 0,
+                           metrics=False)
             step_s.append(time.perf_counter() - ts)
         torch.cuda.synchronize()
         return time.perf_counter() - t0, step_s

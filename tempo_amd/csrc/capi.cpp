@@ -143,6 +143,19 @@ struct ResultHolder {
     resize(i + 1);
     set(i, id, il, s, e, b, en, sv, svl, nm, nml);
   }
+  void clear() {  // (for reuse: sizes to zero, capacities kept)
+    pub = tsg_result{};
+    ids.clear();
+    id_len.clear();
+    for (auto *v : {&start, &end, &entry, &svc_off, &name_off}) v->clear();
+    for (auto *v : {&dur, &block, &svc_len, &name_len}) v->clear();
+    arena_size = 0;
+    svc_p.clear();
+    name_p.clear();
+    bstatus.clear();
+    berr_s.clear();
+    berr.clear();
+  }
   const char *svc(size_t i) const { return arena + svc_off[i]; }
   const char *name(size_t i) const { return arena + name_off[i]; }
   void finalize() {
@@ -173,6 +186,48 @@ struct ResultHolder {
   }
 };
 static_assert(offsetof(ResultHolder, pub) == 0, "pub first");
+
+// Result holders are recycled (a query per ~60 us allocates a dozen arrays and a name
+// arena; reusing them keeps allocation and first-touch page faults off the step)
+struct HolderPool {
+  std::mutex mu;
+  std::vector<ResultHolder *> free;
+  ~HolderPool() {
+    for (auto *h : free) delete h;
+  }
+};
+static HolderPool &holder_pool() {
+  static HolderPool *p = new HolderPool();  // (leaked on purpose: results may be freed at exit)
+  return *p;
+}
+static ResultHolder *acquire_holder() {
+  HolderPool &hp = holder_pool();
+  {
+    std::lock_guard<std::mutex> lk(hp.mu);
+    if (!hp.free.empty()) {
+      ResultHolder *h = hp.free.back();
+      hp.free.pop_back();
+      return h;
+    }
+  }
+  return new ResultHolder();
+}
+static void release_holder(ResultHolder *h) {
+  if (!h) return;
+  HolderPool &hp = holder_pool();
+  if (h->arena_cap <= (64u << 20) && h->start.capacity() <= (1u << 20)) {
+    h->clear();
+    std::lock_guard<std::mutex> lk(hp.mu);
+    if (hp.free.size() < 16) {
+      hp.free.push_back(h);
+      return;
+    }
+  }
+  delete h;
+}
+struct HolderRelease {
+  void operator()(ResultHolder *h) const { release_holder(h); }
+};
 
 struct LookupHolder {
   tsg_lookup_result pub{};
@@ -483,8 +538,8 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     check_cancel();
     const uint32_t limit = opts ? opts->limit : 0;
     const uint32_t flags = opts ? opts->flags : 0;
-    auto *res = new ResultHolder();
-    std::unique_ptr<ResultHolder> guard_res(res);
+    auto *res = acquire_holder();
+    std::unique_ptr<ResultHolder, HolderRelease> guard_res(res);
     tsg_metrics &m = res->pub.metrics;
     std::memset(&m, 0, sizeof m);
     res->set_blocks(nblocks);
@@ -665,11 +720,11 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
 void tsg_result_free(tsg_result *r) {
   if (prof_on()) {
     const auto t0 = std::chrono::steady_clock::now();
-    delete reinterpret_cast<ResultHolder *>(r);
+    release_holder(reinterpret_cast<ResultHolder *>(r));
     prof_add("result_free", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     return;
   }
-  delete reinterpret_cast<ResultHolder *>(r);
+  release_holder(reinterpret_cast<ResultHolder *>(r));
 }
 
 int tsg_kernel_times(tsg_ctx *ctx, uint64_t *ns, size_t cap, size_t *n) {

@@ -387,7 +387,7 @@ class Engine:
             lib().tsg_result_free(rp)
 
     def search_raw(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0,
-                   flags: int = 0):
+                   flags: int = 0, metrics: bool = True):
         """tsg_search without unpacking the matches into Python objects: returns
         (match count, SearchMetrics). The result arrays are assembled by libtsg as
         for any caller (what the Go shim would receive) and then freed. The ctypes
@@ -411,6 +411,10 @@ class Engine:
         rc = fn(*args)
         if rc:
             _check(rc)
+        if not metrics:  # (match count only)
+            n = rp.contents.n
+            free(rp)
+            return n, None
         r = rp.contents
         n, m = r.n, r.metrics
         met = SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 for st in $1; do
   envs=()
   [ "${st%%@*}" != "default" ] && for kv in ${st//,/ }; do case $kv in HIP_*) envs+=("$kv");; *) envs+=("TSG_${kv%%@*}");; esac; done
-  env "${envs[@]}" timeout -k 10 300 python bench.py --steps ${STEPS:-200} --warmup 10 --cpu-baseline 0 --limit-steps 0 \
+  env "${envs[@]}" timeout -k 10 300 python bench.py --steps ${STEPS:-200} --warmup 10 --cpu-baseline 0 --limit-steps 0 --cfg3 0 --concurrent-steps 0 \
     --mall-steps ${MALL:-0} --workdir /tmp/tsgw > gpurun_out/env_$st.json 2> gpurun_out/env_$st.err || { echo "$st failed"; tail -3 gpurun_out/env_$st.err; exit 1; }
   python3 -c "
 import json,sys
