@@ -43,8 +43,16 @@ PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # the one-launch path; TSG_NO_FAST=1 forces the general path (prep + search kernels).
 # The last template argument of the one-launch kernel is segment mode (per-workgroup
 # record segments; TSG_NO_SEG=1 forces look-back mode).
-KERNEL = ("search_kernel<3, true, true, true>" if os.environ.get("TSG_NO_FAST")
-          else "search_fast_kernel<3, true, true, true, %s>" % ("false" if os.environ.get("TSG_NO_SEG") else "true"))
+# Narrow full scans (limit 0) run the pool kernel (one workgroup per CU, CU-wide work
+# pool); TSG_NO_POOL=1 keeps them on the one-launch segment kernel.
+if os.environ.get("TSG_NO_FAST"):
+    KERNEL = "search_kernel<3, true, true, true>"
+elif os.environ.get("TSG_NO_SEG"):
+    KERNEL = "search_fast_kernel<3, true, true, true, false>"
+elif os.environ.get("TSG_NO_POOL") or os.environ.get("TSG_NO_NARROW"):
+    KERNEL = "search_fast_kernel<3, true, true, true, true>"
+else:
+    KERNEL = "search_pool_kernel<3, true, true, %s>" % ("false" if os.environ.get("TSG_POOL_NT", "1") == "0" else "true")
 # HBM-side bytes per launch of KERNEL from separate rocprofv3 --pmc passes
 # (FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE), written by
 # tools/pmc_summary.py --out; keyed by workload so other sizes report null.

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <set>
 #include <utility>
 
 #include "engine.hpp"
@@ -112,6 +113,29 @@ struct DeviceCtx {
   bool steal_off = std::getenv("TSG_STEAL") == nullptr;
   uint32_t seg_cap = 16;                                  // segment-mode records per workgroup (limit 0), adaptive
   bool seg_off = std::getenv("TSG_NO_SEG") != nullptr;    // one-launch path: always look-back mode
+  // pool path (search_pool_kernel: narrow full scans, one workgroup per CU). TSG_NO_POOL=1
+  // disables it; TSG_POOL_DYN = percent of the units claimed dynamically (default 20),
+  // TSG_POOL_CHUNK = log2 units per dynamic claim (4), TSG_POOL_LOOK = claims of lookahead (32),
+  // TSG_POOL_WAVES = waves per workgroup (16)
+  bool pool_off = std::getenv("TSG_NO_POOL") != nullptr;
+  uint32_t pool_skip = 0;  // queries left to skip the pool after a record-buffer overflow
+  static uint32_t env_u32(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi) {
+    const char *e = std::getenv(name);
+    if (!e) return dflt;
+    const long v = std::atol(e);
+    return v < long(lo) ? lo : v > long(hi) ? hi : uint32_t(v);
+  }
+  uint32_t pool_dyn_pct = env_u32("TSG_POOL_DYN", 20, 0, 100);
+  uint32_t pool_chunk_shift = env_u32("TSG_POOL_CHUNK", 4, 0, 10);
+  uint32_t pool_lookahead = env_u32("TSG_POOL_LOOK", 32, 0, 1024);
+  uint32_t pool_waves = env_u32("TSG_POOL_WAVES", 16, 2, 16);  // waves per workgroup (one workgroup per CU)
+  // TSG_POOL_NT=0: default-policy stream loads (non-temporal measured faster: kernel p50
+  // 32.8 vs 34.5 us, profiles/r02_pool)
+  bool pool_nt = env_u32("TSG_POOL_NT", 1, 0, 1) != 0;
+  uint32_t pool_seg = 32;  // host segment records per workgroup (adaptive: grows on overflow, halves when sparse)
+  DevBuf pool_head;  // two dynamic-chunk counters (128 B apart): a launch uses one, zeroes the other
+  uint32_t pool_parity = 0;
+  std::set<const void *> pool_attr;  // pool kernels whose dynamic LDS limit has been raised
   // TSG_PER_CU=k (1..16): scan workgroups per CU in the grid plan instead of the
   // occupancy (k above it oversubscribes: later workgroups start as earlier ones retire)
   int per_cu_override = [] {

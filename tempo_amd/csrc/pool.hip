@@ -1,0 +1,556 @@
+// pool.hip — MI355X (gfx950) pool search: narrow full scans (limit 0) of Tempo search
+// blocks with one workgroup per CU and a CU-wide work pool. The same predicates,
+// records and result order as search_fast_kernel (search.hip); see DESIGN.md §4.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "search_common.hpp"
+
+namespace tsg {
+
+// ------------------------------------------------------------------------------------
+// pool search: narrow full scans (limit 0) with a CU-wide work pool
+//
+// One 1024-thread workgroup per CU (16 waves; its LDS request keeps a second one off the
+// CU). The query's blocks form one space of 512-entry units (a wave tile: 8 entries per
+// lane). A workgroup owns a static run of units, handed out one unit per claim from an
+// LDS counter to whichever of its waves is free, so the waves of a CU finish together
+// whatever order the CU's issue arbitration serves them in (the static split's four
+// workgroups per CU finished as a ladder 22/25/28/33 us, profiles/r02_prio). The last
+// units of the launch are claimed in chunks from one device counter (dequeue: one
+// returning atomic per chunk, issued `lookahead` claims before the chunk is needed), so
+// CUs that the fabric serves faster take more of them. Matches go to the workgroup's LDS
+// record buffer as they are found (gathered from the cold columns right away; record
+// order inside a workgroup is claim order — the host sorts each block's records by scan
+// position, which is the reference order), then to the workgroup's segment of pinned
+// host memory with write-through stores, then its count. Records beyond the LDS capacity
+// are counted, not kept: the host then reruns the query on the segment/look-back path.
+constexpr int kPoolWaves = 16;
+constexpr int kPoolThreads = kPoolWaves * 64;
+constexpr uint32_t kPoolTile = 512;       // entries per unit (wave tile)
+constexpr uint32_t kPoolChunks = 1024;    // dynamic chunks one workgroup can take
+constexpr uint32_t kPoolPending = 0xffffffffu, kPoolNone = 0xfffffffeu;
+static_assert(kColPad % kPoolTile == 0, "column padding covers whole units");
+
+struct PoolBlk {           // 64 B, staged in LDS
+  const uint32_t *scan;    // dur32 | start_s | end_s, npad entries each
+  const uint8_t *col[4];   // one-byte term columns
+  uint32_t npad, nent;
+  uint32_t ubase;          // first unit of the block in the launch's unit space
+  uint32_t bmi4, nsets4;   // per term: bitmap index into `bms`, value-set count (bytes)
+  uint32_t block_idx;
+};
+static_assert(sizeof(PoolBlk) == 64, "pool block layout");
+struct PoolArgs {
+  PoolBlk blk[kArgSegs];
+  const DevBlockDesc *desc[kArgSegs];  // cold columns (ids, times, names) of matches
+  uint32_t bms[kArgBms][8];
+  uint32_t nsegs, units, static_per_wg, dyn0;  // static run of workgroup w: [w*S, w*S+S); dynamic [dyn0, units)
+  uint32_t chunk_shift, lookahead, rec_cap, seg_cap, has_min, has_max, min32, max32, start_s, end_s;
+  unsigned *head;       // this launch's dynamic-chunk counter (zero at launch)
+  unsigned *head_next;  // the next launch's counter: zeroed by this one
+  uint8_t *recs;        // pinned host: workgroup w's first seg_cap records at w * seg_cap (rec_cap: LDS records)
+  uint32_t *counts;     // pinned host: workgroup w's match count, stored after its records
+  unsigned long long *stamps;
+};
+static_assert(sizeof(PoolArgs) <= 4096, "kernel arguments");
+
+// A pointer read from LDS by every lane (same value), moved to SGPRs. (readfirstlane
+// returns int: each half goes through uint32_t, or the low half sign-extends.)
+template <typename T>
+__device__ __forceinline__ T *uniform_ptr(T *p) {
+  const uint64_t v = uint64_t(uintptr_t(p));
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(v)));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(v >> 32)));
+  return reinterpret_cast<T *>((uint64_t(hi) << 32) | lo);
+}
+
+template <int NT>
+struct PoolRegs {
+  u32x4 d[kSteps], s[kSteps], e[kSteps];
+  uint32_t tv[NT > 0 ? NT : 1][kSteps];
+  uint32_t blk, e0;  // wave-uniform: block slot, first entry of the unit in its block
+};
+
+// Stream loads: default cache policy, or non-temporal (NTL: `nt`, the once-read filter
+// columns do not displace the L2 / MALL lines other work reuses).
+template <bool NTL>
+__device__ __forceinline__ u32x4 stream4(const uint32_t *p, uint64_t e) {
+  if constexpr (NTL) return __builtin_nontemporal_load(G<u32x4>(p + e));
+  else return *G<u32x4>(p + e);
+}
+template <bool NTL>
+__device__ __forceinline__ uint32_t stream1(const uint8_t *p, uint64_t e) {
+  if constexpr (NTL) return __builtin_nontemporal_load(G<uint32_t>(p + e));
+  else return *G<uint32_t>(p + e);
+}
+
+template <int NT, bool DUR, bool RANGE, bool NTL>
+__global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A) {
+  const unsigned long long t_start = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  __shared__ __attribute__((aligned(16))) PoolBlk s_blk[kArgSegs];
+  __shared__ uint32_t s_ub[kArgSegs + 1];
+  __shared__ uint32_t s_bm[kArgBms * 8];
+  __shared__ uint32_t s_chunk[kPoolChunks];
+  __shared__ uint32_t s_next, s_nrec;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long s_rec[];  // rec_cap x 6 words
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = blockIdx.x, nsegs = A.nsegs, units = A.units;
+  // ---- stage the launch's tables (one vector round trip from the kernel arguments)
+  {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(A.blk);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(s_blk);
+    for (uint32_t i = tid; i < nsegs * 16; i += blockDim.x) dst[i] = src[i];
+    if (uint32_t(tid) <= nsegs) s_ub[tid] = uint32_t(tid) < nsegs ? A.blk[tid].ubase : units;
+    if (tid < kArgBms * 8) s_bm[tid] = reinterpret_cast<const uint32_t *>(A.bms)[tid];
+    for (uint32_t i = tid; i < kPoolChunks; i += blockDim.x) s_chunk[i] = kPoolPending;
+    if (tid == 0) {
+      s_next = 0;
+      s_nrec = 0;
+      if (w == 0) __hip_atomic_store(A.head_next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  unsigned long long *const stamps = A.stamps;
+  if (stamps && tid == 0) {
+    stamps[uint64_t(w) * kStampSlots] = t_start;
+    stamps[uint64_t(w) * kStampSlots + 1] = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+    const unsigned long long xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+    stamps[uint64_t(w) * kStampSlots + 8] = (xcc << 32) | hw;
+  }
+  const uint32_t S = A.static_per_wg, L = A.lookahead, cs = A.chunk_shift;
+  const uint32_t rec_cap = A.rec_cap;
+  // claim -> unit (or kPoolNone): claims below S are this workgroup's static run; claim
+  // S + k*C + off is unit `off` of its k-th dynamic chunk, which the claim L before the
+  // chunk's first one requested from the device counter (so a wave rarely waits for it)
+  auto claim = [&]() -> uint32_t {
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(&s_next, 1u);
+    c = __builtin_amdgcn_readfirstlane(c);
+    if (c + L >= S) {
+      const uint32_t t = c + L - S;
+      const uint32_t k = t >> cs;
+      if ((t & ((1u << cs) - 1)) == 0 && k < kPoolChunks) {
+        // chunks are requested in order (chunk k after chunk k-1 has its answer), so once
+        // one comes back empty every later one is empty too and a wave may stop at the
+        // first empty claim without stranding units this workgroup took
+        if (lane == 0) {
+          uint32_t prev = 0;
+          if (k > 0)
+            while ((prev = __hip_atomic_load(&s_chunk[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
+                   kPoolPending)
+              __builtin_amdgcn_s_sleep(2);
+          uint32_t val = kPoolNone;
+          if (prev != kPoolNone) {
+            const uint32_t g = __hip_atomic_fetch_add(A.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t u0 = uint64_t(A.dyn0) + (uint64_t(g) << cs);
+            if (u0 < units) val = uint32_t(u0);
+          }
+          __hip_atomic_store(&s_chunk[k], val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+    if (c < S) return w * S + c;
+    const uint32_t d = c - S, k = d >> cs;
+    if (k >= kPoolChunks) return kPoolNone;
+    uint32_t v;
+    while ((v = __hip_atomic_load(&s_chunk[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == kPoolPending)
+      __builtin_amdgcn_s_sleep(2);
+    v = __builtin_amdgcn_readfirstlane(v);
+    if (v == kPoolNone) return kPoolNone;
+    const uint32_t u = v + (d & ((1u << cs) - 1));
+    return u < units ? u : kPoolNone;
+  };
+  // unit -> block slot: lanes test the block boundaries, the ballot counts those passed
+  auto load = [&](PoolRegs<NT> &R, uint32_t u) {
+    const bool past = uint32_t(lane) < nsegs && u >= s_ub[lane + 1];
+    const uint32_t b = __popcll(__ballot(past));
+    R.blk = b;
+    const PoolBlk &B = s_blk[b];
+    const uint32_t npad = __builtin_amdgcn_readfirstlane(B.npad);
+    const uint32_t *scan = uniform_ptr(B.scan);
+    R.e0 = (u - __builtin_amdgcn_readfirstlane(B.ubase)) * kPoolTile;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) {
+      const uint64_t e = uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
+      if (DUR) R.d[k] = stream4<NTL>(scan, e);
+      if (RANGE) {
+        R.s[k] = stream4<NTL>(scan + npad, e);
+        R.e[k] = stream4<NTL>(scan + 2ull * npad, e);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
+      if (NT <= 0) break;
+      const uint8_t *col = uniform_ptr(B.col[q]);
+#pragma unroll
+      for (int k = 0; k < kSteps; k++)
+        R.tv[q][k] = stream1<NTL>(col, uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
+    }
+  };
+  auto eval = [&](const PoolRegs<NT> &R) {
+    const PoolBlk &B = s_blk[R.blk];
+    const uint32_t n = __builtin_amdgcn_readfirstlane(B.nent);
+    const uint32_t bmi4 = __builtin_amdgcn_readfirstlane(B.bmi4), ns4 = __builtin_amdgcn_readfirstlane(B.nsets4);
+    uint32_t mask = 0;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (R.e0 + uint32_t(k) * 256 + uint32_t(lane) * 4 + j < n) mask |= 1u << (4 * k + j);
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) {
+      const uint32_t dv[4] = {R.d[k].x, R.d[k].y, R.d[k].z, R.d[k].w};
+      const uint32_t sv[4] = {R.s[k].x, R.s[k].y, R.s[k].z, R.s[k].w};
+      const uint32_t ev[4] = {R.e[k].x, R.e[k].y, R.e[k].z, R.e[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        bool ok = true;
+        if (DUR) ok = (!A.has_min || dv[j] >= A.min32) && (!A.has_max || dv[j] <= A.max32);
+        if (RANGE) ok = ok && A.start_s <= ev[j] && A.end_s >= sv[j];  // req.Start <= endSeconds && req.End >= startSeconds
+#pragma unroll
+        for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
+          if (NT <= 0) break;
+          const uint32_t x = (R.tv[q][k] >> (8 * j)) & 0xffu;
+          const uint32_t wd = s_bm[((bmi4 >> (8 * q)) & 0xffu) * 8 + (x >> 5)];
+          ok = ok && (x < ((ns4 >> (8 * q)) & 0xffu)) && ((wd >> (x & 31)) & 1u);
+        }
+        if (!ok) mask &= ~(1u << (4 * k + j));
+      }
+    }
+    if (__ballot(mask != 0) == 0) return;
+    // matches: slots in the workgroup's LDS record buffer, record fields gathered now
+    const DevBlockDesc *D = A.desc[R.blk];
+    const auto *Dc = K4(D);
+    const uint8_t *ids = Dc->ids;
+    const uint64_t *st_ns = Dc->start_ns, *en_ns = Dc->end_ns;
+    const uint32_t *names = Dc->names;
+    const uint8_t *id_len = Dc->id_len;
+    const uint32_t bidx = __builtin_amdgcn_readfirstlane(B.block_idx);
+    const uint32_t cnt = __popc(mask);
+    uint32_t slot = 0;
+    if (cnt) slot = atomicAdd(&s_nrec, cnt);
+    for (int b = 0; b < 4 * kSteps; b++) {
+      if (!(mask & (1u << b))) continue;
+      const uint32_t r = slot++;
+      if (r >= rec_cap) continue;
+      const uint32_t ei = R.e0 + uint32_t(b >> 2) * 256 + uint32_t(lane) * 4 + uint32_t(b & 3);
+      const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
+      const uint64_t st = G(st_ns)[ei], en = G(en_ns)[ei];
+      const uint64_t nm = G(reinterpret_cast<const uint64_t *>(names))[ei];
+      const uint32_t il = G(id_len)[ei];
+      unsigned long long *d = s_rec + uint64_t(r) * 6;
+      d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
+      d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
+      d[2] = st;
+      d[3] = en;
+      d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
+      d[5] = nm;
+    }
+  };
+  // ---- scan: two units in flight per wave
+  PoolRegs<NT> ra, rb;
+  uint32_t ua = claim();
+  if (ua != kPoolNone) {
+    load(ra, ua);
+    uint32_t ub = claim();
+    if (ub != kPoolNone) load(rb, ub);
+    for (;;) {
+      eval(ra);
+      if (ub == kPoolNone) break;
+      ua = claim();
+      if (ua != kPoolNone) load(ra, ua);
+      eval(rb);
+      if (ua == kPoolNone) break;
+      ub = claim();
+      if (ub != kPoolNone) load(rb, ub);
+    }
+  }
+  __syncthreads();
+  if (stamps && tid == 0) {
+    stamps[uint64_t(w) * kStampSlots + 2] = __builtin_amdgcn_s_memrealtime();
+    stamps[uint64_t(w) * kStampSlots + 3] = __builtin_amdgcn_s_memrealtime();
+  }
+  // ---- records to the workgroup's host segment (write-through), then the count
+  const uint32_t total = s_nrec;
+  const uint32_t nw = min(total, min(rec_cap, A.seg_cap)) * 6;
+  if (nw) {
+    auto *dst = reinterpret_cast<unsigned long long *>(A.recs) + uint64_t(w) * A.seg_cap * 6;
+    for (uint32_t i = tid; i < nw; i += blockDim.x) host_store(dst + i, s_rec[i]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (tid == 0) {
+    host_store(A.counts + w, total);
+    if (stamps) stamps[uint64_t(w) * kStampSlots + 4] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// host
+using PoolFn = void (*)(PoolArgs);
+template <int NT, bool NTL>
+static PoolFn pick_pool3(bool dur, bool range) {
+  if (dur && range) return search_pool_kernel<NT, true, true, NTL>;
+  if (dur) return search_pool_kernel<NT, true, false, NTL>;
+  if (range) return search_pool_kernel<NT, false, true, NTL>;
+  return search_pool_kernel<NT, false, false, NTL>;
+}
+template <bool NTL>
+static PoolFn pick_pool_t(uint32_t nterms, bool dur, bool range) {
+  switch (nterms) {
+    case 0: return pick_pool3<0, NTL>(dur, range);
+    case 1: return pick_pool3<1, NTL>(dur, range);
+    case 2: return pick_pool3<2, NTL>(dur, range);
+    case 3: return pick_pool3<3, NTL>(dur, range);
+    default: return pick_pool3<4, NTL>(dur, range);
+  }
+}
+static PoolFn pick_pool(uint32_t nterms, bool dur, bool range, bool ntl) {
+  return ntl ? pick_pool_t<true>(nterms, dur, range) : pick_pool_t<false>(nterms, dur, range);
+}
+
+// One search_pool_kernel launch for a narrow full scan (limit 0). Returns false, with
+// nothing written to `out`, when a workgroup found more matches than its record buffer
+// holds: the caller then runs the segment / look-back path.
+bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
+                        uint32_t flags, const std::vector<ScanSeg> &segs, const std::vector<NarrowSeg> &nsegv,
+                        const std::vector<std::array<uint32_t, 8>> &nbms,
+                        const std::vector<std::array<uint8_t, kArgTerms>> &nbmi,
+                        const std::vector<const DevBlockDesc *> &seg_desc, bool has_dur, Tracer &tr, SearchOut &out) {
+  hipStream_t s = dc.stream;
+  const uint32_t nsegs = uint32_t(segs.size()), W = uint32_t(dc.num_cu);
+  PoolArgs PA;
+  std::memset(&PA, 0, sizeof PA);
+  uint32_t U = 0;
+  for (uint32_t i = 0; i < nsegs; i++) {
+    PoolBlk &b = PA.blk[i];
+    const NarrowSeg &ns = nsegv[i];
+    b.scan = ns.scan;
+    for (uint32_t t = 0; t < q.nterms; t++) {
+      b.col[t] = ns.ncol + uint64_t(ns.slot[t]) * ns.npad;
+      b.bmi4 |= uint32_t(nbmi[i][t]) << (8 * t);
+      b.nsets4 |= uint32_t(ns.nsets[t]) << (8 * t);
+    }
+    b.npad = ns.npad;
+    b.nent = uint32_t(segs[i].n);
+    b.ubase = U;
+    b.block_idx = segs[i].block_idx;
+    PA.desc[i] = seg_desc[i];
+    const uint64_t u = (segs[i].n + kPoolTile - 1) / kPoolTile;
+    if (uint64_t(U) + u >= (1ull << 31)) return false;
+    U += uint32_t(u);
+  }
+  for (size_t j = 0; j < nbms.size(); j++)
+    for (int x = 0; x < 8; x++) PA.bms[j][x] = nbms[j][size_t(x)];
+  // static runs: (100 - dyn)% of the units split evenly; the rest in dynamic chunks
+  const uint32_t S = uint32_t(uint64_t(U) * (100 - dc.pool_dyn_pct) / 100 / W);
+  uint32_t cs = dc.pool_chunk_shift;
+  while (((U - S * W + (1u << cs) - 1) >> cs) + 64 > kPoolChunks) cs++;
+  PA.nsegs = nsegs;
+  PA.units = U;
+  PA.static_per_wg = S;
+  PA.dyn0 = S * W;
+  PA.chunk_shift = cs;
+  PA.lookahead = std::min(dc.pool_lookahead, S);
+  PA.has_min = q.has_min;
+  PA.has_max = q.has_max;
+  PA.min32 = uint32_t(q.min_ns);  // (narrow mode: thresholds below 2^32-1 ns)
+  PA.max32 = uint32_t(q.max_ns);
+  PA.start_s = q.start_s;
+  PA.end_s = q.end_s;
+  // LDS: the record buffer is sized so that one workgroup takes more than half a CU. The
+  // host segments are smaller (dc.pool_seg records per workgroup, adaptive): the records
+  // of a sparse query stay on a few pages of pinned memory
+  constexpr size_t kPoolLds = 96 << 10;
+  const uint32_t rec_cap = uint32_t(kPoolLds / sizeof(MatchRec));
+  PA.rec_cap = rec_cap;
+  const size_t hdr = 256, cntb = align_up(size_t(W) * 4, 256);
+  if (dc.pool_head.ensure(256)) HIP_OK(hipMemsetAsync(dc.pool_head.p, 0, dc.pool_head.cap, s));  // then self-resetting
+  unsigned *heads = static_cast<unsigned *>(dc.pool_head.p);
+  static const bool want_stamps = std::getenv("TSG_STAMPS") != nullptr;
+  if (want_stamps) {
+    dc.stamps.ensure(size_t(W) * kStampSlots * 8);
+    HIP_OK(hipMemsetAsync(dc.stamps.p, 0, size_t(W) * kStampSlots * 8, s));
+    PA.stamps = static_cast<unsigned long long *>(dc.stamps.p);
+  }
+  const PoolFn fn = pick_pool(q.nterms, has_dur, q.has_range, dc.pool_nt);
+  if (!dc.pool_attr.count(reinterpret_cast<const void *>(fn))) {
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               int(kPoolLds)));
+    dc.pool_attr.insert(reinterpret_cast<const void *>(fn));
+  }
+  const uint32_t threads = 64 * dc.pool_waves;
+  const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
+  hipEvent_t e0 = dc.es0, e1 = dc.es1;
+  const bool defer = !time_scan && (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
+  uint32_t *counts = nullptr;
+  const uint8_t *recs = nullptr;
+  auto launch = [&](bool first) {
+    PA.seg_cap = dc.pool_seg;
+    dc.hres.ensure(hdr + cntb + size_t(W) * PA.seg_cap * sizeof(MatchRec));
+    uint8_t *base = static_cast<uint8_t *>(dc.hres.p);
+    counts = reinterpret_cast<uint32_t *>(base + hdr);
+    recs = base + hdr + cntb;
+    PA.counts = counts;
+    PA.recs = base + hdr + cntb;
+    PA.head = heads + 32 * dc.pool_parity;
+    PA.head_next = heads + 32 * (dc.pool_parity ^ 1u);
+    std::fill_n(counts, W, kCountPending);  // (each workgroup stores its count last)
+    if (first && time_all) HIP_OK(hipEventRecord(dc.ev0, s));
+    if (first && (time_scan || defer)) HIP_OK(hipEventRecord(e0, s));
+    fn<<<W, threads, kPoolLds, s>>>(PA);
+    HIP_OK(hipGetLastError());
+    if (first && (time_scan || defer)) HIP_OK(hipEventRecord(e1, s));
+    if (first && time_all) HIP_OK(hipEventRecord(dc.ev1, s));
+    dc.pool_parity ^= 1u;
+  };
+  // completion: every workgroup's count (stored after its records completed, read with
+  // acquire loads); finished segments are pulled into this core's caches meanwhile; the
+  // stream is queried now and then so that a kernel that dies fails the search
+  auto wait = [&] {
+    thread_local std::vector<uint8_t> seen;
+    seen.assign(W, 0);
+    const uint32_t seg = PA.seg_cap;
+    uint32_t lo = 0;
+    for (uint32_t it = 1; lo < W; it++) {
+      for (uint32_t w = lo; w < W; w++) {
+        if (seen[w]) {
+          if (w == lo) lo++;
+          continue;
+        }
+        const uint32_t c = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE);
+        if (c == kCountPending) continue;
+        seen[w] = 1;
+        if (w == lo) lo++;
+        const uint8_t *p0 = recs + uint64_t(w) * seg * sizeof(MatchRec);
+        for (uint64_t o = 0; o < uint64_t(std::min(c, seg)) * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
+      }
+      if (lo == W) break;
+      if ((it & 255u) == 0) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) {
+          bool all = true;
+          for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
+          if (all) break;
+          fail(TSG_E_DEVICE, "pool search kernel completed without storing every workgroup count");
+        }
+        if (e != hipErrorNotReady) HIP_OK(e);
+      }
+      __builtin_ia32_pause();
+    }
+  };
+  auto scan_counts = [&](uint64_t &total, uint32_t &maxc) {
+    total = 0;
+    maxc = 0;
+    for (uint32_t w = 0; w < W; w++) {
+      total += counts[w];
+      maxc = std::max(maxc, counts[w]);
+    }
+  };
+  tr.mark("plan");
+  launch(true);
+  tr.mark("search");
+  wait();
+  tr.mark("sync");
+  if (want_stamps) print_stamps(dc, W, true);
+  uint64_t total = 0;
+  uint32_t maxc = 0;
+  scan_counts(total, maxc);
+  if (maxc > rec_cap) {  // dense: this query (and the next few) take the other paths
+    dc.pool_skip = 16;
+    return false;
+  }
+  if (maxc > dc.pool_seg) {  // a host segment overflowed: larger segments, launch again
+    uint32_t want = 32;
+    while (want < maxc) want <<= 1;
+    dc.pool_seg = std::min(want, rec_cap);
+    launch(false);
+    wait();
+    scan_counts(total, maxc);
+  } else if (dc.pool_seg > 32 && uint64_t(maxc) * 8 < dc.pool_seg) {
+    dc.pool_seg >>= 1;  // sparse again: smaller segments from the next query on
+  }
+  const uint32_t seg = PA.seg_cap;
+  float ms = 0, sms = 0;
+  if (time_all) {
+    HIP_OK(hipEventSynchronize(dc.ev1));
+    HIP_OK(hipEventElapsedTime(&ms, dc.ev0, dc.ev1));
+  }
+  if (time_scan) {
+    HIP_OK(hipEventSynchronize(e1));
+    HIP_OK(hipEventElapsedTime(&sms, e0, e1));
+  }
+  out.kernel_ns = uint64_t(double(ms) * 1e6);
+  out.scan_ns = uint64_t(double(sms) * 1e6);
+  tr.mark("events");
+  // records: the blocks' order in the launch, the entry index within a block (the
+  // reference scan order) = the record's position in the launch's unit space. Ordered
+  // by one bucket pass over that position (about one record per bucket) and an
+  // insertion fix-up; a crowded bucket is sorted on its own.
+  uint32_t max_idx = 0;
+  for (const auto &sg : segs) max_idx = std::max(max_idx, sg.block_idx);
+  thread_local std::vector<uint32_t> pos, bucket;
+  pos.assign(size_t(max_idx) + 1, 0);
+  for (uint32_t i = 0; i < nsegs; i++) pos[segs[i].block_idx] = i;
+  thread_local std::vector<uint64_t> keys, sorted;
+  thread_local std::vector<SearchOut::Rec> tmp;
+  keys.resize(total);
+  sorted.resize(total);
+  tmp.resize(total);
+  uint64_t nrec = 0;
+  for (uint32_t w = 0; w < W; w++) {
+    if (!counts[w]) continue;
+    std::memcpy(&tmp[nrec], recs + uint64_t(w) * seg * sizeof(MatchRec), counts[w] * sizeof(MatchRec));
+    nrec += counts[w];
+  }
+  thread_local std::vector<uint64_t> per;
+  per.assign(nsegs, 0);
+  const uint64_t span = uint64_t(U) * kPoolTile;  // positions < span <= 2^31 * 512
+  for (uint64_t i = 0; i < total; i++) {
+    const uint32_t bi = tmp[i].block_il & 0xffffffu;
+    const uint32_t ps = bi <= max_idx ? pos[bi] : 0;
+    per[ps]++;
+    const uint64_t at = uint64_t(PA.blk[ps].ubase) * kPoolTile + tmp[i].entry;
+    keys[i] = (at << 20) | i;  // (< 2^20 records per launch)
+  }
+  uint32_t lb = 6;
+  while ((1ull << lb) < total && lb < 20) lb++;
+  uint32_t sb = 0;
+  while (((span - 1) >> sb) >= (1ull << lb)) sb++;  // bucket of the largest position < 2^lb
+  bucket.assign((size_t(1) << lb) + 1, 0);
+  for (uint64_t i = 0; i < total; i++) bucket[size_t((keys[i] >> 20) >> sb) + 1]++;
+  for (size_t b = 1; b < bucket.size(); b++) bucket[b] += bucket[b - 1];
+  for (uint64_t i = 0; i < total; i++) sorted[bucket[size_t((keys[i] >> 20) >> sb)]++] = keys[i];
+  // (bucket[b] is now the end of bucket b)
+  for (size_t b = 0, lo = 0; b + 1 < bucket.size(); lo = bucket[b], b++) {
+    const size_t hi = bucket[b];
+    if (hi - lo <= 1) continue;
+    if (hi - lo > 32) {
+      std::sort(sorted.begin() + lo, sorted.begin() + hi);
+      continue;
+    }
+    for (size_t i = lo + 1; i < hi; i++) {
+      const uint64_t k = sorted[i];
+      size_t j = i;
+      while (j > lo && sorted[j - 1] > k) {
+        sorted[j] = sorted[j - 1];
+        j--;
+      }
+      sorted[j] = k;
+    }
+  }
+  out.recs.resize(total);
+  for (uint64_t i = 0; i < total; i++) out.recs[i] = tmp[sorted[i] & 0xfffffu];
+  for (uint32_t i = 0; i < nsegs; i++)
+    for (size_t bi = 0; bi < blocks.size(); bi++)
+      if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = per[i];
+  out.scan_bytes += uint64_t(W) * 4 + total * 32;  // + workgroup counts, + id/start/end of each record
+  tr.mark("post");
+  return true;
+}
+
+}  // namespace tsg

@@ -26,7 +26,7 @@
 #include <cstring>
 #include <type_traits>
 
-#include "devctx.hpp"
+#include "search_common.hpp"
 
 namespace tsg {
 
@@ -50,31 +50,6 @@ struct ScanTerm {
   uint32_t lds_off;    // word offset of the LDS copy, or ~0u (read global)
   uint32_t bm_words;
 };
-struct ScanSeg {
-  uint64_t n;
-  const uint32_t *dur32;
-  const uint64_t *dur64;
-  const uint32_t *start_s, *end_s;
-  const uint8_t *ids;
-  const uint64_t *start_ns, *end_ns;
-  const uint32_t *names;
-  const uint8_t *id_len;
-  uint32_t tail, nunits;        // scan units (kUnit entries) in the block; the last `tail` tiles of
-                                // them are claimed dynamically (segment mode: work stealing)
-  uint32_t first_wg, nwg, tpw;  // workgroups owning this block (units split evenly), max tiles per workgroup
-  uint32_t term0, nterms, lds_words;
-  uint32_t block_idx, steal_base;  // claim counter value at launch start (tail tiles)
-  uint64_t cap;  // limit mode: records kept from this block
-};
-struct MatchRec {  // == SearchOut::Rec
-  uint8_t id[16];
-  uint64_t start, end;
-  uint32_t entry;
-  uint32_t block_il;  // block index | id length << 24
-  uint32_t svc, name;
-};
-static_assert(sizeof(MatchRec) == 48, "record layout");
-static_assert(sizeof(MatchRec) == sizeof(SearchOut::Rec), "record layout");
 
 struct ScanParams {
   const ScanSeg *segs;
@@ -117,28 +92,9 @@ struct ScanParams {
   unsigned *steal;  // tail claim counters, one per block slot (128 B apart), monotonic
 };
 
-constexpr int kThreads = 256;
-constexpr int kSteps = 2;                     // 8 entries per thread per tile
-constexpr int kTile = kThreads * 4 * kSteps;  // 2048 entries
-constexpr uint32_t kMaskAll = (1u << (4 * kSteps)) - 1;
-constexpr int kUnit = kThreads * 4;           // 1024 entries: workgroup ranges are whole units
-constexpr uint32_t kNoLds = 0xffffffffu;
 
 // ------------------------------------------------------------------------------------
 // dictionary match
-// Pointers inside descriptors are generic to the compiler; casting them to the
-// global address space turns flat loads (which wait on vmcnt AND lgkmcnt) into
-// global_load_dword{,x2,x4}.
-template <typename T>
-__device__ __forceinline__ const __attribute__((address_space(1))) T *G(const T *p) {
-  return (const __attribute__((address_space(1))) T *)(p);
-}
-template <typename T>
-__device__ __forceinline__ const __attribute__((address_space(1))) T *G(const void *p) {
-  return (const __attribute__((address_space(1))) T *)(p);
-}
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ bool dev_contains(const uint8_t *h, uint32_t hl, const uint8_t *nd, uint32_t nl) {
   if (nl == 0) return true;  // bytes.Contains(x, "") (pitfall P7)
@@ -250,10 +206,6 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
 // tile load is in bounds; entries past n are only masked off.
 static_assert(kColPad % (kThreads * 4 * kSteps) == 0, "column padding covers whole tiles");
 
-// (tile registers are kept as 128-bit vectors, not 4 scalars: a quad returned by one
-// dwordx4 load then stays one register tuple across the loop, instead of being
-// copied into scalar registers right after the load, which waits for it)
-__device__ __forceinline__ u32x4 load4_u32(const uint32_t *p, uint64_t e) { return *G<u32x4>(p + e); }
 // 4 consecutive column values, raw (decoded by col_at). Branch-free over the
 // (wave-uniform) width: 4 dword loads whose addresses collapse onto the first
 // dword for narrow columns (same cache line, no extra HBM bytes). A width switch
@@ -434,15 +386,6 @@ __device__ __forceinline__ uint32_t wg_order(const ScanParams &P, bool use_ticke
   return __builtin_amdgcn_readfirstlane(s_ticket);
 }
 
-// Stores to pinned host memory (records, counts, header): relaxed system-scope
-// stores, i.e. write-through, no cache maintenance. A workgroup makes them complete
-// with one s_waitcnt before it arrives at the completion counter; no L2 writeback /
-// invalidate fence (a per-workgroup __threadfence_system() stalls the whole L2 of
-// its XCD while the other workgroups stream).
-template <typename T>
-__device__ __forceinline__ void host_store(T *p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 // The matches of one tile (bit 4k+j of `mask` <-> entry tile0 + 1024k + 4*tid + j)
 // in scan order (k, thread, j): ranks from a wave scan of kSteps packed 16-bit
@@ -510,12 +453,10 @@ __device__ __forceinline__ void emit_tile(const ScanSeg &S, uint32_t mask, uint6
 //   fails the query loudly). Only workgroups with matches (and the last one, which
 //   writes the header) look back.
 // Phase 3 (emit): records in scan order straight into the pinned host buffer.
-constexpr uint32_t kStampSlots = 9;     // TSG_STAMPS: start setup scan lookback end | desc staged inlds | hw id
 constexpr uint32_t kLdsTiles = 16;      // tiles per workgroup whose masks stay in LDS
 constexpr uint32_t kMaxTpw = 2048;      // tiles per workgroup (per-tile counts in LDS)
 constexpr uint32_t kSpinMax = 1u << 22; // look-back poll bound (~seconds): never reached unless broken
 constexpr uint32_t kMaxSegs = 2048;
-constexpr uint32_t kCountPending = 0xffffffffu;  // segment mode: a workgroup count not stored yet (host sentinel)
 
 // workgroup -> block and per-block record caps, from the device descriptors
 struct DescSegs {
@@ -834,7 +775,6 @@ __global__ void __launch_bounds__(kThreads) search_kernel(ScanParams P) {
 // (agent-scope stores: untorn, no fences needed). The scan workgroups behind them
 // poll the granules of their block's terms, then scan. Dispatch is in index
 // order, so the producers are resident or done; polls are bounded.
-constexpr int kArgSegs = 32, kArgTerms = 4, kArgNeedle = 256, kArgBms = 16;
 constexpr uint32_t kFastStageWords = 6144;  // 24 KiB: one dictionary's offsets + bytes + value bits + set CSR
 struct QArgs {
   const DevBlockDesc *blk[kArgSegs];
@@ -882,13 +822,6 @@ __device__ __forceinline__ bool lds_contains(const uint8_t *h, uint32_t hl, cons
   return false;
 }
 
-// Resident descriptors are immutable while a search runs: read them through the
-// constant address space so uniform reads become scalar loads (s_load, one round
-// trip for all fields) instead of vector loads serialised by vmcnt.
-template <typename T>
-__device__ __forceinline__ const __attribute__((address_space(4))) T *K4(const T *p) {
-  return (const __attribute__((address_space(4))) T *)(p);
-}
 __device__ __forceinline__ DevKeyDesc key_desc(const DevBlockDesc *B, uint32_t k) {
   const auto *p = K4(reinterpret_cast<const DevKeyDesc *>(B + 1)) + k;
   DevKeyDesc r;
@@ -1338,7 +1271,6 @@ __global__ void __launch_bounds__(kThreads, 3)
 
 // ------------------------------------------------------------------------------------
 // host
-static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 using ScanFn = void (*)(ScanParams);
 using FastFn = void (*)(uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
@@ -1383,35 +1315,9 @@ static ScanFn pick_scan(uint32_t nterms, bool dur, bool range, bool w1) {
   }
 }
 
-struct Tracer {
-  bool on;
-  std::chrono::steady_clock::time_point t0, last;
-  char buf[512];
-  int len = 0;
-  bool prof = prof_on();
-  Tracer() : on(std::getenv("TSG_TRACE") != nullptr) {
-    if (on || prof) t0 = last = std::chrono::steady_clock::now();
-  }
-  void mark(const char *name) {
-    if (!on && !prof) return;
-    auto now = std::chrono::steady_clock::now();
-    if (prof) {
-      prof_add(name, std::chrono::duration<double, std::micro>(now - last).count());
-      last = now;
-      if (!on) return;
-    }
-    len += std::snprintf(buf + len, sizeof buf - size_t(len), " %s=%.1f", name,
-                         std::chrono::duration<double, std::micro>(now - last).count());
-    last = now;
-  }
-  ~Tracer() {
-    if (on && len) std::fprintf(stderr, "[tsg] device_search us:%s total=%.1f\n", buf,
-                                std::chrono::duration<double, std::micro>(last - t0).count());
-  }
-};
 
 // TSG_STAMPS: where a launch's time goes (us from the first workgroup start; 100 MHz clock)
-static void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast) {
+void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast) {
   std::vector<unsigned long long> st(size_t(nwg) * kStampSlots);
   HIP_OK(hipMemcpy(st.data(), dc.stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
   unsigned long long t0 = ~0ull;
@@ -1465,6 +1371,8 @@ static void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast) {
   std::fprintf(stderr, "\n");
 }
 
+
+
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
                    uint32_t limit, uint32_t flags, SearchOut &out) {
   Tracer tr;
@@ -1497,15 +1405,6 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // workgroups need to match the dictionaries themselves
   std::vector<std::array<uint16_t, kArgTerms>> seg_keys;
   std::vector<const DevBlockDesc *> seg_desc;
-  // narrow mode: per block its scan / one-byte column bases and per term the column slot
-  // and interned dictionary
-  struct NarrowSeg {
-    const uint32_t *scan;
-    const uint8_t *ncol;
-    uint32_t npad;
-    std::array<uint8_t, kArgTerms> slot, nsets;
-    std::array<const NarrowDict *, kArgTerms> dict;
-  };
   std::vector<NarrowSeg> nsegv;
   bool all_narrow = q.nterms <= uint32_t(kArgTerms);
   uint32_t fast_stage = 0, fast_bm = 0, fast_bm8 = 0, fast_vbits = 0, fast_words = 1, fast_self = 0;
@@ -1691,6 +1590,12 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   };
   uint32_t seg = limit ? limit : dc.seg_cap;
   if (!seg_fits(seg)) seg = 0;
+  // ---- pool path: narrow full scans (search_pool_kernel); falls through to the
+  // segment / look-back paths below when a workgroup's matches overflow its LDS buffer
+  if (fast && narrow && !limit && !dc.seg_off && !dc.pool_off) {
+    if (dc.pool_skip) dc.pool_skip--;
+    else if (pool_search(dc, blocks, q, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out)) return;
+  }
   const FastFn fast_seg = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, true) : nullptr;
   const FastFn fast_lb = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, false) : nullptr;
   const void *kfn = fast ? reinterpret_cast<const void *>(seg ? fast_seg : fast_lb)
