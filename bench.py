@@ -68,7 +68,7 @@ def pmc_traffic(workload_key):
     w = d.get(workload_key, {})
     for name, ent in w.items():
         if KERNEL.replace(" ", "") in name.replace(" ", ""):  # rocprof: "void tsg::search_fast_kernel<...>(tsg::QArgs)"
-            return ent.get("traffic_bytes_per_launch"), w.get("_source")
+            return ent.get("traffic_bytes_per_launch"), ent.get("source", w.get("_source"))
     return None, None
 
 

@@ -55,8 +55,11 @@ def main():
                 merged = json.load(f)
         except (OSError, ValueError):
             merged = {}
-        out["_source"] = args.source
-        merged[args.workload] = out
+        for k in out:
+            out[k]["source"] = args.source
+        w = merged.setdefault(args.workload, {})
+        w.update(out)  # (other kernels measured on this workload keep their entries)
+        w["_source"] = args.source
         with open(args.out, "w") as f:
             json.dump(merged, f, indent=1)
 
