@@ -115,7 +115,7 @@ struct DeviceCtx {
   bool seg_off = std::getenv("TSG_NO_SEG") != nullptr;    // one-launch path: always look-back mode
   // pool path (search_pool_kernel: narrow full scans, one workgroup per CU). TSG_NO_POOL=1
   // disables it; TSG_POOL_DYN = percent of the units claimed dynamically (default 20),
-  // TSG_POOL_CHUNK = log2 units per dynamic claim (4), TSG_POOL_LOOK = claims of lookahead (32),
+  // TSG_POOL_CHUNK = log2 units per dynamic claim (4), TSG_POOL_LOOK = claims of lookahead (8),
   // TSG_POOL_WAVES = waves per workgroup (16)
   bool pool_off = std::getenv("TSG_NO_POOL") != nullptr;
   uint32_t pool_skip = 0;  // queries left to skip the pool after a record-buffer overflow
@@ -127,11 +127,12 @@ struct DeviceCtx {
   }
   uint32_t pool_dyn_pct = env_u32("TSG_POOL_DYN", 20, 0, 100);
   uint32_t pool_chunk_shift = env_u32("TSG_POOL_CHUNK", 4, 0, 10);
-  uint32_t pool_lookahead = env_u32("TSG_POOL_LOOK", 32, 0, 1024);
+  uint32_t pool_lookahead = env_u32("TSG_POOL_LOOK", 8, 0, 1024);  // (32: kernel p50 +1.5 us, profiles/r02_pool)
   uint32_t pool_waves = env_u32("TSG_POOL_WAVES", 16, 2, 16);  // waves per workgroup (one workgroup per CU)
   // TSG_POOL_NT=0: default-policy stream loads (non-temporal measured faster: kernel p50
   // 32.8 vs 34.5 us, profiles/r02_pool)
   bool pool_nt = env_u32("TSG_POOL_NT", 1, 0, 1) != 0;
+  uint32_t pool_rec = env_u32("TSG_POOL_REC", 1u << 20, 1, 1u << 20);  // TSG_POOL_REC: LDS records per workgroup below the 2048 that fit (tests)
   uint32_t pool_seg = 32;  // host segment records per workgroup (adaptive: grows on overflow, halves when sparse)
   DevBuf pool_head;  // two dynamic-chunk counters (128 B apart): a launch uses one, zeroes the other
   uint32_t pool_parity = 0;

@@ -366,7 +366,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   // host segments are smaller (dc.pool_seg records per workgroup, adaptive): the records
   // of a sparse query stay on a few pages of pinned memory
   constexpr size_t kPoolLds = 96 << 10;
-  const uint32_t rec_cap = uint32_t(kPoolLds / sizeof(MatchRec));
+  const uint32_t rec_cap = std::min(dc.pool_rec, uint32_t(kPoolLds / sizeof(MatchRec)));
   PA.rec_cap = rec_cap;
   const size_t hdr = 256, cntb = align_up(size_t(W) * 4, 256);
   if (dc.pool_head.ensure(256)) HIP_OK(hipMemsetAsync(dc.pool_head.p, 0, dc.pool_head.cap, s));  // then self-resetting
@@ -460,17 +460,23 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   uint64_t total = 0;
   uint32_t maxc = 0;
   scan_counts(total, maxc);
-  if (maxc > rec_cap) {  // dense: this query (and the next few) take the other paths
-    dc.pool_skip = 16;
-    return false;
-  }
-  if (maxc > dc.pool_seg) {  // a host segment overflowed: larger segments, launch again
-    uint32_t want = 32;
-    while (want < maxc) want <<= 1;
-    dc.pool_seg = std::min(want, rec_cap);
-    launch(false);
-    wait();
-    scan_counts(total, maxc);
+  // A workgroup's count depends on which dynamic chunks it won, so a rerun can overflow
+  // where the first launch did not: launch until every count fits its segment (segments
+  // double each time, at most up to the LDS buffer), or leave for the other paths.
+  if (maxc > PA.seg_cap) {
+    for (;;) {
+      if (maxc > rec_cap) {  // dense: this query (and the next few) take the other paths
+        dc.pool_skip = 16;
+        return false;
+      }
+      if (maxc <= PA.seg_cap) break;
+      uint32_t want = 2 * PA.seg_cap;  // (headroom: the next launch's split differs)
+      while (want < maxc) want <<= 1;
+      dc.pool_seg = std::min(want, rec_cap);
+      launch(false);
+      wait();
+      scan_counts(total, maxc);
+    }
   } else if (dc.pool_seg > 32 && uint64_t(maxc) * 8 < dc.pool_seg) {
     dc.pool_seg >>= 1;  // sparse again: smaller segments from the next query on
   }
