@@ -544,7 +544,9 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     std::memset(&m, 0, sizeof m);
     res->set_blocks(nblocks);
     // block filter on the host (header), device work grouped per device
-    std::vector<int> state(nblocks, 0);  // 0 no meta, 1 skipped, 2 inspected
+    // (per-query scratch kept per thread: no allocations once warm)
+    thread_local std::vector<int> state;
+    state.assign(nblocks, 0);  // 0 no meta, 1 skipped, 2 inspected
     for (size_t i = 0; i < nblocks; i++) {
       Block &b = blocks[i]->b;
       if (!b.host->has_meta) continue;
@@ -554,17 +556,28 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       state[i] = ok ? 2 : 1;
     }
     // Blocks [b0, b1) on their devices, one device_search per device (concurrently).
-    std::list<std::pair<DeviceCtx *, SearchOut>> outs;  // (stable: per_block points into recs)
-    std::vector<std::pair<const SearchOut::Rec *, size_t>> per_block(nblocks, {nullptr, 0});
+    // device outputs: a deque keeps them in place (per_block points into their records);
+    // entries are reused across queries, their record vectors keep their capacity
+    thread_local std::deque<SearchOut> outs;
+    size_t outs_used = 0;
+    thread_local std::vector<std::pair<const SearchOut::Rec *, size_t>> per_block;
+    per_block.assign(nblocks, {nullptr, 0});
     size_t nrec = 0;
     auto search_range = [&](size_t b0, size_t b1) {
-      std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, Block *>>> per_dev;
-      for (size_t i = b0; i < b1; i++)
-        if (state[i] == 2 && blocks[i]->b.dc) per_dev[blocks[i]->b.dc].push_back({uint32_t(i), &blocks[i]->b});
+      // blocks per device, in first-seen device order (a handful of devices: linear search)
+      std::vector<std::pair<DeviceCtx *, std::vector<std::pair<uint32_t, Block *>>>> per_dev;
+      for (size_t i = b0; i < b1; i++) {
+        if (state[i] != 2 || !blocks[i]->b.dc) continue;
+        DeviceCtx *dc = blocks[i]->b.dc;
+        size_t d = 0;
+        while (d < per_dev.size() && per_dev[d].first != dc) d++;
+        if (d == per_dev.size()) per_dev.push_back({dc, {}});
+        per_dev[d].second.push_back({uint32_t(i), &blocks[i]->b});
+      }
       std::vector<SearchOut *> slots;
-      for (auto &kv : per_dev) {
-        outs.push_back({kv.first, SearchOut()});
-        slots.push_back(&outs.back().second);
+      for (size_t d = 0; d < per_dev.size(); d++) {
+        if (outs_used == outs.size()) outs.emplace_back();
+        slots.push_back(&outs[outs_used++]);
       }
       std::vector<std::thread> th;
       std::vector<std::exception_ptr> errs(slots.size());
@@ -578,6 +591,11 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
             // before every chunk
             const size_t nl = list.size(), step = kChunk ? kChunk : nl;
             SearchOut &o = *slots[slot];
+            if (nl <= step) {  // one chunk: the device's list as it is
+              check_cancel();
+              device_search(*dc, list, *q, limit, flags, o);
+              return;
+            }
             for (size_t c0 = 0; c0 < nl; c0 += step) {
               check_cancel();
               const std::vector<std::pair<uint32_t, Block *>> part(list.begin() + c0,

@@ -32,6 +32,7 @@ constexpr int kPoolThreads = kPoolWaves * 64;
 constexpr uint32_t kPoolTile = 512;       // entries per unit (wave tile)
 constexpr uint32_t kPoolChunks = 1024;    // dynamic chunks one workgroup can take
 constexpr uint32_t kPoolPending = 0xffffffffu, kPoolNone = 0xfffffffeu;
+constexpr uint32_t kPoolSpinMax = 1u << 24;  // LDS poll bound (~1 s of s_sleep 2)
 static_assert(kColPad % kPoolTile == 0, "column padding covers whole units");
 
 struct PoolBlk {           // 64 B, staged in LDS
@@ -54,6 +55,7 @@ struct PoolArgs {
   uint8_t *recs;        // pinned host: workgroup w's first seg_cap records at w * seg_cap (rec_cap: LDS records)
   uint32_t *counts;     // pinned host: workgroup w's match count, stored after its records
   unsigned long long *stamps;
+  uint32_t *err;        // pinned host: set when an LDS poll ran past its bound (the host fails the query)
 };
 static_assert(sizeof(PoolArgs) <= 4096, "kernel arguments");
 
@@ -123,6 +125,19 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
   }
   const uint32_t S = A.static_per_wg, L = A.lookahead, cs = A.chunk_shift;
   const uint32_t rec_cap = A.rec_cap;
+  // An LDS chunk slot once its answer is in. Bounded: never reached unless the protocol
+  // is broken, and then the query fails on the host instead of the GPU hanging.
+  auto poll_chunk = [&](uint32_t k) -> uint32_t {
+    uint32_t v, spins = 0;
+    while ((v = __hip_atomic_load(&s_chunk[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == kPoolPending) {
+      if (++spins > kPoolSpinMax) {
+        host_store(A.err, 1u);
+        return kPoolNone;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    return v;
+  };
   // claim -> unit (or kPoolNone): claims below S are this workgroup's static run; claim
   // S + k*C + off is unit `off` of its k-th dynamic chunk, which the claim L before the
   // chunk's first one requested from the device counter (so a wave rarely waits for it)
@@ -139,10 +154,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
         // first empty claim without stranding units this workgroup took
         if (lane == 0) {
           uint32_t prev = 0;
-          if (k > 0)
-            while ((prev = __hip_atomic_load(&s_chunk[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
-                   kPoolPending)
-              __builtin_amdgcn_s_sleep(2);
+          if (k > 0) prev = poll_chunk(k - 1);
           uint32_t val = kPoolNone;
           if (prev != kPoolNone) {
             const uint32_t g = __hip_atomic_fetch_add(A.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -156,9 +168,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     if (c < S) return w * S + c;
     const uint32_t d = c - S, k = d >> cs;
     if (k >= kPoolChunks) return kPoolNone;
-    uint32_t v;
-    while ((v = __hip_atomic_load(&s_chunk[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == kPoolPending)
-      __builtin_amdgcn_s_sleep(2);
+    uint32_t v = poll_chunk(k);
     v = __builtin_amdgcn_readfirstlane(v);
     if (v == kPoolNone) return kPoolNone;
     const uint32_t u = v + (d & ((1u << cs) - 1));
@@ -367,6 +377,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   // of a sparse query stay on a few pages of pinned memory
   constexpr size_t kPoolLds = 96 << 10;
   const uint32_t rec_cap = std::min(dc.pool_rec, uint32_t(kPoolLds / sizeof(MatchRec)));
+  if (uint64_t(W) * rec_cap > (1u << 20)) return false;  // (record slots are 20-bit in the host's sort keys)
   PA.rec_cap = rec_cap;
   const size_t hdr = 256, cntb = align_up(size_t(W) * 4, 256);
   if (dc.pool_head.ensure(256)) HIP_OK(hipMemsetAsync(dc.pool_head.p, 0, dc.pool_head.cap, s));  // then self-resetting
@@ -397,6 +408,8 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     recs = base + hdr + cntb;
     PA.counts = counts;
     PA.recs = base + hdr + cntb;
+    PA.err = reinterpret_cast<uint32_t *>(base);
+    *reinterpret_cast<volatile uint32_t *>(base) = 0;
     PA.head = heads + 32 * dc.pool_parity;
     PA.head_next = heads + 32 * (dc.pool_parity ^ 1u);
     std::fill_n(counts, W, kCountPending);  // (each workgroup stores its count last)
@@ -444,6 +457,8 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     }
   };
   auto scan_counts = [&](uint64_t &total, uint32_t &maxc) {
+    if (__atomic_load_n(PA.err, __ATOMIC_ACQUIRE))
+      fail(TSG_E_DEVICE, "pool search: a workgroup's chunk poll ran past its bound (claim protocol broken)");
     total = 0;
     maxc = 0;
     for (uint32_t w = 0; w < W; w++) {
@@ -503,26 +518,25 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   pos.assign(size_t(max_idx) + 1, 0);
   for (uint32_t i = 0; i < nsegs; i++) pos[segs[i].block_idx] = i;
   thread_local std::vector<uint64_t> keys, sorted;
-  thread_local std::vector<SearchOut::Rec> tmp;
   keys.resize(total);
   sorted.resize(total);
-  tmp.resize(total);
-  uint64_t nrec = 0;
-  for (uint32_t w = 0; w < W; w++) {
-    if (!counts[w]) continue;
-    std::memcpy(&tmp[nrec], recs + uint64_t(w) * seg * sizeof(MatchRec), counts[w] * sizeof(MatchRec));
-    nrec += counts[w];
-  }
+  // keys straight from the pinned segments: position << 20 | record slot (w * seg + i);
+  // the gather below reads the same lines again, from cache
+  const auto *prec = reinterpret_cast<const SearchOut::Rec *>(recs);
   thread_local std::vector<uint64_t> per;
   per.assign(nsegs, 0);
   const uint64_t span = uint64_t(U) * kPoolTile;  // positions < span <= 2^31 * 512
-  for (uint64_t i = 0; i < total; i++) {
-    const uint32_t bi = tmp[i].block_il & 0xffffffu;
-    const uint32_t ps = bi <= max_idx ? pos[bi] : 0;
-    per[ps]++;
-    const uint64_t at = uint64_t(PA.blk[ps].ubase) * kPoolTile + tmp[i].entry;
-    keys[i] = (at << 20) | i;  // (< 2^20 records per launch)
-  }
+  uint64_t nrec = 0;
+  for (uint32_t w = 0; w < W; w++)
+    for (uint32_t i = 0; i < counts[w]; i++) {
+      const uint64_t slot = uint64_t(w) * seg + i;  // (< 256 x 2048 < 2^20)
+      const SearchOut::Rec &r = prec[slot];
+      const uint32_t bi = r.block_il & 0xffffffu;
+      const uint32_t ps = bi <= max_idx ? pos[bi] : 0;
+      per[ps]++;
+      const uint64_t at = uint64_t(PA.blk[ps].ubase) * kPoolTile + r.entry;
+      keys[nrec++] = (at << 20) | slot;
+    }
   uint32_t lb = 6;
   while ((1ull << lb) < total && lb < 20) lb++;
   uint32_t sb = 0;
@@ -550,7 +564,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     }
   }
   out.recs.resize(total);
-  for (uint64_t i = 0; i < total; i++) out.recs[i] = tmp[sorted[i] & 0xfffffu];
+  for (uint64_t i = 0; i < total; i++) out.recs[i] = prec[sorted[i] & 0xfffffu];
   for (uint32_t i = 0; i < nsegs; i++)
     for (size_t bi = 0; bi < blocks.size(); bi++)
       if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = per[i];

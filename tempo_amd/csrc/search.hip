@@ -1385,13 +1385,34 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     dc.num_cu = prop.multiProcessorCount;
   }
 
-  // ---- plan
-  std::vector<ScanSeg> segs;
-  std::vector<ScanTerm> terms;
-  std::vector<DictJob> jobs;
-  std::vector<uint32_t> set_jobs, set_items(1, 0), term_bm_base;
-  std::vector<uint8_t> needles;
-  std::vector<uint32_t> needle_off(q.nterms);
+  // ---- plan (scratch vectors kept per thread: no allocation per query once warm)
+  struct PlanScratch {
+    std::vector<ScanSeg> segs;
+    std::vector<ScanTerm> terms;
+    std::vector<DictJob> jobs;
+    std::vector<uint32_t> set_jobs, set_items, term_bm_base, needle_off;
+    std::vector<uint8_t> needles;
+    std::vector<std::array<uint16_t, kArgTerms>> seg_keys;
+    std::vector<const DevBlockDesc *> seg_desc;
+    std::vector<NarrowSeg> nsegv;
+    std::vector<int> kidx;
+    std::string key;
+  };
+  thread_local PlanScratch ps;
+  auto &segs = ps.segs;
+  auto &terms = ps.terms;
+  auto &jobs = ps.jobs;
+  auto &set_jobs = ps.set_jobs, &set_items = ps.set_items, &term_bm_base = ps.term_bm_base;
+  auto &needles = ps.needles;
+  auto &needle_off = ps.needle_off;
+  segs.clear();
+  terms.clear();
+  jobs.clear();
+  set_jobs.clear();
+  set_items.assign(1, 0);
+  term_bm_base.clear();
+  needles.clear();
+  needle_off.assign(q.nterms, 0);
   for (uint32_t t = 0; t < q.nterms; t++) {
     needle_off[t] = uint32_t(needles.size());
     needles.insert(needles.end(), q.values[t], q.values[t] + q.value_lens[t]);
@@ -1403,19 +1424,24 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   constexpr uint32_t kLdsBudgetWords = 8192;  // 32 KiB per workgroup
   // one-launch path bookkeeping: per block key indices and LDS words its
   // workgroups need to match the dictionaries themselves
-  std::vector<std::array<uint16_t, kArgTerms>> seg_keys;
-  std::vector<const DevBlockDesc *> seg_desc;
-  std::vector<NarrowSeg> nsegv;
+  auto &seg_keys = ps.seg_keys;
+  auto &seg_desc = ps.seg_desc;
+  auto &nsegv = ps.nsegv;
+  seg_keys.clear();
+  seg_desc.clear();
+  nsegv.clear();
   bool all_narrow = q.nterms <= uint32_t(kArgTerms);
   uint32_t fast_stage = 0, fast_bm = 0, fast_bm8 = 0, fast_vbits = 0, fast_words = 1, fast_self = 0;
   for (auto &bp : blocks) {
     Block &b = *bp.second;
     const DevBlock &d = b.dev;
     if (d.n == 0 || q.exhaustive) continue;
-    std::vector<int> kidx(q.nterms);
+    auto &kidx = ps.kidx;
+    kidx.assign(q.nterms, 0);
     bool dead = false;  // a key absent from the block: FindTag fails for every entry
     for (uint32_t t = 0; t < q.nterms && !dead; t++) {
-      auto it = b.host->key_index.find(std::string(reinterpret_cast<const char *>(q.keys[t]), q.key_lens[t]));
+      ps.key.assign(reinterpret_cast<const char *>(q.keys[t]), q.key_lens[t]);
+      auto it = b.host->key_index.find(ps.key);
       if (it == b.host->key_index.end()) dead = true;
       else kidx[t] = it->second;
     }
@@ -1538,8 +1564,10 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // narrow mode: the value-set bitmap of every (dictionary, term) pair, matched here on
   // the host (bytes.Contains per value, a set matches when one of its values does);
   // identical dictionaries of different blocks are matched once
-  std::vector<std::array<uint32_t, 8>> nbms;
-  std::vector<std::array<uint8_t, kArgTerms>> nbmi(segs.size());
+  thread_local std::vector<std::array<uint32_t, 8>> nbms;
+  thread_local std::vector<std::array<uint8_t, kArgTerms>> nbmi;
+  nbms.clear();
+  nbmi.assign(segs.size(), {});
   const bool need64 = (q.has_min && q.min_ns >= 0xffffffffULL) || (q.has_max && q.max_ns >= 0xffffffffULL);
   bool narrow = all_narrow && !need64 && !dc.narrow_off && nsegs <= uint32_t(kArgSegs) &&
                 needles.size() <= size_t(kArgNeedle);

@@ -11,6 +11,10 @@ if has test; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
   ok_rc $rc || exit $rc
+  # narrow full scans on the one-launch segment kernel instead of the pool kernel
+  TSG_NO_POOL=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py tests/test_gpu_configs.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_nopool.log 2>&1
+  rc=$?; echo "pytest gpu (TSG_NO_POOL) rc=$rc"; tail -5 gpurun_out/pytest_gpu_nopool.log
+  ok_rc $rc || exit $rc
   # the general (prep kernel + descriptor) search path, forced
   TSG_NO_FAST=1 timeout -k 10 600 python -m pytest tests/test_gpu_search.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu_nofast.log 2>&1
   rc=$?; echo "pytest gpu (TSG_NO_FAST) rc=$rc"; tail -5 gpurun_out/pytest_gpu_nofast.log
