@@ -95,7 +95,7 @@ def node_cpus(node):
 
 
 def idlest(cpus, k, window=0.3):
-    """The k CPUs of `cpus` with the most idle time over `window` seconds (/proc/stat):
+    """k CPUs of `cpus` on the k cores with the most idle time over `window` seconds (/proc/stat):
     the GPU box shares its host with other jobs, and a search thread that lands on a
     busy core loses tens of microseconds per step to preemption."""
     def snap():
@@ -111,7 +111,22 @@ def idlest(cpus, k, window=0.3):
     a = snap()
     time.sleep(window)
     b = snap()
-    return sorted(sorted(cpus, key=lambda c: -(b.get(c, 0) - a.get(c, 0)))[:k])
+    idle = {c: b.get(c, 0) - a.get(c, 0) for c in cpus}
+    # whole cores: a CPU whose SMT sibling is busy shares its core's issue slots, so a
+    # core counts as idle as its busiest thread; one CPU per core, the k idlest cores
+    cores = {}
+    for c in cpus:
+        try:
+            sib = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+        except OSError:
+            sib = str(c)
+        cores.setdefault(sib, []).append(c)
+    ranked = sorted(cores.values(), key=lambda th: (-min(idle[t] for t in th), min(th)))
+    pick = [min(th) for th in ranked[:k]]
+    if len(pick) < k:  # (fewer cores than k: fill with the idlest remaining CPUs)
+        rest = sorted((c for c in cpus if c not in pick), key=lambda c: -idle[c])
+        pick += rest[:k - len(pick)]
+    return sorted(pick)
 
 
 def cpu_model():
