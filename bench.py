@@ -170,6 +170,8 @@ def parse():
                          "stream, pinned output and resident copy of the set) driven by as many host threads")
     ap.add_argument("--concurrent-steps", type=int, default=64,
                     help="queries per stream in the concurrent leg (0 = skip)")
+    ap.add_argument("--merge-steps", type=int, default=20,
+                    help="N > 1: distributed full-scan queries with the frontend merge on rank 0 (0 = off)")
     ap.add_argument("--cfg3-blocks", type=int, default=25)
     ap.add_argument("--cfg3-entries", type=int, default=5_000_000)
     ap.add_argument("--cfg3-steps", type=int, default=64)
@@ -426,6 +428,43 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, gen_thread=Non
     return res
 
 
+def merge_leg(args, eng, base, pipe, rank, world, dist):
+    """N > 1: the query as the frontend serves it (modules/frontend/searchsharding.go:32-125):
+    every rank searches its block shard (full scan, the config-2 query), packs its ordered
+    match list into byte tensors, rank 0 gathers them (tempo_amd.shard.distributed_search_packed)
+    and merges. A few hundred records per rank: gathered on the host over a gloo group
+    (north_star: "host-merged where that is cheaper"; the RCCL form of the same gather is
+    covered by the packed-gather tests). Latency per query is the max over ranks."""
+    from datetime import timedelta
+
+    import torch
+    from tempo_amd import shard
+    try:
+        g = dist.new_group(backend="gloo", timeout=timedelta(seconds=120))
+        nb = len(base) * world
+        everything = 1 << 30  # (full scan: the frontend merge keeps every distinct trace)
+        local = lambda: eng.search(base, pipe)  # noqa: E731
+        merged = shard.distributed_search_packed(local, everything, nb, device="cpu", group=g)
+        dist.barrier(group=g)
+        ts = []
+        for _ in range(args.merge_steps):
+            t0 = time.perf_counter()
+            merged = shard.distributed_search_packed(local, everything, nb, device="cpu", group=g)
+            dist.barrier(group=g)
+            ts.append(time.perf_counter() - t0)
+        tt = torch.tensor([sum(ts)], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=g)
+        res = {"queries": args.merge_steps, "ranks": world, "step_us": pct([x * 1e6 for x in ts]),
+               "entries_per_s": len(base) * args.entries * world * args.merge_steps / float(tt.item()),
+               "transport": "gloo (host) gather of packed records to rank 0, then merge"}
+        if rank == 0:
+            res["merged_traces"] = len(merged[0])
+            res["inspected_traces"] = merged[1].inspected_traces
+        return res
+    except Exception as e:  # (the main line above is already measured; report, do not fail)
+        return {"error": repr(e)}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -612,6 +651,9 @@ def main():
 
     if args.cfg3:
         out["cfg3"] = cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, cfg3_thread)
+
+    if world > 1 and args.merge_steps:
+        out["merge"] = merge_leg(args, eng, base, pipe, rank, world, dist)
 
     gc.enable()
     if rank == 0 and world == 1 and args.cpu_baseline:
