@@ -323,7 +323,8 @@ static PoolFn pick_pool(uint32_t nterms, bool dur, bool range, bool ntl) {
   return ntl ? pick_pool_t<true>(nterms, dur, range) : pick_pool_t<false>(nterms, dur, range);
 }
 
-// One search_pool_kernel launch for a narrow full scan (limit 0). Returns false, with
+// One search_pool_kernel launch for a narrow search (every block scanned whole; a limit
+// cuts each block's records to its first `cap` on the host). Returns false, with
 // nothing written to `out`, when a workgroup found more matches than its record buffer
 // holds: the caller then runs the segment / look-back path.
 bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
@@ -563,12 +564,28 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       sorted[j] = k;
     }
   }
+  // limit L (segs[i].cap = min(L, n)): each block's first L matches in scan order, as the
+  // one-launch kernel's per-block caps keep them; the sorted records of a block are
+  // contiguous, so the cut keeps a prefix of each block's run
   out.recs.resize(total);
-  for (uint64_t i = 0; i < total; i++) out.recs[i] = prec[sorted[i] & 0xfffffu];
-  for (uint32_t i = 0; i < nsegs; i++)
+  uint64_t kept = 0;
+  for (uint64_t i = 0, run = 0, ps = ~0ull; i < total; i++) {
+    const SearchOut::Rec &r = prec[sorted[i] & 0xfffffu];
+    const uint32_t bi = r.block_il & 0xffffffu;
+    const uint64_t seg_i = bi <= max_idx ? pos[bi] : 0;
+    if (seg_i != ps) {
+      ps = seg_i;
+      run = 0;
+    }
+    if (run++ < segs[seg_i].cap) out.recs[kept++] = r;
+  }
+  out.recs.resize(kept);
+  for (uint32_t i = 0; i < nsegs; i++) {
+    per[i] = std::min<uint64_t>(per[i], segs[i].cap);
     for (size_t bi = 0; bi < blocks.size(); bi++)
       if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = per[i];
-  out.scan_bytes += uint64_t(W) * 4 + total * 32;  // + workgroup counts, + id/start/end of each record
+  }
+  out.scan_bytes += uint64_t(W) * 4 + kept * 32;  // + workgroup counts, + id/start/end of each record
   tr.mark("post");
   return true;
 }

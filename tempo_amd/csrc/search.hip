@@ -1618,9 +1618,9 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   };
   uint32_t seg = limit ? limit : dc.seg_cap;
   if (!seg_fits(seg)) seg = 0;
-  // ---- pool path: narrow full scans (search_pool_kernel); falls through to the
+  // ---- pool path: narrow searches (search_pool_kernel); falls through to the
   // segment / look-back paths below when a workgroup's matches overflow its LDS buffer
-  if (fast && narrow && !limit && !dc.seg_off && !dc.pool_off) {
+  if (fast && narrow && !dc.seg_off && !dc.pool_off) {
     if (dc.pool_skip) dc.pool_skip--;
     else if (pool_search(dc, blocks, q, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out)) return;
   }

@@ -1,4 +1,4 @@
-"""GPU parity of the pool path (pool.hip search_pool_kernel: narrow full scans, limit 0).
+"""GPU parity of the pool path (pool.hip search_pool_kernel: narrow searches).
 
 The pool kernel hands 512-entry units to whichever wave of a CU is free and the last
 units of the launch to whichever CU asks first, so records reach the host in claim
@@ -42,10 +42,10 @@ def request(q):
                            max_duration_ms=q.get("max_ms", 0), start=q.get("start", 0), end=q.get("end", 0))
 
 
-def run(engine, paths, q):
+def run(engine, paths, q, limit=0):
     blocks = [engine.open_block(p) for p in paths]
     try:
-        got, met = engine.search(blocks, T.Pipeline(request(q)), limit=0)
+        got, met = engine.search(blocks, T.Pipeline(request(q)), limit=limit)
     finally:
         for b in blocks:
             b.close()
@@ -53,8 +53,8 @@ def run(engine, paths, q):
                                        met.skipped_blocks)
 
 
-def oracle(paths, q):
-    exp, omet, st = O.search([O.Block(p) for p in paths], limit=0, nthreads=16, **q)
+def oracle(paths, q, limit=0):
+    exp, omet, st = O.search([O.Block(p) for p in paths], limit=limit, nthreads=1 if limit else 16, **q)
     assert st == 0
     return [match_key(m) for m in exp], (omet["traces_inspected"], omet["bytes_inspected"],
                                          omet["blocks_inspected"], omet["blocks_skipped"])
@@ -76,6 +76,15 @@ def ragged(tmp_path_factory):
 @pytest.mark.parametrize("qi", range(len(QUERIES)))
 def test_pool_ragged_32_blocks(engine, ragged, qi):
     assert run(engine, ragged, QUERIES[qi]) == oracle(ragged, QUERIES[qi])
+
+
+@pytest.mark.parametrize("limit", [1, 20, 700])
+def test_pool_limit(engine, ragged, limit):
+    """Limit queries: every block of the wave scanned whole, each block cut to its first L
+    matches on the host (the one-launch kernel's per-block caps); the consumer's distinct-id
+    stop and the two-wave early exit stay in tsg_search."""
+    for q in (CFG2, dict(tags={"service.name": "svc-07"})):
+        assert run(engine, ragged, q, limit) == oracle(ragged, q, limit)
 
 
 def test_pool_tiny_searches(engine, ragged):
