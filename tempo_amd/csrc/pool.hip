@@ -359,7 +359,11 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     for (int x = 0; x < 8; x++) PA.bms[j][x] = nbms[j][size_t(x)];
   // static runs: (100 - dyn)% of the units split evenly; the rest in dynamic chunks
   const uint32_t S = uint32_t(uint64_t(U) * (100 - dc.pool_dyn_pct) / 100 / W);
+  // units per dynamic claim: TSG_POOL_CHUNK (16), but at most half a workgroup's static
+  // run — on a small search (the first wave of a limit query: ~12 static units per
+  // workgroup) a 16-unit chunk more than doubles the work of the workgroups that win one
   uint32_t cs = dc.pool_chunk_shift;
+  while (cs > 0 && (1u << cs) > std::max(1u, S / 2)) cs--;
   while (((U - S * W + (1u << cs) - 1) >> cs) + 64 > kPoolChunks) cs++;
   PA.nsegs = nsegs;
   PA.units = U;
