@@ -133,6 +133,10 @@ struct DeviceCtx {
   // 32.8 vs 34.5 us, profiles/r02_pool)
   bool pool_nt = env_u32("TSG_POOL_NT", 1, 0, 1) != 0;
   uint32_t pool_rec = env_u32("TSG_POOL_REC", 1u << 20, 1, 1u << 20);  // TSG_POOL_REC: LDS records per workgroup below the 2048 that fit (tests)
+  // TSG_POOL_SMALL: a search whose static run would be below this many units per
+  // workgroup is split statically whole (no device-counter claims); 0 keeps the dynamic
+  // tail at every size (tests)
+  uint32_t pool_small = env_u32("TSG_POOL_SMALL", 32, 0, 1u << 20);
   uint32_t pool_seg = 32;  // host segment records per workgroup (adaptive: grows on overflow, halves when sparse)
   DevBuf pool_head;  // two dynamic-chunk counters (128 B apart): a launch uses one, zeroes the other
   uint32_t pool_parity = 0;

@@ -165,7 +165,10 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
         }
       }
     }
-    if (c < S) return w * S + c;
+    if (c < S) {  // (a small search's last static runs end at `units`: past it, no work)
+      const uint32_t u = w * S + c;
+      return u < units ? u : kPoolNone;
+    }
     const uint32_t d = c - S, k = d >> cs;
     if (k >= kPoolChunks) return kPoolNone;
     uint32_t v = poll_chunk(k);
@@ -358,13 +361,17 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   for (size_t j = 0; j < nbms.size(); j++)
     for (int x = 0; x < 8; x++) PA.bms[j][x] = nbms[j][size_t(x)];
   // static runs: (100 - dyn)% of the units split evenly; the rest in dynamic chunks
-  const uint32_t S = uint32_t(uint64_t(U) * (100 - dc.pool_dyn_pct) / 100 / W);
-  // units per dynamic claim: TSG_POOL_CHUNK (16), but at most half a workgroup's static
-  // run — on a small search (the first wave of a limit query: ~12 static units per
-  // workgroup) a 16-unit chunk more than doubles the work of the workgroups that win one
+  uint32_t S = uint32_t(uint64_t(U) * (100 - dc.pool_dyn_pct) / 100 / W);
+  // small searches (a limit query's first wave, one block): every unit static. Their
+  // refill triggers would all fall in the first two claim rounds, and chunks are
+  // requested strictly in order: a chain of device-counter round trips (limit-20 first
+  // wave, 2 M entries: 16.5 us kernel)
+  if (S < dc.pool_small) S = uint32_t((uint64_t(U) + W - 1) / W);
+  // units per dynamic claim: TSG_POOL_CHUNK (16), at most half a workgroup's static run
   uint32_t cs = dc.pool_chunk_shift;
   while (cs > 0 && (1u << cs) > std::max(1u, S / 2)) cs--;
-  while (((U - S * W + (1u << cs) - 1) >> cs) + 64 > kPoolChunks) cs++;
+  const uint32_t dyn_units = U > S * W ? U - S * W : 0u;
+  while (((dyn_units + (1u << cs) - 1) >> cs) + 64 > kPoolChunks) cs++;
   PA.nsegs = nsegs;
   PA.units = U;
   PA.static_per_wg = S;

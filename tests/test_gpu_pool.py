@@ -73,25 +73,46 @@ def ragged(tmp_path_factory):
     return paths
 
 
+@pytest.fixture(scope="module")
+def dyn_engine():
+    """An engine that keeps the dynamic tail (device-counter chunks) at every search size
+    (TSG_POOL_SMALL=0; by default a search under 32 static units per workgroup, i.e.
+    under ~5 M entries, is split statically whole)."""
+    os.environ["TSG_POOL_SMALL"] = "0"
+    try:
+        e = T.Engine()
+    finally:
+        del os.environ["TSG_POOL_SMALL"]
+    yield e
+    e.close()
+
+
 @pytest.mark.parametrize("qi", range(len(QUERIES)))
-def test_pool_ragged_32_blocks(engine, ragged, qi):
-    assert run(engine, ragged, QUERIES[qi]) == oracle(ragged, QUERIES[qi])
+def test_pool_ragged_32_blocks(engine, dyn_engine, ragged, qi):
+    exp = oracle(ragged, QUERIES[qi])
+    assert run(engine, ragged, QUERIES[qi]) == exp
+    assert run(dyn_engine, ragged, QUERIES[qi]) == exp
 
 
 @pytest.mark.parametrize("limit", [1, 20, 700])
-def test_pool_limit(engine, ragged, limit):
+def test_pool_limit(engine, dyn_engine, ragged, limit):
     """Limit queries: every block of the wave scanned whole, each block cut to its first L
     matches on the host (the one-launch kernel's per-block caps); the consumer's distinct-id
     stop and the two-wave early exit stay in tsg_search."""
     for q in (CFG2, dict(tags={"service.name": "svc-07"})):
-        assert run(engine, ragged, q, limit) == oracle(ragged, q, limit)
+        exp = oracle(ragged, q, limit)
+        assert run(engine, ragged, q, limit) == exp
+        assert run(dyn_engine, ragged, q, limit) == exp
 
 
-def test_pool_tiny_searches(engine, ragged):
-    """Fewer units than CUs: no static run, every unit claimed from the device counter."""
+def test_pool_tiny_searches(engine, dyn_engine, ragged):
+    """Fewer units than CUs: workgroups without units (static split), or no static run at
+    all and every unit claimed from the device counter (dynamic tail kept)."""
     for paths in (ragged[:1], ragged[:5], ragged[2:11]):
         for q in QUERIES[:4]:
-            assert run(engine, paths, q) == oracle(paths, q)
+            exp = oracle(paths, q)
+            assert run(engine, paths, q) == exp
+            assert run(dyn_engine, paths, q) == exp
 
 
 def test_pool_dense_fallback_then_sparse(ragged):
@@ -117,7 +138,7 @@ def test_pool_dense_fallback_then_sparse(ragged):
         small.close()
 
 
-def test_pool_segment_growth_and_shrink(engine, ragged):
+def test_pool_segment_growth_and_shrink(dyn_engine, ragged):
     """Host segments grow for a query with tens of matches per workgroup (a rerun's split
     differs from the first launch's: it can overflow again), then halve back over sparse
     queries; every query in the sequence stays exact."""
@@ -125,7 +146,7 @@ def test_pool_segment_growth_and_shrink(engine, ragged):
     exp = {"cfg2": oracle(ragged, CFG2), "one": oracle(ragged, one)}
     assert len(exp["one"][0]) > 32 * 256  # (more than a 32-record segment per workgroup on average)
     for name in ["cfg2", "one", "cfg2", "cfg2", "cfg2", "cfg2", "one", "cfg2"]:
-        assert run(engine, ragged, CFG2 if name == "cfg2" else one) == exp[name]
+        assert run(dyn_engine, ragged, CFG2 if name == "cfg2" else one) == exp[name]
 
 
 def test_pool_matches_segment_engine(engine, ragged):
