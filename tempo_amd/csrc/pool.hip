@@ -364,8 +364,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   uint32_t S = uint32_t(uint64_t(U) * (100 - dc.pool_dyn_pct) / 100 / W);
   // small searches (a limit query's first wave, one block): every unit static. Their
   // refill triggers would all fall in the first two claim rounds, and chunks are
-  // requested strictly in order: a chain of device-counter round trips (limit-20 first
-  // wave, 2 M entries: 16.5 us kernel)
+  // requested strictly in order: a chain of device-counter round trips
   if (S < dc.pool_small) S = uint32_t((uint64_t(U) + W - 1) / W);
   // units per dynamic claim: TSG_POOL_CHUNK (16), at most half a workgroup's static run
   uint32_t cs = dc.pool_chunk_shift;
