@@ -22,7 +22,14 @@
  *                         (modules/ingester/instance_search.go:45-70) with
  *                         search.CombineSearchResults (tempodb/search/util.go:40-62)
  *   tsg_block_tags /      BackendSearchBlock.Tags / TagValues
- *   tsg_block_tag_values  (tempodb/search/backend_search_block.go:145-181)
+ *   tsg_block_tag_values  (tempodb/search/backend_search_block.go:145-181),
+ *                         StreamingSearchBlock.Tags / TagValues
+ *                         (tempodb/search/streaming_search_block.go:97-116)
+ *   tsg_search_tags /     instance.SearchTags / SearchTagValues
+ *   tsg_search_tag_values (modules/ingester/instance_search.go:187-273)
+ *   tsg_live_block_open_mem  the live traces instance.searchLiveTraces walks
+ *                         (modules/ingester/instance_search.go:83-130), searched by
+ *                         tsg_search like any other block
  *   tsg_v2block_open /    v2.BackendBlock.find: bloom shard select + bloom test +
  *   tsg_lookup_ids        index lower_bound (tempodb/encoding/v2/backend_block.go:38-92,
  *                         tempodb/encoding/common/bloom.go:83-93,
@@ -45,7 +52,7 @@
 extern "C" {
 #endif
 
-#define TSG_ABI_VERSION 3
+#define TSG_ABI_VERSION 4
 
 /* Status codes. */
 #define TSG_OK 0
@@ -208,6 +215,22 @@ int tsg_wal_block_open(tsg_ctx *ctx, const char *path, int device_hint, tsg_bloc
 int tsg_wal_block_open_mem(tsg_ctx *ctx, const uint8_t *data, size_t len, int encoding, int device_hint,
                            tsg_block **out);
 
+/* ---- live traces (instance.searchLiveTraces) -------------------------------------- */
+/* A snapshot of the ingester's live traces (i.traces, in its iteration order), copied in:
+ * segment i = bytes[seg_off[i], seg_off[i+1]) is one searchData buffer as the distributor
+ * pushed it (a SearchEntry flatbuffer; liveTrace.searchData, modules/ingester/trace.go:37,76-80),
+ * trace t owns segments [trace_seg[t], trace_seg[t+1]) (trace_seg[0] = 0, trace_seg[ntraces] =
+ * nsegs; a trace without search data has none). tsg_search on the handle restates
+ * searchLiveTraces (instance_search.go:83-130): every segment is matched on its own
+ * (Pipeline.Matches), a trace's matching segments are combined with CombineSearchResults
+ * (tempodb/search/util.go:40-62) into one result whose entry_idx is the trace's position;
+ * tracesInspected += 1 per trace visited, bytesInspected += every segment's length; no block
+ * filter, no blocksInspected. Under a limit the consumer stops after the trace that brings the
+ * L-th distinct id (the deterministic refinement). A segment shorter than 4 bytes
+ * -> TSG_E_CORRUPT (the reference's entry.Reset panics). */
+int tsg_live_block_open_mem(tsg_ctx *ctx, const uint8_t *bytes, const uint64_t *seg_off, size_t nsegs,
+                            const uint64_t *trace_seg, size_t ntraces, int device_hint, tsg_block **out);
+
 typedef struct tsg_block_info {
   uint64_t entries;
   uint64_t pages;
@@ -225,14 +248,31 @@ typedef struct tsg_block_info {
                               after the pages before it (0 = none) */
   int32_t index_truncated; /* 1: an index record failed (checksum, framing, zero record): the block
                               ends silently before it, as the reference's Search does */
+  int32_t live;            /* 1: live traces (tsg_live_block_open_mem) */
+  int32_t pad0;
+  uint64_t traces;         /* live: traces (entries = their segments); otherwise = entries */
 } tsg_block_info;
 int tsg_block_info_get(const tsg_block *b, tsg_block_info *out);
 
-/* BackendSearchBlock.Tags / TagValues from the block header. Output is a
- * packed list: u32 len + bytes, repeated; *out_n = count. Free with tsg_free. */
+/* SearchableBlock.Tags / TagValues of one block: a backend block's search-header (Tags: every
+ * key of the header rollup; TagValues: FindTag on it), a WAL block's mutable header (the
+ * exact key's values), live traces (Tags: every key of every segment; TagValues: FindTag on
+ * every segment). Output is a packed list, sorted and unique: u32 len + bytes, repeated;
+ * *out_n = count. Free with tsg_free. A backend block opened without search data ->
+ * TSG_E_NOT_FOUND (its readSearchHeader fails with ErrDoesNotExist). */
 int tsg_block_tags(const tsg_block *b, uint8_t **out, size_t *out_len, size_t *out_n);
 int tsg_block_tag_values(const tsg_block *b, const uint8_t *key, size_t klen, uint8_t **out,
                          size_t *out_len, size_t *out_n);
+/* instance.SearchTags / SearchTagValues over an instance's searchable blocks: live blocks
+ * first, then the others in caller order (WAL head + append blocks, then local blocks, as the
+ * ingester visits them); the first block error fails the call. TagValues applies
+ * util.MapSizeWithinLimit (sum of the distinct values' lengths < max_bytes) after the live
+ * blocks and again after all blocks and returns an EMPTY list when it fails, as the reference
+ * does to protect the querier (overrides MaxBytesPerTagValuesQuery, default 5e6);
+ * max_bytes < 0 = no check. Same output format as tsg_block_tags. */
+int tsg_search_tags(tsg_block *const *blocks, size_t nblocks, uint8_t **out, size_t *out_len, size_t *out_n);
+int tsg_search_tag_values(tsg_block *const *blocks, size_t nblocks, const uint8_t *key, size_t klen,
+                          int64_t max_bytes, uint8_t **out, size_t *out_len, size_t *out_n);
 void tsg_free(void *p);
 
 /* Search blocks[0..nblocks) with the normalised query. Blocks may live on

@@ -102,6 +102,14 @@ def lib():
         L.orc_colblock_entries.restype = C.c_uint64
         L.orc_columnar_search.argtypes = [C.POINTER(vp), C.c_uint32, C.POINTER(Request), C.c_int,
                                           C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.orc_live_block_load_mem.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
+                                              C.POINTER(vp)]
+        pp = C.POINTER(C.POINTER(C.c_uint8))
+        sz = C.POINTER(C.c_size_t)
+        L.orc_block_tags.argtypes = [vp, pp, sz, sz]
+        L.orc_block_tag_values.argtypes = [vp, C.c_char_p, C.c_size_t, pp, sz, sz]
+        L.orc_search_tags.argtypes = [C.POINTER(vp), C.c_uint32, pp, sz, sz]
+        L.orc_search_tag_values.argtypes = [C.POINTER(vp), C.c_uint32, C.c_char_p, C.c_size_t, C.c_int64, pp, sz, sz]
         L.orc_v2_shard_count.argtypes = [vp]
         L.orc_v2_shard_count.restype = C.c_uint32
         _lib = L
@@ -141,6 +149,76 @@ class Block:
         if getattr(self, "h", None) and _lib is not None:
             _lib.orc_block_free(self.h)
             self.h = None
+
+
+def live_wire(traces):
+    """[[segment bytes, ...] per trace] -> (bytes, seg_off u64[nsegs+1], trace_seg u64[ntraces+1])."""
+    import numpy as np
+    segs = [s for t in traces for s in t]
+    seg_off = np.zeros(len(segs) + 1, dtype=np.uint64)
+    if segs:
+        seg_off[1:] = np.cumsum([len(s) for s in segs])
+    trace_seg = np.zeros(len(traces) + 1, dtype=np.uint64)
+    if traces:
+        trace_seg[1:] = np.cumsum([len(t) for t in traces])
+    return b"".join(segs), seg_off, trace_seg
+
+
+class LiveBlock:
+    """Live traces (instance.searchLiveTraces): traces = [[segment, ...], ...] in the
+    ingester's iteration order; each segment a SearchEntry flatbuffer."""
+
+    def __init__(self, traces):
+        data, seg_off, trace_seg = live_wire(traces)
+        self._keep = (data, seg_off, trace_seg)
+        self.h = C.c_void_p()
+        rc = lib().orc_live_block_load_mem(data, seg_off.ctypes.data, len(seg_off) - 1, trace_seg.ctypes.data,
+                                           len(trace_seg) - 1, C.byref(self.h))
+        if rc != 0:
+            raise OSError(f"orc_live_block_load_mem -> {rc}")
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_block_free(self.h)
+            self.h = None
+
+
+def _strings(fn, *args):
+    out, ln, n = C.POINTER(C.c_uint8)(), C.c_size_t(), C.c_size_t()
+    rc = fn(*args, C.byref(out), C.byref(ln), C.byref(n))
+    if rc != 0:
+        return rc, None
+    b = C.string_at(out, ln.value) if ln.value else b""
+    lib().orc_free(out)
+    res, o = [], 0
+    for _ in range(n.value):
+        k = int.from_bytes(b[o:o + 4], "little")
+        res.append(b[o + 4:o + 4 + k])
+        o += 4 + k
+    return 0, res
+
+
+def block_tags(block):
+    """(status, sorted tag names) of one block (oracle)."""
+    return _strings(lib().orc_block_tags, block.h)
+
+
+def block_tag_values(block, key):
+    key = key.encode() if isinstance(key, str) else key
+    return _strings(lib().orc_block_tag_values, block.h, key, len(key))
+
+
+def search_tags(blocks):
+    """instance.SearchTags over blocks (live blocks first): (status, sorted names)."""
+    arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+    return _strings(lib().orc_search_tags, arr, len(blocks))
+
+
+def search_tag_values(blocks, key, max_bytes=-1):
+    """instance.SearchTagValues over blocks (live first, MapSizeWithinLimit checks)."""
+    key = key.encode() if isinstance(key, str) else key
+    arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+    return _strings(lib().orc_search_tag_values, arr, len(blocks), key, len(key), max_bytes)
 
 
 def _unpack(res):

@@ -840,6 +840,11 @@ static int unmarshal_advance(const uint8_t **buf, size_t *len, const uint8_t **i
 /* backend search block                                                        */
 struct orc_block {
   int wal; /* a search WAL file (StreamingSearchBlock): data = the file, enc from its name */
+  int live; /* live traces (instance.searchLiveTraces): data = segment bytes, seg_off/trace_seg */
+  uint32_t ntraces;
+  uint64_t nsegs;
+  uint64_t *seg_off;   /* nsegs + 1 offsets into data */
+  uint64_t *trace_seg; /* ntraces + 1: first segment of each trace */
   int has_meta;
   int enc;
   char version[16];
@@ -879,6 +884,8 @@ int orc_block_load(const char *dir, orc_block **out) {
 }
 void orc_block_free(orc_block *b) {
   if (!b) return;
+  free(b->seg_off);
+  free(b->trace_seg);
   free(b->header);
   free(b->index);
   free(b->data);
@@ -988,8 +995,11 @@ static int result_from_entry(const fbt *e, uint32_t bidx, uint64_t scan_pos, mli
 typedef int (*consume_fn)(void *ctx, const orc_match *m);
 static int wal_search(const orc_block *b, uint32_t bidx, const orc_pipeline *p, mlist *out, consume_fn consume,
                       void *cctx, int *quit);
+static int live_search(const orc_block *b, uint32_t bidx, const orc_pipeline *p, mlist *out, consume_fn consume,
+                       void *cctx, int *quit);
 static int block_search(const orc_block *b, uint32_t bidx, const orc_pipeline *p, mlist *out,
                         consume_fn consume, void *cctx, int *quit) {
+  if (b->live) return live_search(b, bidx, p, out, consume, cctx, quit);
   if (b->wal) return wal_search(b, bidx, p, out, consume, cctx, quit);
   if (!b->has_meta) return ORC_OK; /* ErrDoesNotExist -> nil (:191-203) */
   if (strcmp(b->version, "v2") != 0) return ORC_UNSUPPORTED_ENCODING; /* encoding.FromVersion */
@@ -1968,6 +1978,269 @@ done:
   free(recs);
   kvset_free(&hdr);
   return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* live traces (modules/ingester/instance_search.go:83-130)                     */
+int orc_live_block_load_mem(const uint8_t *bytes, const uint64_t *seg_off, uint64_t nsegs, const uint64_t *trace_seg,
+                            uint32_t ntraces, orc_block **out) {
+  if (nsegs && (!seg_off || !bytes)) return ORC_INVALID;
+  if (!trace_seg || trace_seg[0] != 0 || trace_seg[ntraces] != nsegs) return ORC_INVALID;
+  for (uint32_t t = 0; t < ntraces; t++)
+    if (trace_seg[t] > trace_seg[t + 1]) return ORC_INVALID;
+  for (uint64_t i = 0; i < nsegs; i++)
+    if (seg_off[i] > seg_off[i + 1]) return ORC_INVALID;
+  orc_block *b = (orc_block *)calloc(1, sizeof(*b));
+  b->live = 1;
+  b->has_meta = 1;
+  strcpy(b->version, "v2");
+  b->ntraces = ntraces;
+  b->nsegs = nsegs;
+  const uint64_t total = nsegs ? seg_off[nsegs] - seg_off[0] : 0;
+  b->data = (uint8_t *)malloc(total ? total : 1);
+  if (total) memcpy(b->data, bytes + seg_off[0], total);
+  b->data_len = total;
+  b->seg_off = (uint64_t *)malloc((nsegs + 1) * sizeof(uint64_t));
+  for (uint64_t i = 0; i <= nsegs; i++) b->seg_off[i] = nsegs ? seg_off[i] - seg_off[0] : 0;
+  b->trace_seg = (uint64_t *)malloc(((uint64_t)ntraces + 1) * sizeof(uint64_t));
+  memcpy(b->trace_seg, trace_seg, ((uint64_t)ntraces + 1) * sizeof(uint64_t));
+  *out = b;
+  return ORC_OK;
+}
+
+/* searchLiveTraces: per trace (the caller's order = the ingester's map iteration),
+ * sr.Quit() check, AddTraceInspected(1); per segment AddBytesInspected(len(s)) and
+ * p.Matches(entry) on its own; the matching segments' results combined with
+ * CombineSearchResults (tempodb/search/util.go:40-62); one AddResult per trace.
+ * entry_idx = the trace's position. No block filter, no blocksInspected. */
+static int live_search(const orc_block *b, uint32_t bidx, const orc_pipeline *p, mlist *out, consume_fn consume,
+                       void *cctx, int *quit) {
+  for (uint32_t t = 0; t < b->ntraces; t++) {
+    if (*quit) break;
+    out->met.traces_inspected += 1;
+    uint64_t mi = UINT64_MAX; /* index of this trace's result in out->m */
+    for (uint64_t sgi = b->trace_seg[t]; sgi < b->trace_seg[t + 1]; sgi++) {
+      const uint8_t *seg = b->data + b->seg_off[sgi];
+      const size_t sl = (size_t)(b->seg_off[sgi + 1] - b->seg_off[sgi]);
+      out->met.bytes_inspected += sl;
+      if (sl < 4) return ORC_CORRUPT; /* (entry.Reset panics on a buffer without a root offset) */
+      fbt e = fb_root(seg, sl);
+      if (!pipeline_matches(p, &e)) continue;
+      if (mi == UINT64_MAX) {
+        orc_match *m;
+        int rc = result_from_entry(&e, bidx, t, out, &m);
+        if (rc) return rc;
+        mi = out->n - 1;
+        continue;
+      }
+      /* CombineSearchResults(existing, GetSearchResultFromData(entry)) */
+      orc_match *x = &out->m[mi];
+      uint32_t il = 0;
+      const uint8_t *tid = NULL;
+      uint16_t io = fb_offset(&e, VT_ENTRY_ID);
+      if (io) tid = fb_byte_vector(&e, io + e.pos, &il);
+      if (il > 16) return ORC_CORRUPT;
+      static const uint8_t zero[16];
+      if (memcmp(x->id, zero, 16) == 0) { /* existing.TraceID == "" (an all-zero id trims to "") */
+        memset(x->id, 0, 16);
+        if (il) memcpy(x->id + 16 - il, tid, il);
+        x->id_len = il;
+      }
+      uint32_t sl2, nl2;
+      const uint8_t *sv = entry_get(&e, "root.service.name", &sl2);
+      const uint8_t *nv = entry_get(&e, "root.name", &nl2);
+      if (x->svc_len == 0 && sl2) { x->svc_off = ml_str(out, sv, sl2); x->svc_len = sl2; }
+      x = &out->m[mi];
+      if (x->name_len == 0 && nl2) { x->name_off = ml_str(out, nv, nl2); x->name_len = nl2; }
+      x = &out->m[mi];
+      const uint64_t st = fb_u64(&e, VT_ENTRY_START), en = fb_u64(&e, VT_ENTRY_END);
+      const uint32_t dur = (uint32_t)((en - st) / 1000000ULL);
+      if (x->start_ns > st) x->start_ns = st;
+      if (x->duration_ms < dur) x->duration_ms = dur;
+    }
+    if (mi != UINT64_MAX && consume && consume(cctx, &out->m[mi])) *quit = 1;
+  }
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* SearchTags / SearchTagValues                                                 */
+typedef struct strset {
+  kvset s; /* (string, "") pairs */
+} strset;
+static void ss_add(strset *s, const uint8_t *p, size_t n) { kvset_add(&s->s, p, n, (const uint8_t *)"", 0); }
+static int ss_pack(strset *s, uint8_t **out, size_t *len, size_t *n) { /* sorted, unique, u32 len + bytes */
+  kvset_unique(&s->s);
+  size_t total = 0;
+  for (size_t i = 0; i < s->s.n; i++) total += 4 + s->s.p[i].kl;
+  uint8_t *b = (uint8_t *)malloc(total ? total : 1);
+  size_t o = 0;
+  for (size_t i = 0; i < s->s.n; i++) {
+    uint32_t l = (uint32_t)s->s.p[i].kl;
+    memcpy(b + o, &l, 4);
+    if (l) memcpy(b + o + 4, s->s.p[i].k, l);
+    o += 4 + l;
+  }
+  *out = b;
+  *len = total;
+  *n = s->s.n;
+  kvset_free(&s->s);
+  memset(s, 0, sizeof *s);
+  return ORC_OK;
+}
+static uint64_t ss_bytes(strset *s) { /* util.MapSizeWithinLimit's sum over the set's keys */
+  kvset_unique(&s->s);
+  uint64_t t = 0;
+  for (size_t i = 0; i < s->s.n; i++) t += s->s.p[i].kl;
+  return t;
+}
+/* the mutable header of a WAL block: every (key, value) of every replayed page's entry
+ * (SearchBlockHeaderMutable.AddEntry, SearchBlockHeader_util.go:21-43) */
+static void wal_header_pairs(const orc_block *b, kvset *hdr) {
+  size_t off = 0;
+  while (off < b->data_len) {
+    if (b->data_len - off < 6) break;
+    uint32_t total = le32(b->data + off);
+    if (total < 6 || total > b->data_len - off) break;
+    uint8_t *page;
+    size_t pl;
+    if (data_read_page(b->data, b->data_len, b->enc, off, total, &page, &pl)) break;
+    const uint8_t *cur = page, *id, *obj;
+    size_t cl = pl, objl;
+    uint32_t idl;
+    if (unmarshal_advance(&cur, &cl, &id, &idl, &obj, &objl) != 0 || cl != 0) { free(page); break; }
+    fbt e = fb_root(obj, objl);
+    entry_pairs(&e, hdr);
+    free(page);
+    off += total;
+  }
+}
+/* Tags of one searchable block into s: BackendSearchBlock.Tags (header keys,
+ * backend_search_block.go:145-162), StreamingSearchBlock.Tags (mutable header keys,
+ * streaming_search_block.go:97-105), live traces (every segment's keys,
+ * instance_search.go:191-200). A backend block without search data: the header read
+ * fails (ErrDoesNotExist) -> ORC_NOT_FOUND. */
+static int block_tags(const orc_block *b, strset *s) {
+  if (b->live) {
+    for (uint64_t i = 0; i < b->nsegs; i++) {
+      const size_t sl = (size_t)(b->seg_off[i + 1] - b->seg_off[i]);
+      if (sl < 4) return ORC_CORRUPT;
+      fbt e = fb_root(b->data + b->seg_off[i], sl);
+      uint32_t nt = tc_len(&e, VT_ENTRY_TAGS);
+      for (uint32_t j = 0; j < nt; j++) {
+        fbt kv;
+        tc_tag(&e, VT_ENTRY_TAGS, j, &kv);
+        uint32_t kl;
+        const uint8_t *k = kv_key(&kv, &kl);
+        ss_add(s, k ? k : (const uint8_t *)"", kl);
+      }
+    }
+    return ORC_OK;
+  }
+  if (b->wal) {
+    if (b->enc != 0 && b->enc != 6) return ORC_UNSUPPORTED_ENCODING;
+    kvset hdr;
+    memset(&hdr, 0, sizeof hdr);
+    wal_header_pairs(b, &hdr);
+    for (size_t i = 0; i < hdr.n; i++) ss_add(s, hdr.p[i].k, hdr.p[i].kl);
+    kvset_free(&hdr);
+    return ORC_OK;
+  }
+  if (!b->has_meta) return ORC_NOT_FOUND;
+  fbt h = fb_root(b->header, b->header_len);
+  uint32_t nt = tc_len(&h, VT_HDR_TAGS);
+  for (uint32_t j = 0; j < nt; j++) {
+    fbt kv;
+    tc_tag(&h, VT_HDR_TAGS, j, &kv);
+    uint32_t kl;
+    const uint8_t *k = kv_key(&kv, &kl);
+    ss_add(s, k ? k : (const uint8_t *)"", kl);
+  }
+  return ORC_OK;
+}
+static void kv_values_into(const fbt *kv, strset *s) {
+  uint32_t vn = kv_value_len(kv);
+  for (uint32_t j = 0; j < vn; j++) {
+    uint32_t vl;
+    const uint8_t *v = kv_value(kv, j, &vl);
+    ss_add(s, v ? v : (const uint8_t *)"", vl);
+  }
+}
+/* TagValues: FindTag on the header (backend_search_block.go:164-181); the mutable
+ * header's values of exactly that key (streaming_search_block.go:107-116); FindTag on
+ * every live segment (instance_search.go:229-240). */
+static int block_tag_values(const orc_block *b, const uint8_t *key, size_t kl, strset *s) {
+  if (b->live) {
+    for (uint64_t i = 0; i < b->nsegs; i++) {
+      const size_t sl = (size_t)(b->seg_off[i + 1] - b->seg_off[i]);
+      if (sl < 4) return ORC_CORRUPT;
+      fbt e = fb_root(b->data + b->seg_off[i], sl), kv;
+      if (find_tag(&e, VT_ENTRY_TAGS, key, kl, &kv)) kv_values_into(&kv, s);
+    }
+    return ORC_OK;
+  }
+  if (b->wal) {
+    if (b->enc != 0 && b->enc != 6) return ORC_UNSUPPORTED_ENCODING;
+    kvset hdr;
+    memset(&hdr, 0, sizeof hdr);
+    wal_header_pairs(b, &hdr);
+    for (size_t i = 0; i < hdr.n; i++)
+      if (hdr.p[i].kl == kl && (kl == 0 || memcmp(hdr.p[i].k, key, kl) == 0)) ss_add(s, hdr.p[i].v, hdr.p[i].vl);
+    kvset_free(&hdr);
+    return ORC_OK;
+  }
+  if (!b->has_meta) return ORC_NOT_FOUND;
+  fbt h = fb_root(b->header, b->header_len), kv;
+  if (find_tag(&h, VT_HDR_TAGS, key, kl, &kv)) kv_values_into(&kv, s);
+  return ORC_OK;
+}
+int orc_block_tags(const orc_block *b, uint8_t **out, size_t *len, size_t *n) {
+  strset s;
+  memset(&s, 0, sizeof s);
+  int rc = block_tags(b, &s);
+  if (rc) { kvset_free(&s.s); return rc; }
+  return ss_pack(&s, out, len, n);
+}
+int orc_block_tag_values(const orc_block *b, const uint8_t *key, size_t kl, uint8_t **out, size_t *len, size_t *n) {
+  strset s;
+  memset(&s, 0, sizeof s);
+  int rc = block_tag_values(b, key, kl, &s);
+  if (rc) { kvset_free(&s.s); return rc; }
+  return ss_pack(&s, out, len, n);
+}
+/* instance.SearchTags (instance_search.go:187-215): live traces first, then every block
+ * (WAL, then local: the caller's order); the first block error fails the request. */
+int orc_search_tags(orc_block *const *blocks, uint32_t nblocks, uint8_t **out, size_t *len, size_t *n) {
+  strset s;
+  memset(&s, 0, sizeof s);
+  for (int pass = 0; pass < 2; pass++)
+    for (uint32_t i = 0; i < nblocks; i++) {
+      if ((blocks[i]->live != 0) != (pass == 0)) continue;
+      int rc = block_tags(blocks[i], &s);
+      if (rc) { kvset_free(&s.s); return rc; }
+    }
+  return ss_pack(&s, out, len, n);
+}
+/* instance.SearchTagValues (instance_search.go:217-273): live traces, then the size check
+ * (util.MapSizeWithinLimit: sum of value lengths < max_bytes, else an EMPTY response),
+ * then every block and the check again. max_bytes < 0: no check. */
+int orc_search_tag_values(orc_block *const *blocks, uint32_t nblocks, const uint8_t *key, size_t kl, int64_t max_bytes,
+                          uint8_t **out, size_t *len, size_t *n) {
+  strset s;
+  memset(&s, 0, sizeof s);
+  for (int pass = 0; pass < 2; pass++) {
+    for (uint32_t i = 0; i < nblocks; i++) {
+      if ((blocks[i]->live != 0) != (pass == 0)) continue;
+      int rc = block_tag_values(blocks[i], key, kl, &s);
+      if (rc) { kvset_free(&s.s); return rc; }
+    }
+    if (max_bytes >= 0 && !((int64_t)ss_bytes(&s) < max_bytes)) {
+      kvset_free(&s.s);
+      memset(&s, 0, sizeof s);
+      return ss_pack(&s, out, len, n);
+    }
+  }
+  return ss_pack(&s, out, len, n);
 }
 
 /* SearchEntryMutable{id, tags, start, end}.ToBytes through the builder restatement

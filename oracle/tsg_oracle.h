@@ -76,6 +76,13 @@ int orc_block_load(const char *dir, orc_block **out);
 /* A search WAL file "<blockID>:<tenant>:v2:<encoding>[:...]" (StreamingSearchBlock):
  * orc_search replays it (header, sort, dedupe/combine) and searches it. */
 int orc_wal_block_load(const char *path, orc_block **out);
+/* Live traces (instance.searchLiveTraces, modules/ingester/instance_search.go:83-130):
+ * segment i = bytes[seg_off[i], seg_off[i+1]) (a SearchEntry flatbuffer as pushed),
+ * trace t = segments [trace_seg[t], trace_seg[t+1]) (a trace may have none). orc_search
+ * matches every segment on its own and combines a trace's matches (CombineSearchResults);
+ * entry_idx = the trace's position; no block filter, no blocksInspected. */
+int orc_live_block_load_mem(const uint8_t *bytes, const uint64_t *seg_off, uint64_t nsegs, const uint64_t *trace_seg,
+                            uint32_t ntraces, orc_block **out);
 void orc_block_free(orc_block *b);
 uint64_t orc_block_bytes(const orc_block *b);
 
@@ -92,6 +99,18 @@ int orc_pipeline_matches_entry(const orc_request *req, const uint8_t *fb, size_t
 int orc_pipeline_matches_block(const orc_request *req, const uint8_t *fb, size_t len);
 int orc_contains_tag_entry(const uint8_t *fb, size_t len, const uint8_t *k, size_t kl,
                            const uint8_t *v, size_t vl);
+
+/* Tags / TagValues of one block (backend: search-header, backend_search_block.go:145-181;
+ * WAL: the replayed mutable header, streaming_search_block.go:97-116; live: every segment,
+ * instance_search.go:187-240) and the instance aggregation (live blocks first, then the
+ * others in order; TagValues' MapSizeWithinLimit check after each, max_bytes < 0 = off).
+ * Output: sorted unique strings, u32 len + bytes each (malloc'd; orc_free). A backend block
+ * without search data -> ORC_NOT_FOUND (readSearchHeader fails). */
+int orc_block_tags(const orc_block *b, uint8_t **out, size_t *len, size_t *n);
+int orc_block_tag_values(const orc_block *b, const uint8_t *key, size_t kl, uint8_t **out, size_t *len, size_t *n);
+int orc_search_tags(orc_block *const *blocks, uint32_t nblocks, uint8_t **out, size_t *len, size_t *n);
+int orc_search_tag_values(orc_block *const *blocks, uint32_t nblocks, const uint8_t *key, size_t kl, int64_t max_bytes,
+                          uint8_t **out, size_t *len, size_t *n);
 
 /* hashes */
 uint64_t orc_xxhash64(const uint8_t *p, size_t n);

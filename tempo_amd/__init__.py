@@ -6,7 +6,7 @@ bloom/index trace-ID lookup (+ device findOne), and the proto-object
 BackendBlock.Search. ``tempo_amd.tsg`` is the ctypes host mirror.
 """
 from .tsg import (  # noqa: F401
-    BackendSearchBlock, Engine, StreamingSearchBlock, Pipeline, SearchMetrics, SearchRequest, TraceSearchMetadata, TsgError, V2Block,
+    BackendSearchBlock, Engine, StreamingSearchBlock, LiveTraces, live_wire, Pipeline, SearchMetrics, SearchRequest, TraceSearchMetadata, TsgError, V2Block,
     ENC_NONE, ENC_SNAPPY, SEARCH_TIME_ALL, SEARCH_TIME_DEFER, SEARCH_TIME_SCAN, fb_search_entry, fb_search_header, lib, synth_search_block, synth_v2_block,
     write_search_block, write_wal_search, wal_filename, ProtoBlock, ProtoSearchResponse, write_v2_block, go_parse,
     TSG_OK, TSG_E_NOT_FOUND, TSG_E_CORRUPT, TSG_E_UNSUPPORTED_ENCODING, TSG_E_DEVICE, TSG_E_CANCELLED, TSG_E_OOM,

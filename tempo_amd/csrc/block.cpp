@@ -618,4 +618,58 @@ void decode_wal_search_block(const uint8_t *file, size_t len, int enc, HostBlock
   canonicalize_narrow_keys(hb);
 }
 
+void decode_live_block(const uint8_t *bytes, const uint64_t *seg_off, uint64_t nsegs, const uint64_t *trace_seg,
+                       uint32_t ntraces, HostBlock &hb) {
+  hb = HostBlock();
+  hb.has_meta = true;
+  hb.live = true;
+  hb.meta.version = "v2";
+  hb.meta.encoding = 0;
+  if (trace_seg[0] != 0 || trace_seg[ntraces] != nsegs) fail(TSG_E_INVALID, "trace_seg must run from 0 to nsegs");
+  for (uint32_t t = 0; t < ntraces; t++)
+    if (trace_seg[t] > trace_seg[t + 1]) fail(TSG_E_INVALID, "trace_seg must be non-decreasing");
+  for (uint64_t i = 0; i < nsegs; i++)
+    if (seg_off[i] > seg_off[i + 1]) fail(TSG_E_INVALID, "seg_off must be non-decreasing");
+  hb.trace_row0.assign(size_t(ntraces) + 1, 0);
+  hb.trace_bytes0.assign(size_t(ntraces) + 1, 0);
+  hb.row_trace.reserve(nsegs);
+  std::vector<KeyBuild> kb;
+  PageParse pp;
+  for (uint32_t t = 0; t < ntraces; t++) {
+    uint64_t tb = 0;
+    for (uint64_t i = trace_seg[t]; i < trace_seg[t + 1]; i++) {
+      const uint64_t len = seg_off[i + 1] - seg_off[i];
+      // (entry.Reset reads the root offset: a segment shorter than 4 bytes panics the reference)
+      if (len < 4) fail(TSG_E_CORRUPT, "live segment shorter than a flatbuffer root offset");
+      pp = PageParse();
+      pp.buf.assign(bytes + seg_off[i], bytes + seg_off[i + 1]);
+      pp.fb_bytes = len;  // sr.AddBytesInspected(len(s))
+      pp.nentries = 1;
+      pp.tag_begin.push_back(0);
+      FbTable e = FbTable::root(pp.buf.data(), pp.buf.size());
+      std::unordered_map<uint32_t, uint32_t> memo;
+      parse_entry(e, pp.buf.data(), 0, pp, memo);
+      merge_page(hb, kb, pp);
+      hb.row_trace.push_back(t);
+      tb += len;
+    }
+    hb.trace_row0[t + 1] = hb.n;
+    hb.trace_bytes0[t + 1] = hb.trace_bytes0[t] + tb;
+  }
+  for (auto &kc : hb.keys) kc.col.resize(hb.n, kNone);
+  // TagValues (instance_search.go:229-240): FindTag on every segment. A row's key column
+  // holds the set FindTag lands on for that key, so the values are those of the sets used.
+  for (size_t k = 0; k < hb.keys.size(); k++) {
+    const KeyColumn &kc = hb.keys[k];
+    std::vector<uint8_t> used(kc.nsets(), 0);
+    for (uint32_t c : kc.col)
+      if (c != kNone) used[c] = 1;
+    auto &dst = hb.stream_tags[kc.name];
+    for (uint32_t s = 0; s < kc.nsets(); s++)
+      if (used[s])
+        for (uint32_t j = kc.set_off[s]; j < kc.set_off[s + 1]; j++) dst.insert(std::string(hb.dict_value(int(k), kc.set_vals[j])));
+  }
+  canonicalize_narrow_keys(hb);
+}
+
 }  // namespace tsg

@@ -137,7 +137,17 @@ struct HostBlock {
   bool index_truncated = false;
   int stop_status = 0;
   std::string stop_msg;
+  // WAL blocks: the mutable header's (key -> values) map (Tags / TagValues / block filter).
+  // Live blocks: per key the values FindTag reaches in some segment (TagValues).
   std::map<std::string, std::set<std::string>> stream_tags;
+  // Live traces (instance.searchLiveTraces, modules/ingester/instance_search.go:83-130): one
+  // row per search-data segment, rows in trace order; trace t = rows [trace_row0[t],
+  // trace_row0[t+1]) (a trace may have none), trace_bytes0 = prefix sums of the segments'
+  // lengths (bytesInspected). No header: searched without a block filter.
+  bool live = false;
+  std::vector<uint32_t> row_trace;
+  std::vector<uint64_t> trace_row0, trace_bytes0;
+  uint32_t ntraces() const { return trace_row0.empty() ? 0u : uint32_t(trace_row0.size() - 1); }
   SearchMeta meta;
   std::vector<uint8_t> header;  // raw search-header flatbuffer (kept for MatchesBlock/Tags)
   uint64_t min_dur = 0, max_dur = 0;
@@ -173,6 +183,11 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
 // equal ids combined, each resulting entry one scan position whose bytesInspected
 // is its object length.
 void decode_wal_search_block(const uint8_t *file, size_t len, int enc, HostBlock &out);
+// Live traces: segment i = bytes[seg_off[i], seg_off[i+1]) (a SearchEntry flatbuffer as the
+// distributor wrote it), trace t = segments [trace_seg[t], trace_seg[t+1]). Every segment is
+// one row (its own Matches, pitfall P3 resolved per table as for WAL entries).
+void decode_live_block(const uint8_t *bytes, const uint64_t *seg_off, uint64_t nsegs, const uint64_t *trace_seg,
+                       uint32_t ntraces, HostBlock &out);
 // wal.ParseFilename (tempodb/wal/wal.go:179-219): blockID:tenant:version:encoding[:dataEncoding]
 int parse_wal_filename(const std::string &name, std::string &version);
 

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <deque>
 #include <list>
+#include <set>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -387,6 +388,16 @@ int tsg_wal_block_open_mem(tsg_ctx *ctx, const uint8_t *data, size_t len, int en
     open_common(ctx, [&](HostBlock &h) { decode_wal_search_block(data, len, encoding, h); }, device_hint, out);
   });
 }
+int tsg_live_block_open_mem(tsg_ctx *ctx, const uint8_t *bytes, const uint64_t *seg_off, size_t nsegs,
+                            const uint64_t *trace_seg, size_t ntraces, int device_hint, tsg_block **out) {
+  if (!ctx || !out || !trace_seg || (nsegs && (!bytes || !seg_off)) || ntraces > 0xffffffffu) return TSG_E_INVALID;
+  return guard([&] {
+    static const uint64_t zero = 0;
+    const uint64_t *so = nsegs ? seg_off : &zero;
+    open_common(ctx, [&](HostBlock &h) { decode_live_block(bytes, so, nsegs, trace_seg, uint32_t(ntraces), h); },
+                device_hint, out);
+  });
+}
 int tsg_block_clone(tsg_ctx *ctx, const tsg_block *src, int device_hint, tsg_block **out) {
   if (!ctx || !src || !out) return TSG_E_INVALID;
   return guard([&] {
@@ -425,6 +436,9 @@ int tsg_block_info_get(const tsg_block *b, tsg_block_info *o) {
   o->partial = h.partial ? 1 : 0;
   o->stop_status = h.stop_status;
   o->index_truncated = h.index_truncated ? 1 : 0;
+  o->live = h.live ? 1 : 0;
+  o->pad0 = 0;
+  o->traces = h.live ? h.ntraces() : h.n;
   return TSG_OK;
 }
 
@@ -444,72 +458,119 @@ static void pack_strings(const std::vector<std::string> &v, uint8_t **out, size_
   *n = v.size();
 }
 
-// BackendSearchBlock.Tags / TagValues (backend_search_block.go:145-181) on the header rollup
+// SearchableBlock.Tags / TagValues of one block into a set (sorted, unique):
+// BackendSearchBlock (backend_search_block.go:145-181) on the header rollup,
+// StreamingSearchBlock (streaming_search_block.go:97-116) on the replayed mutable header,
+// live traces (instance_search.go:191-200, 229-240) on every segment.
+static void block_tags_into(const tsg_block *b, std::set<std::string> &keys) {
+  const HostBlock &h = *b->b.host;
+  if (h.live) {  // every KeyValues key of every segment (with or without values)
+    for (const auto &kc : h.keys) keys.insert(kc.name);
+    return;
+  }
+  if (h.streaming) {
+    for (auto &kv : h.stream_tags) keys.insert(kv.first);
+    return;
+  }
+  if (!h.has_meta) fail(TSG_E_NOT_FOUND, "search-header does not exist");
+  const auto &hb = h.header;
+  FbTable t = FbTable::root(hb.data(), hb.size());
+  uint16_t o = t.field(kHdrTags);
+  uint32_t cnt = o ? t.vector_len(o) : 0, st = o ? t.vector_start(o) : 0;
+  FbTable kv{hb.data(), hb.size(), 0};
+  for (uint32_t i = 0; i < cnt; i++) {
+    kv.pos = t.indirect(st + 4 * i);
+    uint16_t ko = kv.field(kKvKey);
+    keys.insert(std::string(ko ? kv.byte_vector(kv.pos + ko) : std::string_view()));
+  }
+}
+static void block_tag_values_into(const tsg_block *b, std::string_view key, std::set<std::string> &vals) {
+  const HostBlock &h = *b->b.host;
+  if (h.live || h.streaming) {
+    auto it = h.stream_tags.find(std::string(key));
+    if (it != h.stream_tags.end()) vals.insert(it->second.begin(), it->second.end());
+    return;
+  }
+  if (!h.has_meta) fail(TSG_E_NOT_FOUND, "search-header does not exist");
+  const auto &hb = h.header;
+  FbTable t = FbTable::root(hb.data(), hb.size());
+  uint16_t o = t.field(kHdrTags);
+  uint32_t cnt = o ? t.vector_len(o) : 0, st = o ? t.vector_start(o) : 0;
+  FbTable kv{hb.data(), hb.size(), 0};
+  uint32_t i = 0, j = cnt;  // FindTag binary search (searchdata_util.go:63-100)
+  bool found = false;
+  while (i < j) {
+    uint32_t m = (i + j) >> 1;
+    kv.pos = t.indirect(st + 4 * m);
+    uint16_t ko = kv.field(kKvKey);
+    std::string_view kk = ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
+    int c = bytes_compare(reinterpret_cast<const uint8_t *>(kk.data()), kk.size(),
+                          reinterpret_cast<const uint8_t *>(key.data()), key.size());
+    if (c == 0) {
+      found = true;
+      break;
+    }
+    if (c < 0) j = m;
+    else i = m + 1;
+  }
+  if (!found) return;
+  uint16_t vo = kv.field(kKvValue);
+  uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
+  for (uint32_t q = 0; q < vn; q++) vals.insert(std::string(kv.byte_vector(vs + 4 * q)));
+}
+static void pack_set(const std::set<std::string> &v, uint8_t **out, size_t *len, size_t *n) {
+  pack_strings(std::vector<std::string>(v.begin(), v.end()), out, len, n);
+}
+
 int tsg_block_tags(const tsg_block *b, uint8_t **out, size_t *len, size_t *n) {
   if (!b || !out || !len || !n) return TSG_E_INVALID;
   return guard([&] {
-    std::vector<std::string> keys;
-    const auto &hb = b->b.host->header;
-    if (b->b.host->streaming) {  // StreamingSearchBlock.Tags: the mutable header's keys
-      for (auto &kv : b->b.host->stream_tags) keys.push_back(kv.first);
-    } else if (b->b.host->has_meta) {
-      FbTable h = FbTable::root(hb.data(), hb.size());
-      uint16_t o = h.field(kHdrTags);
-      uint32_t cnt = o ? h.vector_len(o) : 0, st = o ? h.vector_start(o) : 0;
-      std::unordered_set<std::string> seen;
-      FbTable kv{hb.data(), hb.size(), 0};
-      for (uint32_t i = 0; i < cnt; i++) {
-        kv.pos = h.indirect(st + 4 * i);
-        uint16_t ko = kv.field(kKvKey);
-        std::string k(ko ? kv.byte_vector(kv.pos + ko) : std::string_view());
-        if (seen.insert(k).second) keys.push_back(k);
-      }
-    }
-    pack_strings(keys, out, len, n);
+    std::set<std::string> keys;
+    block_tags_into(b, keys);
+    pack_set(keys, out, len, n);
   });
 }
 int tsg_block_tag_values(const tsg_block *b, const uint8_t *key, size_t klen, uint8_t **out, size_t *len,
                          size_t *n) {
-  if (!b || !out || !len || !n) return TSG_E_INVALID;
+  if (!b || !out || !len || !n || (klen && !key)) return TSG_E_INVALID;
   return guard([&] {
-    std::vector<std::string> vals;
-    const auto &hb = b->b.host->header;
-    if (b->b.host->streaming) {  // StreamingSearchBlock.TagValues
-      auto it = b->b.host->stream_tags.find(std::string(reinterpret_cast<const char *>(key), klen));
-      if (it != b->b.host->stream_tags.end()) vals.assign(it->second.begin(), it->second.end());
-    } else if (b->b.host->has_meta) {
-      FbTable h = FbTable::root(hb.data(), hb.size());
-      uint16_t o = h.field(kHdrTags);
-      uint32_t cnt = o ? h.vector_len(o) : 0, st = o ? h.vector_start(o) : 0;
-      std::string_view k(reinterpret_cast<const char *>(key), klen);
-      FbTable kv{hb.data(), hb.size(), 0};
-      uint32_t i = 0, j = cnt;  // FindTag binary search (searchdata_util.go:63-100)
-      bool found = false;
-      while (i < j) {
-        uint32_t m = (i + j) >> 1;
-        kv.pos = h.indirect(st + 4 * m);
-        uint16_t ko = kv.field(kKvKey);
-        std::string_view kk = ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
-        int c = bytes_compare(reinterpret_cast<const uint8_t *>(kk.data()), kk.size(),
-                              reinterpret_cast<const uint8_t *>(k.data()), k.size());
-        if (c == 0) {
-          found = true;
+    std::set<std::string> vals;
+    block_tag_values_into(b, std::string_view(reinterpret_cast<const char *>(key), klen), vals);
+    pack_set(vals, out, len, n);
+  });
+}
+// instance.SearchTags (instance_search.go:187-215): live traces, then WAL and local blocks
+int tsg_search_tags(tsg_block *const *blocks, size_t nblocks, uint8_t **out, size_t *len, size_t *n) {
+  if ((nblocks && !blocks) || !out || !len || !n) return TSG_E_INVALID;
+  return guard([&] {
+    std::set<std::string> keys;
+    for (int pass = 0; pass < 2; pass++)
+      for (size_t i = 0; i < nblocks; i++)
+        if (blocks[i]->b.host->live == (pass == 0)) block_tags_into(blocks[i], keys);
+    pack_set(keys, out, len, n);
+  });
+}
+// instance.SearchTagValues (instance_search.go:217-273) with util.MapSizeWithinLimit
+// (pkg/util/map_size.go:4-11) after the live traces and after every block
+int tsg_search_tag_values(tsg_block *const *blocks, size_t nblocks, const uint8_t *key, size_t klen,
+                          int64_t max_bytes, uint8_t **out, size_t *len, size_t *n) {
+  if ((nblocks && !blocks) || (klen && !key) || !out || !len || !n) return TSG_E_INVALID;
+  return guard([&] {
+    const std::string_view k(reinterpret_cast<const char *>(key), klen);
+    std::set<std::string> vals;
+    for (int pass = 0; pass < 2; pass++) {
+      for (size_t i = 0; i < nblocks; i++)
+        if (blocks[i]->b.host->live == (pass == 0)) block_tag_values_into(blocks[i], k, vals);
+      if (max_bytes >= 0) {
+        int64_t size = 0;
+        for (const auto &v : vals) size += int64_t(v.size());
+        if (!(size < max_bytes)) {  // "exceeded limit": an empty response
+          vals.clear();
           break;
-        }
-        if (c < 0) j = m;
-        else i = m + 1;
-      }
-      if (found) {
-        uint16_t vo = kv.field(kKvValue);
-        uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
-        std::unordered_set<std::string> seen;
-        for (uint32_t q = 0; q < vn; q++) {
-          std::string v(kv.byte_vector(vs + 4 * q));
-          if (seen.insert(v).second) vals.push_back(v);
         }
       }
     }
-    pack_strings(vals, out, len, n);
+    pack_set(vals, out, len, n);
   });
 }
 
@@ -547,9 +608,15 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     // (per-query scratch kept per thread: no allocations once warm)
     thread_local std::vector<int> state;
     state.assign(nblocks, 0);  // 0 no meta, 1 skipped, 2 inspected
+    bool any_live = false;
     for (size_t i = 0; i < nblocks; i++) {
       Block &b = blocks[i]->b;
       if (!b.host->has_meta) continue;
+      if (b.host->live) {  // searchLiveTraces: no block filter
+        state[i] = 2;
+        any_live = true;
+        continue;
+      }
       bool ok = b.host->streaming
                     ? pipeline_matches_stream_header(*q, b.host->min_dur, b.host->max_dur, b.host->stream_tags)
                     : pipeline_matches_block(*q, b.host->header.data(), b.host->header.size());
@@ -563,6 +630,10 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     thread_local std::vector<std::pair<const SearchOut::Rec *, size_t>> per_block;
     per_block.assign(nblocks, {nullptr, 0});
     size_t nrec = 0;
+    // live blocks: a trace's result combines all its matching segments, so their rows are
+    // not capped per block; a launch holding one runs without per-block caps (the others'
+    // extra records are never consumed: ids are unique within a non-live block)
+    const uint32_t dlimit = any_live ? 0u : limit;
     auto search_range = [&](size_t b0, size_t b1) {
       // blocks per device, in first-seen device order (a handful of devices: linear search)
       std::vector<std::pair<DeviceCtx *, std::vector<std::pair<uint32_t, Block *>>>> per_dev;
@@ -593,7 +664,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
             SearchOut &o = *slots[slot];
             if (nl <= step) {  // one chunk: the device's list as it is
               check_cancel();
-              device_search(*dc, list, *q, limit, flags, o);
+              device_search(*dc, list, *q, dlimit, flags, o);
               return;
             }
             for (size_t c0 = 0; c0 < nl; c0 += step) {
@@ -601,11 +672,11 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
               const std::vector<std::pair<uint32_t, Block *>> part(list.begin() + c0,
                                                                    list.begin() + std::min(nl, c0 + step));
               if (c0 == 0) {
-                device_search(*dc, part, *q, limit, flags, o);
+                device_search(*dc, part, *q, dlimit, flags, o);
                 continue;
               }
               SearchOut more;
-              device_search(*dc, part, *q, limit, flags, more);
+              device_search(*dc, part, *q, dlimit, flags, more);
               o.recs.insert(o.recs.end(), more.recs.begin(), more.recs.end());
               o.device_bytes += more.device_bytes;
               o.kernel_ns += more.kernel_ns;
@@ -642,6 +713,59 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       m.kernel_ns += wave_k;
       m.scan_kernel_ns += wave_s;
     };
+    // searchLiveTraces' per-trace results: the block's matching rows (segments) come in row
+    // order = trace order; consecutive rows of one trace fold into one result with
+    // CombineSearchResults (tempodb/search/util.go:40-62)
+    struct LiveRec {
+      uint32_t trace;
+      uint8_t id[16];
+      uint8_t il;
+      uint64_t start, end;
+      uint32_t dur;
+      uint64_t row;
+      std::string_view sv, nm;
+    };
+    thread_local std::vector<LiveRec> live_recs;
+    auto rec_names = [&](const HostBlock &h, const SearchOut::Rec *r, std::string_view &sv, std::string_view &nm) {
+      sv = nm = std::string_view();
+      if (h.svc_key >= 0 && r->svc != kNone) sv = h.dict_value(h.svc_key, r->svc);
+      if (h.name_key >= 0 && r->name != kNone) nm = h.dict_value(h.name_key, r->name);
+    };
+    auto combine_live = [&](size_t i) {
+      live_recs.clear();
+      const HostBlock &h = *blocks[i]->b.host;
+      static const uint8_t zero[16] = {};
+      for (size_t ri = 0; ri < per_block[i].second; ri++) {
+        const SearchOut::Rec *r = per_block[i].first + ri;
+        const uint32_t t = h.row_trace[r->entry];
+        std::string_view sv, nm;
+        rec_names(h, r, sv, nm);
+        const uint32_t dur = uint32_t((r->end - r->start) / 1000000ULL);  // util.go:33
+        if (!live_recs.empty() && live_recs.back().trace == t) {
+          LiveRec &x = live_recs.back();
+          if (std::memcmp(x.id, zero, 16) == 0) {  // existing.TraceID == "" (all-zero ids trim to "")
+            std::memcpy(x.id, r->id, 16);
+            x.il = uint8_t(r->block_il >> 24);
+          }
+          if (x.sv.empty()) x.sv = sv;
+          if (x.nm.empty()) x.nm = nm;
+          if (x.start > r->start) x.start = r->start;
+          if (x.dur < dur) x.dur = dur;
+          continue;
+        }
+        LiveRec x;
+        x.trace = t;
+        std::memcpy(x.id, r->id, 16);
+        x.il = uint8_t(r->block_il >> 24);
+        x.start = r->start;
+        x.end = r->end;
+        x.dur = dur;
+        x.row = r->entry;
+        x.sv = sv;
+        x.nm = nm;
+        live_recs.push_back(x);
+      }
+    };
     // Early exit (limit > 0): the consumer stops at the L-th distinct
     // id in block order, so the blocks behind that point are never needed. A first wave
     // searches the leading blocks (>= 1/8 of the entries); only if the consumer has not
@@ -664,11 +788,20 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     if (b1 < nblocks) {
       std::unordered_set<std::string> seen;
       bool stop = false;
-      for (size_t i = 0; i < b1 && !stop; i++)
+      for (size_t i = 0; i < b1 && !stop; i++) {
+        if (state[i] == 2 && blocks[i]->b.host->live) {
+          combine_live(i);
+          for (size_t ri = 0; ri < live_recs.size() && !stop; ri++) {
+            seen.insert(std::string(reinterpret_cast<const char *>(live_recs[ri].id), 16));
+            stop = seen.size() >= limit;
+          }
+          continue;
+        }
         for (size_t ri = 0; ri < per_block[i].second && !stop; ri++) {
           seen.insert(std::string(reinterpret_cast<const char *>(per_block[i].first[ri].id), 16));
           stop = seen.size() >= limit;
         }
+      }
       if (!stop) search_range(b1, nblocks);
       check_cancel();
     }
@@ -682,6 +815,29 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     for (size_t i = 0; i < nblocks && !stopped; i++) {
       const HostBlock &h = *blocks[i]->b.host;
       if (state[i] == 0) continue;  // meta missing: no-op (backend_search_block.go:191-203)
+      if (h.live) {  // searchLiveTraces (instance_search.go:99-128)
+        combine_live(i);
+        uint64_t stop_trace = UINT64_MAX;
+        for (const LiveRec &x : live_recs) {
+          res->set(nout, x.id, x.il, x.start, x.end, uint32_t(i), x.trace, x.sv.data(), x.sv.size(), x.nm.data(),
+                   x.nm.size());
+          res->dur[nout++] = x.dur;
+          if (limit) {
+            distinct.insert(std::string(reinterpret_cast<const char *>(x.id), 16));
+            if (distinct.size() >= limit) {
+              stopped = true;
+              stop_trace = x.trace;
+              break;
+            }
+          }
+        }
+        // AddTraceInspected(1) and the segments' bytes for every trace visited: all of
+        // them, or those up to the one whose result closed the consumer
+        const uint64_t nt = stopped ? stop_trace + 1 : h.ntraces();
+        m.traces_inspected += uint32_t(nt);
+        m.bytes_inspected += h.trace_bytes0[nt];
+        continue;
+      }
       m.bytes_inspected += h.header.size();
       if (state[i] == 1) {
         m.blocks_skipped++;

@@ -98,7 +98,8 @@ class _BlockInfo(C.Structure):
                 ("header_bytes", C.c_uint64), ("fb_bytes", C.c_uint64), ("device_bytes", C.c_uint64),
                 ("min_dur_ns", C.c_uint64), ("max_dur_ns", C.c_uint64), ("device", C.c_int32),
                 ("encoding", C.c_int32), ("streaming", C.c_int32), ("partial", C.c_int32),
-                ("stop_status", C.c_int32), ("index_truncated", C.c_int32)]
+                ("stop_status", C.c_int32), ("index_truncated", C.c_int32), ("live", C.c_int32),
+                ("pad0", C.c_int32), ("traces", C.c_uint64)]
 
 
 class _LookupOpts(C.Structure):
@@ -145,7 +146,7 @@ EXPORTED = [
     "tsg_find_result_free", "tsg_proto_block_open", "tsg_proto_block_close", "tsg_proto_block_info",
     "tsg_proto_search", "tsg_proto_result_free", "tsg_go_parse", "tsg_write_v2_block",
     "tsg_write_search_block", "tsg_write_wal_search", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
-    "tsg_synth_v2_block",
+    "tsg_synth_v2_block", "tsg_live_block_open_mem", "tsg_search_tags", "tsg_search_tag_values",
 ]
 
 _lib = None
@@ -177,6 +178,11 @@ def lib():
         L.tsg_wal_block_open_mem.argtypes = [vp, C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(vp)]
         L.tsg_write_wal_search.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int]
         L.tsg_block_info_get.argtypes = [vp, C.POINTER(_BlockInfo)]
+        L.tsg_live_block_open_mem.argtypes = [vp, C.c_char_p, vp, C.c_size_t, vp, C.c_size_t, C.c_int, C.POINTER(vp)]
+        L.tsg_search_tags.argtypes = [C.POINTER(vp), C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
+                                      C.POINTER(C.c_size_t)]
+        L.tsg_search_tag_values.argtypes = [C.POINTER(vp), C.c_size_t, C.c_char_p, C.c_size_t, C.c_int64,
+                                            C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
         L.tsg_block_tags.argtypes = [vp, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
         L.tsg_block_tag_values.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
                                            C.POINTER(C.c_size_t)]
@@ -373,6 +379,21 @@ class Engine:
     def open_block(self, path: str, device: int = 0) -> "BackendSearchBlock":
         return BackendSearchBlock(self, path, device)
 
+    def open_live_traces(self, traces: Sequence[Sequence[bytes]], device: int = 0) -> "LiveTraces":
+        """A snapshot of the ingester's live traces (each a list of searchData segments, in
+        the ingester's iteration order) resident on a device (tsg_live_block_open_mem)."""
+        return LiveTraces(self, traces, device)
+
+    def search_tags(self, blocks: Sequence["BackendSearchBlock"]) -> List[bytes]:
+        """instance.SearchTags over the blocks (live ones first; tsg_search_tags)."""
+        return _packed(lib().tsg_search_tags, _handles(blocks), len(blocks))
+
+    def search_tag_values(self, blocks: Sequence["BackendSearchBlock"], key: bytes, max_bytes: int = -1) -> List[bytes]:
+        """instance.SearchTagValues (tsg_search_tag_values): max_bytes = the tenant's
+        MaxBytesPerTagValuesQuery (an over-limit set returns []); -1 = no check."""
+        key = key.encode() if isinstance(key, str) else key
+        return _packed(lib().tsg_search_tag_values, _handles(blocks), len(blocks), key, len(key), max_bytes)
+
     def search(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0, flags: int = 0,
                query_id: int = 0):
         """Ordered match sequence + metrics (tsg_search). flags: SEARCH_TIME_*; query_id
@@ -548,6 +569,24 @@ class Engine:
             self.h = None
 
 
+def _handles(blocks):
+    return (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+
+
+def _packed(fn, *args):
+    """A packed string list (u32 len + bytes each) from fn(*args, &out, &len, &n)."""
+    p, ln, n = C.POINTER(C.c_uint8)(), C.c_size_t(), C.c_size_t()
+    _check(fn(*args, C.byref(p), C.byref(ln), C.byref(n)))
+    buf = C.string_at(p, ln.value) if ln.value else b""
+    lib().tsg_free(p)
+    out, o = [], 0
+    for _ in range(n.value):
+        (l,) = struct.unpack_from("<I", buf, o)
+        out.append(buf[o + 4:o + 4 + l])
+        o += 4 + l
+    return out
+
+
 class BackendSearchBlock:
     """A backend search block resident on one device (tsg_block)."""
 
@@ -571,16 +610,7 @@ class BackendSearchBlock:
         return {f: getattr(i, f) for f, _ in _BlockInfo._fields_}
 
     def _strings(self, fn, *args):
-        p, ln, n = C.POINTER(C.c_uint8)(), C.c_size_t(), C.c_size_t()
-        _check(fn(self.h, *args, C.byref(p), C.byref(ln), C.byref(n)))
-        buf = C.string_at(p, ln.value) if ln.value else b""
-        lib().tsg_free(p)
-        out, o = [], 0
-        for _ in range(n.value):
-            (l,) = struct.unpack_from("<I", buf, o)
-            out.append(buf[o + 4:o + 4 + l])
-            o += 4 + l
-        return out
+        return _packed(fn, self.h, *args)
 
     def tags(self):
         return self._strings(lib().tsg_block_tags)
@@ -602,6 +632,33 @@ class StreamingSearchBlock(BackendSearchBlock):
 
     def __init__(self, eng: Engine, path: str, device: int = 0):
         super().__init__(eng, path, device, _wal=True)
+
+
+def live_wire(traces: Sequence[Sequence[bytes]]):
+    """[[segment, ...] per trace] -> (bytes, seg_off u64[nsegs + 1], trace_seg u64[ntraces + 1])."""
+    import numpy as np
+    segs = [sg for t in traces for sg in t]
+    seg_off = np.zeros(len(segs) + 1, dtype=np.uint64)
+    if segs:
+        seg_off[1:] = np.cumsum([len(sg) for sg in segs])
+    trace_seg = np.zeros(len(traces) + 1, dtype=np.uint64)
+    if len(traces):
+        trace_seg[1:] = np.cumsum([len(t) for t in traces])
+    return b"".join(segs), seg_off, trace_seg
+
+
+class LiveTraces(BackendSearchBlock):
+    """The ingester's live traces (instance.searchLiveTraces, modules/ingester/
+    instance_search.go:83-130) as one resident block: a row per searchData segment;
+    tsg_search matches each segment and combines a trace's matches into one result."""
+
+    def __init__(self, eng: Engine, traces: Sequence[Sequence[bytes]], device: int = 0):
+        self.path = None
+        self.h = C.c_void_p()
+        data, seg_off, trace_seg = live_wire(traces)
+        _check(lib().tsg_live_block_open_mem(eng.h, data, seg_off.ctypes.data, len(seg_off) - 1,
+                                             trace_seg.ctypes.data, len(trace_seg) - 1, device, C.byref(self.h)))
+        eng._open.add(self)
 
 
 @dataclass

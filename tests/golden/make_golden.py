@@ -13,6 +13,8 @@ Sources (reference checkout, Grafana Tempo ~v1.4.1):
   * tempodb/search/backend_search_block_test.go:24-88 TestBackendSearchBlockSearch
   * tempodb/search/streaming_search_block_test.go:101-154 metrics expectations
   * tempodb/encoding/common/bloom_test.go:120-154    TestBloomShardCount clamps
+  * modules/ingester/instance_search_test.go:41-97,331-371 TestInstanceSearch /
+    TestInstanceSearchMetrics live-trace stage (parsed: trace counts, tag, fraction)
 The pipeline tables use time.Now()-relative timestamps in Go; they are pinned
 here at a fixed NOW so the vectors are reproducible (the predicates only depend
 on differences and second truncation, which the chosen NOW keeps identical).
@@ -124,6 +126,29 @@ def contains_tag_table():
     }
 
 
+def instance_search_vectors():
+    """The live-trace stage of TestInstanceSearch and TestInstanceSearchMetrics, parsed from
+    the test source: trace counts, the annotated fraction and the tag."""
+    src = open(os.path.join(REF, "modules/ingester/instance_search_test.go")).read()
+    t1 = src[src.index("func TestInstanceSearch(t"): src.index("func TestInstanceSearchNoData")]
+    n1 = int(re.search(r"numTraces := (\d+)", t1).group(1))
+    frac = int(re.search(r"searchAnnotatedFractionDenominator := (\d+)", t1).group(1))
+    key = re.search(r'var tagKey = "([^"]*)"', t1).group(1)
+    val = re.search(r'var tagValue = "([^"]*)"', t1).group(1)
+    t2 = src[src.index("func TestInstanceSearchMetrics"): src.index("func BenchmarkInstanceSearchUnderLoad")]
+    n2 = int(re.search(r"numTraces := uint32\((\d+)\)", t2).group(1))
+    k2, v2 = re.search(r'data.AddTag\("([^"]*)", "([^"]*)"\)', t2).groups()
+    return {
+        # every `frac`-th of n1 live traces carries search data {key: val}; Search(key=val)
+        # returns n1 / frac traces (:95); the others are live traces with no segments
+        "search": {"num_traces": n1, "annotated_every": frac, "tag": [key, val], "expected_results": n1 // frac},
+        # n2 live traces, one segment each; an exhaustive search inspects every trace and
+        # the sum of the segments' lengths (:368-370)
+        "metrics": {"num_traces": n2, "tag": [k2, v2], "expected_traces_inspected": n2,
+                    "expected_bytes": "sum of len(searchData)"},
+    }
+
+
 def main():
     out = {
         "_provenance": "transcribed from the reference's tests by tests/golden/make_golden.py",
@@ -141,6 +166,7 @@ def main():
             {"name": "skips block", "req": {"nomatch": "nomatch"}, "results": 0, "blocks_inspected": 0,
              "traces_inspected": 0, "blocks_skipped": 1},
         ]},
+        "instance_search_live": instance_search_vectors(),
         # TestBloomShardCount (bloom_test.go:120-154) + ValidateShardCount
         "bloom_shard_count": [
             {"name": "too many shards", "fp": 0.01, "shard_size": 1, "estimated_objects": 100000,

@@ -38,7 +38,7 @@ def test_no_device_fails_loudly():
 
 
 def test_abi_version():
-    assert T.lib().tsg_abi_version() == 3
+    assert T.lib().tsg_abi_version() == 4
 
 
 @pytest.mark.parametrize("req,terms", [
