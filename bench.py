@@ -431,8 +431,8 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, gen_thread=Non
 def merge_leg(args, eng, base, pipe, rank, world, dist):
     """N > 1: the query as the frontend serves it (modules/frontend/searchsharding.go:32-125):
     every rank searches its block shard (full scan, the config-2 query), packs its ordered
-    match list into byte tensors, rank 0 gathers them (tempo_amd.shard.distributed_search_packed)
-    and merges. A few hundred records per rank: gathered on the host over a gloo group
+    match list into a wire buffer (tsg_result_pack), rank 0 gathers them
+    (tempo_amd.shard.distributed_search_packed) and merges them in libtsg (tsg_wire_merge). A few hundred records per rank: gathered on the host over a gloo group
     (north_star: "host-merged where that is cheaper"; the RCCL form of the same gather is
     covered by the packed-gather tests). Latency per query is the max over ranks."""
     from datetime import timedelta
@@ -443,13 +443,13 @@ def merge_leg(args, eng, base, pipe, rank, world, dist):
         g = dist.new_group(backend="gloo", timeout=timedelta(seconds=120))
         nb = len(base) * world
         everything = 1 << 30  # (full scan: the frontend merge keeps every distinct trace)
-        local = lambda: eng.search(base, pipe)  # noqa: E731
-        merged = shard.distributed_search_packed(local, everything, nb, device="cpu", group=g)
+        local = lambda: eng.search_wire(base, pipe)  # noqa: E731  (tsg_result_pack: no per-record Python)
+        merged = shard.distributed_search_packed(local, everything, nb, device="cpu", group=g, columns=True)
         dist.barrier(group=g)
         ts = []
         for _ in range(args.merge_steps):
             t0 = time.perf_counter()
-            merged = shard.distributed_search_packed(local, everything, nb, device="cpu", group=g)
+            merged = shard.distributed_search_packed(local, everything, nb, device="cpu", group=g, columns=True)
             dist.barrier(group=g)
             ts.append(time.perf_counter() - t0)
         tt = torch.tensor([sum(ts)], dtype=torch.float64)
@@ -458,8 +458,9 @@ def merge_leg(args, eng, base, pipe, rank, world, dist):
                "entries_per_s": len(base) * args.entries * world * args.merge_steps / float(tt.item()),
                "transport": "gloo (host) gather of packed records to rank 0, then merge"}
         if rank == 0:
-            res["merged_traces"] = len(merged[0])
-            res["inspected_traces"] = merged[1].inspected_traces
+            res["merged_traces"] = len(merged)
+            res["inspected_traces"] = merged.metrics.inspected_traces
+            res["block_errors"] = sum(1 for x in merged.block_status if x)
         return res
     except Exception as e:  # (the main line above is already measured; report, do not fail)
         return {"error": repr(e)}

@@ -115,7 +115,8 @@ typedef struct tsg_metrics {
   uint32_t traces_inspected;
   uint32_t blocks_inspected;
   uint32_t blocks_skipped;
-  uint32_t pad0;
+  uint32_t reruns;            /* extra search-kernel launches (a workgroup's records overflowed
+                                 its buffer); their device time is in kernel_ns / scan_kernel_ns */
   uint64_t bytes_inspected;
   uint64_t device_bytes_read; /* algorithmic bytes the scan kernels touched */
   uint64_t kernel_ns;         /* device time of the search kernels (HIP events) */
@@ -136,7 +137,7 @@ typedef struct tsg_result {
   const uint32_t *duration_ms; /* uint32((end-start)/1e6), util.go:33 */
   const uint32_t *block_idx;   /* index into the caller's block array */
   const uint64_t *entry_idx;   /* scan position inside the block */
-  const char *const *root_service; /* NUL-terminated copies; lengths below */
+  const char *const *root_service; /* (not NUL-terminated) lengths below */
   const uint32_t *root_service_len;
   const char *const *root_name;
   const uint32_t *root_name_len;
@@ -150,6 +151,13 @@ typedef struct tsg_result {
   uint64_t nblocks;
   const int32_t *block_status;
   const char *const *block_error;
+  /* Every name above as one blob: root_service[i] == names + root_service_off[i] (likewise
+   * root_name). Equal names of one dictionary share their bytes, so a dense result's blob
+   * stays small; a packed transport (tempo_amd/shard.py) ships it as it is. */
+  const char *names;
+  uint64_t names_len;
+  const uint64_t *root_service_off;
+  const uint64_t *root_name_off;
 } tsg_result;
 
 /* Options for tsg_search. */
@@ -160,7 +168,11 @@ typedef struct tsg_result {
 typedef struct tsg_search_opts {
   uint32_t limit;  /* 0 = no limit (every match) */
   uint32_t flags;  /* TSG_SEARCH_TIME_* (timing events cost a few us per search; off by default) */
-  uint64_t query_id; /* for tsg_cancel; 0 = not cancellable */
+  uint64_t query_id; /* for tsg_cancel; 0 = not cancellable. tsg_cancel on an id while its search
+                        runs stops it at the next device chunk or wave (TSG_E_CANCELLED); a cancel
+                        for an id whose search finished recently is ignored (it cannot fail a later
+                        search that reuses the id); one for an id not seen yet waits up to 10 s for
+                        its search to start. */
 } tsg_search_opts;
 
 /* ---- context --------------------------------------------------------------- */
@@ -293,6 +305,44 @@ int tsg_kernel_times(tsg_ctx *ctx, uint64_t *ns, size_t cap, size_t *n);
  * layout as tsg_result (block_idx/entry_idx = first occurrence). */
 int tsg_results_combine(const tsg_result *in, uint32_t max_results, tsg_result **out);
 
+/* ---- multi-GPU fan-out: packed responses and the frontend merge ------------------ */
+/* A response (one rank's / one job's tempopb.SearchResponse) as one byte buffer, for the
+ * gather to the merging rank (tempo_amd/shard.py). Little endian, sections 8-byte aligned:
+ *   tsg_wire_header | n x tsg_trace_rec | (nnames + 1) x u32 name offsets | names bytes |
+ *   nblocks x i32 block status | errors (per block with a non-zero status, in block order:
+ *   u32 length + message bytes)
+ * A record's names are indices into the name table (entry 0 = ""). */
+#define TSG_WIRE_MAGIC 0x57475354u /* "TSGW" */
+#define TSG_WIRE_VERSION 1u
+typedef struct tsg_trace_rec { /* tempopb.TraceSearchMetadata (pkg/tempopb/tempo.proto:72-79) */
+  uint8_t trace_id[16];        /* right-aligned (hex TraceID = these bytes, leading zeros trimmed) */
+  uint64_t start_ns;
+  uint32_t duration_ms;
+  uint32_t root_service; /* name table index */
+  uint32_t root_name;
+  uint8_t trace_id_len;
+  uint8_t pad[3];
+} tsg_trace_rec;
+typedef struct tsg_wire_header {
+  uint32_t magic, version;
+  uint64_t n, nnames, names_len, nblocks, errors_len;
+  uint64_t traces_inspected, bytes_inspected, blocks_inspected, blocks_skipped, skipped_traces; /* SearchMetrics */
+  uint64_t reserved;
+} tsg_wire_header;
+/* A tsg_result as a wire buffer (malloc'd; tsg_free). */
+int tsg_result_pack(const tsg_result *r, uint8_t **out, size_t *out_len);
+/* searchResponse (modules/frontend/searchsharding.go:32-125) over wire responses in the given
+ * order: before each response, shouldQuit (more than `limit` distinct traces taken) stops the
+ * merge; addResponse keeps the first record of every TraceID and sums InspectedTraces /
+ * InspectedBytes / SkippedBlocks / SkippedTraces; InspectedBlocks = total_blocks (set by the
+ * sharder, :221); result sorts by start time descending (ties: first position, a deterministic
+ * form of sort.Slice). Block statuses and errors of every response are carried in order. The
+ * merged response is written as a wire buffer into the caller's `out` (cap bytes; the sum of
+ * the input lengths always suffices): *out_len = its length; TSG_E_INVALID with *out_len = the
+ * needed size when cap is too small. Host code, no device needed; parallel over host threads. */
+int tsg_wire_merge(const uint8_t *const *wires, const size_t *lens, size_t n, uint64_t limit, uint64_t total_blocks,
+                   uint8_t *out, size_t cap, size_t *out_len);
+
 /* ---- v2 trace blocks: batched trace-ID lookup --------------------------------- */
 /* Reads <block_dir>/{meta.json,bloom-N...,index}; verifies index page checksums. */
 int tsg_v2block_open(tsg_ctx *ctx, const char *block_dir, int device_hint, tsg_v2block **out);
@@ -375,16 +425,18 @@ typedef struct tsg_proto_request {
 } tsg_proto_request;
 typedef struct tsg_proto_result {
   uint32_t n; /* TraceSearchMetadata, in object order */
-  const uint8_t *trace_ids;     /* object ids, trace_id_off / trace_id_len into this */
+  const uint8_t *trace_ids;     /* object ids (any length), trace_id_off / trace_id_len into this */
   const uint32_t *trace_id_off;
-  const uint8_t *trace_id_len;
-  const char *const *root_service_name;
-  const char *const *root_trace_name;
+  const uint32_t *trace_id_len;
+  const char *const *root_service_name; /* NUL-terminated, but proto strings may hold NUL bytes: */
+  const char *const *root_trace_name;   /* read them with the lengths below */
   const uint64_t *start_time_unix_nano;
   const uint32_t *duration_ms;
   const uint32_t *object_idx;   /* position of the object in the block's iterator order */
   uint64_t inspected_traces, inspected_bytes, skipped_traces; /* SearchMetrics */
   uint64_t kernel_ns;
+  const uint32_t *root_service_name_len;
+  const uint32_t *root_trace_name_len;
 } tsg_proto_result;
 int tsg_proto_block_open(tsg_ctx *ctx, const char *block_dir, int device_hint, tsg_proto_block **out);
 void tsg_proto_block_close(tsg_proto_block *b);

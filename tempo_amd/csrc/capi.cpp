@@ -7,7 +7,10 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <deque>
+#include <functional>
+#include <memory>
 #include <list>
 #include <set>
 #include <thread>
@@ -20,8 +23,99 @@
 #include "proto.hpp"
 #include "writer.hpp"
 
+// One persistent host thread per device for multi-device calls: a search or lookup whose
+// blocks span devices hands each further device's part to that device's worker (the caller
+// runs the first device's part itself) instead of starting a thread per device per call.
+struct DevWorker {
+  std::mutex m;
+  std::condition_variable cv;
+  std::deque<std::function<void()>> q;
+  bool stop = false;
+  std::thread th;
+  DevWorker() : th([this] { run(); }) {}
+  ~DevWorker() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      stop = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+  void run() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return stop || !q.empty(); });
+        if (q.empty()) return;
+        f = std::move(q.front());
+        q.pop_front();
+      }
+      f();
+    }
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      q.push_back(std::move(f));
+    }
+    cv.notify_one();
+  }
+};
+// Completion of a set of submitted parts.
+struct Latch {
+  std::mutex m;
+  std::condition_variable cv;
+  size_t left;
+  explicit Latch(size_t n) : left(n) {}
+  void done() {
+    std::lock_guard<std::mutex> lk(m);
+    if (--left == 0) cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(m);
+    cv.wait(lk, [&] { return left == 0; });
+  }
+};
+
 struct tsg_ctx {
   tsg::Ctx c;
+  std::mutex wmu;
+  std::unordered_map<const void *, std::unique_ptr<DevWorker>> workers;  // per DeviceCtx
+  DevWorker &worker(const void *dc) {
+    std::lock_guard<std::mutex> lk(wmu);
+    auto &w = workers[dc];
+    if (!w) w = std::make_unique<DevWorker>();
+    return *w;
+  }
+  // Runs part(i) for i in [0, n): part 0 on the calling thread, the others on the workers
+  // of key(i)'s device; exceptions are collected and the first rethrown.
+  template <class Key, class Part>
+  void fan_out(size_t n, Key &&key, Part &&part) {
+    if (n == 1) {
+      part(size_t(0));
+      return;
+    }
+    std::vector<std::exception_ptr> errs(n);
+    Latch latch(n - 1);
+    for (size_t i = 1; i < n; i++)
+      worker(key(i)).submit([&, i] {
+        try {
+          part(i);
+        } catch (...) {
+          errs[i] = std::current_exception();
+        }
+        latch.done();
+      });
+    try {
+      part(size_t(0));
+    } catch (...) {
+      errs[0] = std::current_exception();
+    }
+    latch.wait();
+    for (auto &e : errs)
+      if (e) std::rethrow_exception(e);
+  }
   // tsg_cancel: query ids cancelled and not yet seen finishing (bounded, FIFO eviction).
   // A search with that id checks the set between device chunks and waves
   // (cooperative, like BackendSearchBlock.Search's per-page sr.Quit()).
@@ -112,12 +206,52 @@ struct ResultHolder {
     id_len.reserve(n);
     if (24 * n > arena_cap) arena_grow(24 * n);
   }
+  // names are interned by source: every name comes from a block's host dictionary (or an
+  // earlier result), so one dictionary value is copied into the arena once per result and
+  // records share its offset (a dense result's arena stays small, and a packed transport
+  // can ship the arena as it is)
+  struct InternSlot {
+    const char *p;
+    uint32_t l;
+    uint64_t off;
+  };
+  std::vector<InternSlot> intern;
+  size_t intern_used = 0;
+  uint64_t intern_lookup(const char *p, size_t l) {
+    if (intern.empty()) intern.assign(1024, InternSlot{nullptr, 0, 0});
+    if (2 * (intern_used + 1) > intern.size()) {  // grow: rehash
+      std::vector<InternSlot> old;
+      old.swap(intern);
+      intern.assign(2 * old.size(), InternSlot{nullptr, 0, 0});
+      intern_used = 0;
+      for (const auto &x : old)
+        if (x.p) intern_insert(x.p, x.l, x.off);
+    }
+    const size_t mask = intern.size() - 1;
+    size_t h = (uintptr_t(p) * 0x9E3779B97F4A7C15ull ^ l) >> 7;
+    for (;; h++) {
+      InternSlot &x = intern[h & mask];
+      if (!x.p) {
+        x = InternSlot{p, uint32_t(l), arena_size};
+        intern_used++;
+        if (arena_size + l > arena_cap) arena_grow(arena_size + l);
+        std::memcpy(arena + arena_size, p, l);
+        arena_size += l;
+        return x.off;
+      }
+      if (x.p == p && x.l == l) return x.off;
+    }
+  }
+  void intern_insert(const char *p, uint32_t l, uint64_t off) {
+    const size_t mask = intern.size() - 1;
+    size_t h = (uintptr_t(p) * 0x9E3779B97F4A7C15ull ^ l) >> 7;
+    while (intern[h & mask].p) h++;
+    intern[h & mask] = InternSlot{p, l, off};
+    intern_used++;
+  }
   void set_str(std::vector<uint64_t> &off, std::vector<uint32_t> &len, size_t i, const char *p, size_t l) {
-    off[i] = arena_size;
     len[i] = uint32_t(l);
-    if (arena_size + l > arena_cap) arena_grow(arena_size + l);
-    if (l) std::memcpy(arena + arena_size, p, l);
-    arena_size += l;
+    off[i] = l ? intern_lookup(p, l) : 0;
   }
   size_t size() const { return start.size(); }
   void resize(size_t n) {
@@ -151,6 +285,8 @@ struct ResultHolder {
     for (auto *v : {&start, &end, &entry, &svc_off, &name_off}) v->clear();
     for (auto *v : {&dur, &block, &svc_len, &name_len}) v->clear();
     arena_size = 0;
+    if (intern_used) std::fill(intern.begin(), intern.end(), InternSlot{nullptr, 0, 0});
+    intern_used = 0;
     svc_p.clear();
     name_p.clear();
     bstatus.clear();
@@ -179,6 +315,10 @@ struct ResultHolder {
     pub.root_service_len = svc_len.data();
     pub.root_name = name_p.data();
     pub.root_name_len = name_len.data();
+    pub.names = arena ? arena : "";
+    pub.names_len = arena_size;
+    pub.root_service_off = svc_off.data();
+    pub.root_name_off = name_off.data();
     berr.resize(bstatus.size());
     for (size_t i = 0; i < bstatus.size(); i++) berr[i] = bstatus[i] ? berr_s[i].c_str() : nullptr;
     pub.nblocks = bstatus.size();
@@ -244,8 +384,7 @@ static_assert(offsetof(FindHolder, pub) == 0, "pub first");
 struct ProtoHolder {
   tsg_proto_result pub{};
   std::vector<uint8_t> ids;
-  std::vector<uint32_t> id_off, dur, obj;
-  std::vector<uint8_t> id_len;
+  std::vector<uint32_t> id_off, dur, obj, id_len, svc_len, root_len;
   std::vector<uint64_t> start;
   std::vector<std::string> svc, root;
   std::vector<const char *> svc_p, root_p;
@@ -312,6 +451,10 @@ int tsg_init(const tsg_options *opts, tsg_ctx **out) {
 }
 void tsg_shutdown(tsg_ctx *ctx) {
   if (!ctx) return;
+  {
+    std::lock_guard<std::mutex> lk(ctx->wmu);
+    ctx->workers.clear();  // (joins the device workers: idle, no call is in flight)
+  }
   ctx_shutdown(ctx->c);
   delete ctx;
 }
@@ -650,53 +793,43 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         if (outs_used == outs.size()) outs.emplace_back();
         slots.push_back(&outs[outs_used++]);
       }
-      std::vector<std::thread> th;
-      std::vector<std::exception_ptr> errs(slots.size());
-      size_t k = 0;
-      for (auto &kv : per_dev) {
-        const size_t slot = k++;
-        auto work = [&, slot, dc = kv.first, &list = kv.second]() {
-          try {
-            // chunks of at most kChunk blocks, one launch each (the one-launch path
-            // carries 32 blocks in its kernel arguments); cancellation is checked
-            // before every chunk
-            const size_t nl = list.size(), step = kChunk ? kChunk : nl;
-            SearchOut &o = *slots[slot];
-            if (nl <= step) {  // one chunk: the device's list as it is
-              check_cancel();
-              device_search(*dc, list, *q, dlimit, flags, o);
-              return;
-            }
-            for (size_t c0 = 0; c0 < nl; c0 += step) {
-              check_cancel();
-              const std::vector<std::pair<uint32_t, Block *>> part(list.begin() + c0,
-                                                                   list.begin() + std::min(nl, c0 + step));
-              if (c0 == 0) {
-                device_search(*dc, part, *q, dlimit, flags, o);
-                continue;
-              }
-              SearchOut more;
-              device_search(*dc, part, *q, dlimit, flags, more);
-              o.recs.insert(o.recs.end(), more.recs.begin(), more.recs.end());
-              o.device_bytes += more.device_bytes;
-              o.kernel_ns += more.kernel_ns;
-              o.scan_ns += more.scan_ns;
-              o.scan_bytes += more.scan_bytes;
-            }
-          } catch (...) {
-            errs[slot] = std::current_exception();
+      auto work = [&](size_t slot) {
+        DeviceCtx *dc = per_dev[slot].first;
+        const auto &list = per_dev[slot].second;
+        // chunks of at most kChunk blocks, one launch each (the one-launch path
+        // carries 32 blocks in its kernel arguments); cancellation is checked
+        // before every chunk
+        const size_t nl = list.size(), step = kChunk ? kChunk : nl;
+        SearchOut &o = *slots[slot];
+        if (nl <= step) {  // one chunk: the device's list as it is
+          check_cancel();
+          device_search(*dc, list, *q, dlimit, flags, o);
+          return;
+        }
+        for (size_t c0 = 0; c0 < nl; c0 += step) {
+          check_cancel();
+          const std::vector<std::pair<uint32_t, Block *>> part(list.begin() + c0,
+                                                               list.begin() + std::min(nl, c0 + step));
+          if (c0 == 0) {
+            device_search(*dc, part, *q, dlimit, flags, o);
+            continue;
           }
-        };
-        if (per_dev.size() == 1) work();
-        else th.emplace_back(work);
-      }
-      for (auto &t : th) t.join();
-      for (auto &e : errs)
-        if (e) std::rethrow_exception(e);
+          SearchOut more;
+          device_search(*dc, part, *q, dlimit, flags, more);
+          o.recs.insert(o.recs.end(), more.recs.begin(), more.recs.end());
+          o.device_bytes += more.device_bytes;
+          o.kernel_ns += more.kernel_ns;
+          o.scan_ns += more.scan_ns;
+          o.scan_bytes += more.scan_bytes;
+          o.reruns += more.reruns;
+        }
+      };
+      if (!per_dev.empty()) ctx->fan_out(per_dev.size(), [&](size_t i) { return per_dev[i].first; }, work);
       // per block match lists in scan order (each device's records are grouped by block already)
       uint64_t wave_k = 0, wave_s = 0;  // devices run concurrently: a wave takes its slowest
       for (SearchOut *o : slots) {
         m.device_bytes_read += o->device_bytes;
+        m.reruns += o->reruns;
         wave_k = std::max<uint64_t>(wave_k, o->kernel_ns);
         wave_s = std::max<uint64_t>(wave_s, o->scan_ns);
         m.scan_bytes += o->scan_bytes;
@@ -990,7 +1123,7 @@ void tsg_v2block_close(tsg_v2block *b) {
 // per-device hit lists (each sorted by (id, block)) are merged into one (id, block) order.
 extern "C++" {
 template <class Out, class Run>
-static void per_device_merge(tsg_v2block *const *blocks, size_t nblocks, Out &out, Run &&run,
+static void per_device_merge(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, Out &out, Run &&run,
                              void (*append)(Out &, const Out &, size_t)) {
   std::vector<DeviceCtx *> order;
   std::unordered_map<DeviceCtx *, std::vector<std::pair<uint32_t, V2Block *>>> per_dev;
@@ -1004,19 +1137,8 @@ static void per_device_merge(tsg_v2block *const *blocks, size_t nblocks, Out &ou
     return;
   }
   std::vector<Out> parts(order.size());
-  std::vector<std::exception_ptr> errs(order.size());
-  std::vector<std::thread> th;
-  for (size_t d = 0; d < order.size(); d++)
-    th.emplace_back([&, d] {
-      try {
-        run(*order[d], per_dev[order[d]], parts[d]);
-      } catch (...) {
-        errs[d] = std::current_exception();
-      }
-    });
-  for (auto &t : th) t.join();
-  for (auto &e : errs)
-    if (e) std::rethrow_exception(e);
+  ctx->fan_out(order.size(), [&](size_t d) { return order[d]; },
+               [&](size_t d) { run(*order[d], per_dev[order[d]], parts[d]); });
   // k-way merge by (id_idx, block_idx)
   std::vector<size_t> pos(parts.size(), 0);
   out = Out();
@@ -1059,7 +1181,7 @@ int tsg_lookup_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, con
   return guard([&] {
     auto *h = new LookupHolder();
     std::unique_ptr<LookupHolder> g(h);
-    per_device_merge(blocks, nblocks, h->o,
+    per_device_merge(ctx, blocks, nblocks, h->o,
                      [&](DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>> &list, LookupOut &o) {
                        device_lookup(dc, list, ids, nids, opts, o);
                      },
@@ -1082,7 +1204,7 @@ int tsg_find_ids(tsg_ctx *ctx, tsg_v2block *const *blocks, size_t nblocks, const
   return guard([&] {
     auto *h = new FindHolder();
     std::unique_ptr<FindHolder> g(h);
-    per_device_merge(blocks, nblocks, h->o,
+    per_device_merge(ctx, blocks, nblocks, h->o,
                      [&](DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>> &list, FindOut &o) {
                        device_find(dc, list, ids, nids, opts, o);
                      },
@@ -1211,6 +1333,8 @@ int tsg_proto_search(tsg_ctx *ctx, tsg_proto_block *b, const tsg_proto_request *
     for (size_t i = 0; i < h->svc.size(); i++) {
       h->svc_p.push_back(h->svc[i].c_str());
       h->root_p.push_back(h->root[i].c_str());
+      h->svc_len.push_back(uint32_t(h->svc[i].size()));
+      h->root_len.push_back(uint32_t(h->root[i].size()));
     }
     tsg_proto_result &r = h->pub;
     r.n = uint32_t(o.traces.size());
@@ -1219,6 +1343,8 @@ int tsg_proto_search(tsg_ctx *ctx, tsg_proto_block *b, const tsg_proto_request *
     r.trace_id_len = h->id_len.data();
     r.root_service_name = h->svc_p.data();
     r.root_trace_name = h->root_p.data();
+    r.root_service_name_len = h->svc_len.data();
+    r.root_trace_name_len = h->root_len.data();
     r.start_time_unix_nano = h->start.data();
     r.duration_ms = h->dur.data();
     r.object_idx = h->obj.data();

@@ -131,6 +131,7 @@ struct SearchOut {
   std::vector<uint64_t> block_counts;
   uint64_t device_bytes = 0, kernel_ns = 0;
   uint64_t scan_ns = 0, scan_bytes = 0;
+  uint32_t reruns = 0;  // extra launches after a record overflow (timed into scan_ns / kernel_ns when timing)
 };
 // Runs the device pipeline for a set of (block index, block) pairs that share
 // one device. limit 0 = every match; limit L = each block's first L matches.

@@ -1,0 +1,546 @@
+// merge.cpp — the frontend's response merge over packed responses (host code behind the C
+// ABI): searchResponse.addResponse / shouldQuit / result (modules/frontend/searchsharding.go:
+// 71-125) for the multi-GPU search fan-out, where every rank (GPU) answers for its block
+// shard and rank 0 merges. Responses travel as one byte buffer each ("wire", include/tsg.h):
+// 40-byte TraceSearchMetadata records with the names as a per-response table, the metrics and
+// the per-block statuses. Merging 10^6-10^7 records is a parallel hash-partitioned dedupe
+// (first occurrence in response order wins) and an LSD radix sort by start time.
+#include <sys/mman.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cstdlib>
+#include <mutex>
+#include <cstring>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "common.hpp"
+#include "tsg.h"
+
+namespace tsg {
+void set_last_error(const std::string &m);
+
+static_assert(sizeof(tsg_trace_rec) == 40, "wire record layout");
+static_assert(sizeof(tsg_wire_header) == 96, "wire header layout");
+
+static size_t pad8(size_t x) { return (x + 7) & ~size_t(7); }
+static void *big_alloc(size_t bytes);
+
+struct WireView {
+  const tsg_wire_header *h = nullptr;
+  const tsg_trace_rec *recs = nullptr;
+  const uint32_t *name_off = nullptr;
+  const char *names = nullptr;
+  const int32_t *status = nullptr;
+  const uint8_t *errors = nullptr;
+};
+
+static size_t wire_size(uint64_t n, uint64_t nnames, uint64_t names_len, uint64_t nblocks, uint64_t errors_len) {
+  return sizeof(tsg_wire_header) + pad8(n * sizeof(tsg_trace_rec)) + pad8((nnames + 1) * 4) + pad8(names_len) +
+         pad8(nblocks * 4) + pad8(errors_len);
+}
+
+static WireView wire_view(const uint8_t *p, size_t len) {
+  if (!p || len < sizeof(tsg_wire_header)) fail(TSG_E_INVALID, "wire buffer too small");
+  WireView v;
+  v.h = reinterpret_cast<const tsg_wire_header *>(p);
+  if (v.h->magic != TSG_WIRE_MAGIC || v.h->version != TSG_WIRE_VERSION) fail(TSG_E_INVALID, "not a tsg wire buffer");
+  const tsg_wire_header &h = *v.h;
+  if (h.n > (1ull << 40) || h.nnames > (1ull << 32) || h.names_len > (1ull << 40) || h.nblocks > (1ull << 32) ||
+      h.errors_len > (1ull << 40) || wire_size(h.n, h.nnames, h.names_len, h.nblocks, h.errors_len) > len)
+    fail(TSG_E_INVALID, "wire buffer truncated");
+  size_t o = sizeof(tsg_wire_header);
+  v.recs = reinterpret_cast<const tsg_trace_rec *>(p + o);
+  o += pad8(h.n * sizeof(tsg_trace_rec));
+  v.name_off = reinterpret_cast<const uint32_t *>(p + o);
+  o += pad8((h.nnames + 1) * 4);
+  v.names = reinterpret_cast<const char *>(p + o);
+  o += pad8(h.names_len);
+  v.status = reinterpret_cast<const int32_t *>(p + o);
+  o += pad8(h.nblocks * 4);
+  v.errors = p + o;
+  if (v.name_off[0] != 0 || v.name_off[h.nnames] != h.names_len) fail(TSG_E_INVALID, "wire name table");
+  for (uint64_t i = 0; i < h.nnames; i++)
+    if (v.name_off[i] > v.name_off[i + 1]) fail(TSG_E_INVALID, "wire name table");
+  return v;
+}
+
+// Allocates a wire of the given sizes (zeroed padding) and returns pointers to its sections.
+struct WireOut {
+  uint8_t *base = nullptr;
+  size_t len = 0;
+  tsg_wire_header *h = nullptr;
+  tsg_trace_rec *recs = nullptr;
+  uint32_t *name_off = nullptr;
+  char *names = nullptr;
+  int32_t *status = nullptr;
+  uint8_t *errors = nullptr;
+};
+static WireOut wire_at(uint8_t *base, uint64_t n, uint64_t nnames, uint64_t names_len, uint64_t nblocks,
+                       uint64_t errors_len) {
+  WireOut w;
+  w.len = wire_size(n, nnames, names_len, nblocks, errors_len);
+  // every byte is written by the caller except section padding: zeroed here, the rest is not
+  w.base = base;
+  w.h = reinterpret_cast<tsg_wire_header *>(w.base);
+  size_t o = sizeof(tsg_wire_header);
+  w.recs = reinterpret_cast<tsg_trace_rec *>(w.base + o);
+  o += pad8(n * sizeof(tsg_trace_rec));
+  w.name_off = reinterpret_cast<uint32_t *>(w.base + o);
+  o += pad8((nnames + 1) * 4);
+  w.names = reinterpret_cast<char *>(w.base + o);
+  o += pad8(names_len);
+  w.status = reinterpret_cast<int32_t *>(w.base + o);
+  o += pad8(nblocks * 4);
+  w.errors = w.base + o;
+  std::memset(w.h, 0, sizeof(tsg_wire_header));
+  w.h->magic = TSG_WIRE_MAGIC;
+  w.h->version = TSG_WIRE_VERSION;
+  w.h->n = n;
+  w.h->nnames = nnames;
+  w.h->names_len = names_len;
+  w.h->nblocks = nblocks;
+  w.h->errors_len = errors_len;
+  auto zpad = [&](void *end_used, size_t used) {
+    const size_t p = pad8(used) - used;
+    if (p) std::memset(static_cast<uint8_t *>(end_used), 0, p);
+  };
+  zpad(reinterpret_cast<uint8_t *>(w.recs) + n * sizeof(tsg_trace_rec), n * sizeof(tsg_trace_rec));
+  zpad(reinterpret_cast<uint8_t *>(w.name_off) + (nnames + 1) * 4, (nnames + 1) * 4);
+  zpad(w.names + names_len, names_len);
+  zpad(reinterpret_cast<uint8_t *>(w.status) + nblocks * 4, nblocks * 4);
+  zpad(w.errors + errors_len, errors_len);
+  return w;
+}
+static WireOut wire_alloc(uint64_t n, uint64_t nnames, uint64_t names_len, uint64_t nblocks, uint64_t errors_len) {
+  return wire_at(static_cast<uint8_t *>(big_alloc(wire_size(n, nnames, names_len, nblocks, errors_len))), n, nnames,
+                 names_len, nblocks, errors_len);
+}
+
+// tsg_result -> wire: the records as TraceSearchMetadata, the names interned into a table
+// (the result's name arena already shares equal dictionary values: one table entry per arena
+// string, entry 0 = "").
+static void result_pack(const tsg_result &r, uint8_t **out, size_t *len) {
+  std::unordered_map<uint64_t, uint32_t> idx;  // (arena offset << 24 | length) -> table entry
+  std::vector<std::pair<uint64_t, uint32_t>> table{{0, 0}};
+  uint64_t names_len = 0;
+  auto name_index = [&](uint64_t off, uint32_t l) -> uint32_t {
+    if (l == 0) return 0;
+    if (l >= (1u << 24) || off >= (1ull << 40)) fail(TSG_E_UNSUPPORTED, "name too long to pack");
+    const uint64_t key = (off << 24) | l;
+    auto it = idx.find(key);
+    if (it != idx.end()) return it->second;
+    const uint32_t k = uint32_t(table.size());
+    table.push_back({off, l});
+    names_len += l;
+    idx.emplace(key, k);
+    return k;
+  };
+  std::vector<uint32_t> svc(r.n), nm(r.n);
+  for (uint64_t i = 0; i < r.n; i++) {
+    svc[i] = name_index(r.root_service_off[i], r.root_service_len[i]);
+    nm[i] = name_index(r.root_name_off[i], r.root_name_len[i]);
+  }
+  if (names_len >= (1ull << 32)) fail(TSG_E_UNSUPPORTED, "names too large to pack");
+  uint64_t errors_len = 0;
+  for (uint64_t b = 0; b < r.nblocks; b++)
+    if (r.block_status[b]) errors_len += 4 + (r.block_error[b] ? std::strlen(r.block_error[b]) : 0);
+  WireOut w = wire_alloc(r.n, table.size(), names_len, r.nblocks, errors_len);
+  w.h->traces_inspected = r.metrics.traces_inspected;
+  w.h->bytes_inspected = r.metrics.bytes_inspected;
+  w.h->blocks_inspected = r.metrics.blocks_inspected;
+  w.h->blocks_skipped = r.metrics.blocks_skipped;
+  w.h->skipped_traces = 0;  // (the flatbuffer path skips no trace: SearchOptions.MaxBytes is the proto path's)
+  for (uint64_t i = 0; i < r.n; i++) {
+    tsg_trace_rec &x = w.recs[i];
+    std::memcpy(x.trace_id, r.trace_id[i], 16);
+    x.trace_id_len = r.trace_id_len[i];
+    x.start_ns = r.start_ns[i];
+    x.duration_ms = r.duration_ms[i];
+    x.root_service = svc[i];
+    x.root_name = nm[i];
+  }
+  uint64_t o = 0;
+  w.name_off[0] = 0;
+  for (size_t k = 1; k < table.size(); k++) {
+    std::memcpy(w.names + o, r.names + table[k].first, table[k].second);
+    o += table[k].second;
+    w.name_off[k] = uint32_t(o);
+  }
+  uint8_t *e = w.errors;
+  for (uint64_t b = 0; b < r.nblocks; b++) {
+    w.status[b] = r.block_status[b];
+    if (!r.block_status[b]) continue;
+    const uint32_t l = r.block_error[b] ? uint32_t(std::strlen(r.block_error[b])) : 0u;
+    std::memcpy(e, &l, 4);
+    if (l) std::memcpy(e + 4, r.block_error[b], l);
+    e += 4 + l;
+  }
+  *out = w.base;
+  *len = w.len;
+}
+
+static inline uint64_t id_hash(const uint8_t *id) {
+  uint64_t a, b;
+  std::memcpy(&a, id, 8);
+  std::memcpy(&b, id + 8, 8);
+  uint64_t h = (a ^ 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull;
+  h ^= (b + (h >> 29)) * 0x94D049BB133111EBull;
+  return h ^ (h >> 31);
+}
+
+// Runs f(t) for t in [0, n) on n threads (the caller runs t = 0).
+template <class F>
+static void run_threads(size_t n, F &&f) {
+  if (n <= 1) {
+    f(size_t(0));
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < n; t++) th.emplace_back([&f, t] { f(t); });
+  f(size_t(0));
+  for (auto &x : th) x.join();
+}
+
+// Grow-only scratch buffers, kept between merges (a merging rank merges every query: fresh
+// allocations would pay a page fault per 4 KiB each time); 2 MiB aligned and advised as
+// huge pages where the kernel allows it.
+static void *big_alloc(size_t bytes) {
+  void *p = nullptr;
+  const size_t al = size_t(2) << 20;
+  if (posix_memalign(&p, al, std::max(bytes, size_t(64)))) throw std::bad_alloc();
+  if (bytes >= al) madvise(p, bytes, MADV_HUGEPAGE);
+  return p;
+}
+template <class T>
+struct Scratch {
+  T *p = nullptr;
+  size_t cap = 0;
+  T *get(size_t n) {
+    if (n > cap) {
+      std::free(p);
+      cap = std::max(n, cap + cap / 2);
+      p = static_cast<T *>(big_alloc(cap * sizeof(T)));
+    }
+    return p;
+  }
+};
+struct MergeScratch {
+  std::mutex mu;
+  Scratch<uint64_t> hs, keys, keys2;
+  struct Ent {
+    uint64_t a, b;  // the id
+    uint32_t g;
+    uint32_t h;  // hash bits for the bucket's set
+  };
+  Scratch<Ent> ents;
+  Scratch<uint8_t> first;
+  Scratch<uint32_t> sel;
+};
+static MergeScratch &merge_scratch() {
+  static MergeScratch *s = new MergeScratch();
+  return *s;
+}
+
+// searchResponse over the responses in order: addResponse (first record per TraceID wins;
+// InspectedBytes / InspectedTraces / SkippedBlocks / SkippedTraces summed), shouldQuit before
+// each response (more than `limit` distinct traces already), result (start time descending;
+// ties: first position, so the merge is deterministic where Go's sort.Slice is not).
+static void wire_merge(const std::vector<WireView> &in, uint64_t limit, uint64_t total_blocks, uint8_t *out,
+                       size_t cap, size_t *len) {
+  const size_t nr = in.size();
+  std::vector<uint64_t> base(nr + 1, 0);
+  for (size_t r = 0; r < nr; r++) base[r + 1] = base[r] + in[r].h->n;
+  const uint64_t N = base[nr];
+  if (N >= (1ull << 32)) fail(TSG_E_UNSUPPORTED, "too many records to merge (max 2^32)");
+  MergeScratch &S = merge_scratch();
+  std::lock_guard<std::mutex> lk(S.mu);
+  const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t T = N >= (1u << 16) ? std::min<size_t>(hw, 16) : 1;
+  auto resp_of = [&](uint64_t g) { return size_t(std::upper_bound(base.begin(), base.end(), g) - base.begin()) - 1; };
+  auto rec = [&](uint64_t g) -> const tsg_trace_rec & {
+    const size_t r = resp_of(g);
+    return in[r].recs[g - base[r]];
+  };
+  // record ranges per thread (contiguous, in g order)
+  std::vector<uint64_t> cut(T + 1);
+  for (size_t t = 0; t <= T; t++) cut[t] = N * t / T;
+  // 1. first occurrence per trace id: (id, g) partitioned by hash into buckets, g order kept
+  //    inside every bucket (per-thread histograms, threads' ranges in order), then each
+  //    bucket deduped with a small open-addressing set
+  constexpr int kBits = 10;
+  constexpr size_t kB = size_t(1) << kBits;
+  uint64_t *hs = S.hs.get(N);
+  std::vector<uint32_t> hist(T * kB, 0);
+  run_threads(T, [&](size_t t) {
+    uint32_t *hh = &hist[t * kB];
+    for (uint64_t g = cut[t]; g < cut[t + 1];) {
+      const size_t r = resp_of(g);
+      const uint64_t e = std::min(cut[t + 1], base[r + 1]);
+      for (; g < e; g++) {
+        const uint64_t h = id_hash(in[r].recs[g - base[r]].trace_id);
+        hs[g] = h;
+        hh[h >> (64 - kBits)]++;
+      }
+    }
+  });
+  std::vector<uint32_t> bstart(kB + 1, 0);
+  {
+    uint32_t acc = 0;
+    for (size_t k = 0; k < kB; k++) {
+      bstart[k] = acc;
+      for (size_t t = 0; t < T; t++) {
+        const uint32_t c = hist[t * kB + k];
+        hist[t * kB + k] = acc;  // -> this thread's first slot in bucket k
+        acc += c;
+      }
+    }
+    bstart[kB] = acc;
+  }
+  auto *ents = S.ents.get(N);
+  run_threads(T, [&](size_t t) {
+    uint32_t *pos = &hist[t * kB];
+    for (uint64_t g = cut[t]; g < cut[t + 1];) {
+      const size_t r = resp_of(g);
+      const uint64_t e = std::min(cut[t + 1], base[r + 1]);
+      for (; g < e; g++) {
+        const uint64_t h = hs[g];
+        MergeScratch::Ent &x = ents[pos[h >> (64 - kBits)]++];
+        std::memcpy(&x.a, in[r].recs[g - base[r]].trace_id, 8);
+        std::memcpy(&x.b, in[r].recs[g - base[r]].trace_id + 8, 8);
+        x.g = uint32_t(g);
+        x.h = uint32_t(h);
+      }
+    }
+  });
+  uint8_t *first = S.first.get(N);
+  std::memset(first, 0, N);
+  {
+    std::atomic<size_t> next{0};
+    run_threads(T, [&](size_t) {
+      std::vector<uint32_t> slot;
+      for (;;) {
+        const size_t k = next.fetch_add(1);
+        if (k >= kB) break;
+        const uint32_t lo = bstart[k], hi = bstart[k + 1];
+        if (lo == hi) continue;
+        size_t cap = 16;
+        while (cap < 2 * size_t(hi - lo)) cap <<= 1;
+        slot.assign(cap, 0xffffffffu);
+        for (uint32_t i = lo; i < hi; i++) {
+          const MergeScratch::Ent &x = ents[i];
+          for (size_t s = x.h & (cap - 1);; s = (s + 1) & (cap - 1)) {
+            if (slot[s] == 0xffffffffu) {
+              slot[s] = i;
+              first[x.g] = 1;
+              break;
+            }
+            const MergeScratch::Ent &o = ents[slot[s]];
+            if (o.a == x.a && o.b == x.b) break;  // seen earlier (g order within the bucket)
+          }
+        }
+      }
+    });
+  }
+  // 2. shouldQuit before each response: distinct traces taken so far > limit
+  size_t taken = 0;
+  {
+    std::vector<uint64_t> per(nr, 0);
+    run_threads(std::min(T, nr), [&](size_t t) {
+      for (size_t r = t; r < nr; r += std::min(T, nr))
+        for (uint64_t g = base[r]; g < base[r + 1]; g++) per[r] += first[g];
+    });
+    uint64_t distinct = 0;
+    for (size_t r = 0; r < nr; r++) {
+      if (distinct > limit) break;
+      distinct += per[r];
+      taken = r + 1;
+    }
+  }
+  const uint64_t Nt = base[taken];
+  // selected records (first occurrences in the taken responses), in g order, and the
+  // start-time range
+  std::vector<uint64_t> cnt(T + 1, 0), smin_t(T, UINT64_MAX), smax_t(T, 0);
+  std::vector<uint64_t> cutt(T + 1);
+  for (size_t t = 0; t <= T; t++) cutt[t] = Nt * t / T;
+  run_threads(T, [&](size_t t) {
+    uint64_t c = 0, lo = UINT64_MAX, hi = 0;
+    for (uint64_t g = cutt[t]; g < cutt[t + 1]; g++)
+      if (first[g]) {
+        c++;
+        const uint64_t st = rec(g).start_ns;
+        lo = std::min(lo, st);
+        hi = std::max(hi, st);
+      }
+    cnt[t + 1] = c;
+    smin_t[t] = lo;
+    smax_t[t] = hi;
+  });
+  for (size_t t = 0; t < T; t++) cnt[t + 1] += cnt[t];
+  const size_t M = size_t(cnt[T]);
+  uint64_t smin = UINT64_MAX, smax = 0;
+  for (size_t t = 0; t < T; t++) {
+    smin = std::min(smin, smin_t[t]);
+    smax = std::max(smax, smax_t[t]);
+  }
+  uint32_t *sel = S.sel.get(std::max<size_t>(M, 1));
+  // 3. start descending, ties by position: one u64 key (smax - start) << gbits | g when it
+  //    fits (parallel sort of chunks + pairwise merges), else a pair sort
+  int gbits = 0;
+  while (gbits < 64 && (Nt >> gbits)) gbits++;
+  int kbits = 0;
+  while (kbits < 64 && M && ((smax - smin) >> kbits)) kbits++;
+  if (M > 0 && kbits + gbits <= 64) {
+    uint64_t *key = S.keys.get(M), *key2 = S.keys2.get(M);
+    run_threads(T, [&](size_t t) {
+      uint64_t o = cnt[t];
+      for (uint64_t g = cutt[t]; g < cutt[t + 1]; g++)
+        if (first[g]) key[o++] = ((smax - rec(g).start_ns) << gbits) | g;
+    });
+    // MSD pass on the top 12 bits (per-thread histograms, parallel scatter), then every
+    // bucket sorted on its own (keys are unique: g is in them)
+    const int tb = kbits + gbits, sh = tb > 12 ? tb - 12 : 0;
+    constexpr size_t kSB = 4096;
+    std::vector<uint32_t> sh_hist(T * kSB, 0);
+    std::vector<size_t> kb(T + 1);
+    for (size_t t = 0; t <= T; t++) kb[t] = M * t / T;
+    run_threads(T, [&](size_t t) {
+      uint32_t *hh = &sh_hist[t * kSB];
+      for (size_t i = kb[t]; i < kb[t + 1]; i++) hh[key[i] >> sh]++;
+    });
+    std::vector<uint32_t> sb(kSB + 1, 0);
+    {
+      uint32_t acc = 0;
+      for (size_t k = 0; k < kSB; k++) {
+        sb[k] = acc;
+        for (size_t t = 0; t < T; t++) {
+          const uint32_t c = sh_hist[t * kSB + k];
+          sh_hist[t * kSB + k] = acc;
+          acc += c;
+        }
+      }
+      sb[kSB] = acc;
+    }
+    run_threads(T, [&](size_t t) {
+      uint32_t *pos = &sh_hist[t * kSB];
+      for (size_t i = kb[t]; i < kb[t + 1]; i++) key2[pos[key[i] >> sh]++] = key[i];
+    });
+    {
+      std::atomic<size_t> next{0};
+      run_threads(T, [&](size_t) {
+        for (;;) {
+          const size_t k0 = next.fetch_add(64);
+          if (k0 >= kSB) break;
+          for (size_t k = k0; k < std::min(kSB, k0 + 64); k++) std::sort(key2 + sb[k], key2 + sb[k + 1]);
+        }
+      });
+    }
+    const uint64_t *src = key2;
+    const uint64_t gmask = gbits >= 64 ? ~0ull : ((1ull << gbits) - 1);
+    run_threads(T, [&](size_t t) {
+      for (size_t i = kb[t]; i < kb[t + 1]; i++) sel[i] = uint32_t(src[i] & gmask);
+    });
+  } else if (M > 0) {
+    std::vector<std::pair<uint64_t, uint32_t>> kv(M);
+    size_t o = 0;
+    for (uint64_t g = 0; g < Nt; g++)
+      if (first[g]) kv[o++] = {smax - rec(g).start_ns, uint32_t(g)};
+    std::sort(kv.begin(), kv.end());
+    for (size_t i = 0; i < M; i++) sel[i] = kv[i].second;
+  }
+  // 4. the merged response: names of the taken responses concatenated (indices rebased)
+  std::vector<uint64_t> name_base(taken + 1, 0), bytes_base(taken + 1, 0);
+  for (size_t r = 0; r < taken; r++) {
+    name_base[r + 1] = name_base[r] + in[r].h->nnames;
+    bytes_base[r + 1] = bytes_base[r] + in[r].h->names_len;
+  }
+  if (bytes_base[taken] >= (1ull << 32) || name_base[taken] >= (1ull << 32))
+    fail(TSG_E_UNSUPPORTED, "merged names too large");
+  uint64_t nblocks = 0, errors_len = 0;
+  for (size_t r = 0; r < nr; r++) {
+    nblocks += in[r].h->nblocks;
+    errors_len += in[r].h->errors_len;
+  }
+  const size_t need = wire_size(M, name_base[taken], bytes_base[taken], nblocks, errors_len);
+  *len = need;
+  if (need > cap) fail(TSG_E_INVALID, "merge output buffer too small");
+  WireOut w = wire_at(out, M, name_base[taken], bytes_base[taken], nblocks, errors_len);
+  for (size_t r = 0; r < taken; r++) {
+    const tsg_wire_header &h = *in[r].h;
+    w.h->traces_inspected += h.traces_inspected;
+    w.h->bytes_inspected += h.bytes_inspected;
+    w.h->blocks_skipped += h.blocks_skipped;
+    w.h->skipped_traces += h.skipped_traces;
+    for (uint64_t k = 0; k < h.nnames; k++) w.name_off[name_base[r] + k] = uint32_t(bytes_base[r] + in[r].name_off[k]);
+    if (h.names_len) std::memcpy(w.names + bytes_base[r], in[r].names, h.names_len);
+  }
+  w.name_off[name_base[taken]] = uint32_t(bytes_base[taken]);
+  w.h->blocks_inspected = total_blocks;  // set by the sharder (searchsharding.go:221), not summed
+  // block statuses / errors of every response (a response not taken still ran: its
+  // errors are reported), in response order = global block order
+  {
+    uint64_t bo = 0, eo = 0;
+    for (size_t r = 0; r < nr; r++) {
+      const tsg_wire_header &h = *in[r].h;
+      if (h.nblocks) std::memcpy(w.status + bo, in[r].status, h.nblocks * 4);
+      if (h.errors_len) std::memcpy(w.errors + eo, in[r].errors, h.errors_len);
+      bo += h.nblocks;
+      eo += h.errors_len;
+    }
+  }
+  run_threads(M >= (1u << 16) ? T : 1, [&](size_t t) {
+    const size_t TT = M >= (1u << 16) ? T : 1;
+    for (size_t i = M * t / TT; i < M * (t + 1) / TT; i++) {
+      const uint64_t g = sel[i];
+      const size_t r = resp_of(g);
+      tsg_trace_rec x = in[r].recs[g - base[r]];
+      x.root_service = uint32_t(name_base[r] + x.root_service);
+      x.root_name = uint32_t(name_base[r] + x.root_name);
+      w.recs[i] = x;
+    }
+  });
+}
+
+template <typename F>
+static int guard_merge(F &&f) {
+  try {
+    f();
+    return TSG_OK;
+  } catch (const Error &e) {
+    set_last_error(e.what());
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    set_last_error("out of memory");
+    return TSG_E_OOM;
+  } catch (const std::exception &e) {
+    set_last_error(e.what());
+    return TSG_E_INVALID;
+  }
+}
+
+}  // namespace tsg
+
+using namespace tsg;
+
+extern "C" {
+
+int tsg_result_pack(const tsg_result *r, uint8_t **out, size_t *len) {
+  if (!r || !out || !len) return TSG_E_INVALID;
+  return guard_merge([&] { result_pack(*r, out, len); });
+}
+
+int tsg_wire_merge(const uint8_t *const *wires, const size_t *lens, size_t n, uint64_t limit, uint64_t total_blocks,
+                   uint8_t *out, size_t cap, size_t *len) {
+  if ((n && (!wires || !lens)) || (cap && !out) || !len) return TSG_E_INVALID;
+  return guard_merge([&] {
+    std::vector<WireView> v;
+    v.reserve(n);
+    for (size_t i = 0; i < n; i++) v.push_back(wire_view(wires[i], lens[i]));
+    wire_merge(v, limit, total_blocks, out, cap, len);
+  });
+}
+
+}  // extern "C"

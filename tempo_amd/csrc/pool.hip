@@ -489,6 +489,8 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   // A workgroup's count depends on which dynamic chunks it won, so a rerun can overflow
   // where the first launch did not: launch until every count fits its segment (segments
   // double each time, at most up to the LDS buffer), or leave for the other paths.
+  uint32_t reruns = 0;
+  float rerun_ms = 0;
   if (maxc > PA.seg_cap) {
     for (;;) {
       if (maxc > rec_cap) {  // dense: this query (and the next few) take the other paths
@@ -499,8 +501,18 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       uint32_t want = 2 * PA.seg_cap;  // (headroom: the next launch's split differs)
       while (want < maxc) want <<= 1;
       dc.pool_seg = std::min(want, rec_cap);
+      // a rerun produces the records: its time counts too
+      if (time_scan) HIP_OK(hipEventRecord(dc.mk0, s));
       launch(false);
+      if (time_scan) HIP_OK(hipEventRecord(dc.mk1, s));
       wait();
+      if (time_scan) {
+        float ms = 0;
+        HIP_OK(hipEventSynchronize(dc.mk1));
+        HIP_OK(hipEventElapsedTime(&ms, dc.mk0, dc.mk1));
+        rerun_ms += ms;
+      }
+      reruns++;
       scan_counts(total, maxc);
     }
   } else if (dc.pool_seg > 32 && uint64_t(maxc) * 8 < dc.pool_seg) {
@@ -516,8 +528,9 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     HIP_OK(hipEventSynchronize(e1));
     HIP_OK(hipEventElapsedTime(&sms, e0, e1));
   }
-  out.kernel_ns = uint64_t(double(ms) * 1e6);
-  out.scan_ns = uint64_t(double(sms) * 1e6);
+  out.kernel_ns = uint64_t(double(ms + (time_all ? rerun_ms : 0.f)) * 1e6);
+  out.scan_ns = uint64_t(double(sms + rerun_ms) * 1e6);
+  out.reruns = reruns;
   tr.mark("events");
   // records: the blocks' order in the launch, the entry index within a block (the
   // reference scan order) = the record's position in the launch's unit space. Ordered

@@ -769,8 +769,9 @@ void proto_load_host(ProtoBlock &b, const std::string &dir) {
     PageObjs &po = pages[p];
     for (size_t j = 0; j < po.ids.size(); j++, t++) {
       b.id_off.push_back(uint32_t(b.ids.size()));
-      b.id_len.push_back(uint8_t(std::min<size_t>(po.ids[j].size(), 255)));
-      b.ids.insert(b.ids.end(), po.ids[j].begin(), po.ids[j].begin() + std::min<size_t>(po.ids[j].size(), 255));
+      if (b.ids.size() + po.ids[j].size() >= (1ull << 32)) fail(TSG_E_UNSUPPORTED, "object ids larger than 4 GiB in one block");
+      b.id_len.push_back(uint32_t(po.ids[j].size()));
+      b.ids.insert(b.ids.end(), po.ids[j].begin(), po.ids[j].end());
       b.obj_len.push_back(uint32_t(po.bodies[j].size()));
       b.fr_start.push_back(po.fr_start[j]);
       b.fr_end.push_back(po.fr_end[j]);

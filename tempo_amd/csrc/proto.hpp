@@ -49,7 +49,7 @@ struct ProtoBlock {
   // per object (host)
   std::vector<uint8_t> ids;
   std::vector<uint32_t> id_off;
-  std::vector<uint8_t> id_len;
+  std::vector<uint32_t> id_len;  // (object ids of any length: v2 objects are not limited to 16 bytes)
   std::vector<uint32_t> obj_len;
   std::vector<uint64_t> start_ns;       // traceStart (min span start; MaxUint64 without spans)
   std::vector<uint32_t> dur_ms, st_sec, en_sec, fr_start, fr_end;

@@ -3,28 +3,29 @@
 One process per GPU. The search path partitions by block (the frontend shards a
 query into per-block jobs, modules/frontend/searchsharding.go:325-367), so each
 rank searches only its own resident blocks with no data-path collective. The one
-exchange is the final, small gather of per-rank responses to rank 0, which then
-merges them the way the frontend's `searchResponse` does
-(searchsharding.go:32-125):
+exchange is the final gather of per-rank responses to rank 0, which then merges
+them the way the frontend's `searchResponse` does (searchsharding.go:32-125):
 
 * `addResponse` (searchsharding.go:71-86): traces keyed by trace ID, first one
   seen wins (no CombineSearchResults here); InspectedBytes / InspectedTraces /
-  SkippedBlocks summed; InspectedBlocks is set by the sharder to the number of
-  blocks in the query (searchsharding.go:221), not summed.
+  SkippedBlocks / SkippedTraces summed; InspectedBlocks is set by the sharder to
+  the number of blocks in the query (searchsharding.go:221), not summed.
 * `shouldQuit` (searchsharding.go:88-105): stop taking responses once the map
-  holds more than `limit` traces.
+  holds more than `limit` traces (or a job failed: `on_error="raise"`).
 * `result` (searchsharding.go:107-125): traces sorted by start time descending.
 
 The reference consumes job responses in completion order (racy); here they are
-consumed in rank order, and the sort is stable (ties keep first-seen order),
-which makes the merged response deterministic.
+consumed in rank order and ties keep first-seen order, which makes the merged
+response deterministic.
 
-Two transports for the gather: `distributed_search` pickles the responses
-(`gather_object`: fine for limit-bounded responses), `distributed_search_packed`
-packs them into two byte tensors (fixed 68-byte records + a names blob) and
-gathers those with `dist.gather` — on the GPUs (backend "nccl" = RCCL) the bytes
-move device to device over xGMI, which is what a GB-scale full-scan match list
-needs. Both merge identically.
+Responses travel packed ("wire" buffers, include/tsg.h): 40-byte
+TraceSearchMetadata records, the names as a per-response table, the metrics and
+every block's status and error. A rank packs its tsg_result in libtsg
+(`Engine.search_wire`, tsg_result_pack), the wires are gathered as byte tensors
+(`dist.gather`: RCCL over xGMI on the GPUs, gloo on the CPU) and rank 0 merges
+them in libtsg (tsg_wire_merge: parallel hash-partitioned first-wins dedupe +
+radix sort by start time); numpy views read the merged buffer. No per-record
+Python on the path.
 
 Trace-ID lookup shards the probe ids instead (bloom + index replicated on every
 rank, tempodb.Find's fan-out over blocks stays rank-local): `shard_ids` gives each
@@ -32,11 +33,22 @@ rank a contiguous id slice and `distributed_lookup` gathers the per-rank hit
 tables (int64 rows id, block, record, start, length); concatenated in rank order
 they are already sorted by (id, block).
 """
+import ctypes as C
 import struct
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple, Union
 
-from .tsg import SearchMetrics, TraceSearchMetadata
+import numpy as np
+
+from .tsg import SearchMetrics, TraceSearchMetadata, TsgError, _check, lib
+
+WIRE_MAGIC = 0x57475354
+WIRE_VERSION = 1
+_HDR = struct.Struct("<II5Q5QQ")  # tsg_wire_header
+assert _HDR.size == 96
+REC_DTYPE = np.dtype([("trace_id", "V16"), ("start_ns", "<u8"), ("duration_ms", "<u4"), ("root_service", "<u4"),
+                      ("root_name", "<u4"), ("trace_id_len", "u1"), ("pad", "V3")])  # tsg_trace_rec
+assert REC_DTYPE.itemsize == 40
 
 
 def shard_range(n_blocks: int, world: int, rank: int) -> range:
@@ -46,54 +58,155 @@ def shard_range(n_blocks: int, world: int, rank: int) -> range:
     return range(n_blocks * rank // world, n_blocks * (rank + 1) // world)
 
 
+def _pad8(x):
+    return (x + 7) & ~7
+
+
 @dataclass
-class SearchResponse:
-    """searchsharding.go:32-125, consumed in a fixed order."""
-    limit: int
-    inspected_blocks: int = 0
-    inspected_bytes: int = 0
-    inspected_traces: int = 0
-    skipped_blocks: int = 0
-    traces: Dict[str, TraceSearchMetadata] = field(default_factory=dict)
+class Response:
+    """A tempopb.SearchResponse in columns: `recs` (REC_DTYPE), the name table
+    (`names[name_off[k]:name_off[k+1]]`), the metrics and every block's status."""
+    recs: np.ndarray
+    name_off: np.ndarray
+    names: bytes
+    metrics: SearchMetrics
+    block_status: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    block_errors: List[Optional[str]] = field(default_factory=list)
 
-    def add_response(self, traces: Sequence[TraceSearchMetadata], metrics: SearchMetrics) -> None:
-        for t in traces:
-            key = t.trace_id_hex  # the map key is the hex TraceID string
-            if key not in self.traces:
-                self.traces[key] = t
-        self.inspected_bytes += metrics.inspected_bytes
-        self.inspected_traces += metrics.inspected_traces
-        self.skipped_blocks += metrics.skipped_blocks
+    def __len__(self):
+        return len(self.recs)
 
-    def should_quit(self) -> bool:
-        return len(self.traces) > self.limit
+    def name(self, k: int) -> str:
+        return self.names[int(self.name_off[k]):int(self.name_off[k + 1])].decode(errors="replace")
 
-    def result(self) -> Tuple[List[TraceSearchMetadata], SearchMetrics]:
-        out = sorted(self.traces.values(), key=lambda t: -t.start_time_unix_nano)
-        return out, SearchMetrics(self.inspected_traces, self.inspected_bytes, self.inspected_blocks,
-                                  self.skipped_blocks)
+    def traces(self) -> List[TraceSearchMetadata]:
+        """The records as TraceSearchMetadata objects (for small responses)."""
+        r = self.recs
+        return [TraceSearchMetadata(trace_id=bytes(r["trace_id"][i]), trace_id_len=int(r["trace_id_len"][i]),
+                                    root_service_name=self.name(r["root_service"][i]),
+                                    root_trace_name=self.name(r["root_name"][i]),
+                                    start_time_unix_nano=int(r["start_ns"][i]), duration_ms=int(r["duration_ms"][i]))
+                for i in range(len(r))]
+
+    def hex_ids(self) -> List[str]:
+        """util.TraceIDToHexString of every record (pkg/util/traceid.go:46-52)."""
+        return [bytes(x).hex().lstrip("0") for x in self.recs["trace_id"]]
+
+
+def response_from_traces(traces: Sequence[TraceSearchMetadata], metrics: SearchMetrics) -> Response:
+    """A Response from TraceSearchMetadata objects (test stand-ins, small lists)."""
+    table = {"": 0}
+    recs = np.zeros(len(traces), REC_DTYPE)
+    for i, t in enumerate(traces):
+        s = table.setdefault(t.root_service_name, len(table))
+        n = table.setdefault(t.root_trace_name, len(table))
+        recs[i] = (bytes(t.trace_id).rjust(16, b"\0")[-16:], t.start_time_unix_nano, t.duration_ms, s, n,
+                   t.trace_id_len, b"\0\0\0")
+    enc = [k.encode() for k in table]
+    off = np.zeros(len(enc) + 1, np.uint32)
+    off[1:] = np.cumsum([len(b) for b in enc]) if enc else []
+    st = np.asarray(metrics.block_status or [], np.int32)
+    errs = list(metrics.block_errors or [None] * len(st))
+    return Response(recs, off, b"".join(enc), metrics, st, errs)
+
+
+def to_wire(resp: Response) -> np.ndarray:
+    """Response -> wire buffer (uint8 array), numpy only."""
+    n, nn, nl = len(resp.recs), len(resp.name_off) - 1, len(resp.names)
+    st = np.asarray(resp.block_status, np.int32)
+    err = b"".join(struct.pack("<I", len(e.encode())) + e.encode() for s, e in zip(st, resp.block_errors) if s)
+    size = _HDR.size + _pad8(40 * n) + _pad8(4 * (nn + 1)) + _pad8(nl) + _pad8(4 * len(st)) + _pad8(len(err))
+    buf = np.empty(size, np.uint8)
+    m = resp.metrics
+    _HDR.pack_into(buf, 0, WIRE_MAGIC, WIRE_VERSION, n, nn, nl, len(st), len(err), m.inspected_traces,
+                   m.inspected_bytes, m.inspected_blocks, m.skipped_blocks, m.skipped_traces, 0)
+    o = _HDR.size
+    for part in (np.ascontiguousarray(resp.recs, REC_DTYPE).view(np.uint8).reshape(-1),
+                 np.ascontiguousarray(resp.name_off, np.uint32).view(np.uint8), np.frombuffer(resp.names, np.uint8),
+                 st.view(np.uint8), np.frombuffer(err, np.uint8)):
+        buf[o:o + part.size] = part
+        buf[o + part.size:o + _pad8(part.size)] = 0
+        o += _pad8(part.size)
+    return buf
+
+
+def from_wire(buf) -> Response:
+    """Wire buffer -> Response (numpy views into `buf` where possible)."""
+    b = np.frombuffer(buf, np.uint8) if not isinstance(buf, np.ndarray) else buf.view(np.uint8).reshape(-1)
+    (magic, ver, n, nn, nl, nb, el, it, ib, ibl, sb, skt, _) = _HDR.unpack_from(b, 0)
+    if magic != WIRE_MAGIC or ver != WIRE_VERSION:
+        raise ValueError("not a tsg wire buffer")
+    o = _HDR.size
+    recs = b[o:o + 40 * n].view(REC_DTYPE)
+    o += _pad8(40 * n)
+    off = b[o:o + 4 * (nn + 1)].view(np.uint32)
+    o += _pad8(4 * (nn + 1))
+    names = b[o:o + nl].tobytes()
+    o += _pad8(nl)
+    st = b[o:o + 4 * nb].view(np.int32)
+    o += _pad8(4 * nb)
+    eb = b[o:o + el].tobytes()
+    errs, e = [], 0
+    for s in st:
+        if s:
+            (k,) = struct.unpack_from("<I", eb, e)
+            errs.append(eb[e + 4:e + 4 + k].decode(errors="replace"))
+            e += 4 + k
+        else:
+            errs.append(None)
+    met = SearchMetrics(it, ib, ibl, sb, block_status=st.tolist(), block_errors=errs, skipped_traces=skt)
+    return Response(recs, off, names, met, st, errs)
+
+
+def _as_bytes_ptr(w):
+    a = np.ascontiguousarray(np.frombuffer(w, np.uint8) if not isinstance(w, np.ndarray) else w.view(np.uint8))
+    return a, a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def merge_wires(wires: Sequence, limit: int, total_blocks: int, out: Optional[np.ndarray] = None) -> Response:
+    """The frontend merge (tsg_wire_merge) of wire responses in order -> merged Response.
+    `out`: a caller-owned uint8 buffer to merge into (reused across queries: no allocation
+    and no page faults per merge; the Response's arrays are views into it); grown if short."""
+    keep = [_as_bytes_ptr(w) for w in wires]
+    n = len(keep)
+    ptrs = (C.POINTER(C.c_uint8) * max(n, 1))(*[p for _, p in keep])
+    lens = (C.c_size_t * max(n, 1))(*[a.size for a, _ in keep])
+    need = max(_HDR.size, sum(a.size for a, _ in keep))  # the merged wire is never longer
+    if out is None or out.size < need:
+        out = np.empty(need, np.uint8)
+    ln = C.c_size_t()
+    _check(lib().tsg_wire_merge(ptrs, lens, n, min(int(limit), 2**64 - 1), total_blocks, out.ctypes.data, out.size,
+                                C.byref(ln)))
+    return from_wire(out[:ln.value])
+
+
+def _raise_first_error(resp: Response):
+    for s, e in zip(resp.block_status, resp.block_errors):
+        if s:
+            raise TsgError(int(s), e or "search job failed")
 
 
 def merge_responses(responses: Sequence[Tuple[Sequence[TraceSearchMetadata], SearchMetrics]],
-                    limit: int, total_blocks: int) -> Tuple[List[TraceSearchMetadata], SearchMetrics]:
-    """Frontend merge of per-shard responses, in shard order."""
-    r = SearchResponse(limit=limit, inspected_blocks=total_blocks)
-    for traces, met in responses:
-        if r.should_quit():
-            break
-        r.add_response(traces, met)
-    return r.result()
+                    limit: int, total_blocks: int, on_error: str = "keep"
+                    ) -> Tuple[List[TraceSearchMetadata], SearchMetrics]:
+    """Frontend merge of per-shard (traces, metrics) responses, in shard order.
+
+    on_error: "keep" returns every block's status / error in the metrics (the ingester logs
+    a failed block and keeps the others' results, instance_search.go:179-182); "raise"
+    raises the first one, as a failed job does to the frontend request (setError ->
+    shouldQuit, searchsharding.go:64-69,88-94)."""
+    merged = merge_wires([to_wire(response_from_traces(t, m)) for t, m in responses], limit, total_blocks)
+    if on_error == "raise":
+        _raise_first_error(merged)
+    return merged.traces(), merged.metrics
 
 
 def distributed_search(search_local: Callable[[], Tuple[List[TraceSearchMetadata], SearchMetrics]],
-                       limit: int, total_blocks: int, group=None, dst: int = 0
+                       limit: int, total_blocks: int, group=None, dst: int = 0, on_error: str = "keep"
                        ) -> Optional[Tuple[List[TraceSearchMetadata], SearchMetrics]]:
-    """Run this rank's search, gather the responses on `dst`, merge there.
-
-    `search_local` returns this rank's querier response (e.g.
-    `Engine.search_request` over the rank's blocks). Returns the merged
-    response on `dst`, None elsewhere. Works on any torch.distributed backend
-    (gloo for CPU tests, nccl = RCCL on the GPUs)."""
+    """Run this rank's search, gather the responses on `dst` (pickled: gather_object,
+    fine for limit-bounded responses), merge there. Returns the merged response on `dst`,
+    None elsewhere. Works on any torch.distributed backend."""
     import torch.distributed as dist
     mine = search_local()
     world = dist.get_world_size(group)
@@ -102,90 +215,91 @@ def distributed_search(search_local: Callable[[], Tuple[List[TraceSearchMetadata
     dist.gather_object(mine, got, dst=dst, group=group)
     if rank != dst:
         return None
-    return merge_responses(got, limit, total_blocks)
+    return merge_responses(got, limit, total_blocks, on_error)
 
 
-# ---- packed transport (tensors, not pickles) -------------------------------------
-# record: id[16] | id_len u8 | pad[3] | duration_ms u32 | start_ns u64 | end_ns u64 |
-#         entry_idx u64 | block_idx u32 | service off u32, len u32 | name off u32, len u32
-_REC = struct.Struct("<16sB3xIQQQIIIII")
-assert _REC.size == 68
+_GATHER_CACHE = {}  # (device, slot, role) -> grow-only 1-D uint8 tensors reused across gathers
 
 
-def pack_traces(traces: Sequence[TraceSearchMetadata]):
-    """(records bytes, names bytes) for a response's traces, in order."""
-    recs = bytearray()
-    names = bytearray()
-    for t in traces:
-        svc = t.root_service_name.encode()
-        nm = t.root_trace_name.encode()
-        so, no = len(names), len(names) + len(svc)
-        names += svc + nm
-        recs += _REC.pack(bytes(t.trace_id).ljust(16, b"\0")[:16], t.trace_id_len, t.duration_ms,
-                          t.start_time_unix_nano, t.end_time_unix_nano, t.entry_idx, t.block_idx,
-                          so, len(svc), no, len(nm))
-    return bytes(recs), bytes(names)
+def _cached(device, slot, width):
+    import torch
+    key = (str(device), slot)
+    t = _GATHER_CACHE.get(key)
+    if t is None or t.numel() < width:
+        t = torch.empty(max(width, 1), dtype=torch.uint8, device=device)
+        _GATHER_CACHE[key] = t
+    return t[:width]
 
 
-def unpack_traces(recs: bytes, names: bytes) -> List[TraceSearchMetadata]:
-    out = []
-    for i in range(len(recs) // _REC.size):
-        (tid, tlen, dur, st, en, ent, blk, so, sl, no, nl) = _REC.unpack_from(recs, i * _REC.size)
-        out.append(TraceSearchMetadata(trace_id=tid, trace_id_len=tlen,
-                                       root_service_name=names[so:so + sl].decode(),
-                                       root_trace_name=names[no:no + nl].decode(), start_time_unix_nano=st,
-                                       duration_ms=dur, end_time_unix_nano=en, block_idx=blk, entry_idx=ent))
-    return out
-
-
-def _gather_bytes(parts: Sequence[bytes], device, group, dst):
-    """Gather variable-length byte strings (one list per rank) to `dst` as tensors:
-    sizes first (one int64 per part), then every part padded to the longest."""
+def _gather_bytes(parts: Sequence, device, group, dst):
+    """Gather variable-length byte buffers (one list per rank) to `dst` as tensors: sizes
+    first, then every part padded to the longest of any rank. The send and receive tensors
+    are kept between calls (a query's gather then allocates nothing and takes no page faults);
+    a numpy part that is already that long is sent without a copy."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    sizes = torch.tensor([len(p) for p in parts], dtype=torch.int64, device=device)
+    arrs = [p if isinstance(p, np.ndarray) else np.frombuffer(bytearray(p), np.uint8) for p in parts]
+    sizes = torch.tensor([a.size for a in arrs], dtype=torch.int64, device=device)
     all_sizes = [torch.empty_like(sizes) for _ in range(world)] if rank == dst else None
     dist.gather(sizes, all_sizes, dst=dst, group=group)
-    # the longest part of any rank: a max all-reduce, so every rank pads alike
-    mx = sizes.max().clone() if len(parts) else torch.zeros((), dtype=torch.int64, device=device)
+    mx = sizes.max().clone() if arrs else torch.zeros((), dtype=torch.int64, device=device)
     dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
     width = max(1, int(mx.item()))
-    buf = torch.zeros((len(parts), width), dtype=torch.uint8, device=device)
-    for i, p in enumerate(parts):
-        if p:
-            buf[i, :len(p)] = torch.frombuffer(bytearray(p), dtype=torch.uint8).to(device)
-    bufs = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
-    dist.gather(buf, bufs, dst=dst, group=group)
+    result = [] if rank == dst else None
+    for i, a in enumerate(arrs):
+        if a.size == width and a.flags.writeable and a.flags.c_contiguous and str(device) == "cpu":
+            t = torch.from_numpy(a)
+        else:
+            t = _cached(device, ("send", i), width)
+            if a.size:
+                t[:a.size].copy_(torch.from_numpy(np.ascontiguousarray(a)))
+            if a.size < width:
+                t[a.size:].zero_()
+        recv = [_cached(device, ("recv", i, r), width) for r in range(world)] if rank == dst else None
+        dist.gather(t, recv, dst=dst, group=group)
+        if rank == dst:
+            result.append(recv)
     if rank != dst:
         return None
     out = []
     for r in range(world):
         sz = all_sizes[r].cpu().tolist()
-        host = bufs[r].cpu().numpy()
-        out.append([host[i, :sz[i]].tobytes() for i in range(len(parts))])
+        out.append([result[i][r][:sz[i]].cpu().numpy() for i in range(len(arrs))])
     return out
 
 
-def distributed_search_packed(search_local: Callable[[], Tuple[List[TraceSearchMetadata], SearchMetrics]],
-                              limit: int, total_blocks: int, device=None, group=None, dst: int = 0
-                              ) -> Optional[Tuple[List[TraceSearchMetadata], SearchMetrics]]:
-    """`distributed_search` with the responses moved as byte tensors on `device`
-    (a CUDA device with the nccl backend: RCCL over xGMI; the CPU with gloo)."""
+WireSource = Union[bytes, np.ndarray, Response, Tuple[Sequence[TraceSearchMetadata], SearchMetrics]]
+
+
+def _wire_of(x: WireSource) -> np.ndarray:
+    if isinstance(x, np.ndarray):
+        return x.view(np.uint8).reshape(-1)
+    if isinstance(x, (bytes, bytearray)):
+        return np.frombuffer(bytearray(x), np.uint8)
+    if isinstance(x, Response):
+        return to_wire(x)
+    traces, met = x
+    return to_wire(response_from_traces(traces, met))
+
+
+def distributed_search_packed(search_local: Callable[[], WireSource], limit: int, total_blocks: int, device=None,
+                              group=None, dst: int = 0, on_error: str = "keep", columns: bool = False):
+    """`distributed_search` with the responses moved as wire buffers (byte tensors on
+    `device`: a CUDA device with the nccl backend = RCCL over xGMI; the CPU with gloo) and
+    merged in libtsg. `search_local` returns this rank's response: a wire buffer
+    (`Engine.search_wire`), a Response, or (traces, metrics). On `dst`: the merged
+    response as (traces, metrics), or the Response with columns=True; None elsewhere."""
     import torch.distributed as dist
-    traces, met = search_local()
-    recs, names = pack_traces(traces)
-    mets = struct.pack("<QQQQ", met.inspected_traces, met.inspected_bytes, met.inspected_blocks,
-                       met.skipped_blocks)
-    got = _gather_bytes([recs, names, mets], device or "cpu", group, dst)
+    wire = _wire_of(search_local())
+    got = _gather_bytes([wire], device or "cpu", group, dst)
     if dist.get_rank(group) != dst:
         return None
-    responses = []
-    for r_recs, r_names, r_mets in got:
-        it, ib, ibl, sk = struct.unpack("<QQQQ", r_mets)
-        responses.append((unpack_traces(r_recs, r_names), SearchMetrics(it, ib, ibl, sk)))
-    return merge_responses(responses, limit, total_blocks)
+    merged = merge_wires([g[0] for g in got], limit, total_blocks)
+    if on_error == "raise":
+        _raise_first_error(merged)
+    return merged if columns else (merged.traces(), merged.metrics)
 
 
 def shard_ids(n_ids: int, world: int, rank: int) -> range:
@@ -198,13 +312,12 @@ def distributed_lookup(lookup_local: Callable[[object], object], ids, device=Non
     returns the global hit table (int64 rows: id, block, record, start, length) sorted
     by (id, block), others None. `lookup_local(id_slice)` returns the rank's table with
     slice-local id indices (e.g. `lambda x: engine.lookup(blocks, x)[0]`)."""
-    import numpy as np
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     sl = shard_ids(len(ids), world, rank)
     hits = np.asarray(lookup_local(ids[sl.start:sl.stop]), dtype=np.int64).reshape(-1, 5).copy()
     hits[:, 0] += sl.start
-    got = _gather_bytes([hits.tobytes()], device or "cpu", group, dst)
+    got = _gather_bytes([hits.view(np.uint8).reshape(-1)], device or "cpu", group, dst)
     if rank != dst:
         return None
-    return np.concatenate([np.frombuffer(g[0], dtype=np.int64).reshape(-1, 5) for g in got])
+    return np.concatenate([np.frombuffer(g[0].tobytes(), dtype=np.int64).reshape(-1, 5) for g in got])

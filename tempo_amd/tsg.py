@@ -73,7 +73,7 @@ class _Query(C.Structure):
 
 class _Metrics(C.Structure):
     _fields_ = [("traces_inspected", C.c_uint32), ("blocks_inspected", C.c_uint32),
-                ("blocks_skipped", C.c_uint32), ("pad0", C.c_uint32), ("bytes_inspected", C.c_uint64),
+                ("blocks_skipped", C.c_uint32), ("reruns", C.c_uint32), ("bytes_inspected", C.c_uint64),
                 ("device_bytes_read", C.c_uint64), ("kernel_ns", C.c_uint64),
                 ("scan_kernel_ns", C.c_uint64), ("scan_bytes", C.c_uint64)]
 
@@ -86,7 +86,8 @@ class _Result(C.Structure):
                 ("root_service", C.POINTER(C.c_char_p)), ("root_service_len", C.POINTER(C.c_uint32)),
                 ("root_name", C.POINTER(C.c_char_p)), ("root_name_len", C.POINTER(C.c_uint32)),
                 ("metrics", _Metrics), ("nblocks", C.c_uint64), ("block_status", C.POINTER(C.c_int32)),
-                ("block_error", C.POINTER(C.c_char_p))]
+                ("block_error", C.POINTER(C.c_char_p)), ("names", C.c_void_p), ("names_len", C.c_uint64),
+                ("root_service_off", C.POINTER(C.c_uint64)), ("root_name_off", C.POINTER(C.c_uint64))]
 
 
 class _SearchOpts(C.Structure):
@@ -123,11 +124,12 @@ class _ProtoRequest(C.Structure):
 
 class _ProtoResult(C.Structure):
     _fields_ = [("n", C.c_uint32), ("trace_ids", C.POINTER(C.c_uint8)), ("trace_id_off", C.POINTER(C.c_uint32)),
-                ("trace_id_len", C.POINTER(C.c_uint8)), ("root_service_name", C.POINTER(C.c_char_p)),
-                ("root_trace_name", C.POINTER(C.c_char_p)), ("start_time_unix_nano", C.POINTER(C.c_uint64)),
+                ("trace_id_len", C.POINTER(C.c_uint32)), ("root_service_name", C.POINTER(C.c_void_p)),
+                ("root_trace_name", C.POINTER(C.c_void_p)), ("start_time_unix_nano", C.POINTER(C.c_uint64)),
                 ("duration_ms", C.POINTER(C.c_uint32)), ("object_idx", C.POINTER(C.c_uint32)),
                 ("inspected_traces", C.c_uint64), ("inspected_bytes", C.c_uint64), ("skipped_traces", C.c_uint64),
-                ("kernel_ns", C.c_uint64)]
+                ("kernel_ns", C.c_uint64), ("root_service_name_len", C.POINTER(C.c_uint32)),
+                ("root_trace_name_len", C.POINTER(C.c_uint32))]
 
 
 class _LookupResult(C.Structure):
@@ -147,6 +149,7 @@ EXPORTED = [
     "tsg_proto_search", "tsg_proto_result_free", "tsg_go_parse", "tsg_write_v2_block",
     "tsg_write_search_block", "tsg_write_wal_search", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
     "tsg_synth_v2_block", "tsg_live_block_open_mem", "tsg_search_tags", "tsg_search_tag_values",
+    "tsg_result_pack", "tsg_wire_merge",
 ]
 
 _lib = None
@@ -179,6 +182,9 @@ def lib():
         L.tsg_write_wal_search.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int]
         L.tsg_block_info_get.argtypes = [vp, C.POINTER(_BlockInfo)]
         L.tsg_live_block_open_mem.argtypes = [vp, C.c_char_p, vp, C.c_size_t, vp, C.c_size_t, C.c_int, C.POINTER(vp)]
+        L.tsg_result_pack.argtypes = [C.POINTER(_Result), C.POINTER(u8p), C.POINTER(C.c_size_t)]
+        L.tsg_wire_merge.argtypes = [C.POINTER(u8p), C.POINTER(C.c_size_t), C.c_size_t, C.c_uint64, C.c_uint64,
+                                     vp, C.c_size_t, C.POINTER(C.c_size_t)]
         L.tsg_search_tags.argtypes = [C.POINTER(vp), C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
                                       C.POINTER(C.c_size_t)]
         L.tsg_search_tag_values.argtypes = [C.POINTER(vp), C.c_size_t, C.c_char_p, C.c_size_t, C.c_int64,
@@ -325,6 +331,7 @@ class SearchMetrics:
     # matches (a damaged data page), with the message
     block_status: List[int] = field(default_factory=list)
     block_errors: List[Optional[str]] = field(default_factory=list)
+    skipped_traces: int = 0  # SearchMetrics.SkippedTraces (the proto path's MaxBytes skips; 0 here)
 
 
 def _unpack(rp) -> (List[TraceSearchMetadata], SearchMetrics):
@@ -443,6 +450,36 @@ class Engine:
         free(rp)
         return n, met
 
+    def search_wire(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0,
+                    combine: Optional[int] = None, flags: int = 0):
+        """tsg_search (+ tsg_results_combine when `combine` is set: instance.Search's
+        consumer) packed by tsg_result_pack into a wire buffer (numpy uint8): what a rank
+        ships to the merging rank (tempo_amd.shard). No per-record Python."""
+        import numpy as np
+        arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+        opts = _SearchOpts(limit=limit, flags=flags)
+        rp = C.POINTER(_Result)()
+        _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
+        fin = None
+        try:
+            src = rp
+            if combine is not None:
+                fin = C.POINTER(_Result)()
+                _check(lib().tsg_results_combine(rp, combine, C.byref(fin)))
+                src = fin
+            out, ln = C.POINTER(C.c_uint8)(), C.c_size_t()
+            _check(lib().tsg_result_pack(src, C.byref(out), C.byref(ln)))
+            try:
+                buf = np.empty(ln.value, np.uint8)
+                C.memmove(buf.ctypes.data, out, ln.value)
+                return buf
+            finally:
+                lib().tsg_free(out)
+        finally:
+            if fin is not None:
+                lib().tsg_result_free(fin)
+            lib().tsg_result_free(rp)
+
     def cancel(self, query_id: int):
         """tsg_cancel: the search running (or about to run) with this id stops at its next
         chunk boundary with TSG_E_CANCELLED (the Go shim maps ctx.Done() to this)."""
@@ -551,8 +588,11 @@ class Engine:
                 tl = r.trace_id_len[i]
                 tid = C.string_at(C.addressof(r.trace_ids.contents) + r.trace_id_off[i], tl) if tl else b""
                 traces.append(TraceSearchMetadata(
-                    trace_id=tid, trace_id_len=tl, root_service_name=r.root_service_name[i].decode("utf-8", "surrogateescape"),
-                    root_trace_name=r.root_trace_name[i].decode("utf-8", "surrogateescape"),
+                    trace_id=tid, trace_id_len=tl,
+                    root_service_name=C.string_at(r.root_service_name[i], r.root_service_name_len[i]).decode(
+                        "utf-8", "surrogateescape"),
+                    root_trace_name=C.string_at(r.root_trace_name[i], r.root_trace_name_len[i]).decode(
+                        "utf-8", "surrogateescape"),
                     start_time_unix_nano=r.start_time_unix_nano[i], duration_ms=r.duration_ms[i]))
                 objs.append(r.object_idx[i])
             return ProtoSearchResponse(traces, r.inspected_traces, r.inspected_bytes, r.skipped_traces, objs,

@@ -1,7 +1,7 @@
 """Rank-sharded search on the GPU: one libtsg context per rank on the
 device, each searching its block shard through the engine (instance.Search: limit cut,
-combine, sort), each response packed into the byte records the gather moves
-(tempo_amd.shard.pack_traces), unpacked and merged with the frontend rule
+combine, sort), each response packed by libtsg into the wire buffer the gather moves
+(Engine.search_wire -> tsg_result_pack), merged in libtsg with the frontend rule
 (modules/frontend/searchsharding.go:32-125). Expected: the same merge applied to the
 oracle's per-shard querier responses. The transport itself (gloo / RCCL gather of the
 packed tensors) is covered by test_shard_gloo.py; ranks as processes by bench.py's merge
@@ -51,19 +51,19 @@ def test_rank_contexts_pack_and_merge(world, limit):
             paths.append(p)
         req = T.SearchRequest(tags=QUERY["tags"], min_duration_ms=QUERY["min_ms"], max_duration_ms=QUERY["max_ms"],
                               start=QUERY["start"], end=QUERY["end"], limit=limit)
-        responses = []
+        wires = []
         for r in range(world):  # one context per rank, its shard resident on the device
             eng = T.Engine(devices=[0])
             try:
                 mine = [eng.open_block(paths[i]) for i in shard.shard_range(len(paths), world, r)]
-                traces, met = eng.search_request(mine, req, limit)
+                # instance.Search's consumer (limit cut, combine, sort), packed: what the gather moves
+                wires.append(eng.search_wire(mine, T.Pipeline(req), limit=limit, combine=limit))
                 for b in mine:
                     b.close()
             finally:
                 eng.close()
-            recs, names = shard.pack_traces(traces)  # what the gather moves
-            responses.append((shard.unpack_traces(recs, names), met))
-        got = _key(shard.merge_responses(responses, limit, len(paths)))
+        m = shard.merge_wires(wires, limit, len(paths))
+        got = _key((m.traces(), m.metrics))
         exp = _key(shard.merge_responses(
             [_oracle_response([paths[i] for i in shard.shard_range(len(paths), world, r)], limit)
              for r in range(world)], limit, len(paths)))

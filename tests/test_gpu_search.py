@@ -368,8 +368,16 @@ def test_cancel(engine, tmp_path):
                 assert e.code == T.TSG_E_CANCELLED
                 outcomes.append("cancelled")
             th.join()
-            engine.search([], pipe, query_id=qid)  # forget an id whose cancel came after the search
+            # a cancel that came after its search returned is dropped: the id can
+            # be reused at once
+            again, _ = engine.search(blocks, pipe, query_id=qid)
+            assert [tsg_key(m) for m in again] == [tsg_key(m) for m in full]
         print("cancel outcomes:", outcomes)
+        # the race in its plain form: search, then a late cancel, then the id again
+        engine.search(blocks[:1], pipe, query_id=4242)
+        engine.cancel(4242)
+        got, _ = engine.search(blocks, pipe, query_id=4242)
+        assert [tsg_key(m) for m in got] == [tsg_key(m) for m in full]
     finally:
         for b in blocks:
             b.close()

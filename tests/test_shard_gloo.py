@@ -120,13 +120,143 @@ def test_shard_range_partitions():
         shard.shard_range(4, 2, 2)
 
 
-def test_pack_roundtrip():
+def test_wire_roundtrip():
     ts = [T.TraceSearchMetadata(trace_id=bytes(range(i, i + 16)), trace_id_len=16 - (i % 9),
-                                root_service_name="svc-%d" % i, root_trace_name="op\u00e9-%d" % i,
-                                start_time_unix_nano=10 ** 18 + i, duration_ms=i * 7, end_time_unix_nano=2 * 10 ** 18,
-                                block_idx=i % 3, entry_idx=2 ** 40 + i) for i in range(50)]
-    assert shard.unpack_traces(*shard.pack_traces(ts)) == ts
-    assert shard.unpack_traces(*shard.pack_traces([])) == []
+                                root_service_name="svc-%d" % (i % 4), root_trace_name="op\u00e9-%d" % i,
+                                start_time_unix_nano=10 ** 18 + i, duration_ms=i * 7) for i in range(50)]
+    met = T.SearchMetrics(11, 22, 3, 4, block_status=[0, 2, 0], block_errors=[None, "damaged page", None],
+                          skipped_traces=5)
+    r = shard.from_wire(shard.to_wire(shard.response_from_traces(ts, met)))
+    assert r.traces() == ts
+    assert (r.metrics.inspected_traces, r.metrics.inspected_bytes, r.metrics.inspected_blocks,
+            r.metrics.skipped_blocks, r.metrics.skipped_traces) == (11, 22, 3, 4, 5)
+    assert r.metrics.block_status == [0, 2, 0] and r.metrics.block_errors == [None, "damaged page", None]
+    e = shard.from_wire(shard.to_wire(shard.response_from_traces([], T.SearchMetrics(0, 0, 0, 0))))
+    assert e.traces() == [] and len(e) == 0
+
+
+def _ref_merge(responses, limit, total_blocks):
+    """searchResponse restated per record (searchsharding.go:71-125), deterministic ties."""
+    seen, it, ib, sb, skt = {}, 0, 0, 0, 0
+    for traces, met in responses:
+        if len(seen) > limit:  # shouldQuit
+            break
+        for t in traces:
+            seen.setdefault(t.trace_id_hex, (len(seen), t))
+        it, ib, sb = it + met.inspected_traces, ib + met.inspected_bytes, sb + met.skipped_blocks
+        skt += met.skipped_traces
+    out = [t for _, t in sorted(seen.values(), key=lambda x: (-x[1].start_time_unix_nano, x[0]))]
+    return out, (it, ib, total_blocks, sb, skt)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_native_merge_matches_restatement(seed):
+    """tsg_wire_merge vs the per-record restatement: duplicate ids across and inside
+    responses (first wins), equal start times (first position wins), ids that differ only in
+    leading zeros (one hex TraceID), the quit rule at several limits."""
+    rng = random.Random(seed)
+    pool = [bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(300)]
+    pool += [bytes(12) + bytes(rng.getrandbits(8) for _ in range(4)) for _ in range(20)]
+    responses = []
+    for r in range(rng.randrange(1, 6)):
+        ts = []
+        for _ in range(rng.randrange(0, 200)):
+            tid = rng.choice(pool)
+            il = 16 if tid[0] else rng.choice([4, 8, 16])
+            ts.append(T.TraceSearchMetadata(trace_id=tid, trace_id_len=il, root_service_name=rng.choice(["", "a", "bb"]),
+                                            root_trace_name=rng.choice(["", "x", "yy"]),
+                                            start_time_unix_nano=rng.choice([5, 7, 10 ** 18 + rng.randrange(1000)]),
+                                            duration_ms=rng.randrange(100)))
+        nb = rng.randrange(0, 4)
+        st = [rng.choice([0, 0, 2]) for _ in range(nb)]
+        met = T.SearchMetrics(rng.randrange(1000), rng.randrange(10 ** 6), nb, rng.randrange(3), block_status=st,
+                              block_errors=["e%d" % i if s else None for i, s in enumerate(st)],
+                              skipped_traces=rng.randrange(5))
+        responses.append((ts, met))
+    for limit in (0, 1, 5, 50, 10 ** 9):
+        got, met = shard.merge_responses(responses, limit, 17)
+        exp, em = _ref_merge(responses, limit, 17)
+        assert [(t.trace_id_hex, t.start_time_unix_nano, t.duration_ms, t.root_service_name, t.root_trace_name,
+                 t.trace_id_len) for t in got] == \
+            [(t.trace_id_hex, t.start_time_unix_nano, t.duration_ms, t.root_service_name, t.root_trace_name,
+              t.trace_id_len) for t in exp]
+        assert (met.inspected_traces, met.inspected_bytes, met.inspected_blocks, met.skipped_blocks,
+                met.skipped_traces) == em
+        assert met.block_status == [s for _, m in responses for s in m.block_status]
+    bad = [r for r in responses if any(r[1].block_status)]
+    if bad:
+        with pytest.raises(T.TsgError):
+            shard.merge_responses(responses, 10 ** 9, 17, on_error="raise")
+
+
+def _synthetic_wire(rank, n, nnames=2500):
+    """A rank's full-scan response of n records built with numpy (no GPU here): random ids
+    (a slice shared with the other rank), start times over an hour, a name table."""
+    import numpy as np
+    rng = np.random.default_rng(1000 + rank)
+    recs = np.zeros(n, shard.REC_DTYPE)
+    ids = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    ids[: n // 100] = np.random.default_rng(7).integers(0, 256, (n // 100, 16), dtype=np.uint8)  # shared
+    recs["trace_id"] = ids.view("V16").ravel()
+    recs["trace_id_len"] = 16
+    recs["start_ns"] = 1_700_000_000 * 10 ** 9 + rng.integers(0, 3600 * 10 ** 9, n, dtype=np.uint64)
+    recs["duration_ms"] = rng.integers(0, 5000, n, dtype=np.uint32)
+    recs["root_service"] = rng.integers(1, nnames, n, dtype=np.uint32)
+    recs["root_name"] = rng.integers(1, nnames, n, dtype=np.uint32)
+    names = [b""] + [b"name-%05d" % k for k in range(1, nnames)]
+    off = np.zeros(nnames + 1, np.uint32)
+    off[1:] = np.cumsum([len(x) for x in names])
+    return shard.Response(recs, off, b"".join(names), T.SearchMetrics(n, 40 * n, 5, 0))
+
+
+def _merge_perf_worker(rank, world, port, n, outdir):
+    import json
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        resp = _synthetic_wire(rank, n)
+        times = []
+        for _ in range(5):
+            dist.barrier()
+            t0 = time.perf_counter()
+            merged = shard.distributed_search_packed(lambda: resp, 1 << 62, 10, columns=True)
+            t = time.perf_counter() - t0
+            import torch
+            tt = torch.tensor([t], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            times.append(float(tt.item()))
+        if rank == 0:
+            st = merged.recs["start_ns"]
+            with open(os.path.join(outdir, "perf.json"), "w") as f:
+                json.dump({"times": times, "n": len(merged), "sorted": bool((st[:-1] >= st[1:]).all()),
+                           "inspected": merged.metrics.inspected_traces}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def run_merge_perf(n=1_000_000, world=2):
+    """Times pack + gloo gather + merge of n synthetic records per rank (world ranks)."""
+    import json
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_merge_perf_worker, args=(world, _free_port(), n, td), nprocs=world, join=True)
+        with open(os.path.join(td, "perf.json")) as f:
+            return json.load(f)
+
+
+def test_gloo_merge_one_million_per_rank():
+    """pack + gloo gather + merge of 1 M records per rank with no
+    per-record Python (the rank's response is packed into one numpy wire buffer, gathered
+    as one tensor, merged in libtsg). TSG_MERGE_BOUND_MS sets the bound: 100 when run on the
+    GPU box's host (a CPU-only pytest process there, profiles/r03_merge/), 2000 by default in
+    the build container, whose 8 shared CPUs sort 2 M u64 in ~35 ms with numpy alone."""
+    n = 1_000_000
+    r = run_merge_perf(n)
+    assert r["sorted"] and r["inspected"] == 2 * n
+    assert r["n"] == 2 * n - n // 100  # the shared slice appears once
+    best = min(r["times"][1:])
+    print(f"pack + gloo gather + merge of 2 x {n} records: best {best * 1e3:.1f} ms, all {r['times']}")
+    assert best * 1e3 < float(os.environ.get("TSG_MERGE_BOUND_MS", "2000")), r["times"]
 
 
 def _lookup_worker(rank, world, port, paths, ids, outdir):
