@@ -116,12 +116,47 @@ struct tsg_ctx {
     for (auto &e : errs)
       if (e) std::rethrow_exception(e);
   }
-  // tsg_cancel: query ids cancelled and not yet seen finishing (bounded, FIFO eviction).
-  // A search with that id checks the set between device chunks and waves
-  // (cooperative, like BackendSearchBlock.Search's per-page sr.Quit()).
+  // tsg_cancel (cooperative, like BackendSearchBlock.Search's per-page sr.Quit()): a search
+  // with a query id registers it while it runs and checks for a cancel between device
+  // chunks and waves. A cancel for a running id marks it; for an id that finished recently
+  // (the usual timeout race: the cancel lands just after the search returned) it is
+  // dropped, so it cannot fail a later search that reuses the id; for an id not seen yet it
+  // is kept for kPendingNs (a cancel that overtakes its search start) and then expires.
   std::mutex cmu;
-  std::unordered_set<uint64_t> cancelled;
-  std::deque<uint64_t> corder;
+  std::unordered_map<uint64_t, int> active;        // id -> searches running with it
+  std::unordered_set<uint64_t> cancelled;          // marks on running ids
+  std::unordered_map<uint64_t, uint64_t> pending;  // id -> time of a cancel before its search
+  std::unordered_set<uint64_t> recent;             // ids of finished searches (FIFO, bounded)
+  std::deque<uint64_t> recent_order;
+  static constexpr uint64_t kPendingNs = 10'000'000'000ull;
+  static uint64_t now_ns() {
+    return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now().time_since_epoch())
+                        .count());
+  }
+  void cancel(uint64_t qid) {
+    std::lock_guard<std::mutex> lk(cmu);
+    if (active.count(qid)) {
+      cancelled.insert(qid);
+    } else if (!recent.count(qid)) {
+      if (pending.size() >= 4096) {  // expire, then bound
+        const uint64_t t = now_ns();
+        for (auto it = pending.begin(); it != pending.end();) it = t - it->second > kPendingNs ? pending.erase(it) : ++it;
+        if (pending.size() >= 4096) pending.erase(pending.begin());
+      }
+      pending[qid] = now_ns();
+    }
+  }
+  void begin(uint64_t qid) {
+    if (!qid) return;
+    std::lock_guard<std::mutex> lk(cmu);
+    active[qid]++;
+    auto it = pending.find(qid);
+    if (it != pending.end()) {
+      if (now_ns() - it->second <= kPendingNs) cancelled.insert(qid);
+      pending.erase(it);
+    }
+  }
   bool is_cancelled(uint64_t qid) {
     if (!qid) return false;
     std::lock_guard<std::mutex> lk(cmu);
@@ -130,7 +165,18 @@ struct tsg_ctx {
   void forget(uint64_t qid) {
     if (!qid) return;
     std::lock_guard<std::mutex> lk(cmu);
-    if (cancelled.erase(qid)) corder.erase(std::remove(corder.begin(), corder.end(), qid), corder.end());
+    auto it = active.find(qid);
+    if (it != active.end() && --it->second == 0) {
+      active.erase(it);
+      cancelled.erase(qid);
+    }
+    if (recent.insert(qid).second) {
+      recent_order.push_back(qid);
+      if (recent_order.size() > 4096) {
+        recent.erase(recent_order.front());
+        recent_order.pop_front();
+      }
+    }
   }
 };
 struct tsg_block {
@@ -465,14 +511,7 @@ int tsg_device_numa_node(tsg_ctx *ctx, int dev) {
 }
 int tsg_cancel(tsg_ctx *ctx, uint64_t qid) {
   if (!ctx || !qid) return TSG_E_INVALID;
-  std::lock_guard<std::mutex> lk(ctx->cmu);
-  if (ctx->cancelled.insert(qid).second) {
-    ctx->corder.push_back(qid);
-    if (ctx->corder.size() > 4096) {  // ids cancelled but never searched: keep the newest
-      ctx->cancelled.erase(ctx->corder.front());
-      ctx->corder.pop_front();
-    }
-  }
+  ctx->cancel(qid);
   return TSG_OK;
 }
 
@@ -730,6 +769,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
   using clk = std::chrono::steady_clock;
   const clk::time_point t_in = trace ? clk::now() : clk::time_point();
   const uint64_t qid = opts ? opts->query_id : 0;
+  ctx->begin(qid);
   struct Forget {  // the id is done with once this search returns, cancelled or not
     tsg_ctx *c;
     uint64_t q;

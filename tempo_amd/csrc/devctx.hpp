@@ -138,6 +138,9 @@ struct DeviceCtx {
   // tail at every size (tests)
   uint32_t pool_small = env_u32("TSG_POOL_SMALL", 32, 0, 1u << 20);
   uint32_t pool_seg = 32;  // host segment records per workgroup (adaptive: grows on overflow, halves when sparse)
+  // TSG_POOL_STATIC=0: the claim-based pool kernel (LDS claims + dynamic chunks) instead of
+  // the static-run kernel (search_static_kernel)
+  bool pool_static = env_u32("TSG_POOL_STATIC", 1, 0, 1) != 0;
   DevBuf pool_head;  // two dynamic-chunk counters (128 B apart): a launch uses one, zeroes the other
   uint32_t pool_parity = 0;
   std::set<const void *> pool_attr;  // pool kernels whose dynamic LDS limit has been raised

@@ -163,12 +163,13 @@ static void result_pack(const tsg_result &r, uint8_t **out, size_t *len) {
     x.root_service = svc[i];
     x.root_name = nm[i];
   }
+  // entry k spans name_off[k] .. name_off[k + 1] (entry 0 = "")
   uint64_t o = 0;
   w.name_off[0] = 0;
-  for (size_t k = 1; k < table.size(); k++) {
-    std::memcpy(w.names + o, r.names + table[k].first, table[k].second);
-    o += table[k].second;
-    w.name_off[k] = uint32_t(o);
+  for (size_t k = 0; k < table.size(); k++) {
+    if (k) std::memcpy(w.names + o, r.names + table[k].first, table[k].second);
+    o += k ? table[k].second : 0;
+    w.name_off[k + 1] = uint32_t(o);
   }
   uint8_t *e = w.errors;
   for (uint64_t b = 0; b < r.nblocks; b++) {

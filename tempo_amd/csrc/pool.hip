@@ -48,6 +48,7 @@ struct PoolArgs {
   PoolBlk blk[kArgSegs];
   const DevBlockDesc *desc[kArgSegs];  // cold columns (ids, times, names) of matches
   uint32_t bms[kArgBms][8];
+  uint32_t ubase[kArgSegs + 1];  // first unit of each block, units at nsegs (static kernel's block walk)
   uint32_t nsegs, units, static_per_wg, dyn0;  // static run of workgroup w: [w*S, w*S+S); dynamic [dyn0, units)
   uint32_t chunk_shift, lookahead, rec_cap, seg_cap, has_min, has_max, min32, max32, start_s, end_s;
   unsigned *head;       // this launch's dynamic-chunk counter (zero at launch)
@@ -303,6 +304,193 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
 }
 
 // ------------------------------------------------------------------------------------
+// static search: the pool kernel's loads, predicates and record hand-off without its
+// machinery. One 1024-thread workgroup per CU; wave g of the launch owns the contiguous
+// unit run [g * U / NW, (g + 1) * U / NW) of the launch's unit space (NW waves, runs differ
+// by at most one unit), two units in flight. The block of a unit comes from the wave's own
+// walk over the kernel arguments' unit bases (scalar loads, once per block boundary), not
+// from LDS: the first loads are issued before anything is staged, and nothing is claimed.
+// (scan_probe.hip measured this shape at 27.0 us for 150 MB against 32.4 us for the pool
+// kernel with its LDS claims, staging and dynamic chunks.)
+template <int NT, bool DUR, bool RANGE, bool NTL>
+__global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs A) {
+  const unsigned long long t_start = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  __shared__ uint32_t s_bm[kArgBms * 8];
+  __shared__ uint32_t s_nrec;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long s_rec[];  // rec_cap x 6 words
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = blockIdx.x, nsegs = A.nsegs, units = A.units;
+  const uint32_t nwv = blockDim.x >> 6;
+  const uint32_t wave = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6));
+  const uint32_t NW = gridDim.x * nwv, gw = w * nwv + wave;
+  const uint32_t u_begin = uint32_t(uint64_t(units) * gw / NW), u_end = uint32_t(uint64_t(units) * (gw + 1) / NW);
+  // the wave's current block (all scalar)
+  uint32_t b = 0;
+  while (b + 1 < nsegs && u_begin >= A.ubase[b + 1]) b++;
+  struct Blk {
+    const uint32_t *scan;
+    const uint8_t *col[NT > 0 ? NT : 1];
+    uint32_t npad, nent, ub, ue, bmi4, nsets4, block_idx;
+  } B;
+  auto set_block = [&](uint32_t bb) {
+    const PoolBlk &P = A.blk[bb];
+    B.scan = P.scan;
+#pragma unroll
+    for (int q = 0; q < (NT > 0 ? NT : 1); q++)
+      if (NT > 0) B.col[q] = P.col[q];
+    B.npad = P.npad;
+    B.nent = P.nent;
+    B.ub = A.ubase[bb];
+    B.ue = A.ubase[bb + 1];
+    B.bmi4 = P.bmi4;
+    B.nsets4 = P.nsets4;
+    B.block_idx = P.block_idx;
+  };
+  set_block(b);
+  struct Regs {
+    u32x4 d[kSteps], s[kSteps], e[kSteps];
+    uint32_t tv[NT > 0 ? NT : 1][kSteps];
+    uint32_t e0;
+  };
+  auto load = [&](Regs &R, uint32_t u) {
+    if (u >= B.ue) {  // (runs are short and blocks long: at most a step or two)
+      while (b + 1 < nsegs && u >= A.ubase[b + 1]) b++;
+      set_block(b);
+    }
+    R.e0 = (u - B.ub) * kPoolTile;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) {
+      const uint64_t e = uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
+      if (DUR) R.d[k] = stream4<NTL>(B.scan, e);
+      if (RANGE) {
+        R.s[k] = stream4<NTL>(B.scan + B.npad, e);
+        R.e[k] = stream4<NTL>(B.scan + 2ull * B.npad, e);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
+      if (NT <= 0) break;
+#pragma unroll
+      for (int k = 0; k < kSteps; k++)
+        R.tv[q][k] = stream1<NTL>(B.col[q], uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
+    }
+  };
+  const uint32_t rec_cap = A.rec_cap;
+  // (evaluated right after the unit's load, while the block state still describes it)
+  auto eval = [&](const Regs &R, uint32_t bslot) {
+    const PoolBlk &P = A.blk[bslot];
+    const uint32_t n = P.nent, bmi4 = P.bmi4, ns4 = P.nsets4;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (R.e0 + uint32_t(k) * 256 + uint32_t(lane) * 4 + j < n) mask |= 1u << (4 * k + j);
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) {
+      const uint32_t dv[4] = {R.d[k].x, R.d[k].y, R.d[k].z, R.d[k].w};
+      const uint32_t sv[4] = {R.s[k].x, R.s[k].y, R.s[k].z, R.s[k].w};
+      const uint32_t ev[4] = {R.e[k].x, R.e[k].y, R.e[k].z, R.e[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        bool ok = true;
+        if (DUR) ok = (!A.has_min || dv[j] >= A.min32) && (!A.has_max || dv[j] <= A.max32);
+        if (RANGE) ok = ok && A.start_s <= ev[j] && A.end_s >= sv[j];
+#pragma unroll
+        for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
+          if (NT <= 0) break;
+          const uint32_t x = (R.tv[q][k] >> (8 * j)) & 0xffu;
+          const uint32_t wd = s_bm[((bmi4 >> (8 * q)) & 0xffu) * 8 + (x >> 5)];
+          ok = ok && (x < ((ns4 >> (8 * q)) & 0xffu)) && ((wd >> (x & 31)) & 1u);
+        }
+        if (!ok) mask &= ~(1u << (4 * k + j));
+      }
+    }
+    if (__ballot(mask != 0) == 0) return;
+    const DevBlockDesc *D = A.desc[bslot];
+    const auto *Dc = K4(D);
+    const uint8_t *ids = Dc->ids;
+    const uint64_t *st_ns = Dc->start_ns, *en_ns = Dc->end_ns;
+    const uint32_t *names = Dc->names;
+    const uint8_t *id_len = Dc->id_len;
+    const uint32_t bidx = P.block_idx;
+    const uint32_t cnt = __popc(mask);
+    uint32_t slot = 0;
+    if (cnt) slot = atomicAdd(&s_nrec, cnt);
+    for (int bit = 0; bit < 4 * kSteps; bit++) {
+      if (!(mask & (1u << bit))) continue;
+      const uint32_t r = slot++;
+      if (r >= rec_cap) continue;
+      const uint32_t ei = R.e0 + uint32_t(bit >> 2) * 256 + uint32_t(lane) * 4 + uint32_t(bit & 3);
+      const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
+      const uint64_t st = G(st_ns)[ei], en = G(en_ns)[ei];
+      const uint64_t nm = G(reinterpret_cast<const uint64_t *>(names))[ei];
+      const uint32_t il = G(id_len)[ei];
+      unsigned long long *d = s_rec + uint64_t(r) * 6;
+      d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
+      d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
+      d[2] = st;
+      d[3] = en;
+      d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
+      d[5] = nm;
+    }
+  };
+  // the first unit's loads go out before anything is staged
+  Regs ra, rb;
+  uint32_t u = u_begin, ba = b, bb = b;
+  if (u < u_end) {
+    load(ra, u);
+    ba = b;
+  }
+  if (tid < kArgBms * 8) s_bm[tid] = reinterpret_cast<const uint32_t *>(A.bms)[tid];
+  if (tid == 0) s_nrec = 0;
+  __syncthreads();
+  unsigned long long *const stamps = A.stamps;
+  if (stamps && tid == 0) {
+    stamps[uint64_t(w) * kStampSlots] = t_start;
+    stamps[uint64_t(w) * kStampSlots + 1] = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+    const unsigned long long xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+    stamps[uint64_t(w) * kStampSlots + 8] = (xcc << 32) | hw;
+  }
+  // two units in flight: ra (u), rb (u + 1)
+  while (u < u_end) {
+    const bool has_b = u + 1 < u_end;
+    if (has_b) {
+      load(rb, u + 1);
+      bb = b;
+    }
+    eval(ra, ba);
+    if (!has_b) break;
+    const bool has_a = u + 2 < u_end;
+    if (has_a) {
+      load(ra, u + 2);
+      ba = b;
+    }
+    eval(rb, bb);
+    u += 2;
+  }
+  __syncthreads();
+  if (stamps && tid == 0) {
+    stamps[uint64_t(w) * kStampSlots + 2] = __builtin_amdgcn_s_memrealtime();
+    stamps[uint64_t(w) * kStampSlots + 3] = __builtin_amdgcn_s_memrealtime();
+  }
+  // ---- records to the workgroup's host segment (write-through), then the count
+  const uint32_t total = s_nrec;
+  const uint32_t nw = min(total, min(rec_cap, A.seg_cap)) * 6;
+  if (nw) {
+    auto *dst = reinterpret_cast<unsigned long long *>(A.recs) + uint64_t(w) * A.seg_cap * 6;
+    for (uint32_t i = tid; i < nw; i += blockDim.x) host_store(dst + i, s_rec[i]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (tid == 0) {
+    host_store(A.counts + w, total);
+    if (stamps) stamps[uint64_t(w) * kStampSlots + 4] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // host
 using PoolFn = void (*)(PoolArgs);
 template <int NT, bool NTL>
@@ -324,6 +512,26 @@ static PoolFn pick_pool_t(uint32_t nterms, bool dur, bool range) {
 }
 static PoolFn pick_pool(uint32_t nterms, bool dur, bool range, bool ntl) {
   return ntl ? pick_pool_t<true>(nterms, dur, range) : pick_pool_t<false>(nterms, dur, range);
+}
+template <int NT, bool NTL>
+static PoolFn pick_static3(bool dur, bool range) {
+  if (dur && range) return search_static_kernel<NT, true, true, NTL>;
+  if (dur) return search_static_kernel<NT, true, false, NTL>;
+  if (range) return search_static_kernel<NT, false, true, NTL>;
+  return search_static_kernel<NT, false, false, NTL>;
+}
+template <bool NTL>
+static PoolFn pick_static_t(uint32_t nterms, bool dur, bool range) {
+  switch (nterms) {
+    case 0: return pick_static3<0, NTL>(dur, range);
+    case 1: return pick_static3<1, NTL>(dur, range);
+    case 2: return pick_static3<2, NTL>(dur, range);
+    case 3: return pick_static3<3, NTL>(dur, range);
+    default: return pick_static3<4, NTL>(dur, range);
+  }
+}
+static PoolFn pick_static(uint32_t nterms, bool dur, bool range, bool ntl) {
+  return ntl ? pick_static_t<true>(nterms, dur, range) : pick_static_t<false>(nterms, dur, range);
 }
 
 // One search_pool_kernel launch for a narrow search (every block scanned whole; a limit
@@ -354,10 +562,12 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     b.ubase = U;
     b.block_idx = segs[i].block_idx;
     PA.desc[i] = seg_desc[i];
+    PA.ubase[i] = U;
     const uint64_t u = (segs[i].n + kPoolTile - 1) / kPoolTile;
     if (uint64_t(U) + u >= (1ull << 31)) return false;
     U += uint32_t(u);
   }
+  PA.ubase[nsegs] = U;
   for (size_t j = 0; j < nbms.size(); j++)
     for (int x = 0; x < 8; x++) PA.bms[j][x] = nbms[j][size_t(x)];
   // static runs: (100 - dyn)% of the units split evenly; the rest in dynamic chunks
@@ -399,7 +609,8 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     HIP_OK(hipMemsetAsync(dc.stamps.p, 0, size_t(W) * kStampSlots * 8, s));
     PA.stamps = static_cast<unsigned long long *>(dc.stamps.p);
   }
-  const PoolFn fn = pick_pool(q.nterms, has_dur, q.has_range, dc.pool_nt);
+  const PoolFn fn = dc.pool_static ? pick_static(q.nterms, has_dur, q.has_range, dc.pool_nt)
+                                   : pick_pool(q.nterms, has_dur, q.has_range, dc.pool_nt);
   if (!dc.pool_attr.count(reinterpret_cast<const void *>(fn))) {
     HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                int(kPoolLds)));
@@ -430,7 +641,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     HIP_OK(hipGetLastError());
     if (first && (time_scan || defer)) HIP_OK(hipEventRecord(e1, s));
     if (first && time_all) HIP_OK(hipEventRecord(dc.ev1, s));
-    dc.pool_parity ^= 1u;
+    if (!dc.pool_static) dc.pool_parity ^= 1u;  // (the static kernel claims nothing)
   };
   // completion: every workgroup's count (stored after its records completed, read with
   // acquire loads); finished segments are pulled into this core's caches meanwhile; the

@@ -403,3 +403,29 @@ def test_block_clone(engine, tmp_path):
     assert (gmet.inspected_traces, gmet.inspected_bytes) == (emet.inspected_traces, emet.inspected_bytes)
     for c in clones:
         c.close()
+
+
+def test_header_min_dur_quirk_skips_block(engine, tmp_path):
+    """Pitfall P1 through a full search: SearchBlockHeaderMutable.AddEntry overwrites a zero
+    MinDur with the next entry's duration (pkg/tempofb/SearchBlockHeader_util.go:37-43), so
+    the stored MinDur (5 s) exceeds the block's true minimum (0). MatchesBlock compares the
+    stored value with MaxDurationMs (tempodb/search/pipeline.go:53-56): a MaxDuration query
+    skips the whole block although its zero-duration entry matches; the block without the
+    quirk is inspected. Both on the on-disk header, as the reference."""
+    t0 = 1_700_000_000 * 10**9
+    quirk = [{"id": ref_id(1), "start": t0, "end": t0, "tags": {"k": ["a"]}},            # dur 0 (AddEntry first)
+             {"id": ref_id(2), "start": t0, "end": t0 + 5 * 10**9, "tags": {"k": ["a"]}},  # 5 s: MinDur := 5 s
+             {"id": ref_id(3), "start": t0, "end": t0 + 6 * 10**9, "tags": {"k": ["a"]}}]
+    plain = [{"id": ref_id(4), "start": t0, "end": t0 + 10**6, "tags": {"k": ["a"]}},     # 1 ms
+             {"id": ref_id(5), "start": t0, "end": t0 + 5 * 10**9, "tags": {"k": ["a"]}}]
+    pq = write_block(str(tmp_path), "quirk", quirk)
+    pp = write_block(str(tmp_path), "plain", plain)
+    assert engine.open_block(pq).info()["min_dur_ns"] == 5 * 10**9  # the stored (overwritten) MinDur
+    got, met, exp, omet = both(engine, [pq, pp], tags={"k": "a"}, max_ms=1000)
+    assert met.skipped_blocks == 1 and met.inspected_blocks == 1
+    assert [(m.block_idx, m.trace_id) for m in got] == [(1, ref_id(4))]  # ref_id(1) (0 ns) is not found
+    assert_parity(got, met, exp, omet)
+    # without MaxDuration the quirk block is searched and its zero-duration entry matches
+    got, met, exp, omet = both(engine, [pq, pp], tags={"k": "a"})
+    assert met.skipped_blocks == 0 and ref_id(1) in [m.trace_id for m in got]
+    assert_parity(got, met, exp, omet)

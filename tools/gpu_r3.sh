@@ -1,0 +1,71 @@
+#!/bin/bash
+# Round-3 GPU-box session: stages chosen by $1 (comma list). Every GPU step runs under its
+# own timeout; the script stops at the first failure (no retries).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STAGES="${1:-merge,live,probe,bench}"
+has() { [[ ",$STAGES," == *",$1,"* ]]; }
+ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 0 pass, 1 test failures (no crash)
+
+if has merge; then  # CPU only (a fresh process, no device touched): the merge path's host cost
+  TSG_MERGE_BOUND_MS=100 timeout -k 10 300 python -u -m pytest tests/test_shard_gloo.py -x -v -s -p no:cacheprovider \
+    -k "million or native_merge or wire" > gpurun_out/merge_perf.log 2>&1
+  rc=$?; echo "merge perf rc=$rc"; grep -E "best|passed|failed" gpurun_out/merge_perf.log | tail -3
+  ok_rc $rc || exit $rc
+fi
+if has live; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_live.py tests/test_gpu_multiproc.py tests/test_gpu_proto.py \
+    tests/test_gpu_search.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_live.log 2>&1
+  rc=$?; echo "pytest live rc=$rc"; tail -15 gpurun_out/pytest_live.log
+  ok_rc $rc || exit $rc
+fi
+if has gputest; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest gpu rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
+  ok_rc $rc || exit $rc
+fi
+if has probe; then
+  hipcc -O3 --offload-arch=gfx950 tools/launch_probe.hip -o gpurun_out/launch_probe || exit 1
+  timeout -k 10 120 gpurun_out/launch_probe > gpurun_out/launch_probe.json 2>&1
+  rc=$?; echo "probe rc=$rc"; cat gpurun_out/launch_probe.json
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has stamps; then
+  TSG_STAMPS=1 timeout -k 10 600 python bench.py --steps 6 --warmup 2 --cpu-baseline 0 --cfg3 0 --concurrent-steps 0 \
+    --mall-steps 0 ${BENCH_ARGS:-} > gpurun_out/stamps.json 2> gpurun_out/stamps.err
+  rc=$?; echo "stamps rc=$rc"; grep "stamps" gpurun_out/stamps.err | tail -6
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has quick; then
+  timeout -k 10 600 python bench.py --steps 200 --cpu-baseline 0 --cfg3 0 --concurrent-steps 0 ${BENCH_ARGS:-} \
+    > gpurun_out/quick.json 2> gpurun_out/quick.err
+  rc=$?; echo "quick rc=$rc"; tail -2 gpurun_out/quick.err; cat gpurun_out/quick.json
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has bench; then
+  timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
+  rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.err; cat gpurun_out/bench.json
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has prof; then
+  export TMPDIR=/tmp
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+    python3 bench.py --steps 40 --warmup 3 --cpu-baseline 0 --limit-steps 0 --cfg3 0 --concurrent-steps 0 \
+    --mall-steps 0 ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
+  rc=$?; echo "rocprof rc=$rc"; cat gpurun_out/prof/run_kernel_stats.csv
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has pmc; then
+  export TMPDIR=/tmp
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 -s KILL 600 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv -- \
+      python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 --limit-steps 0 --cfg3 0 --concurrent-steps 0 \
+      --mall-steps 0 ${BENCH_ARGS:-} > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err
+    rc=$?; echo "pmc $c rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+  done
+  python3 tools/pmc_summary.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE --out gpurun_out/pmc_traffic.json \
+    --workload "${PMC_WORKLOAD:-blocks=10,entries=1000000,sets=4}" --source "${PMC_SOURCE:-tools/gpu_r3.sh pmc}" | tee gpurun_out/pmc_summary.txt
+fi
+exit 0
