@@ -939,43 +939,140 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         live_recs.push_back(x);
       }
     };
-    // Early exit (limit > 0): the consumer stops at the L-th distinct
-    // id in block order, so the blocks behind that point are never needed. A first wave
-    // searches the leading blocks (>= 1/8 of the entries); only if the consumer has not
-    // stopped inside them does a second wave search the rest. Each block's matches do
-    // not depend on which other blocks share its launch, so the result is the one-wave
-    // result. limit 0, or a single block: one wave.
-    size_t b1 = nblocks;
-    if (limit && nblocks > 1) {
-      uint64_t total = 0, acc = 0;
-      for (size_t i = 0; i < nblocks; i++)
-        if (state[i] == 2) total += blocks[i]->b.host->n;
-      b1 = 0;
-      while (b1 < nblocks && (acc * 8 < total || acc == 0)) {
-        if (state[b1] == 2) acc += blocks[b1]->b.host->n;
-        b1++;
-      }
-    }
-    search_range(0, b1);
-    check_cancel();
-    if (b1 < nblocks) {
-      std::unordered_set<std::string> seen;
-      bool stop = false;
-      for (size_t i = 0; i < b1 && !stop; i++) {
-        if (state[i] == 2 && blocks[i]->b.host->live) {
-          combine_live(i);
-          for (size_t ri = 0; ri < live_recs.size() && !stop; ri++) {
-            seen.insert(std::string(reinterpret_cast<const char *>(live_recs[ri].id), 16));
-            stop = seen.size() >= limit;
+    // Early exit (limit > 0): the consumer stops at the L-th distinct id in
+    // block order, so nothing behind that point is needed. The blocks' entries form one
+    // sequence (blocks in caller order, scan order inside); progressive waves search its next
+    // stretch — the first TSG_LIMIT_WAVE0 entries (2^21: one 512-entry unit per wave of the
+    // chip), then a stretch sized by the selectivity seen so far (x1.5 the entries the missing
+    // ids need at that rate, at least 4x the last wave) — cutting blocks on unit boundaries,
+    // until the consumer stops inside what has been searched. A block's records over its
+    // parts are its records in scan order, so the result is the one-wave result. Live blocks
+    // are never cut (a trace's segments combine), and once a search leaves the pool kernels
+    // (which take the cut ranges on the device) the waves cut at block boundaries only.
+    static const uint64_t kWave0 = [] {
+      const char *e = std::getenv("TSG_LIMIT_WAVE0");
+      return e ? std::max<uint64_t>(512, uint64_t(std::atoll(e))) : uint64_t(1) << 21;
+    }();
+    if (limit && !any_live) {
+      thread_local std::vector<std::vector<SearchOut::Rec>> acc;  // per block: its records so far
+      if (acc.size() < nblocks) acc.resize(nblocks);
+      for (size_t i = 0; i < nblocks; i++) acc[i].clear();
+      std::unordered_set<std::string> distinct_w;
+      bool stop = false, cut_ok = true;
+      size_t cb = 0;     // cursor: next block ...
+      uint64_t ce = 0;   // ... and its next scan position
+      uint64_t wave = kWave0, scanned = 0, matched = 0;
+      thread_local std::deque<SearchOut> wouts;
+      while (!stop) {
+        while (cb < nblocks && (state[cb] != 2 || !blocks[cb]->b.dc || ce >= blocks[cb]->b.host->n)) {
+          cb++;
+          ce = 0;
+        }
+        if (cb >= nblocks) break;
+        check_cancel();
+        // this wave's parts, grouped per device (first-seen device order)
+        std::vector<DeviceCtx *> devs;
+        std::vector<std::vector<std::pair<uint32_t, Block *>>> lists;
+        std::vector<EntryRanges> rngs;
+        std::vector<std::pair<size_t, uint64_t>> order;  // (block, end) of the parts in sequence order
+        uint64_t want = wave;
+        while (want > 0 && cb < nblocks) {
+          if (state[cb] != 2 || !blocks[cb]->b.dc) {
+            cb++;
+            ce = 0;
+            continue;
           }
-          continue;
+          const uint64_t n = blocks[cb]->b.host->n;
+          uint64_t e1 = n;
+          if (cut_ok && n - ce > want) e1 = std::min(n, (ce + want + 511) / 512 * 512);
+          DeviceCtx *dc = blocks[cb]->b.dc;
+          size_t d = 0;
+          while (d < devs.size() && devs[d] != dc) d++;
+          if (d == devs.size()) {
+            devs.push_back(dc);
+            lists.emplace_back();
+            rngs.emplace_back();
+          }
+          lists[d].push_back({uint32_t(cb), &blocks[cb]->b});
+          rngs[d].push_back({ce, e1});
+          order.push_back({cb, e1});
+          want -= std::min(want, e1 - ce);
+          scanned += e1 - ce;
+          if (e1 >= n) {
+            cb++;
+            ce = 0;
+          } else {
+            ce = e1;
+          }
         }
-        for (size_t ri = 0; ri < per_block[i].second && !stop; ri++) {
-          seen.insert(std::string(reinterpret_cast<const char *>(per_block[i].first[ri].id), 16));
-          stop = seen.size() >= limit;
+        while (wouts.size() < devs.size()) wouts.emplace_back();
+        std::vector<uint8_t> used_pool(devs.size(), 0);
+        ctx->fan_out(devs.size(), [&](size_t i) { return devs[i]; },
+                     [&](size_t i) {
+                       SearchOut &o = wouts[i];
+                       o.recs.clear();
+                       // (a part list longer than one launch's 32 blocks: whole blocks by chunks)
+                       const size_t nl = lists[i].size(), step = kChunk ? kChunk : nl;
+                       for (size_t c0 = 0; c0 < nl; c0 += step) {
+                         const size_t c1 = std::min(nl, c0 + step);
+                         const std::vector<std::pair<uint32_t, Block *>> part(lists[i].begin() + c0,
+                                                                              lists[i].begin() + c1);
+                         const EntryRanges pr(rngs[i].begin() + c0, rngs[i].begin() + c1);
+                         SearchOut more;
+                         device_search(*devs[i], part, *q, 0, flags, more, &pr);
+                         o.recs.insert(o.recs.end(), more.recs.begin(), more.recs.end());
+                         o.device_bytes += more.device_bytes;
+                         o.kernel_ns += more.kernel_ns;
+                         o.scan_ns += more.scan_ns;
+                         o.scan_bytes += more.scan_bytes;
+                         o.reruns += more.reruns;
+                         used_pool[i] = used_pool[i] || more.pool;
+                       }
+                     });
+        uint64_t wk = 0, ws = 0;
+        for (size_t i = 0; i < devs.size(); i++) {
+          SearchOut &o = wouts[i];
+          m.device_bytes_read += o.device_bytes;
+          m.scan_bytes += o.scan_bytes;
+          m.reruns += o.reruns;
+          wk = std::max<uint64_t>(wk, o.kernel_ns);
+          ws = std::max<uint64_t>(ws, o.scan_ns);
+          for (const auto &r : o.recs) acc[r.block_il & 0xffffffu].push_back(r);
+          o.device_bytes = o.kernel_ns = o.scan_ns = o.scan_bytes = 0;
+          o.reruns = 0;
+          if (!used_pool[i]) cut_ok = false;  // (the other paths scan a block from 0: cut at block ends)
         }
+        m.kernel_ns += wk;
+        m.scan_kernel_ns += ws;
+        // the consumer over the stretch just searched (its parts in sequence order)
+        for (size_t k = 0; k < order.size() && !stop; k++) {
+          const size_t bi = order[k].first;
+          const auto &v = acc[bi];
+          for (size_t ri = 0; ri < v.size() && !stop; ri++) {
+            if (v[ri].entry >= order[k].second) break;
+            if (distinct_w.insert(std::string(reinterpret_cast<const char *>(v[ri].id), 16)).second &&
+                distinct_w.size() >= limit)
+              stop = true;
+          }
+        }
+        if (stop) break;
+        // (records of a block over its parts: the check above re-walks a block's earlier
+        // parts; distinct ids are a set, so only new ones count)
+        matched = distinct_w.size();
+        const uint64_t need = limit - matched;
+        uint64_t next = 4 * wave;
+        if (matched > 0) {
+          const double est = double(need) * double(scanned) / double(matched) * 1.5;
+          next = std::max<uint64_t>(next, uint64_t(std::min(est, 1e18)));
+        }
+        wave = next;
       }
-      if (!stop) search_range(b1, nblocks);
+      for (size_t i = 0; i < nblocks; i++) {
+        per_block[i] = {acc[i].data(), acc[i].size()};
+        nrec += acc[i].size();
+      }
+    } else {
+      search_range(0, nblocks);
       check_cancel();
     }
     const clk::time_point t_dev = trace ? clk::now() : clk::time_point();

@@ -132,12 +132,16 @@ struct SearchOut {
   uint64_t device_bytes = 0, kernel_ns = 0;
   uint64_t scan_ns = 0, scan_bytes = 0;
   uint32_t reruns = 0;  // extra launches after a record overflow (timed into scan_ns / kernel_ns when timing)
+  bool pool = false;    // served by the pool kernels (they search entry ranges on the device)
 };
 // Runs the device pipeline for a set of (block index, block) pairs that share
 // one device. limit 0 = every match; limit L = each block's first L matches.
 int device_numa_node(const DeviceCtx &dc);
+// ranges (optional, one per entry of `blocks`): search only scan positions [first, second)
+// of that block (a limit query's progressive waves, tsg_search); records outside are dropped.
+using EntryRanges = std::vector<std::pair<uint64_t, uint64_t>>;
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
-                   uint32_t limit, uint32_t flags, SearchOut &out);
+                   uint32_t limit, uint32_t flags, SearchOut &out, const EntryRanges *ranges = nullptr);
 
 // ---- v2 lookup ---------------------------------------------------------------------
 struct V2Block {

@@ -49,6 +49,7 @@ struct PoolArgs {
   const DevBlockDesc *desc[kArgSegs];  // cold columns (ids, times, names) of matches
   uint32_t bms[kArgBms][8];
   uint32_t ubase[kArgSegs + 1];  // first unit of each block, units at nsegs (static kernel's block walk)
+  uint32_t ebase[kArgSegs];      // scan position of each block's first unit (a limit wave's part of a block)
   uint32_t nsegs, units, static_per_wg, dyn0;  // static run of workgroup w: [w*S, w*S+S); dynamic [dyn0, units)
   uint32_t chunk_shift, lookahead, rec_cap, seg_cap, has_min, has_max, min32, max32, start_s, end_s;
   unsigned *head;       // this launch's dynamic-chunk counter (zero at launch)
@@ -186,7 +187,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     const PoolBlk &B = s_blk[b];
     const uint32_t npad = __builtin_amdgcn_readfirstlane(B.npad);
     const uint32_t *scan = uniform_ptr(B.scan);
-    R.e0 = (u - __builtin_amdgcn_readfirstlane(B.ubase)) * kPoolTile;
+    R.e0 = uint32_t(__builtin_amdgcn_readfirstlane(A.ebase[b])) + (u - __builtin_amdgcn_readfirstlane(B.ubase)) * kPoolTile;
 #pragma unroll
     for (int k = 0; k < kSteps; k++) {
       const uint64_t e = uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
@@ -330,7 +331,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
   struct Blk {
     const uint32_t *scan;
     const uint8_t *col[NT > 0 ? NT : 1];
-    uint32_t npad, nent, ub, ue, bmi4, nsets4, block_idx;
+    uint32_t npad, nent, ub, ue, eb, bmi4, nsets4, block_idx;
   } B;
   auto set_block = [&](uint32_t bb) {
     const PoolBlk &P = A.blk[bb];
@@ -342,6 +343,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
     B.nent = P.nent;
     B.ub = A.ubase[bb];
     B.ue = A.ubase[bb + 1];
+    B.eb = A.ebase[bb];
     B.bmi4 = P.bmi4;
     B.nsets4 = P.nsets4;
     B.block_idx = P.block_idx;
@@ -357,7 +359,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
       while (b + 1 < nsegs && u >= A.ubase[b + 1]) b++;
       set_block(b);
     }
-    R.e0 = (u - B.ub) * kPoolTile;
+    R.e0 = B.eb + (u - B.ub) * kPoolTile;
 #pragma unroll
     for (int k = 0; k < kSteps; k++) {
       const uint64_t e = uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
@@ -563,7 +565,8 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     b.block_idx = segs[i].block_idx;
     PA.desc[i] = seg_desc[i];
     PA.ubase[i] = U;
-    const uint64_t u = (segs[i].n + kPoolTile - 1) / kPoolTile;
+    PA.ebase[i] = uint32_t(segs[i].e0);  // (a multiple of kPoolTile)
+    const uint64_t u = (segs[i].n - segs[i].e0 + kPoolTile - 1) / kPoolTile;
     if (uint64_t(U) + u >= (1ull << 31)) return false;
     U += uint32_t(u);
   }
@@ -769,7 +772,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       const uint32_t bi = r.block_il & 0xffffffu;
       const uint32_t ps = bi <= max_idx ? pos[bi] : 0;
       per[ps]++;
-      const uint64_t at = uint64_t(PA.blk[ps].ubase) * kPoolTile + r.entry;
+      const uint64_t at = uint64_t(PA.blk[ps].ubase) * kPoolTile + (r.entry - PA.ebase[ps]);
       keys[nrec++] = (at << 20) | slot;
     }
   uint32_t lb = 6;

@@ -1373,8 +1373,29 @@ void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast) {
 
 
 
+// A limit wave's part of a block: the records of scan positions outside its range (paths that
+// scan the block from position 0 or to its end) are dropped; the others keep their order.
+static void drop_before_ranges(const std::vector<std::pair<uint32_t, Block *>> &blocks, const EntryRanges &ranges,
+                               SearchOut &out) {
+  thread_local std::vector<uint64_t> lo, hi;
+  uint32_t mx = 0;
+  for (const auto &bp : blocks) mx = std::max(mx, bp.first);
+  lo.assign(size_t(mx) + 1, 0);
+  hi.assign(size_t(mx) + 1, UINT64_MAX);
+  for (size_t i = 0; i < blocks.size(); i++) {
+    lo[blocks[i].first] = ranges[i].first;
+    hi[blocks[i].first] = ranges[i].second;
+  }
+  size_t k = 0;
+  for (size_t r = 0; r < out.recs.size(); r++) {
+    const uint32_t bi = out.recs[r].block_il & 0xffffffu;
+    if (out.recs[r].entry >= lo[bi] && out.recs[r].entry < hi[bi]) out.recs[k++] = out.recs[r];
+  }
+  out.recs.resize(k);
+}
+
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
-                   uint32_t limit, uint32_t flags, SearchOut &out) {
+                   uint32_t limit, uint32_t flags, SearchOut &out, const EntryRanges *ranges) {
   Tracer tr;
   std::lock_guard<std::mutex> lk(dc.mu);
   HIP_OK(hipSetDevice(dc.ordinal));
@@ -1432,10 +1453,19 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   nsegv.clear();
   bool all_narrow = q.nterms <= uint32_t(kArgTerms);
   uint32_t fast_stage = 0, fast_bm = 0, fast_bm8 = 0, fast_vbits = 0, fast_words = 1, fast_self = 0;
-  for (auto &bp : blocks) {
+  for (size_t bi_ = 0; bi_ < blocks.size(); bi_++) {
+    const auto &bp = blocks[bi_];
     Block &b = *bp.second;
     const DevBlock &d = b.dev;
-    if (d.n == 0 || q.exhaustive) continue;
+    // the scanned range [e0, e1): a whole block, or a limit wave's part of it (e0 on a
+    // 512-entry boundary: the pool kernels' unit; other paths scan from 0 and the records
+    // before e0 are dropped below)
+    uint64_t e0 = 0, e1 = d.n;
+    if (ranges) {
+      e1 = std::min<uint64_t>((*ranges)[bi_].second, d.n);
+      e0 = std::min<uint64_t>((*ranges)[bi_].first, e1) / 512 * 512;
+    }
+    if (e1 <= e0 || q.exhaustive) continue;
     auto &kidx = ps.kidx;
     kidx.assign(q.nterms, 0);
     bool dead = false;  // a key absent from the block: FindTag fails for every entry
@@ -1447,7 +1477,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     }
     if (dead) continue;
     ScanSeg sg{};
-    sg.n = d.n;
+    sg.n = e1;
+    sg.e0 = e0;
     sg.dur32 = d.dur32;
     sg.dur64 = d.dur64;
     sg.start_s = d.start_s;
@@ -1544,11 +1575,11 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       fast_bm8 = std::max(fast_bm8, bmw8);
       fast_self = std::max(fast_self, std::min(selfw, 0xfffffffu));
     }
-    sg.nunits = uint32_t((d.n + kUnit - 1) / kUnit);
+    sg.nunits = uint32_t((e1 + kUnit - 1) / kUnit);
     units += sg.nunits;
-    sg.cap = limit ? std::min<uint64_t>(limit, d.n) : d.n;
-    scan_bytes += d.n * per;
-    n_all += d.n;
+    sg.cap = limit ? std::min<uint64_t>(limit, e1) : e1;
+    scan_bytes += (e1 - e0) * per;
+    n_all += e1;
     segs.push_back(sg);
   }
   out.recs.clear();
@@ -1556,6 +1587,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   out.device_bytes = scan_bytes + dict_bytes;
   out.kernel_ns = out.scan_ns = 0;
   out.reruns = 0;
+  out.pool = false;
   out.scan_bytes = scan_bytes;
   if (segs.empty()) return;
   if (segs.size() > kMaxSegs) fail(TSG_E_UNSUPPORTED, "too many blocks per device in one search (max 2048)");
@@ -1623,7 +1655,11 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // segment / look-back paths below when a workgroup's matches overflow its LDS buffer
   if (fast && narrow && !dc.seg_off && !dc.pool_off) {
     if (dc.pool_skip) dc.pool_skip--;
-    else if (pool_search(dc, blocks, q, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out)) return;
+    else if (pool_search(dc, blocks, q, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out)) {
+      if (ranges) drop_before_ranges(blocks, *ranges, out);
+      out.pool = true;
+      return;
+    }
   }
   const FastFn fast_seg = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, true) : nullptr;
   const FastFn fast_lb = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, false) : nullptr;
@@ -2104,6 +2140,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     }
     out.scan_bytes += uint64_t(nwg) * 8 + nrec * 32;  // + published counts, + id/start/end of each record
   }
+  if (ranges) drop_before_ranges(blocks, *ranges, out);
   tr.mark("post");
 }
 

@@ -28,6 +28,7 @@ struct ScanSeg {
   uint32_t term0, nterms, lds_words;
   uint32_t block_idx, steal_base;  // claim counter value at launch start (tail tiles)
   uint64_t cap;  // limit mode: records kept from this block
+  uint64_t e0;   // first scan position searched (a multiple of the pool unit; 0 = the whole block up to n)
 };
 
 struct MatchRec {  // == SearchOut::Rec
