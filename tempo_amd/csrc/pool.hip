@@ -705,7 +705,9 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   // double each time, at most up to the LDS buffer), or leave for the other paths.
   uint32_t reruns = 0;
   float rerun_ms = 0;
-  if (maxc > PA.seg_cap) {
+  // (a workgroup keeps at most min(seg_cap, rec_cap) records: its LDS buffer can be the
+  // smaller one, TSG_POOL_REC)
+  if (maxc > std::min(PA.seg_cap, rec_cap)) {
     for (;;) {
       if (maxc > rec_cap) {  // dense: this query (and the next few) take the other paths
         dc.pool_skip = 16;

@@ -100,6 +100,47 @@ __device__ __forceinline__ uint32_t eval_unit(const Regs &R, const Args &A, cons
   return mask;
 }
 
+struct BigArgs {  // the pool kernel's argument size (~3.7 KB)
+  Args a;
+  uint32_t ubase[kBlocks + 1];
+  uint32_t pad[800];
+  unsigned *hcount;  // pinned host memory
+};
+
+template <bool NT, bool HOSTCOUNT, bool WALK>
+__global__ void __launch_bounds__(1024, 1) static_big(BigArgs BA) {
+  const Args &A = BA.a;
+  __shared__ uint32_t bm[24];
+  if (threadIdx.x < 24) bm[threadIdx.x] = A.bm[threadIdx.x / 8][threadIdx.x % 8];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t units = kBlocks * kUnitsPerBlock;
+  const uint32_t waves = gridDim.x * 16, gw = blockIdx.x * 16 + wave;
+  const uint32_t u0 = uint32_t(uint64_t(units) * gw / waves), u1 = uint32_t(uint64_t(units) * (gw + 1) / waves);
+  uint32_t cnt = 0;
+  if (WALK) {  // the static kernel's walk over the unit bases (scalar loads of the arguments)
+    uint32_t b = 0;
+    while (b + 1 < kBlocks && u0 >= BA.ubase[b + 1]) b++;
+    cnt += b == 0xffffu;
+  }
+  Regs ra, rb;
+  uint32_t u = u0;
+  if (u < u1) load_unit<NT>(ra, A, u, lane);
+  for (; u < u1; u += 2) {
+    if (u + 1 < u1) load_unit<NT>(rb, A, u + 1, lane);
+    cnt += __popc(eval_unit(ra, A, bm));
+    if (u + 2 < u1) load_unit<NT>(ra, A, u + 2, lane);
+    if (u + 1 < u1) cnt += __popc(eval_unit(rb, A, bm));
+  }
+  if (cnt) atomicAdd(A.sink, cnt);
+  if (HOSTCOUNT) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(BA.hcount + blockIdx.x, cnt + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <bool NT>
 __global__ void __launch_bounds__(1024, 1) static1024(Args A) {
   __shared__ uint32_t bm[24];
@@ -195,18 +236,31 @@ int main() {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   const uint32_t units = kBlocks * kUnitsPerBlock;
-  auto run = [&](const char *name, const void *f, unsigned grid, unsigned threads) {
+  unsigned *hcount;
+  CK(hipHostMalloc(&hcount, 4096, hipHostMallocMapped | hipHostMallocCoherent));
+  std::vector<BigArgs> big(4);
+  for (int i = 0; i < 4; i++) {
+    big[i].a = sets[i];
+    for (int b = 0; b <= kBlocks; b++) big[i].ubase[b] = b * kUnitsPerBlock;
+    big[i].hcount = hcount;
+  }
+  auto run = [&](const char *name, const void *f, unsigned grid, unsigned threads, bool bigargs = false,
+                 size_t lds = 0, int nsets = 4) {
     Stat ev, ext;
+    if (lds) CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
     for (int mode = 0; mode < 2; mode++)
       for (int r = 0; r < 64; r++) {
-        Args &A = sets[r % 4];
-        void *args[] = {&A};
+        Args &A = sets[r % nsets];
+        BigArgs &BA = big[r % nsets];
+        void *args1[] = {&A};
+        void *args2[] = {&BA};
+        void **args = bigargs ? args2 : args1;
         if (mode == 0) {
           CK(hipEventRecord(a, s));
-          CK(hipExtLaunchKernel(f, dim3(grid), dim3(threads), args, 0, s, nullptr, nullptr, 0));
+          CK(hipExtLaunchKernel(f, dim3(grid), dim3(threads), args, lds, s, nullptr, nullptr, 0));
           CK(hipEventRecord(b, s));
         } else {
-          CK(hipExtLaunchKernel(f, dim3(grid), dim3(threads), args, 0, s, a, b, 0));
+          CK(hipExtLaunchKernel(f, dim3(grid), dim3(threads), args, lds, s, a, b, 0));
         }
         CK(hipEventSynchronize(b));
         float ms;
@@ -217,9 +271,13 @@ int main() {
     ext.print(name, "ext_events", bytes);
   };
   run("static1024_nt", reinterpret_cast<const void *>(static1024<true>), cu, 1024);
-  run("static1024", reinterpret_cast<const void *>(static1024<false>), cu, 1024);
+  run("static1024_nt_mall", reinterpret_cast<const void *>(static1024<true>), cu, 1024, false, 0, 1);
+  run("big_nt", reinterpret_cast<const void *>(static_big<true, false, false>), cu, 1024, true);
+  run("big_nt_lds96k", reinterpret_cast<const void *>(static_big<true, false, false>), cu, 1024, true, 96 << 10);
+  run("big_nt_hostcount", reinterpret_cast<const void *>(static_big<true, true, false>), cu, 1024, true);
+  run("big_nt_walk", reinterpret_cast<const void *>(static_big<true, false, true>), cu, 1024, true);
+  run("big_nt_all", reinterpret_cast<const void *>(static_big<true, true, true>), cu, 1024, true, 96 << 10);
+  run("big_nt_all_mall", reinterpret_cast<const void *>(static_big<true, true, true>), cu, 1024, true, 96 << 10, 1);
   run("grid256_nt", reinterpret_cast<const void *>(grid256<true, 1>), (units + 3) / 4, 256);
-  run("grid256", reinterpret_cast<const void *>(grid256<false, 1>), (units + 3) / 4, 256);
-  run("grid256x2_nt", reinterpret_cast<const void *>(grid256<true, 2>), (units + 7) / 8, 256);
   return 0;
 }
