@@ -170,6 +170,8 @@ def parse():
                          "stream, pinned output and resident copy of the set) driven by as many host threads")
     ap.add_argument("--concurrent-steps", type=int, default=64,
                     help="queries per stream in the concurrent leg (0 = skip)")
+    ap.add_argument("--shim-steps", type=int, default=200,
+                    help="queries in the shim-pattern leg (one C thread per block, a tsg_search each; 0 = off)")
     ap.add_argument("--merge-steps", type=int, default=20,
                     help="N > 1: distributed full-scan queries with the frontend merge on rank 0 (0 = off)")
     ap.add_argument("--cfg3-blocks", type=int, default=25)
@@ -344,6 +346,36 @@ def concurrent_leg(args, base, pipe, streams, entries, dist, world, local):
             "entries_per_s": entries * n * streams * world / elapsed,
             "queries_per_s": n * streams * world / elapsed,
             "note": "one resident copy of the config-2 set per stream; full scans, same query as the main line"}
+
+
+def shim_leg(args, eng, sets, pipe, entries, nmatch, batched, dist):
+    """The Go shim's call pattern for the ingester: searchLocalBlocks starts a goroutine
+    per block and each calls Search on its own (instance_search.go:164-185), so the shim
+    makes one limit-0 tsg_search per block. Driven from C threads (libtsg_shim_pattern.so:
+    no GIL between calls, as goroutines have none), one per block of the set, each query
+    over the next resident copy like the main line; libtsg coalesces the concurrent calls
+    into one launch per batch (capi.cpp coalesced_search). Reported beside the batched main
+    line (one tsg_search over all blocks)."""
+    # (the spinning caller threads get the GPU node's CPUs, not the main line's 8)
+    mask = os.sched_getaffinity(0)
+    node = eng.numa_node(0)
+    cpus = node_cpus(node) & os.sched_getaffinity(0) if node >= 0 else set()
+    try:
+        if cpus and len(cpus) > len(mask):
+            os.sched_setaffinity(0, cpus)
+        eng.shim_pattern(sets, pipe, 16)  # warm (threads, per-thread scratch, pinned buffers)
+        if dist:
+            dist.barrier()
+        ns, nm = eng.shim_pattern(sets, pipe, args.shim_steps)
+    finally:
+        os.sched_setaffinity(0, mask)
+    assert all(x == nmatch for x in nm), "shim-pattern record count differs from the batched search"
+    rate = entries * len(ns) / (sum(ns) / 1e9)
+    return {"threads": len(sets[0]), "queries": len(ns), "entries_per_s": rate,
+            "vs_batched": rate / batched if batched else None,
+            "query_us": pct([x / 1e3 for x in ns]),
+            "note": "one C thread per block, each a tsg_search over its block (limit 0), per query; "
+                    "concurrent calls coalesced into one launch; per-GPU rate"}
 
 
 def cfg3_path(workdir, rank):
@@ -646,6 +678,9 @@ def main():
         out["limit20"] = {"steps": args.limit_steps, "matches": nl, "traces_inspected": metl.inspected_traces,
                           "step_us": pct([x * 1e6 for x in ls]), "kernel_us": pct([x / 1e3 for x in lk]),
                           "entries_per_s": entries / (sum(ls) / len(ls))}
+
+    if args.shim_steps:
+        out["shim"] = shim_leg(args, eng, sets, pipe, entries, len(got), value / max(1, world), dist)
 
     if args.concurrent_steps and streams > 1:
         out["concurrent"] = concurrent_leg(args, base, pipe, streams, entries, dist, world, local)

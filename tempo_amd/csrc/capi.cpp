@@ -178,6 +178,45 @@ struct tsg_ctx {
       }
     }
   }
+  // Coalescer (group commit) for concurrent searches on one device. The ingester's
+  // searchLocalBlocks starts a goroutine per block and each calls Search on its own
+  // (modules/ingester/instance_search.go:164-185), so the shim makes one tsg_search per
+  // block. A call whose device part is one launch queues it on the device; one queued
+  // caller (the leader) waits a short window for callers still filtering headers, then runs
+  // every queued part with an equal query as ONE launch and hands each caller the records
+  // of its own blocks. A lone caller runs at once (nobody is approaching).
+  struct CoalReq {
+    const std::vector<std::pair<uint32_t, tsg::Block *>> *list;
+    const tsg_query *q;
+    uint32_t limit, flags;
+    tsg::SearchOut *out;
+    std::atomic<bool> done{false};
+    std::exception_ptr err;
+  };
+  struct Coalescer {
+    std::mutex m;
+    std::vector<CoalReq *> pending;
+    std::atomic<bool> busy{false};
+  };
+  std::mutex comu;
+  std::unordered_map<const void *, std::unique_ptr<Coalescer>> coal;  // per DeviceCtx
+  std::atomic<int> approaching{0};  // searches that have not reached their device stage yet
+  Coalescer &coalescer(const void *dc) {
+    std::lock_guard<std::mutex> lk(comu);
+    auto &c = coal[dc];
+    if (!c) c = std::make_unique<Coalescer>();
+    return *c;
+  }
+};
+// A search on its way to the device stage (tsg_ctx::approaching), until leave().
+struct Approach {
+  std::atomic<int> *cnt;
+  std::atomic<bool> left{false};
+  explicit Approach(std::atomic<int> *c) : cnt(c) { cnt->fetch_add(1, std::memory_order_acq_rel); }
+  void leave() {
+    if (!left.exchange(true, std::memory_order_acq_rel)) cnt->fetch_sub(1, std::memory_order_acq_rel);
+  }
+  ~Approach() { leave(); }
 };
 struct tsg_block {
   tsg::Block b;
@@ -756,6 +795,151 @@ int tsg_search_tag_values(tsg_block *const *blocks, size_t nblocks, const uint8_
   });
 }
 
+static bool same_query(const tsg_query &a, const tsg_query &b) {
+  if (&a == &b) return true;
+  if (a.nterms != b.nterms || a.has_min != b.has_min || a.has_max != b.has_max || a.has_range != b.has_range ||
+      a.exhaustive != b.exhaustive || a.min_ns != b.min_ns || a.max_ns != b.max_ns || a.start_s != b.start_s ||
+      a.end_s != b.end_s)
+    return false;
+  for (uint32_t t = 0; t < a.nterms; t++)
+    if (a.key_lens[t] != b.key_lens[t] || a.value_lens[t] != b.value_lens[t] ||
+        std::memcmp(a.keys[t], b.keys[t], a.key_lens[t]) != 0 ||
+        std::memcmp(a.values[t], b.values[t], a.value_lens[t]) != 0)
+      return false;
+  return true;
+}
+
+// device_search through the device's coalescer (tsg_ctx::Coalescer). TSG_COALESCE=0 turns
+// it off; TSG_COALESCE_US (default 30) bounds the leader's wait for approaching callers.
+static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std::pair<uint32_t, Block *>> &list,
+                             const tsg_query &q, uint32_t limit, uint32_t flags, SearchOut &out, Approach &ap) {
+  static const bool on = [] {
+    const char *e = std::getenv("TSG_COALESCE");
+    return !e || std::atoi(e) != 0;
+  }();
+  static const uint64_t window_ns = [] {
+    const char *e = std::getenv("TSG_COALESCE_US");
+    return uint64_t(e ? std::max(0, std::atoi(e)) : 30) * 1000ull;
+  }();
+  constexpr size_t kBatchBlocks = 32;  // one launch's kernel-argument capacity
+  if (!on) {
+    ap.leave();
+    device_search(*dc, list, q, limit, flags, out);
+    return;
+  }
+  tsg_ctx::Coalescer &c = ctx->coalescer(dc);
+  tsg_ctx::CoalReq r;
+  r.list = &list;
+  r.q = &q;
+  r.limit = limit;
+  r.flags = flags;
+  r.out = &out;
+  {
+    std::lock_guard<std::mutex> lk(c.m);
+    c.pending.push_back(&r);
+  }
+  ap.leave();
+  for (uint32_t spins = 0; !r.done.load(std::memory_order_acquire); spins++) {
+    bool expect = false;
+    if (!c.busy.compare_exchange_strong(expect, true, std::memory_order_acq_rel)) {
+      if (spins < 4096) __builtin_ia32_pause();
+      else std::this_thread::yield();
+      continue;
+    }
+    if (r.done.load(std::memory_order_acquire)) {  // served while we took the lead
+      c.busy.store(false, std::memory_order_release);
+      break;
+    }
+    // leader: give callers still on their way a moment to queue (bounded)
+    if (window_ns) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (ctx->approaching.load(std::memory_order_acquire) > 0 &&
+             uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                          .count()) < window_ns)
+        __builtin_ia32_pause();
+    }
+    // the batch: this caller's part first, then every queued part with the same query,
+    // per-block limit and flags, up to one launch's blocks
+    thread_local std::vector<tsg_ctx::CoalReq *> batch;
+    thread_local std::vector<std::pair<uint32_t, Block *>> blist;
+    thread_local std::vector<std::pair<uint32_t, uint32_t>> owner;  // batch position -> (request, caller index)
+    batch.clear();
+    blist.clear();
+    owner.clear();
+    {
+      std::lock_guard<std::mutex> lk(c.m);
+      size_t nb = 0;
+      auto take = [&](size_t k) {
+        tsg_ctx::CoalReq *x = c.pending[k];
+        for (const auto &p : *x->list) {
+          owner.push_back({uint32_t(batch.size()), p.first});
+          blist.push_back({uint32_t(blist.size()), p.second});
+        }
+        nb += x->list->size();
+        batch.push_back(x);
+        c.pending[k] = nullptr;
+      };
+      for (size_t k = 0; k < c.pending.size(); k++)
+        if (c.pending[k] == &r) take(k);
+      for (size_t k = 0; k < c.pending.size(); k++) {
+        tsg_ctx::CoalReq *x = c.pending[k];
+        if (!x || x->limit != limit || x->flags != flags || nb + x->list->size() > kBatchBlocks ||
+            !same_query(*x->q, q))
+          continue;
+        take(k);
+      }
+      c.pending.erase(std::remove(c.pending.begin(), c.pending.end(), nullptr), c.pending.end());
+    }
+    if (batch.size() == 1) {  // alone: straight into the caller's output
+      try {
+        device_search(*dc, list, q, limit, flags, out);
+      } catch (...) {
+        r.err = std::current_exception();
+      }
+      r.done.store(true, std::memory_order_release);
+      c.busy.store(false, std::memory_order_release);
+      break;
+    }
+    thread_local SearchOut bout;
+    std::exception_ptr err;
+    try {
+      device_search(*dc, blist, q, limit, flags, bout);
+    } catch (...) {
+      err = std::current_exception();
+    }
+    // each caller: its blocks' records (the batch's are grouped by position, in order), its
+    // share of the algorithmic bytes (by entries), the launch's device time
+    uint64_t n_all = 0;
+    for (const auto &p : blist) n_all += p.second->host->n;
+    for (size_t k = 0; k < batch.size(); k++) {
+      SearchOut &o = *batch[k]->out;
+      o.recs.clear();
+      o.block_counts.clear();
+      uint64_t n_mine = 0;
+      for (const auto &p : *batch[k]->list) n_mine += p.second->host->n;
+      const double share = n_all ? double(n_mine) / double(n_all) : 0.0;
+      o.device_bytes = uint64_t(double(bout.device_bytes) * share);
+      o.scan_bytes = uint64_t(double(bout.scan_bytes) * share);
+      o.kernel_ns = bout.kernel_ns;
+      o.scan_ns = bout.scan_ns;
+      o.reruns = batch[k] == &r ? bout.reruns : 0;
+      o.pool = bout.pool;
+      batch[k]->err = err;
+    }
+    if (!err)
+      for (const auto &rec : bout.recs) {
+        const auto &ow = owner[rec.block_il & 0xffffffu];
+        SearchOut::Rec x = rec;
+        x.block_il = (rec.block_il & 0xff000000u) | ow.second;
+        batch[ow.first]->out->recs.push_back(x);
+      }
+    for (auto *x : batch) x->done.store(true, std::memory_order_release);
+    c.busy.store(false, std::memory_order_release);
+    break;
+  }
+  if (r.err) std::rethrow_exception(r.err);
+}
+
 int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
                const tsg_search_opts *opts, tsg_result **out) {
   if (!ctx || !q || !out || (nblocks && !blocks)) return TSG_E_INVALID;
@@ -770,6 +954,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
   const clk::time_point t_in = trace ? clk::now() : clk::time_point();
   const uint64_t qid = opts ? opts->query_id : 0;
   ctx->begin(qid);
+  Approach approach(&ctx->approaching);
   struct Forget {  // the id is done with once this search returns, cancelled or not
     tsg_ctx *c;
     uint64_t q;
@@ -841,11 +1026,12 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         // before every chunk
         const size_t nl = list.size(), step = kChunk ? kChunk : nl;
         SearchOut &o = *slots[slot];
-        if (nl <= step) {  // one chunk: the device's list as it is
+        if (nl <= step) {  // one chunk: the device's list as it is (coalesced with concurrent callers)
           check_cancel();
-          device_search(*dc, list, *q, dlimit, flags, o);
+          coalesced_search(ctx, dc, list, *q, dlimit, flags, o, approach);
           return;
         }
+        approach.leave();
         for (size_t c0 = 0; c0 < nl; c0 += step) {
           check_cancel();
           const std::vector<std::pair<uint32_t, Block *>> part(list.begin() + c0,
@@ -864,6 +1050,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
           o.reruns += more.reruns;
         }
       };
+      if (per_dev.empty()) approach.leave();
       if (!per_dev.empty()) ctx->fan_out(per_dev.size(), [&](size_t i) { return per_dev[i].first; }, work);
       // per block match lists in scan order (each device's records are grouped by block already)
       uint64_t wave_k = 0, wave_s = 0;  // devices run concurrently: a wave takes its slowest
@@ -954,6 +1141,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       return e ? std::max<uint64_t>(512, uint64_t(std::atoll(e))) : uint64_t(1) << 21;
     }();
     if (limit && !any_live) {
+      approach.leave();
       thread_local std::vector<std::vector<SearchOut::Rec>> acc;  // per block: its records so far
       if (acc.size() < nblocks) acc.resize(nblocks);
       for (size_t i = 0; i < nblocks; i++) acc[i].clear();

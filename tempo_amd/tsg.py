@@ -223,6 +223,26 @@ def lib():
     return _lib
 
 
+_shim = None
+
+
+def shim_pattern_lib():
+    """libtsg_shim_pattern.so (built next to libtsg by the same Makefile): the shim's
+    per-block call pattern from C threads, for the bench and the coalescer tests."""
+    global _shim
+    if _shim is None:
+        lib()
+        path = os.path.join(os.path.dirname(LIB_PATH), "libtsg_shim_pattern.so")
+        if not os.path.exists(path):
+            raise ImportError(f"libtsg_shim_pattern.so not built at {path}: run __graft_entry__.build()")
+        S = C.CDLL(path)
+        vp = C.c_void_p
+        S.tsgx_shim_pattern.argtypes = [vp, C.POINTER(vp), C.c_size_t, C.c_size_t, C.POINTER(_Query), C.c_uint32,
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        _shim = S
+    return _shim
+
+
 _raw = None
 
 
@@ -484,6 +504,20 @@ class Engine:
         """tsg_cancel: the search running (or about to run) with this id stops at its next
         chunk boundary with TSG_E_CANCELLED (the Go shim maps ctx.Done() to this)."""
         _check(lib().tsg_cancel(self.h, query_id))
+
+    def shim_pattern(self, sets: Sequence[Sequence["BackendSearchBlock"]], pipeline: Pipeline, rounds: int):
+        """The Go shim's ingester call pattern (instance_search.go:164-185) driven from C
+        threads (libtsg_shim_pattern.so): per query, one thread per block, each a limit-0
+        tsg_search over its one block; query r searches sets[r % len(sets)] (equal-sized
+        sets). Returns (per-query wall ns, per-query record counts)."""
+        sp = shim_pattern_lib()
+        nb = len(sets[0])
+        assert nb and all(len(s) == nb for s in sets)
+        arr = (C.c_void_p * (nb * len(sets)))(*[b.h for s in sets for b in s])
+        ns = (C.c_uint64 * rounds)()
+        nm = (C.c_uint64 * rounds)()
+        _check(sp.tsgx_shim_pattern(self.h, arr, nb, len(sets), pipeline.query, rounds, ns, nm))
+        return list(ns), list(nm)
 
     def kernel_times(self, cap: int = 65536) -> List[int]:
         """Durations (ns) of the searches run with SEARCH_TIME_DEFER since the last

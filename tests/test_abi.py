@@ -28,6 +28,15 @@ def test_every_declared_symbol_is_exported():
     assert sorted(tsg.EXPORTED) == syms
 
 
+def test_shim_pattern_driver_loads():
+    """libtsg_shim_pattern.so (the shim's per-block call pattern for the bench) binds to
+    the same libtsg: one copy of the library in the process."""
+    S = tsg.shim_pattern_lib()
+    assert hasattr(S, "tsgx_shim_pattern")
+    maps = open("/proc/self/maps").read()
+    assert len({ln.split()[-1] for ln in maps.splitlines() if ln.endswith("/libtsg.so")}) == 1
+
+
 def test_no_device_fails_loudly():
     import torch
     if torch.cuda.is_available():

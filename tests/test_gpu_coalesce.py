@@ -1,0 +1,169 @@
+"""The device coalescer (capi.cpp coalesced_search): concurrent tsg_search calls on one
+device, each over its own block(s), merged into one launch per batch — the Go shim's call
+pattern for the ingester, where searchLocalBlocks starts a goroutine per block and each
+calls Search on its own (modules/ingester/instance_search.go:164-185).
+
+Every caller must get exactly what it gets alone: its blocks' records (block indices of
+its own call), its metrics, whatever else runs beside it — equal queries coalesce,
+different queries, limits and multi-block calls do not mix up. Expected values: the
+oracle per block (BackendSearchBlock.Search, tempodb/search/backend_search_block.go:184-298).
+Python threads release the GIL inside tsg_search, so the calls overlap on the device; the
+shim's pattern proper (C threads, no GIL) runs through libtsg_shim_pattern.so.
+"""
+import random
+import threading
+
+import pytest
+
+from oracle import oracle as O
+import tempo_amd as T
+from tests.helpers import match_key, tsg_key
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_700_000_000
+QA = dict(tags={"service.name": "svc-07", "http.method": "get"}, min_ms=10, max_ms=1000)
+QB = dict(tags={"http.method": "get", "status.code": "error"}, start=T0 + 100, end=T0 + 2500)
+
+
+def request(q):
+    return T.SearchRequest(tags=dict(q.get("tags", {})), min_duration_ms=q.get("min_ms", 0),
+                           max_duration_ms=q.get("max_ms", 0), start=q.get("start", 0), end=q.get("end", 0))
+
+
+@pytest.fixture(scope="module")
+def blockset(tmp_path_factory):
+    d = tmp_path_factory.mktemp("coal")
+    paths = []
+    for i in range(12):
+        p = str(d / ("b%02d" % i))
+        T.synth_search_block(p, 20_000 + 7_919 * i, seed=900 + i, profile=0, encoding=T.ENC_SNAPPY,
+                             page_size=64 << 10)
+        paths.append(p)
+    return paths
+
+
+def expected(paths, q, limit=0):
+    exp, met, st = O.search([O.Block(p) for p in paths], limit=limit, nthreads=1 if limit else 8, **q)
+    assert st == 0
+    return [match_key(m) for m in exp], (met["traces_inspected"], met["bytes_inspected"], met["blocks_inspected"],
+                                         met["blocks_skipped"])
+
+
+def key(res):
+    got, met = res
+    return [tsg_key(m) for m in got], (met.inspected_traces, met.inspected_bytes, met.inspected_blocks,
+                                       met.skipped_blocks)
+
+
+def test_concurrent_single_block_calls(engine, blockset):
+    """The shim's shape: one thread per block, equal query, limit 0, all released at once."""
+    blocks = [engine.open_block(p) for p in blockset]
+    try:
+        pipe = T.Pipeline(request(QA))
+        exp = [expected([p], QA) for p in blockset]
+        for rnd in range(6):
+            got = [None] * len(blocks)
+            errs = []
+            go = threading.Barrier(len(blocks))
+
+            def worker(i):
+                try:
+                    go.wait()
+                    got[i] = key(engine.search([blocks[i]], pipe))
+                except Exception as e:  # noqa: BLE001
+                    errs.append(e)
+
+            ths = [threading.Thread(target=worker, args=(i,)) for i in range(len(blocks))]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            assert not errs, errs
+            for i in range(len(blocks)):
+                assert got[i] == exp[i], (rnd, i)
+            assert sum(len(g[0]) for g in got) > 0
+    finally:
+        for b in blocks:
+            b.close()
+
+
+def test_mixed_queries_limits_and_block_lists(engine, blockset):
+    """Different queries, per-call limits and multi-block calls at the same time: only
+    equal (query, limit, flags) parts share a launch, and each caller gets its own."""
+    blocks = [engine.open_block(p) for p in blockset]
+    try:
+        rng = random.Random(5)
+        calls = []
+        for k in range(16):
+            q = QA if k % 2 == 0 else QB
+            nb = rng.choice([1, 1, 1, 2, 3])
+            idx = rng.sample(range(len(blocks)), nb)
+            limit = rng.choice([0, 0, 0, 5, 40])
+            calls.append((q, idx, limit))
+        exp = [expected([blockset[i] for i in idx], q, limit) for q, idx, limit in calls]
+        pipes = {id(QA): T.Pipeline(request(QA)), id(QB): T.Pipeline(request(QB))}
+        for rnd in range(4):
+            got = [None] * len(calls)
+            errs = []
+            go = threading.Barrier(len(calls))
+
+            def worker(k):
+                q, idx, limit = calls[k]
+                try:
+                    go.wait()
+                    got[k] = key(engine.search([blocks[i] for i in idx], pipes[id(q)], limit=limit))
+                except Exception as e:  # noqa: BLE001
+                    errs.append(e)
+
+            ths = [threading.Thread(target=worker, args=(k,)) for k in range(len(calls))]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            assert not errs, errs
+            for k in range(len(calls)):
+                assert got[k] == exp[k], (rnd, k, calls[k])
+    finally:
+        for b in blocks:
+            b.close()
+
+
+def test_equal_query_from_distinct_pipelines(engine, blockset):
+    """The shim builds a pipeline per call: equal content coalesces, not equal pointers."""
+    blocks = [engine.open_block(p) for p in blockset[:8]]
+    try:
+        pipes = [T.Pipeline(request(QB)) for _ in blocks]
+        exp = [expected([p], QB) for p in blockset[:8]]
+        got = [None] * len(blocks)
+        go = threading.Barrier(len(blocks))
+
+        def worker(i):
+            go.wait()
+            got[i] = key(engine.search([blocks[i]], pipes[i]))
+
+        ths = [threading.Thread(target=worker, args=(i,)) for i in range(len(blocks))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert got == exp
+    finally:
+        for b in blocks:
+            b.close()
+
+
+def test_shim_pattern_driver(engine, blockset):
+    """libtsg_shim_pattern.so (C threads, the bench's shim leg): every query's record count
+    equals the per-block oracle's, over two rotating sets."""
+    a = [engine.open_block(p) for p in blockset[:10]]
+    b = [x.clone(engine) for x in a]
+    try:
+        pipe = T.Pipeline(request(QA))
+        per = sum(len(expected([p], QA)[0]) for p in blockset[:10])
+        ns, nm = engine.shim_pattern([a, b], pipe, 40)
+        assert nm == [per] * 40
+        assert all(x > 0 for x in ns)
+    finally:
+        for x in a + b:
+            x.close()
