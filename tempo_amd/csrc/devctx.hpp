@@ -141,6 +141,8 @@ struct DeviceCtx {
   // TSG_POOL_STATIC=0: the claim-based pool kernel (LDS claims + dynamic chunks) instead of
   // the static-run kernel (search_static_kernel)
   bool pool_static = env_u32("TSG_POOL_STATIC", 1, 0, 1) != 0;
+  // large dictionaries matched as one byte stream (dict_stream_kernel); 0: a lane per value
+  bool dict_stream = env_u32("TSG_DICT_STREAM", 1, 0, 1) != 0;
   DevBuf pool_head;  // two dynamic-chunk counters (128 B apart): a launch uses one, zeroes the other
   uint32_t pool_parity = 0;
   std::set<const void *> pool_attr;  // pool kernels whose dynamic LDS limit has been raised

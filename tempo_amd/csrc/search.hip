@@ -188,6 +188,18 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
   const DictJob &jb = jobs[set_jobs[lo]];
   uint32_t w = item - prefix[lo];
   uint32_t word = 0;
+  if (jb.identity) {  // a streamed identity job (dict_stream_kernel): value v = set v, 32 match bytes per word
+    const u32x4 *vb = reinterpret_cast<const u32x4 *>(vmatch + jb.vmatch_base + size_t(w) * 32);  // 32-aligned
+    const u32x4 a = vb[0], c = vb[1];
+    const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t x = d[k];  // bytes 0/1; bytes past nvals are zero
+      word |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
+    }
+    bitmaps[jb.bm_base + w] = word;
+    return;
+  }
   for (uint32_t b = 0; b < 32; b++) {
     uint32_t s = w * 32 + b;
     if (s >= jb.nsets) break;
@@ -198,6 +210,161 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
       }
   }
   bitmaps[jb.bm_base + w] = word;
+}
+
+// ------------------------------------------------------------------------------------
+// dict_stream: bytes.Contains over a large dictionary as ONE byte stream
+//
+// A key's value bytes sit back to back (dict_off | dict_bytes), so the substring test
+// of every value is a scan of that stream for the needle, a match counting for the
+// value that holds all of it. One lane per value (prep_kernel) leaves long values
+// (db.statement: 100-2000 B) to a lane each: divergent, uncoalesced byte loops. Here a
+// wave owns a 64 KiB span of the stream and walks it 1 KiB at a time: each lane loads
+// 16 B (one coalesced dwordx4 per lane), the window and the next 1 KiB sit in LDS, a
+// SWAR test of the needle's first two bytes at all 16 positions of a lane picks the
+// candidates, the rest of the needle is compared from LDS, and a verified start maps to
+// its value through the value offsets staged in LDS. Bytes are read once from HBM.
+constexpr uint32_t kStreamSpan = 64u << 10;     // start positions per wave
+constexpr uint32_t kStreamMaxNeedle = 1024;     // the 2 KiB window holds any match that starts in its first half
+constexpr uint64_t kStreamMinBytes = 1u << 20;  // smaller dictionaries: prep_kernel (lane per value)
+constexpr uint32_t kStreamOffs = 128;           // value offsets staged per reload
+struct StreamJob {
+  const uint8_t *base;  // 16-byte aligned: the dictionary bytes start at base + lead
+  const uint32_t *off;  // value offsets, nvals + 1
+  uint64_t nbytes;
+  uint32_t lead, nvals;
+  uint32_t needle_off, needle_len;
+  uint32_t vmatch_base, wave0;  // match bytes (32-aligned); first wave of this job
+};
+static_assert(sizeof(StreamJob) == 48, "StreamJob layout");
+
+// bit 7 of each byte of the result: that byte of x is non-zero (exact, no carries across bytes)
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t x) { return (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u; }
+// bits 7/15/23/31 -> bits 0..3
+__device__ __forceinline__ uint32_t pack_hi_bits(uint32_t c) { return (((c >> 7) * 0x204081u) >> 21) & 0xfu; }
+
+// largest v in [lo, hi) with off[v] <= p (off[lo] <= p < off[hi] or hi = nvals + 1): 64-ary search
+__device__ __forceinline__ uint32_t value_at(const uint32_t *off, uint32_t lo, uint32_t hi, uint64_t p, int lane) {
+  while (hi - lo > 1) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint32_t idx = lo + uint32_t(lane) * step;
+    const bool le = idx < hi && uint64_t(off[idx]) <= p;
+    const uint32_t c = uint32_t(__popcll(__ballot(le)));  // lanes 0..c-1 (monotone offsets)
+    lo = lo + (c - 1) * step;
+    hi = min(hi, lo + step);
+  }
+  return lo;
+}
+
+extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const StreamJob *jobs, uint32_t njobs,
+                                                                    const uint8_t *needles, uint8_t *vmatch) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[2048 + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_nd[kStreamMaxNeedle];
+  __shared__ uint32_t s_off[kStreamOffs + 1];
+  const int lane = threadIdx.x;
+  const uint32_t w = blockIdx.x;
+  uint32_t j = 0;
+  for (uint32_t k = 1; k < njobs; k++)
+    if (jobs[k].wave0 <= w) j = k;
+  const StreamJob J = jobs[j];
+  const uint32_t nl = J.needle_len;
+  const uint64_t end = uint64_t(J.lead) + J.nbytes;  // aligned coordinates of the last byte + 1
+  const uint64_t s0 = uint64_t(w - J.wave0) * kStreamSpan;
+  // start positions q (aligned coordinates) of this wave: [qlo, qhi)
+  const uint64_t qlo = max<uint64_t>(s0, J.lead);
+  const uint64_t qhi = min<uint64_t>(s0 + kStreamSpan, end >= nl ? end - nl + 1 : 0);
+  if (qlo >= qhi) return;
+  for (uint32_t i = lane; i < nl; i += 64) s_nd[i] = needles[J.needle_off + i];
+  const uint32_t n0 = uint32_t(needles[J.needle_off]) * 0x01010101u;
+  const uint32_t n1 = nl > 1 ? uint32_t(needles[J.needle_off + 1]) * 0x01010101u : 0u;
+  auto load16 = [&](uint64_t a) -> u32x4 {  // a: aligned coordinate of this lane's 16 bytes
+    if (a < end) return *reinterpret_cast<const u32x4 *>(J.base + a);
+    return u32x4{0u, 0u, 0u, 0u};
+  };
+  // value offsets of the values around the window: s_off[i] = off[vb + i]
+  uint32_t vb = value_at(J.off, 0, J.nvals + 1, qlo - J.lead, lane), kv = 0;
+  uint64_t cover = 0;  // starts p < cover map through s_off
+  auto stage_offs = [&](uint32_t v) {
+    vb = v;
+    kv = min<uint32_t>(kStreamOffs, J.nvals - v);
+    for (uint32_t i = lane; i <= kv; i += 64) s_off[i] = J.off[v + i];
+    cover = kv == J.nvals - v ? ~0ull : uint64_t(J.off[v + kv]);
+  };
+  stage_offs(vb);
+  uint64_t cq = s0;
+  u32x4 cur = load16(cq + lane * 16), nxt = load16(cq + 1024 + lane * 16);
+  uint32_t last_v = 0xffffffffu;  // this lane's last marked value (skips repeats)
+  for (; cq < qhi; cq += 1024) {
+    const u32x4 nn = load16(cq + 2048 + lane * 16);
+    __syncthreads();  // (previous window's readers done)
+    reinterpret_cast<u32x4 *>(s_win)[lane] = cur;
+    reinterpret_cast<u32x4 *>(s_win)[64 + lane] = nxt;
+    // the offsets must cover every start of this window
+    const uint64_t wlast = min<uint64_t>(cq + 1024, qhi) - 1 - J.lead;
+    if (cover != ~0ull && wlast >= cover) {
+      const uint64_t pfirst = max<uint64_t>(cq, qlo) - J.lead;
+      // staged values [vb, vb + kv) that start at or before pfirst
+      const uint32_t c = uint32_t(__popcll(__ballot(uint32_t(lane) < kv && uint64_t(s_off[lane]) <= pfirst))) +
+                         uint32_t(__popcll(__ballot(uint32_t(lane) + 64 < kv && uint64_t(s_off[64 + lane]) <= pfirst)));
+      const bool beyond = c == kv && uint64_t(s_off[kv]) <= pfirst;
+      __syncthreads();
+      const uint32_t v = beyond ? value_at(J.off, vb + kv, J.nvals + 1, pfirst, lane) : vb + c - 1;
+      stage_offs(v);
+    }
+    __syncthreads();
+    const uint32_t nxw = reinterpret_cast<const uint32_t *>(s_win)[(lane + 1) * 4];  // the next lane's first dword
+    const uint32_t d[5] = {cur.x, cur.y, cur.z, cur.w, nxw};
+    uint32_t cm = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t nz = nz_bytes(d[k] ^ n0);
+      if (nl > 1) nz |= nz_bytes(__builtin_amdgcn_alignbyte(d[k + 1], d[k], 1) ^ n1);
+      cm |= pack_hi_bits(nz ^ 0x80808080u) << (4 * k);
+    }
+    while (cm) {
+      const uint32_t jb = uint32_t(__builtin_ctz(cm));
+      cm &= cm - 1;
+      const uint32_t wo = uint32_t(lane) * 16 + jb;  // window offset of the start
+      const uint64_t q = cq + wo;
+      if (q < qlo || q >= qhi) continue;
+      bool ok = true;
+      for (uint32_t i = 2; i < nl && ok; i++) ok = s_win[wo + i] == s_nd[i];
+      if (!ok) continue;
+      const uint64_t p = q - J.lead;
+      uint32_t v;
+      if (p < cover) {  // in the staged offsets: s_off[lo] <= p < s_off[hi]
+        uint32_t lo = 0, hi = kv;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (uint64_t(s_off[mid]) <= p) lo = mid;
+          else hi = mid;
+        }
+        v = vb + lo;
+      } else {  // (a run of tiny values past the staged ones: search the global offsets)
+        uint32_t lo = vb, hi = J.nvals;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (uint64_t(J.off[mid]) <= p) lo = mid;
+          else hi = mid;
+        }
+        v = lo;
+      }
+      const uint64_t vend = J.off[v + 1];
+      if (p + nl > vend) continue;  // the match runs into the next value
+      if (v != last_v) {
+        vmatch[J.vmatch_base + v] = 1;
+        last_v = v;
+      }
+      // the rest of this lane's starts inside the same value add nothing
+      const uint64_t skip = vend + J.lead;  // aligned coordinate of the value's end
+      if (skip > q + 1) {
+        const uint64_t rel = skip - (cq + uint64_t(lane) * 16);
+        cm &= rel >= 16 ? 0u : ~((1u << uint32_t(rel)) - 1u);
+      }
+    }
+    cur = nxt;
+    nxt = nn;
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1413,6 +1580,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     std::vector<DictJob> jobs;
     std::vector<uint32_t> set_jobs, set_items, term_bm_base, needle_off;
     std::vector<uint8_t> needles;
+    std::vector<StreamJob> stream_jobs;
     std::vector<std::array<uint16_t, kArgTerms>> seg_keys;
     std::vector<const DevBlockDesc *> seg_desc;
     std::vector<NarrowSeg> nsegv;
@@ -1433,6 +1601,9 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   set_items.assign(1, 0);
   term_bm_base.clear();
   needles.clear();
+  auto &stream_jobs = ps.stream_jobs;
+  stream_jobs.clear();
+  uint32_t stream_waves = 0;
   needle_off.assign(q.nterms, 0);
   for (uint32_t t = 0; t < q.nterms; t++) {
     needle_off[t] = uint32_t(needles.size());
@@ -1506,10 +1677,33 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       jb.identity = k.identity ? 1 : 0;
       jb.bm_base = bm_total;
       jb.item_base = items;
-      items += uint32_t(align_up(std::max<uint32_t>(k.nvals, 1), 64));
+      // a large dictionary of values >= 16 B on average: one byte-stream pass
+      // (dict_stream_kernel) instead of a lane per value
+      const bool stream = dc.dict_stream && k.dict_nbytes > kStreamMinBytes && q.value_lens[t] >= 1 &&
+                          q.value_lens[t] <= kStreamMaxNeedle && k.dict_nbytes >= 16ull * k.nvals;
+      if (!stream) items += uint32_t(align_up(std::max<uint32_t>(k.nvals, 1), 64));
       const uint32_t words = (k.nsets + 31) / 32;
       bm_total += words + 2;  // +2: a wave's ballot writes whole 64-value word pairs
-      if (!k.identity) {
+      if (stream) {
+        // match bytes 32-aligned (dict_sets_kernel packs identity words from 32 of them)
+        vmatch_total = uint32_t(align_up(vmatch_total, 32));
+        jb.vmatch_base = vmatch_total;
+        vmatch_total += uint32_t(align_up(k.nvals, 32));
+        set_jobs.push_back(uint32_t(jobs.size()));
+        set_items.push_back(set_items.back() + words);
+        StreamJob sj{};
+        sj.lead = uint32_t(reinterpret_cast<uintptr_t>(k.dict_bytes) & 15u);
+        sj.base = k.dict_bytes - sj.lead;
+        sj.off = k.dict_off;
+        sj.nbytes = k.dict_nbytes;
+        sj.nvals = k.nvals;
+        sj.needle_off = needle_off[t];
+        sj.needle_len = q.value_lens[t];
+        sj.vmatch_base = jb.vmatch_base;
+        sj.wave0 = stream_waves;
+        stream_waves += uint32_t((sj.lead + sj.nbytes + kStreamSpan - 1) / kStreamSpan);
+        stream_jobs.push_back(sj);
+      } else if (!k.identity) {
         jb.vmatch_base = vmatch_total;
         vmatch_total += k.nvals;
         set_jobs.push_back(uint32_t(jobs.size()));
@@ -1843,7 +2037,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     const size_t o_sp = align_up(o_sj + set_jobs.size() * 4, 16);
     const size_t o_nd = align_up(o_sp + set_items.size() * 4, 16);
     const size_t o_ws = align_up(o_nd + needles.size() + 1, 16);
-    const size_t total_desc = align_up(o_ws + size_t(nwg) * 2, 16);
+    const size_t o_stj = align_up(o_ws + size_t(nwg) * 2, 16);
+    const size_t total_desc = align_up(o_stj + stream_jobs.size() * sizeof(StreamJob), 16);
     dc.hdesc.ensure(total_desc);
     dc.desc.ensure(total_desc);
     auto *hd = static_cast<uint8_t *>(dc.hdesc.p);
@@ -1856,6 +2051,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     if (!set_jobs.empty()) std::memcpy(hd + o_sj, set_jobs.data(), set_jobs.size() * 4);
     std::memcpy(hd + o_sp, set_items.data(), set_items.size() * 4);
     if (!needles.empty()) std::memcpy(hd + o_nd, needles.data(), needles.size());
+    if (!stream_jobs.empty()) std::memcpy(hd + o_stj, stream_jobs.data(), stream_jobs.size() * sizeof(StreamJob));
     auto *ws = reinterpret_cast<uint16_t *>(hd + o_ws);
     for (size_t i = 0; i < segs.size(); i++)
       for (uint32_t w = 0; w < segs[i].nwg; w++) ws[segs[i].first_wg + w] = uint16_t(i);
@@ -1867,10 +2063,15 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     }
     tr.mark("desc");
     if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
+    if (!stream_jobs.empty()) HIP_OK(hipMemsetAsync(dc.vmatch.p, 0, vmatch_total, s));
     prep_kernel<<<std::max<uint32_t>(1, (items + 255) / 256), 256, 0, s>>>(
         src, dd, uint32_t(total_desc / 16), uint32_t(o_jobs), uint32_t(o_jb), uint32_t(jobs.size()), items,
         uint32_t(o_nd), uint32_t(needles.size()), static_cast<uint8_t *>(dc.vmatch.p),
         static_cast<uint32_t *>(dc.bitmaps.p));
+    if (!stream_jobs.empty())
+      dict_stream_kernel<<<stream_waves, 64, 0, s>>>(reinterpret_cast<const StreamJob *>(dd + o_stj),
+                                                     uint32_t(stream_jobs.size()), dd + o_nd,
+                                                     static_cast<uint8_t *>(dc.vmatch.p));
     if (set_items.back())
       dict_sets_kernel<<<(set_items.back() + 255) / 256, 256, 0, s>>>(
           reinterpret_cast<const DictJob *>(dd + o_jobs), reinterpret_cast<const uint32_t *>(dd + o_sj),
