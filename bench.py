@@ -174,6 +174,10 @@ def parse():
                     help="queries in the shim-pattern leg (one C thread per block, a tsg_search each; 0 = off)")
     ap.add_argument("--merge-steps", type=int, default=20,
                     help="N > 1: distributed full-scan queries with the frontend merge on rank 0 (0 = off)")
+    ap.add_argument("--cfg4", type=int, default=None, help="config-4 leg (default: on at N=1)")
+    ap.add_argument("--cfg4-blocks", type=int, default=10)
+    ap.add_argument("--cfg4-entries", type=int, default=100_000)
+    ap.add_argument("--cfg4-steps", type=int, default=20)
     ap.add_argument("--cfg3-blocks", type=int, default=25)
     ap.add_argument("--cfg3-entries", type=int, default=5_000_000)
     ap.add_argument("--cfg3-steps", type=int, default=64)
@@ -460,6 +464,82 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, gen_thread=Non
     return res
 
 
+def cfg4_paths(args, workdir, rank):
+    return [os.path.join(workdir, f"r{rank}cfg4_{i}") for i in range(args.cfg4_blocks)]
+
+
+def cfg4_generate(args, workdir, rank):
+    """Config-4 blocks (the high-cardinality profile: ~unique http.url, 100-2000 B
+    db.statement values), written in parallel in a thread at bench start."""
+    import tempo_amd as T
+
+    def one(i_p):
+        i, p = i_p
+        if not os.path.exists(os.path.join(p, "search.meta.json")):
+            T.synth_search_block(p, args.cfg4_entries, seed=4000 + 97 * rank + i, profile=1,
+                                 encoding=T.ENC_SNAPPY, page_size=1024 * 1024)
+    parallel(one, list(enumerate(cfg4_paths(args, workdir, rank))))
+
+
+CFG4_QUERIES = [
+    ("statement+url", dict(tags={"db.statement": "from orders", "http.url": "/carts/"}, min_duration_ms=1)),
+    ("statement_id_range", dict(tags={"db.statement": "where id = 77"}, start=QUERY["start"], end=QUERY["end"])),
+    ("url_prefix", dict(tags={"http.url": "/api/v1/users/12"})),
+]
+
+
+def cfg4_leg(args, eng, workdir, rank, gen_thread=None):
+    """BASELINE config 4: high-cardinality tags (http.url, db.statement) with long values,
+    ContainsTag semantics. Per query: the dictionary pass (every value of the searched keys
+    tested for the needle: dict_stream_kernel over the value bytes, then the value-set
+    bitmaps) and the scan. B_dict = the searched keys' dictionary bytes + offsets; the
+    dictionary pass time = device sequence time (TIME_ALL events) - scan kernel time."""
+    import tempo_amd as T
+    t0 = time.time()
+    if gen_thread is not None:
+        gen_thread.join()
+    cfg4_generate(args, workdir, rank)
+    gen_s = time.time() - t0
+    t0 = time.time()
+    blocks = parallel(eng.open_block, cfg4_paths(args, workdir, rank))
+    load_s = time.time() - t0
+    entries = sum(b.info()["entries"] for b in blocks)
+    log(f"rank {rank}: cfg4 {len(blocks)} x {args.cfg4_entries} entries resident (gen wait {gen_s:.1f}s, "
+        f"load {load_s:.1f}s)")
+    res = {"workload": f"config 4: {len(blocks)} blocks x {args.cfg4_entries} entries, high-cardinality profile "
+                       f"(~unique http.url, 100-2000 B db.statement)", "entries": entries, "load_s": load_s,
+           "queries": {}}
+    for name, q in CFG4_QUERIES:
+        pipe = T.Pipeline(T.SearchRequest(**q))
+        n0, _ = eng.search_raw(blocks, pipe)
+        ts_all, dict_ns, scan_ns, steps = [], [], [], []
+        met = None
+        for i in range(args.cfg4_steps):
+            ts = time.perf_counter()
+            n, met = eng.search_raw(blocks, pipe, flags=T.SEARCH_TIME_ALL)
+            steps.append(time.perf_counter() - ts)
+            assert n == n0
+            ts_all.append(met.kernel_ns)
+            scan_ns.append(met.scan_kernel_ns)
+            dict_ns.append(met.kernel_ns - met.scan_kernel_ns)
+        b_dict = met.device_bytes_read - met.scan_bytes
+        dmed = sorted(dict_ns)[len(dict_ns) // 2]
+        smed = sorted(scan_ns)[len(scan_ns) // 2]
+        res["queries"][name] = {
+            "query": q, "matches": n0,
+            "step_us": pct([x * 1e6 for x in steps]),
+            "entries_per_s": entries / (sorted(steps)[len(steps) // 2]),
+            "dict_pass_us": pct([x / 1e3 for x in dict_ns]), "scan_us": pct([x / 1e3 for x in scan_ns]),
+            "b_dict": b_dict, "scan_bytes": met.scan_bytes,
+            "dict_gbps": b_dict / dmed if dmed else None,
+            "dict_frac": b_dict / dmed / PEAK_HBM_GBPS if dmed else None,
+            "scan_gbps": met.scan_bytes / smed if smed else None,
+        }
+    for b in blocks:
+        b.close()
+    return res
+
+
 def merge_leg(args, eng, base, pipe, rank, world, dist):
     """N > 1: the query as the frontend serves it (modules/frontend/searchsharding.go:32-125):
     every rank searches its block shard (full scan, the config-2 query), packs its ordered
@@ -505,6 +585,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.cfg3 is None:
         args.cfg3 = 1 if world == 1 else 0
+    if args.cfg4 is None:
+        args.cfg4 = 1 if world == 1 else 0
     import torch
     dist = None
     if world > 1:
@@ -522,6 +604,10 @@ def main():
     if args.cfg3:
         cfg3_thread = threading.Thread(target=cfg3_generate, args=(args, workdir, rank), daemon=True)
         cfg3_thread.start()
+    cfg4_thread = None
+    if args.cfg4:
+        cfg4_thread = threading.Thread(target=cfg4_generate, args=(args, workdir, rank), daemon=True)
+        cfg4_thread.start()
     t0 = time.time()
     paths = gen_blocks(workdir, rank, args.blocks, args.entries, threads)
     log(f"rank {rank}: generated {args.blocks} x {args.entries} entries in {time.time() - t0:.1f}s")
@@ -687,6 +773,9 @@ def main():
 
     if args.cfg3:
         out["cfg3"] = cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, cfg3_thread)
+
+    if args.cfg4:
+        out["cfg4"] = cfg4_leg(args, eng, workdir, rank, cfg4_thread)
 
     if world > 1 and args.merge_steps:
         out["merge"] = merge_leg(args, eng, base, pipe, rank, world, dist)
