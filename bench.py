@@ -290,7 +290,9 @@ def cpu_baselines(paths, got, threads):
     out["columnar"] = {
         "value": entries / col_s, "unit": "entries/s", "cores": threads,
         "sample": f"the same {entries} entries decoded once into host columns ({build_s:.1f}s, untimed), "
-                  f"Pipeline predicates over the columns on {threads} threads, {reps} rep(s)",
+                  f"Pipeline predicates over the columns on {threads} threads, {reps} rep(s); threads capped "
+                  f"at 16 = one GPU job's CPU share of the shared GPU box (of {os.cpu_count()} CPUs there), "
+                  f"not every host core; --cpu-threads overrides",
         "parity": cm == len(got) and ch == O.match_hash([(m.block_idx, m.entry_idx) for m in got]),
     }
     return out
