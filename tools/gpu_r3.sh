@@ -31,6 +31,24 @@ if has probe; then
   rc=$?; echo "probe rc=$rc"; cat gpurun_out/launch_probe.json
   [ $rc -eq 0 ] || exit $rc
 fi
+if has lookup; then
+  T="python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider"
+  timeout -k 10 300 $T tests/test_gpu_lookup.py tests/test_gpu_configs.py -k "lookup or find or cfg5 or fixture or blocks or range or devices" \
+    > gpurun_out/lk_tests.log 2>&1
+  rc=$?; echo "lookup tests rc=$rc"; tail -3 gpurun_out/lk_tests.log
+  [ $rc -eq 0 ] || exit $rc
+  for d in 0 1; do
+    TSG_LK_DIR=$d timeout -k 10 400 python tools/bench_lookup.py --cpu-sample 0 ${LK_ARGS:-} > gpurun_out/lookup_dir$d.json 2> gpurun_out/lookup_dir$d.err
+    rc=$?; echo "lookup bench dir=$d rc=$rc"; cat gpurun_out/lookup_dir$d.json
+    [ $rc -eq 0 ] || exit $rc
+  done
+fi
+if has scanprobe; then
+  hipcc -O3 --offload-arch=gfx950 tools/scan_probe.hip -o gpurun_out/scan_probe || exit 1
+  timeout -k 10 180 gpurun_out/scan_probe > gpurun_out/scan_probe.json 2>&1
+  rc=$?; echo "scan probe rc=$rc"; cat gpurun_out/scan_probe.json
+  [ $rc -eq 0 ] || exit $rc
+fi
 if has stamps; then
   TSG_STAMPS=1 timeout -k 10 600 python bench.py --steps 6 --warmup 2 --cpu-baseline 0 --cfg3 0 --concurrent-steps 0 \
     --mall-steps 0 ${BENCH_ARGS:-} > gpurun_out/stamps.json 2> gpurun_out/stamps.err
