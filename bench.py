@@ -354,7 +354,7 @@ def concurrent_leg(args, base, pipe, streams, entries, dist, world, local):
             "note": "one resident copy of the config-2 set per stream; full scans, same query as the main line"}
 
 
-def shim_leg(args, eng, sets, pipe, entries, nmatch, batched, dist):
+def shim_leg(args, eng, sets, pipe, entries, nmatch, batched, dist, all_cpus):
     """The Go shim's call pattern for the ingester: searchLocalBlocks starts a goroutine
     per block and each calls Search on its own (instance_search.go:164-185), so the shim
     makes one limit-0 tsg_search per block. Driven from C threads (libtsg_shim_pattern.so:
@@ -362,10 +362,13 @@ def shim_leg(args, eng, sets, pipe, entries, nmatch, batched, dist):
     over the next resident copy like the main line; libtsg coalesces the concurrent calls
     into one launch per batch (capi.cpp coalesced_search). Reported beside the batched main
     line (one tsg_search over all blocks)."""
-    # (the spinning caller threads get the GPU node's CPUs, not the main line's 8)
+    # (the caller threads get the idlest CPUs of the GPU's node, one per thread + 2, not the
+    # main line's 8: more spinning threads than CPUs would time-slice the leader away)
     mask = os.sched_getaffinity(0)
     node = eng.numa_node(0)
-    cpus = node_cpus(node) & os.sched_getaffinity(0) if node >= 0 else set()
+    cpus = node_cpus(node) & all_cpus if node >= 0 else set()
+    if len(cpus) > len(sets[0]) + 2:
+        cpus = set(idlest(sorted(cpus), len(sets[0]) + 2))
     try:
         if cpus and len(cpus) > len(mask):
             os.sched_setaffinity(0, cpus)
@@ -768,7 +771,7 @@ def main():
                           "entries_per_s": entries / (sum(ls) / len(ls))}
 
     if args.shim_steps:
-        out["shim"] = shim_leg(args, eng, sets, pipe, entries, len(got), value / max(1, world), dist)
+        out["shim"] = shim_leg(args, eng, sets, pipe, entries, len(got), value / max(1, world), dist, all_cpus)
 
     if args.concurrent_steps and streams > 1:
         out["concurrent"] = concurrent_leg(args, base, pipe, streams, entries, dist, world, local)

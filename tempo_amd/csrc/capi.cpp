@@ -197,6 +197,16 @@ struct tsg_ctx {
     std::mutex m;
     std::vector<CoalReq *> pending;
     std::atomic<bool> busy{false};
+    // waiters spin for about one launch, then park here until the leader hands off (an
+    // oversubscribed host must not run a spinning waiter instead of the leader)
+    std::mutex wm;
+    std::condition_variable cv;
+    std::atomic<int> sleepers{0};
+    void wake() {
+      if (sleepers.load(std::memory_order_acquire) == 0) return;
+      std::lock_guard<std::mutex> lk(wm);
+      cv.notify_all();
+    }
   };
   std::mutex comu;
   std::unordered_map<const void *, std::unique_ptr<Coalescer>> coal;  // per DeviceCtx
@@ -839,15 +849,29 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
     c.pending.push_back(&r);
   }
   ap.leave();
+  const auto t_wait = std::chrono::steady_clock::now();
   for (uint32_t spins = 0; !r.done.load(std::memory_order_acquire); spins++) {
     bool expect = false;
-    if (!c.busy.compare_exchange_strong(expect, true, std::memory_order_acq_rel)) {
-      if (spins < 4096) __builtin_ia32_pause();
-      else std::this_thread::yield();
+    if (c.busy.load(std::memory_order_relaxed) ||
+        !c.busy.compare_exchange_strong(expect, true, std::memory_order_acq_rel)) {
+      // spin about one query (a launch + its host work, ~60-120 us; a parked waiter pays a
+      // futex wake-up of tens of us), then park until the leader hands off
+      if ((spins & 63u) != 63u ||
+          std::chrono::steady_clock::now() - t_wait < std::chrono::microseconds(250)) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      std::unique_lock<std::mutex> lk(c.wm);
+      c.sleepers.fetch_add(1, std::memory_order_acq_rel);
+      c.cv.wait_for(lk, std::chrono::microseconds(500), [&] {
+        return r.done.load(std::memory_order_acquire) || !c.busy.load(std::memory_order_acquire);
+      });
+      c.sleepers.fetch_sub(1, std::memory_order_acq_rel);
       continue;
     }
     if (r.done.load(std::memory_order_acquire)) {  // served while we took the lead
       c.busy.store(false, std::memory_order_release);
+      c.wake();
       break;
     }
     // leader: give callers still on their way a moment to queue (bounded)
@@ -898,6 +922,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
       }
       r.done.store(true, std::memory_order_release);
       c.busy.store(false, std::memory_order_release);
+      c.wake();
       break;
     }
     thread_local SearchOut bout;
@@ -935,10 +960,60 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
       }
     for (auto *x : batch) x->done.store(true, std::memory_order_release);
     c.busy.store(false, std::memory_order_release);
+    c.wake();
     break;
   }
   if (r.err) std::rethrow_exception(r.err);
 }
+
+// Distinct trace ids for the consumer's limit count: open addressing over the 16-byte
+// ids (no allocation per insert; a search reuses its thread's table).
+struct IdSet {
+  std::vector<uint64_t> key;  // two words per slot
+  std::vector<uint8_t> used;
+  size_t n = 0;
+  void clear() {
+    n = 0;
+    std::fill(used.begin(), used.end(), uint8_t(0));
+  }
+  size_t size() const { return n; }
+  bool insert(const uint8_t *id) {
+    if ((n + 1) * 2 > used.size()) grow();
+    uint64_t a, b;
+    std::memcpy(&a, id, 8);
+    std::memcpy(&b, id + 8, 8);
+    return put(a, b);
+  }
+
+ private:
+  bool put(uint64_t a, uint64_t b) {
+    const size_t mask = used.size() - 1;
+    uint64_t h = (a ^ (b * 0x9e3779b97f4a7c15ull)) * 0xff51afd7ed558ccdull;
+    h ^= h >> 29;
+    for (size_t i = size_t(h) & mask;; i = (i + 1) & mask) {
+      if (!used[i]) {
+        used[i] = 1;
+        key[2 * i] = a;
+        key[2 * i + 1] = b;
+        n++;
+        return true;
+      }
+      if (key[2 * i] == a && key[2 * i + 1] == b) return false;
+    }
+  }
+  void grow() {
+    std::vector<uint64_t> ok;
+    std::vector<uint8_t> ou;
+    ok.swap(key);
+    ou.swap(used);
+    const size_t cap = std::max<size_t>(64, ou.size() * 2);
+    key.assign(2 * cap, 0);
+    used.assign(cap, 0);
+    n = 0;
+    for (size_t i = 0; i < ou.size(); i++)
+      if (ou[i]) put(ok[2 * i], ok[2 * i + 1]);
+  }
+};
 
 int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
                const tsg_search_opts *opts, tsg_result **out) {
@@ -1145,7 +1220,8 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       thread_local std::vector<std::vector<SearchOut::Rec>> acc;  // per block: its records so far
       if (acc.size() < nblocks) acc.resize(nblocks);
       for (size_t i = 0; i < nblocks; i++) acc[i].clear();
-      std::unordered_set<std::string> distinct_w;
+      thread_local IdSet distinct_w;
+      distinct_w.clear();
       bool stop = false, cut_ok = true;
       size_t cb = 0;     // cursor: next block ...
       uint64_t ce = 0;   // ... and its next scan position
@@ -1238,8 +1314,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
           const auto &v = acc[bi];
           for (size_t ri = 0; ri < v.size() && !stop; ri++) {
             if (v[ri].entry >= order[k].second) break;
-            if (distinct_w.insert(std::string(reinterpret_cast<const char *>(v[ri].id), 16)).second &&
-                distinct_w.size() >= limit)
+            if (distinct_w.insert(v[ri].id) && distinct_w.size() >= limit)
               stop = true;
           }
         }
@@ -1268,7 +1343,8 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     res->resize(nrec);
     size_t nout = 0;
     // consume in caller block order (deterministic refinement of instance.Search)
-    std::unordered_set<std::string> distinct;
+    thread_local IdSet distinct;
+    distinct.clear();
     bool stopped = false;
     for (size_t i = 0; i < nblocks && !stopped; i++) {
       const HostBlock &h = *blocks[i]->b.host;
@@ -1281,7 +1357,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
                    x.nm.size());
           res->dur[nout++] = x.dur;
           if (limit) {
-            distinct.insert(std::string(reinterpret_cast<const char *>(x.id), 16));
+            distinct.insert(x.id);
             if (distinct.size() >= limit) {
               stopped = true;
               stop_trace = x.trace;
@@ -1311,7 +1387,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         res->set(nout++, r->id, uint8_t(r->block_il >> 24), r->start, r->end, uint32_t(i), r->entry, sv.data(),
                  sv.size(), nm.data(), nm.size());
         if (limit) {
-          distinct.insert(std::string(reinterpret_cast<const char *>(r->id), 16));
+          distinct.insert(r->id);
           if (distinct.size() >= limit) {
             stopped = true;
             stop_entry = r->entry;

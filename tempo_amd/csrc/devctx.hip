@@ -36,6 +36,8 @@ void ctx_init(Ctx &c, const tsg_options *opts) {
     // scan timing events: no system-scope fence (no L2 writeback between kernels)
     HIP_OK(hipEventCreateWithFlags(&dc->es0, hipEventDisableSystemFence));
     HIP_OK(hipEventCreateWithFlags(&dc->es1, hipEventDisableSystemFence));
+    HIP_OK(hipEventCreateWithFlags(&dc->er0, hipEventDisableSystemFence));  // (rerun launches)
+    HIP_OK(hipEventCreateWithFlags(&dc->er1, hipEventDisableSystemFence));
     HIP_OK(hipEventCreateWithFlags(&dc->mk0, hipEventDisableTiming | hipEventDisableSystemFence));
     HIP_OK(hipEventCreateWithFlags(&dc->mk1, hipEventDisableTiming | hipEventDisableSystemFence));
     dc->ticket.ensure(64);
@@ -62,6 +64,8 @@ void ctx_shutdown(Ctx &c) {
     (void)hipEventDestroy(dc->ev1);
     (void)hipEventDestroy(dc->es0);
     (void)hipEventDestroy(dc->mk0);
+    (void)hipEventDestroy(dc->er0);
+    (void)hipEventDestroy(dc->er1);
     (void)hipEventDestroy(dc->mk1);
     (void)hipEventDestroy(dc->es1);
     (void)hipStreamDestroy(dc->stream);

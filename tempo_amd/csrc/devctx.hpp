@@ -60,6 +60,14 @@ struct DeviceCtx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, es0 = nullptr, es1 = nullptr;
   hipEvent_t mk0 = nullptr, mk1 = nullptr;  // untimed markers around a launch
+  hipEvent_t er0 = nullptr, er1 = nullptr;  // timing of rerun launches
+  // search kernels timed by events stamped from their own dispatch packet
+  // (hipExtLaunchKernel start/stop events: what rocprofv3's kernel trace measures);
+  // TSG_EXT_EVENTS=0: marker events recorded on the stream before and after the launch
+  bool ext_events = [] {
+    const char *e = std::getenv("TSG_EXT_EVENTS");
+    return !e || std::atoi(e) != 0;
+  }();
   // TSG_MARK (default 0, experiment): bit 0 = an untimed marker event recorded right
   // before each search launch, bit 1 = one right after it. An apparent 16 us/step gain
   // was NUMA placement of the polling thread (profiles/r01_host); with the thread on the
@@ -138,9 +146,12 @@ struct DeviceCtx {
   // tail at every size (tests)
   uint32_t pool_small = env_u32("TSG_POOL_SMALL", 32, 0, 1u << 20);
   uint32_t pool_seg = 32;  // host segment records per workgroup (adaptive: grows on overflow, halves when sparse)
-  // TSG_POOL_STATIC=0: the claim-based pool kernel (LDS claims + dynamic chunks) instead of
-  // the static-run kernel (search_static_kernel)
-  bool pool_static = env_u32("TSG_POOL_STATIC", 1, 0, 1) != 0;
+  // Launches below TSG_POOL_STATIC_UNITS units per workgroup (default 32: ~4 M entries, a
+  // limit query's waves, one block) run the static-run kernel (search_static_kernel: its
+  // first loads go out before anything is staged; limit-wave kernel 16.4 vs 18.3 us);
+  // larger ones the claim-based pool kernel, whose dynamic tail evens the CUs out (config-3
+  // share 287 vs 319 us, profiles/r03_ab). 0: always the pool kernel; a huge value: always static.
+  uint32_t pool_static_units = env_u32("TSG_POOL_STATIC_UNITS", 32, 0, 1u << 30);
   // large dictionaries matched as one byte stream (dict_stream_kernel); 0: a lane per value
   bool dict_stream = env_u32("TSG_DICT_STREAM", 1, 0, 1) != 0;
   DevBuf pool_head;  // two dynamic-chunk counters (128 B apart): a launch uses one, zeroes the other

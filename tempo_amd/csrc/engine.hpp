@@ -161,6 +161,12 @@ struct V2Block {
   uint8_t *d_rec_ids = nullptr; // total_records x 16
   uint64_t *d_rec_start = nullptr;
   uint32_t *d_rec_len = nullptr;
+  // index directory (lookup.hip d_post): the records share their first dir_cp id bytes
+  // (dir_prefix); dir[b] = first record whose next 32 id bits, top dir_bits of them, are
+  // >= b (2^dir_bits + 1 entries). Null when the index is short or not sorted.
+  uint32_t *d_dir = nullptr;
+  uint32_t dir_bits = 0, dir_cp = 0;
+  uint8_t dir_prefix[16] = {};
   uint64_t *d_shard_m = nullptr, *d_shard_k = nullptr, *d_shard_bitlen = nullptr, *d_shard_woff = nullptr;
   // the data file (compressed pages) resident for findOne on the device; enc = meta.json
   // "encoding" (backend.Encoding)

@@ -37,9 +37,12 @@ struct LkBlock {
   const uint64_t *rec_start;
   const uint32_t *rec_len;
   uint32_t shards, records;
-  uint8_t min_id[16], max_id[16];
   uint32_t min_len, max_len;
-  uint32_t block_idx, pad;
+  uint32_t block_idx, dir_bits;
+  const uint32_t *dir;    // index directory (V2Block::d_dir) or null
+  uint64_t pfx[2], pmask[2];  // the records' common id prefix (dir_cp bytes, big-endian halves) and its mask
+  uint64_t mn[2], mx[2];      // min_id / max_id zero-padded to 16 bytes, big-endian halves
+  uint32_t dir_cp, pad;
 };
 
 struct LkSlab {
@@ -124,25 +127,53 @@ __device__ __forceinline__ uint64_t d_mod(uint64_t x, uint64_t m, uint64_t magic
   while (r >= m) r -= m;
   return r;
 }
-__device__ __forceinline__ int d_cmp16(const uint8_t *a, const uint8_t *b, uint32_t bl) {  // bytes.Compare(a[16], b)
-  uint32_t n = bl < 16 ? bl : 16;
-  for (uint32_t i = 0; i < n; i++)
-    if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
-  return 16 == bl ? 0 : (16 < bl ? -1 : 1);
-}
 
 // includeBlock's id range + index lower_bound: first record with
-// bytes.Compare(rec.ID, id) >= 0 (pkg/sort/search.go:5-24), a hit if < TotalRecords
+// bytes.Compare(rec.ID, id) >= 0 (pkg/sort/search.go:5-24), a hit if < TotalRecords.
+// With a directory the search starts in the id's bucket: every record of an earlier
+// bucket is below the id and every record of a later one above it, so the lower bound
+// lies in [dir[b], dir[b+1]] — the same record sort.Search finds over the whole index,
+// after ~2 line fetches instead of the ~6 bottom levels of a 1.6 MB binary search
+// that miss L2 (trace ids are uniform hashes: a handful of records per bucket).
+__device__ __forceinline__ uint64_t d_bswap64(uint64_t x) { return __builtin_bswap64(x); }
+// bytes.Compare of two 16-byte ids held as big-endian halves
+__device__ __forceinline__ int d_cmp128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+  if (ah != bh) return ah < bh ? -1 : 1;
+  if (al != bl) return al < bl ? -1 : 1;
+  return 0;
+}
 __device__ __forceinline__ int32_t d_post(const LkBlock &B, const uint8_t *id) {
-  if (d_cmp16(id, B.min_id, B.min_len) < 0 || d_cmp16(id, B.max_id, B.max_len) > 0) return -1;
+  // the id as a 128-bit big-endian number (constant byte indices: stays in registers)
+  uint64_t ihi = 0, ilo = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    ihi = (ihi << 8) | id[q];
+    ilo = (ilo << 8) | id[8 + q];
+  }
+  // bytes.Compare(id, min/max) with the meta ids zero-padded to 16 bytes: equal padded
+  // means equal first len bytes, and then the 16-byte id is the longer, greater one
+  int cmin = d_cmp128(ihi, ilo, B.mn[0], B.mn[1]);
+  if (cmin == 0 && B.min_len < 16) cmin = 1;
+  int cmax = d_cmp128(ihi, ilo, B.mx[0], B.mx[1]);
+  if (cmax == 0 && B.max_len < 16) cmax = 1;
+  if (cmin < 0 || cmax > 0) return -1;
   uint32_t lo = 0, hi = B.records;
-  while (lo < hi) {
-    uint32_t mid = (lo + hi) >> 1;
-    const uint8_t *r = B.rec_ids + uint64_t(mid) * 16;
-    int c = 0;
-    for (int q = 0; q < 16 && c == 0; q++)
-      if (r[q] != id[q]) c = r[q] < id[q] ? -1 : 1;
-    if (c < 0) lo = mid + 1;
+  if (B.dir) {
+    const uint64_t mhi = B.pmask[0], mlo = B.pmask[1];
+    const uint64_t ph = B.pfx[0], pl = B.pfx[1];
+    if ((ihi & mhi) != ph) return (ihi & mhi) < ph ? (B.records ? 0 : -1) : -1;  // below / above every record
+    if ((ilo & mlo) != pl) return (ilo & mlo) < pl ? (B.records ? 0 : -1) : -1;
+    const uint32_t s = 8 * B.dir_cp;  // the 32 id bits after the prefix
+    const uint64_t top = s == 0 ? ihi : s < 64 ? (ihi << s) | (ilo >> (64 - s)) : ilo << (s - 64);
+    const uint32_t bk = uint32_t(top >> 32) >> (32 - B.dir_bits);
+    lo = B.dir[bk];
+    hi = B.dir[bk + 1];
+  }
+  while (lo < hi) {  // (a record is one 16-byte load)
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint4 v = *reinterpret_cast<const uint4 *>(B.rec_ids + uint64_t(mid) * 16);
+    const uint64_t rh = d_bswap64(uint64_t(v.x) | uint64_t(v.y) << 32), rl = d_bswap64(uint64_t(v.z) | uint64_t(v.w) << 32);
+    if (d_cmp128(rh, rl, ihi, ilo) < 0) lo = mid + 1;
     else hi = mid;
   }
   return lo < B.records ? int32_t(lo) : -1;
@@ -536,6 +567,38 @@ void v2block_open(Ctx &c, V2Block &b, const std::string &dir, int device_hint) {
     rs[i] = recs[i].start;
     rl[i] = recs[i].length;
   }
+  // index directory (d_post): only over a sorted index (the writer's invariant; an
+  // unsorted one keeps the plain binary search, whose answer the directory would not
+  // reproduce). TSG_LK_DIR=0 turns it off.
+  std::vector<uint32_t> rdir;
+  static const bool dir_on = [] {
+    const char *e = std::getenv("TSG_LK_DIR");
+    return !e || std::atoi(e) != 0;
+  }();
+  const size_t n = recs.size();
+  bool sorted = n == b.total_records;
+  for (size_t i = 1; i < n && sorted; i++) sorted = std::memcmp(&rid[(i - 1) * 16], &rid[i * 16], 16) <= 0;
+  if (dir_on && sorted && n >= 64) {
+    uint32_t cp = 0;
+    while (cp < 12 && rid[cp] == rid[(n - 1) * 16 + cp]) cp++;  // (sorted: every record shares it)
+    uint32_t bits = 0;
+    while ((size_t(2) << bits) <= n / 4 && bits < 20) bits++;  // ~4 records per bucket
+    bits = std::max(bits, 1u);
+    rdir.assign((size_t(1) << bits) + 1, uint32_t(n));
+    auto bucket = [&](size_t r) {
+      uint32_t key = 0;
+      for (uint32_t q = 0; q < 4; q++) key = (key << 8) | rid[r * 16 + cp + q];
+      return key >> (32 - bits);
+    };
+    size_t bk = 0;
+    for (size_t r = 0; r < n; r++) {
+      const size_t k = bucket(r);
+      while (bk <= k) rdir[bk++] = uint32_t(r);
+    }
+    b.dir_bits = bits;
+    b.dir_cp = cp;
+    std::memcpy(b.dir_prefix, rid.data(), cp);
+  }
   std::lock_guard<std::mutex> lk(dc.mu);
   HIP_OK(hipSetDevice(dc.ordinal));
   auto up = [&](const void *src, size_t bytes) {
@@ -547,6 +610,7 @@ void v2block_open(Ctx &c, V2Block &b, const std::string &dir, int device_hint) {
   b.d_rec_ids = static_cast<uint8_t *>(up(rid.data(), rid.size()));
   b.d_rec_start = static_cast<uint64_t *>(up(rs.data(), rs.size() * 8));
   b.d_rec_len = static_cast<uint32_t *>(up(rl.data(), rl.size() * 4));
+  if (!rdir.empty()) b.d_dir = static_cast<uint32_t *>(up(rdir.data(), rdir.size() * 4));
   // the data file for findOne on the device (pages stay compressed in HBM)
   b.enc = enc.empty() ? -1 : parse_encoding(enc);
   std::vector<uint8_t> data;
@@ -592,11 +656,23 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
     k.rec_len = b.d_rec_len;
     k.shards = b.shards;
     k.records = b.total_records;
-    std::memcpy(k.min_id, b.min_id.data(), b.min_id.size());
-    std::memcpy(k.max_id, b.max_id.data(), b.max_id.size());
     k.min_len = uint32_t(b.min_id.size());
+    for (uint32_t q = 0; q < 16; q++) {
+      k.mn[q / 8] |= uint64_t(q < b.min_id.size() ? b.min_id[q] : 0u) << (56 - 8 * (q % 8));
+      k.mx[q / 8] |= uint64_t(q < b.max_id.size() ? b.max_id[q] : 0u) << (56 - 8 * (q % 8));
+    }
     k.max_len = uint32_t(b.max_id.size());
     k.block_idx = bp.first;
+    if (b.d_dir) {
+      k.dir = b.d_dir;
+      k.dir_bits = b.dir_bits;
+      k.dir_cp = b.dir_cp;
+      for (uint32_t q = 0; q < 16; q++) {  // big-endian halves of the prefix and its mask
+        const uint64_t byte = q < b.dir_cp ? b.dir_prefix[q] : 0u, m = q < b.dir_cp ? 0xffu : 0u;
+        k.pfx[q / 8] |= byte << (56 - 8 * (q % 8));
+        k.pmask[q / 8] |= m << (56 - 8 * (q % 8));
+      }
+    }
     lb.push_back(k);
   }
   out = LookupOut();

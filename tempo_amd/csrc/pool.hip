@@ -1,6 +1,7 @@
 // pool.hip — MI355X (gfx950) pool search: narrow full scans (limit 0) of Tempo search
 // blocks with one workgroup per CU and a CU-wide work pool. The same predicates,
 // records and result order as search_fast_kernel (search.hip); see DESIGN.md §4.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -612,8 +613,9 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     HIP_OK(hipMemsetAsync(dc.stamps.p, 0, size_t(W) * kStampSlots * 8, s));
     PA.stamps = static_cast<unsigned long long *>(dc.stamps.p);
   }
-  const PoolFn fn = dc.pool_static ? pick_static(q.nterms, has_dur, q.has_range, dc.pool_nt)
-                                   : pick_pool(q.nterms, has_dur, q.has_range, dc.pool_nt);
+  const bool use_static = uint64_t(U) < uint64_t(dc.pool_static_units) * W;
+  const PoolFn fn = use_static ? pick_static(q.nterms, has_dur, q.has_range, dc.pool_nt)
+                               : pick_pool(q.nterms, has_dur, q.has_range, dc.pool_nt);
   if (!dc.pool_attr.count(reinterpret_cast<const void *>(fn))) {
     HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                int(kPoolLds)));
@@ -639,12 +641,21 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     PA.head_next = heads + 32 * (dc.pool_parity ^ 1u);
     std::fill_n(counts, W, kCountPending);  // (each workgroup stores its count last)
     if (first && time_all) HIP_OK(hipEventRecord(dc.ev0, s));
-    if (first && (time_scan || defer)) HIP_OK(hipEventRecord(e0, s));
-    fn<<<W, threads, kPoolLds, s>>>(PA);
-    HIP_OK(hipGetLastError());
-    if (first && (time_scan || defer)) HIP_OK(hipEventRecord(e1, s));
+    // timing: the first launch on e0/e1 (scan time or a deferred pair), a rerun on er0/er1
+    const bool timed = first ? (time_scan || defer) : time_scan;
+    hipEvent_t t0 = first ? e0 : dc.er0, t1 = first ? e1 : dc.er1;
+    if (timed && dc.ext_events) {  // stamped from the dispatch packet itself
+      void *kargs[] = {&PA};
+      HIP_OK(hipExtLaunchKernel(reinterpret_cast<const void *>(fn), dim3(W), dim3(threads), kargs, kPoolLds, s, t0,
+                                t1, 0));
+    } else {
+      if (timed) HIP_OK(hipEventRecord(t0, s));
+      fn<<<W, threads, kPoolLds, s>>>(PA);
+      HIP_OK(hipGetLastError());
+      if (timed) HIP_OK(hipEventRecord(t1, s));
+    }
     if (first && time_all) HIP_OK(hipEventRecord(dc.ev1, s));
-    if (!dc.pool_static) dc.pool_parity ^= 1u;  // (the static kernel claims nothing)
+    if (!use_static) dc.pool_parity ^= 1u;  // (the static kernel claims nothing)
   };
   // completion: every workgroup's count (stored after its records completed, read with
   // acquire loads); finished segments are pulled into this core's caches meanwhile; the
@@ -718,14 +729,12 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       while (want < maxc) want <<= 1;
       dc.pool_seg = std::min(want, rec_cap);
       // a rerun produces the records: its time counts too
-      if (time_scan) HIP_OK(hipEventRecord(dc.mk0, s));
       launch(false);
-      if (time_scan) HIP_OK(hipEventRecord(dc.mk1, s));
       wait();
       if (time_scan) {
         float ms = 0;
-        HIP_OK(hipEventSynchronize(dc.mk1));
-        HIP_OK(hipEventElapsedTime(&ms, dc.mk0, dc.mk1));
+        HIP_OK(hipEventSynchronize(dc.er1));
+        HIP_OK(hipEventElapsedTime(&ms, dc.er0, dc.er1));
         rerun_ms += ms;
       }
       reruns++;

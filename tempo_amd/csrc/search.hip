@@ -2130,11 +2130,10 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       pre[6] = A.mask_words;
       pre[7] = A.nterms;
     }
-    hipEvent_t e0 = dc.es0, e1 = dc.es1;
-    const bool timed = first && time_scan;
+    hipEvent_t e0 = first ? dc.es0 : dc.er0, e1 = first ? dc.es1 : dc.er1;
+    const bool timed = time_scan;  // (a rerun's launch is timed too: it produces the records)
     const bool defer = first && !timed && time_defer && dc.defer_slot(e0, e1);
-    static const bool ext_events = std::getenv("TSG_EXT_EVENTS") != nullptr;
-    if ((timed || defer) && ext_events) {  // events stamped from the dispatch packet (hipExtLaunchKernel)
+    if ((timed || defer) && dc.ext_events) {  // events stamped from the dispatch packet (hipExtLaunchKernel)
       if (fast) A.P = P;
       void *fargs[] = {&pre[0], &pre[1], &pre[2], &pre[3], &pre[4], &pre[5], &pre[6], &pre[7], &P.stamps, &A};
       void *sargs[] = {&P};
@@ -2245,15 +2244,13 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   tr.mark("events");
   // a rerun produces the records: its time counts too, and the reruns are counted
   auto rerun_timed = [&] {
-    if (time_scan) HIP_OK(hipEventRecord(dc.mk0, s));
-    launch(false);
-    if (time_scan) HIP_OK(hipEventRecord(dc.mk1, s));
+    launch(false);  // (timed with er0/er1 under time_scan)
     wait();
     check();
     if (time_scan) {
       float rms = 0;
-      HIP_OK(hipEventSynchronize(dc.mk1));
-      HIP_OK(hipEventElapsedTime(&rms, dc.mk0, dc.mk1));
+      HIP_OK(hipEventSynchronize(dc.er1));
+      HIP_OK(hipEventElapsedTime(&rms, dc.er0, dc.er1));
       out.scan_ns += uint64_t(double(rms) * 1e6);
       if (time_all) out.kernel_ns += uint64_t(double(rms) * 1e6);
     }

@@ -75,14 +75,17 @@ def ragged(tmp_path_factory):
 
 @pytest.fixture(scope="module")
 def dyn_engine():
-    """An engine that keeps the dynamic tail (device-counter chunks) at every search size
-    (TSG_POOL_SMALL=0; by default a search under 32 static units per workgroup, i.e.
-    under ~5 M entries, is split statically whole)."""
+    """An engine that runs the claim-based pool kernel at every search size and keeps its
+    dynamic tail (device-counter chunks) there (TSG_POOL_STATIC_UNITS=0, TSG_POOL_SMALL=0).
+    By default a search under 32 units per workgroup (~4 M entries: every set in this file)
+    runs the static-run kernel, so the default engine covers that one."""
     os.environ["TSG_POOL_SMALL"] = "0"
+    os.environ["TSG_POOL_STATIC_UNITS"] = "0"
     try:
         e = T.Engine()
     finally:
         del os.environ["TSG_POOL_SMALL"]
+        del os.environ["TSG_POOL_STATIC_UNITS"]
     yield e
     e.close()
 

@@ -20,6 +20,13 @@ if has live; then
   rc=$?; echo "pytest live rc=$rc"; tail -15 gpurun_out/pytest_live.log
   ok_rc $rc || exit $rc
 fi
+if has core; then  # the search-kernel tests (pool/static kernels, limits, coalescer, configs, damaged blocks)
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_pool.py tests/test_gpu_search.py tests/test_gpu_coalesce.py \
+    tests/test_gpu_configs.py tests/test_gpu_damaged.py tests/test_gpu_lookup.py -x -v --timeout 200 --timeout-method thread \
+    -p no:cacheprovider > gpurun_out/pytest_core.log 2>&1
+  rc=$?; echo "pytest core rc=$rc"; tail -4 gpurun_out/pytest_core.log
+  [ $rc -eq 0 ] || exit $rc
+fi
 if has gputest; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
@@ -43,6 +50,22 @@ if has lookup; then
     [ $rc -eq 0 ] || exit $rc
   done
 fi
+if has lkprof; then  # config-5 lookup: per-kernel times and line traffic of the count pass
+  export TMPDIR=/tmp
+  LKA="--cpu-sample 0 --check 2000 --steps 3"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/lkprof -o run --output-format csv -- \
+    python3 tools/bench_lookup.py $LKA > gpurun_out/lkprof.json 2> gpurun_out/lkprof.err
+  rc=$?; echo "lk rocprof rc=$rc"; cat gpurun_out/lkprof/run_kernel_stats.csv 2>/dev/null || find gpurun_out/lkprof -name "*stats.csv"
+  [ $rc -eq 0 ] || exit $rc
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 -s KILL 300 rocprofv3 --pmc $c -d gpurun_out/lkpmc_$c -o run --output-format csv -- \
+      python3 tools/bench_lookup.py $LKA > gpurun_out/lkpmc_$c.json 2> gpurun_out/lkpmc_$c.err
+    rc=$?; echo "lk pmc $c rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+  done
+  python3 tools/pmc_summary.py gpurun_out/lkpmc_FETCH_SIZE gpurun_out/lkpmc_WRITE_SIZE --match lookup \
+    --workload "lookup,blocks=200,objects=100000,probes=10000000" --source "tools/gpu_r3.sh lkprof" | tee gpurun_out/lkpmc_summary.txt
+fi
 if has scanprobe; then
   hipcc -O3 --offload-arch=gfx950 tools/scan_probe.hip -o gpurun_out/scan_probe || exit 1
   timeout -k 10 180 gpurun_out/scan_probe > gpurun_out/scan_probe.json 2>&1
@@ -54,6 +77,27 @@ if has stamps; then
     --mall-steps 0 ${BENCH_ARGS:-} > gpurun_out/stamps.json 2> gpurun_out/stamps.err
   rc=$?; echo "stamps rc=$rc"; grep "stamps" gpurun_out/stamps.err | tail -6
   [ $rc -eq 0 ] || exit $rc
+fi
+if has ab; then  # the static-run kernel vs the claim-based pool kernel, same box, same legs
+  for st in 1 0; do
+    TSG_POOL_STATIC=$st timeout -k 10 400 python bench.py --steps 400 --cpu-baseline 0 --concurrent-steps 0 --cfg4 0 \
+      --mall-steps 0 ${BENCH_ARGS:-} > gpurun_out/ab_static$st.json 2> gpurun_out/ab_static$st.err
+    rc=$?; echo "ab static=$st rc=$rc"; tail -2 gpurun_out/ab_static$st.err
+    [ $rc -eq 0 ] || exit $rc
+    TSG_POOL_STATIC=$st TSG_STAMPS=1 timeout -k 10 300 python bench.py --steps 6 --warmup 2 --cpu-baseline 0 --cfg3 0 \
+      --concurrent-steps 0 --cfg4 0 --shim-steps 0 --limit-steps 4 --mall-steps 0 > gpurun_out/stamps_static$st.json 2> gpurun_out/stamps_static$st.err
+    rc=$?; echo "stamps static=$st rc=$rc"; grep "stamps" gpurun_out/stamps_static$st.err | tail -4
+    [ $rc -eq 0 ] || exit $rc
+  done
+  python3 - <<'PY'
+import json
+for st in (1, 0):
+    d = json.load(open(f"gpurun_out/ab_static{st}.json"))
+    print(st, "value", round(d["value"] / 1e9, 1), "frac", round(d["roofline"]["frac"], 3), "kernel", d["latency_us"]["kernel"],
+          "lim20", d["limit20"]["kernel_us"]["p50"], d["limit20"]["step_us"]["p50"],
+          "cfg3", d["cfg3"]["full_scan"]["kernel_us"]["p50"], d["cfg3"]["limit20"]["time_to_first_20_us"]["p50"],
+          "shim", d["shim"]["query_us"]["p50"], d["shim"]["vs_batched"])
+PY
 fi
 if has quick; then
   timeout -k 10 600 python bench.py --steps 200 --cpu-baseline 0 --cfg3 0 --concurrent-steps 0 ${BENCH_ARGS:-} \

@@ -33,12 +33,13 @@ def main():
     ap.add_argument("--out", help="merge into this JSON file (profiles/pmc_traffic.json) under --workload")
     ap.add_argument("--workload", default="blocks=10,entries=1000000")
     ap.add_argument("--source", default="", help="where the passes came from (recorded next to the numbers)")
+    ap.add_argument("--match", default="search,prep,dict", help="kernel name substrings to report (comma list)")
     args = ap.parse_args()
     fetch = per_kernel(args.fetch_dir, "FETCH_SIZE")
     write = per_kernel(args.write_dir, "WRITE_SIZE")
     out = {}
     for k in sorted(set(fetch) | set(write)):
-        if "search" not in k and "prep" not in k:
+        if not any(m in k for m in args.match.split(",")):
             continue
         f = fetch.get(k, [])
         w = write.get(k, [])
