@@ -875,6 +875,9 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
       break;
     }
     // leader: give callers still on their way a moment to queue (bounded)
+    const bool prof = prof_on();
+    const auto t_lead = std::chrono::steady_clock::now();
+    if (prof) prof_add("coal.lead_after_us", std::chrono::duration<double, std::micro>(t_lead - t_wait).count());
     if (window_ns) {
       const auto t0 = std::chrono::steady_clock::now();
       while (ctx->approaching.load(std::memory_order_acquire) > 0 &&
@@ -913,6 +916,10 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
         take(k);
       }
       c.pending.erase(std::remove(c.pending.begin(), c.pending.end(), nullptr), c.pending.end());
+    }
+    if (prof) {
+      prof_add("coal.window_us", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_lead).count());
+      prof_add("coal.batch_callers", double(batch.size()));
     }
     if (batch.size() == 1) {  // alone: straight into the caller's output
       try {
@@ -961,8 +968,10 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
     for (auto *x : batch) x->done.store(true, std::memory_order_release);
     c.busy.store(false, std::memory_order_release);
     c.wake();
+    if (prof) prof_add("coal.lead_total_us", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_lead).count());
     break;
   }
+  if (prof_on()) prof_add("coal.call_us", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_wait).count());
   if (r.err) std::rethrow_exception(r.err);
 }
 

@@ -60,6 +60,7 @@ struct LkParams {
   const uint32_t *direct;    // block ordinals probed one by one (ascending)
   const uint8_t *ids;
   uint64_t nids;
+  uint32_t pair, pad0;  // slab probes two at a time (TSG_LK_PAIR, default 1)
   unsigned long long epoch, ticket_base;
   unsigned long long *ticket, *gran;
   uint64_t *offsets;  // per id: first output slot
@@ -205,8 +206,41 @@ __device__ __forceinline__ void for_each_hit(const LkParams &P, const uint8_t *i
 #pragma unroll
     for (int q = 0; q < 8; q++)  // (columns past J are zero in the table too)
       v[q] = uint32_t(q) * 32 >= S.J ? 0u : uint32_t(q + 1) * 32 <= S.J ? ~0u : (1u << (S.J % 32)) - 1u;
-    // (probes stay a chain with an early exit: issuing all k loads up front needs ~130
-    // VGPRs, and at 3 waves/SIMD the count pass measured 2.35 ms vs 1.74 ms, config 5)
+    // Probes go out two at a time with an early exit after each pair (issuing all k loads
+    // up front needs ~130 VGPRs, and at 3 waves/SIMD the count pass measured 2.35 ms vs
+    // 1.74 ms for the one-at-a-time chain, config 5). A pair's second position repeats the
+    // first past k: AND is idempotent. P.pair = 0: the one-at-a-time chain.
+    if (P.pair) {
+      for (uint64_t i = 0; i < S.k; i += 2) {
+        const uint64_t i1 = i + 1 < S.k ? i + 1 : i;
+        const uint64_t l0 = d_mod(h[i % 2] + i * h[2 + (((i + (i % 2)) % 4) / 2)], S.m, S.m_magic);
+        const uint64_t l1 = d_mod(h[i1 % 2] + i1 * h[2 + (((i1 + (i1 % 2)) % 4) / 2)], S.m, S.m_magic);
+        if (l0 >= S.bitlen || l1 >= S.bitlen) {
+#pragma unroll
+          for (int q = 0; q < 8; q++) v[q] = 0;
+          break;
+        }
+        const uint32_t *p0 = base + l0 * W, *p1 = base + l1 * W;
+        if (W == 8) {
+          const uint4 a0 = *reinterpret_cast<const uint4 *>(p0), b0 = *reinterpret_cast<const uint4 *>(p0 + 4);
+          const uint4 a1 = *reinterpret_cast<const uint4 *>(p1), b1 = *reinterpret_cast<const uint4 *>(p1 + 4);
+          v[0] &= a0.x & a1.x; v[1] &= a0.y & a1.y; v[2] &= a0.z & a1.z; v[3] &= a0.w & a1.w;
+          v[4] &= b0.x & b1.x; v[5] &= b0.y & b1.y; v[6] &= b0.z & b1.z; v[7] &= b0.w & b1.w;
+        } else if (W == 4) {
+          const uint4 a0 = *reinterpret_cast<const uint4 *>(p0), a1 = *reinterpret_cast<const uint4 *>(p1);
+          v[0] &= a0.x & a1.x; v[1] &= a0.y & a1.y; v[2] &= a0.z & a1.z; v[3] &= a0.w & a1.w;
+        } else if (W == 2) {
+          const uint2 a0 = *reinterpret_cast<const uint2 *>(p0), a1 = *reinterpret_cast<const uint2 *>(p1);
+          v[0] &= a0.x & a1.x; v[1] &= a0.y & a1.y;
+        } else {
+          v[0] &= p0[0] & p1[0];
+        }
+        uint32_t any = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) any |= v[q];
+        if (!any) break;
+      }
+    } else
     for (uint64_t i = 0; i < S.k; i++) {
       uint64_t loc = d_mod(h[i % 2] + i * h[2 + (((i + (i % 2)) % 4) / 2)], S.m, S.m_magic);
       if (loc >= S.bitlen) {
@@ -776,6 +810,11 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
   P.ndirect = uint32_t(direct.size());
   P.ids = dd + desc_bytes;
   P.nids = nids;
+  static const uint32_t pair = [] {
+    const char *e = std::getenv("TSG_LK_PAIR");
+    return e ? uint32_t(std::atoi(e) != 0) : 1u;
+  }();
+  P.pair = pair;
   P.epoch = dc.epoch;
   P.ticket_base = dc.ticket_base;
   P.ticket = static_cast<unsigned long long *>(dc.ticket.p);

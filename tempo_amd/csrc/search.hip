@@ -224,10 +224,11 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
 // SWAR test of the needle's first two bytes at all 16 positions of a lane picks the
 // candidates, the rest of the needle is compared from LDS, and a verified start maps to
 // its value through the value offsets staged in LDS. Bytes are read once from HBM.
-constexpr uint32_t kStreamSpan = 64u << 10;     // start positions per wave
+constexpr uint32_t kStreamSpan = 64u << 10;     // start positions per wave (at most; see stream_span)
 constexpr uint32_t kStreamMaxNeedle = 1024;     // the 2 KiB window holds any match that starts in its first half
 constexpr uint64_t kStreamMinBytes = 1u << 20;  // smaller dictionaries: prep_kernel (lane per value)
 constexpr uint32_t kStreamOffs = 128;           // value offsets staged per reload
+constexpr int kStreamAhead = 4;                 // KiB loaded ahead of the window, per wave
 struct StreamJob {
   const uint8_t *base;  // 16-byte aligned: the dictionary bytes start at base + lead
   const uint32_t *off;  // value offsets, nvals + 1
@@ -257,7 +258,8 @@ __device__ __forceinline__ uint32_t value_at(const uint32_t *off, uint32_t lo, u
 }
 
 extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const StreamJob *jobs, uint32_t njobs,
-                                                                    const uint8_t *needles, uint8_t *vmatch) {
+                                                                    const uint8_t *needles, uint8_t *vmatch,
+                                                                    uint32_t span) {
   __shared__ __attribute__((aligned(16))) uint8_t s_win[2048 + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_nd[kStreamMaxNeedle];
   __shared__ uint32_t s_off[kStreamOffs + 1];
@@ -269,10 +271,10 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
   const StreamJob J = jobs[j];
   const uint32_t nl = J.needle_len;
   const uint64_t end = uint64_t(J.lead) + J.nbytes;  // aligned coordinates of the last byte + 1
-  const uint64_t s0 = uint64_t(w - J.wave0) * kStreamSpan;
+  const uint64_t s0 = uint64_t(w - J.wave0) * span;
   // start positions q (aligned coordinates) of this wave: [qlo, qhi)
   const uint64_t qlo = max<uint64_t>(s0, J.lead);
-  const uint64_t qhi = min<uint64_t>(s0 + kStreamSpan, end >= nl ? end - nl + 1 : 0);
+  const uint64_t qhi = min<uint64_t>(s0 + span, end >= nl ? end - nl + 1 : 0);
   if (qlo >= qhi) return;
   for (uint32_t i = lane; i < nl; i += 64) s_nd[i] = needles[J.needle_off + i];
   const uint32_t n0 = uint32_t(needles[J.needle_off]) * 0x01010101u;
@@ -292,10 +294,15 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
   };
   stage_offs(vb);
   uint64_t cq = s0;
-  u32x4 cur = load16(cq + lane * 16), nxt = load16(cq + 1024 + lane * 16);
+  // the next kStreamAhead KiB after the window stay in flight (registers): one 1 KiB load
+  // per step in flight kept the pass latency-bound at ~2.3 TB/s (bench cfg4, r03)
+  u32x4 ring[kStreamAhead + 2];  // ring[0] = the window's first KiB, ring[1] its second
+#pragma unroll
+  for (int k = 0; k < kStreamAhead + 2; k++) ring[k] = load16(cq + uint64_t(k) * 1024 + lane * 16);
   uint32_t last_v = 0xffffffffu;  // this lane's last marked value (skips repeats)
   for (; cq < qhi; cq += 1024) {
-    const u32x4 nn = load16(cq + 2048 + lane * 16);
+    const u32x4 nn = load16(cq + uint64_t(kStreamAhead + 2) * 1024 + lane * 16);
+    const u32x4 cur = ring[0], nxt = ring[1];
     __syncthreads();  // (previous window's readers done)
     reinterpret_cast<u32x4 *>(s_win)[lane] = cur;
     reinterpret_cast<u32x4 *>(s_win)[64 + lane] = nxt;
@@ -362,8 +369,9 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
         cm &= rel >= 16 ? 0u : ~((1u << uint32_t(rel)) - 1u);
       }
     }
-    cur = nxt;
-    nxt = nn;
+#pragma unroll
+    for (int k = 0; k < kStreamAhead + 1; k++) ring[k] = ring[k + 1];
+    ring[kStreamAhead + 1] = nn;
   }
 }
 
@@ -1603,7 +1611,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   needles.clear();
   auto &stream_jobs = ps.stream_jobs;
   stream_jobs.clear();
-  uint32_t stream_waves = 0;
+  uint32_t stream_waves = 0, stream_span = kStreamSpan;
   needle_off.assign(q.nterms, 0);
   for (uint32_t t = 0; t < q.nterms; t++) {
     needle_off[t] = uint32_t(needles.size());
@@ -1700,9 +1708,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
         sj.needle_off = needle_off[t];
         sj.needle_len = q.value_lens[t];
         sj.vmatch_base = jb.vmatch_base;
-        sj.wave0 = stream_waves;
-        stream_waves += uint32_t((sj.lead + sj.nbytes + kStreamSpan - 1) / kStreamSpan);
-        stream_jobs.push_back(sj);
+        stream_jobs.push_back(sj);  // (wave0: after the plan, once the span is known)
       } else if (!k.identity) {
         jb.vmatch_base = vmatch_total;
         vmatch_total += k.nvals;
@@ -2037,6 +2043,20 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     const size_t o_sp = align_up(o_sj + set_jobs.size() * 4, 16);
     const size_t o_nd = align_up(o_sp + set_items.size() * 4, 16);
     const size_t o_ws = align_up(o_nd + needles.size() + 1, 16);
+    // dictionary stream spans: ~16 waves per CU over the pass's bytes, 8-64 KiB each (one
+    // 64 KiB span per wave left a 91 MB dictionary with ~5 waves per CU: latency-bound)
+    if (!stream_jobs.empty()) {
+      uint64_t tot = 0;
+      for (const auto &sj : stream_jobs) tot += sj.lead + sj.nbytes;
+      uint64_t sp = tot / (uint64_t(std::max(dc.num_cu, 1)) * 16);
+      sp = std::min<uint64_t>(kStreamSpan, std::max<uint64_t>(8192, (sp + 1023) / 1024 * 1024));
+      stream_span = uint32_t(sp);
+      stream_waves = 0;
+      for (auto &sj : stream_jobs) {
+        sj.wave0 = stream_waves;
+        stream_waves += uint32_t((sj.lead + sj.nbytes + sp - 1) / sp);
+      }
+    }
     const size_t o_stj = align_up(o_ws + size_t(nwg) * 2, 16);
     const size_t total_desc = align_up(o_stj + stream_jobs.size() * sizeof(StreamJob), 16);
     dc.hdesc.ensure(total_desc);
@@ -2071,7 +2091,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     if (!stream_jobs.empty())
       dict_stream_kernel<<<stream_waves, 64, 0, s>>>(reinterpret_cast<const StreamJob *>(dd + o_stj),
                                                      uint32_t(stream_jobs.size()), dd + o_nd,
-                                                     static_cast<uint8_t *>(dc.vmatch.p));
+                                                     static_cast<uint8_t *>(dc.vmatch.p), stream_span);
     if (set_items.back())
       dict_sets_kernel<<<(set_items.back() + 255) / 256, 256, 0, s>>>(
           reinterpret_cast<const DictJob *>(dd + o_jobs), reinterpret_cast<const uint32_t *>(dd + o_sj),

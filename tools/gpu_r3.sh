@@ -22,7 +22,7 @@ if has live; then
 fi
 if has core; then  # the search-kernel tests (pool/static kernels, limits, coalescer, configs, damaged blocks)
   timeout -k 10 600 python -u -m pytest tests/test_gpu_pool.py tests/test_gpu_search.py tests/test_gpu_coalesce.py \
-    tests/test_gpu_configs.py tests/test_gpu_damaged.py tests/test_gpu_lookup.py -x -v --timeout 200 --timeout-method thread \
+    tests/test_gpu_configs.py tests/test_gpu_damaged.py tests/test_gpu_lookup.py tests/test_gpu_dict_stream.py -x -v --timeout 200 --timeout-method thread \
     -p no:cacheprovider > gpurun_out/pytest_core.log 2>&1
   rc=$?; echo "pytest core rc=$rc"; tail -4 gpurun_out/pytest_core.log
   [ $rc -eq 0 ] || exit $rc
@@ -45,8 +45,8 @@ if has lookup; then
   rc=$?; echo "lookup tests rc=$rc"; tail -3 gpurun_out/lk_tests.log
   [ $rc -eq 0 ] || exit $rc
   for d in 0 1; do
-    TSG_LK_DIR=$d timeout -k 10 400 python tools/bench_lookup.py --cpu-sample 0 ${LK_ARGS:-} > gpurun_out/lookup_dir$d.json 2> gpurun_out/lookup_dir$d.err
-    rc=$?; echo "lookup bench dir=$d rc=$rc"; cat gpurun_out/lookup_dir$d.json
+    TSG_LK_PAIR=$d timeout -k 10 400 python tools/bench_lookup.py --cpu-sample 0 ${LK_ARGS:-} > gpurun_out/lookup_pair$d.json 2> gpurun_out/lookup_pair$d.err
+    rc=$?; echo "lookup bench pair=$d rc=$rc"; cut -c1-260 gpurun_out/lookup_pair$d.json
     [ $rc -eq 0 ] || exit $rc
   done
 fi
@@ -98,6 +98,16 @@ for st in (1, 0):
           "cfg3", d["cfg3"]["full_scan"]["kernel_us"]["p50"], d["cfg3"]["limit20"]["time_to_first_20_us"]["p50"],
           "shim", d["shim"]["query_us"]["p50"], d["shim"]["vs_batched"])
 PY
+fi
+if has hostprof; then  # host phase times (TSG_PROF): the main line + limit-20, then the shim pattern alone
+  TSG_PROF=1 timeout -k 10 300 python bench.py --steps 300 --cpu-baseline 0 --concurrent-steps 0 --cfg3 0 --cfg4 0 \
+    --mall-steps 0 --shim-steps 0 > gpurun_out/hostprof_main.json 2> gpurun_out/hostprof_main.err
+  rc=$?; echo "hostprof main rc=$rc"; tail -30 gpurun_out/hostprof_main.err
+  [ $rc -eq 0 ] || exit $rc
+  TSG_PROF=1 timeout -k 10 300 python bench.py --steps 20 --cpu-baseline 0 --concurrent-steps 0 --cfg3 0 --cfg4 0 \
+    --mall-steps 0 --limit-steps 0 --shim-steps 300 > gpurun_out/hostprof_shim.json 2> gpurun_out/hostprof_shim.err
+  rc=$?; echo "hostprof shim rc=$rc"; tail -30 gpurun_out/hostprof_shim.err
+  [ $rc -eq 0 ] || exit $rc
 fi
 if has quick; then
   timeout -k 10 600 python bench.py --steps 200 --cpu-baseline 0 --cfg3 0 --concurrent-steps 0 ${BENCH_ARGS:-} \
