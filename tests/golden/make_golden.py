@@ -149,6 +149,129 @@ def instance_search_vectors():
     }
 
 
+# ---- cross-checks of the transcribed tables against the reference's test source -------
+# The tables above are typed out; these parsers read the same Go test tables as text and
+# main() refuses to write the fixture unless every case agrees (name, inputs, expectation).
+GO_CONST = {  # identifiers the tables use, checked against their declarations below
+    "trace.StatusCodeTag": ("pkg/model/trace/matches.go", r'StatusCodeTag\s*=\s*"([^"]*)"'),
+    "trace.StatusCodeError": ("pkg/model/trace/matches.go", r'StatusCodeError\s*=\s*"([^"]*)"'),
+}
+
+
+def go_const(name):
+    if name.startswith('"'):
+        return name.strip('"')
+    if name == "strconv.Itoa(int(v1.Status_STATUS_CODE_ERROR))":
+        src = open(os.path.join(REF, "pkg/tempopb/trace/v1/trace.pb.go")).read()
+        return re.search(r"Status_STATUS_CODE_ERROR\s+Status_StatusCode\s*=\s*(\d+)", src).group(1)
+    f, pat = GO_CONST[name]
+    return re.search(pat, open(os.path.join(REF, f)).read()).group(1)
+
+
+def go_cases(src, func):
+    """The {...} case literals of a table-driven test, as {field: raw Go expression}."""
+    body = src[src.index("func " + func + "("):]
+    body = body[body.index("}{") + 2: body.index("\n\t}\n")]
+    cases = []
+    for m in re.finditer(r"\n\t\t\{\n(.*?)\n\t\t\},", body, re.S):
+        f = {}
+        for line in m.group(1).split("\n"):
+            line = line.split("//")[0].strip().rstrip(",")
+            if ":" in line:
+                k, v = line.split(":", 1)
+                f[k.strip()] = v.strip()
+        cases.append(f)
+    return cases
+
+
+def go_map(expr):
+    """map[string]string{...} / map[string][]string{...} with constant keys and values."""
+    inner = expr[expr.index("{") + 1: expr.rindex("}")]
+    out = {}
+    for m in re.finditer(r'([\w."()]+(?:\([^)]*\)\))?)\s*:\s*(\{[^}]*\}|[\w."]+(?:\([^)]*\)\))?)', inner):
+        k, v = go_const(m.group(1)), m.group(2)
+        if v.startswith("{"):
+            out[k] = [go_const(x.strip()) for x in v[1:-1].split(",") if x.strip()]
+        else:
+            out[k] = go_const(v)
+    return out
+
+
+def go_dur(expr):
+    """time.Duration expressions of the tables: [-][n *] time.Unit."""
+    units = {"time.Millisecond": MS, "time.Second": SEC, "time.Minute": MIN}
+    e = expr.replace(" ", "")
+    sign = -1 if e.startswith("-") else 1
+    e = e.lstrip("-")
+    if "*" in e:
+        n, u = e.split("*")
+        return sign * int(n) * units[u]
+    return sign * units[e]
+
+
+def go_time(expr):
+    """time.Now()-relative timestamps at the fixed NOW_NS: .UnixNano() or uint32(...Unix())."""
+    e = expr.strip()
+    secs = e.startswith("uint32(")
+    if secs:
+        e = e[len("uint32("):-1]
+    ns = NOW_NS
+    m = re.match(r"time\.Now\(\)\.Add\((.*)\)\.Unix(Nano)?\(\)$", e)
+    if m:
+        ns += go_dur(m.group(1))
+    elif not re.match(r"time\.Now\(\)\.Unix(Nano)?\(\)$", e):
+        raise ValueError(expr)
+    return unix(ns) if secs else ns
+
+
+def go_num(expr):
+    return int(expr.replace("_", ""))
+
+
+def check_pipeline_tables(t):
+    src = open(os.path.join(REF, "tempodb/search/pipeline_test.go")).read()
+    got = [{"name": go_const(c["name"]), "data": go_map(c["searchData"]), "req": go_map(c["request"]),
+            "match": c["shouldMatch"] == "true"} for c in go_cases(src, "TestPipelineMatchesTags")]
+    assert got == t["tags"], ("TestPipelineMatchesTags", got)
+    got = [{"name": go_const(c["name"]), "start": go_time(c["spanStart"]), "end": go_time(c["spanEnd"]),
+            "min": go_num(c["minDurationMs"]), "max": go_num(c["maxDurationMs"]), "match": c["shouldMatch"] == "true"}
+           for c in go_cases(src, "TestPipelineMatchesTraceDuration")]
+    assert got == t["duration"], ("TestPipelineMatchesTraceDuration", got)
+    got = [{"name": go_const(c["name"]), "start": go_time(c["spanStart"]), "end": go_time(c["spanEnd"]),
+            "rs": go_time(c["reqStart"]) if "reqStart" in c else 0, "re": go_time(c["reqEnd"]) if "reqEnd" in c else 0,
+            "match": c["shouldMatch"] == "true"} for c in go_cases(src, "TestPipelineMatchesTraceStartEnd")]
+    assert got == t["start_end"], ("TestPipelineMatchesTraceStartEnd", got)
+    body = src[src.index("func TestPipelineMatchesBlock("):]
+    tag = re.search(r'commonBlock\.AddTag\("([^"]*)", "([^"]*)"\)', body).groups()
+    mn = go_dur(re.search(r"MinDur = uint64\((.*)\)", body).group(1))
+    mx = go_dur(re.search(r"MaxDur = uint64\((.*)\)", body).group(1))
+    hdr = t["block"]["header"]
+    assert hdr == {"tags": {tag[0]: [tag[1]]}, "min_dur_ns": mn, "max_dur_ns": mx}, ("block header", hdr)
+    got = []
+    for c in go_cases(src, "TestPipelineMatchesBlock"):
+        req = c.get("request", "&tempopb.SearchRequest{}")
+        inner = req[req.index("{") + 1: req.rindex("}")]
+        tags = re.search(r"Tags:\s*(map\[string\]string\{[^}]*\})", inner)
+        mnm = re.search(r"MinDurationMs:\s*([\d_]+)", inner)
+        mxm = re.search(r"MaxDurationMs:\s*([\d_]+)", inner)
+        got.append({"name": go_const(c["name"]), "req": go_map(tags.group(1)) if tags else {},
+                    "min": go_num(mnm.group(1)) if mnm else 0, "max": go_num(mxm.group(1)) if mxm else 0,
+                    "match": c["shouldMatch"] == "true"})
+    assert got == t["block"]["cases"], ("TestPipelineMatchesBlock", got)
+
+
+def check_contains_tag(t):
+    src = open(os.path.join(REF, "pkg/tempofb/searchdata_test.go")).read()
+    body = src[src.index("func TestContainsTag("):]
+    body = body[: body.index("\n}\n")]
+    entry = {}
+    for k, v in re.findall(r'm\.AddTag\("([^"]*)", "([^"]*)"\)', body):
+        entry.setdefault(k, []).append(v)
+    cases = [{"key": k, "value": v, "found": f == "true"}
+             for k, v, f in re.findall(r'\{"([^"]*)", "([^"]*)", (true|false)\}', body)]
+    assert entry == t["entry"] and cases == t["cases"], ("TestContainsTag", entry, cases)
+
+
 def main():
     out = {
         "_provenance": "transcribed from the reference's tests by tests/golden/make_golden.py",
@@ -174,6 +297,10 @@ def main():
             {"name": "too few shards", "fp": 0.01, "shard_size": 10, "estimated_objects": 1, "expected_shards": 1},
         ],
     }
+    check_pipeline_tables(out["pipeline"])
+    check_contains_tag(out["contains_tag"])
+    out["_provenance"] += ("; the pipeline and ContainsTag tables are checked case by case against the "
+                           "Go test source (check_pipeline_tables, check_contains_tag)")
     path = os.path.join(HERE, "known_answers.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
