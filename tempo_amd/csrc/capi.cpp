@@ -26,6 +26,21 @@
 // One persistent host thread per device for multi-device calls: a search or lookup whose
 // blocks span devices hands each further device's part to that device's worker (the caller
 // runs the first device's part itself) instead of starting a thread per device per call.
+// A lock for the short critical sections concurrent searches share (the coalescer's
+// queue, the result-holder pool): a contended std::mutex parks a caller in the kernel and
+// its wake-up costs tens of microseconds, more than the work it guards.
+struct SpinLock {
+  std::atomic<bool> f{false};
+  void lock() {
+    for (uint32_t n = 0;; n++) {
+      if (!f.load(std::memory_order_relaxed) && !f.exchange(true, std::memory_order_acquire)) return;
+      if (n < 4096) __builtin_ia32_pause();
+      else std::this_thread::yield();
+    }
+  }
+  void unlock() { f.store(false, std::memory_order_release); }
+};
+
 struct DevWorker {
   std::mutex m;
   std::condition_variable cv;
@@ -194,7 +209,7 @@ struct tsg_ctx {
     std::exception_ptr err;
   };
   struct Coalescer {
-    std::mutex m;
+    SpinLock m;
     std::vector<CoalReq *> pending;
     std::atomic<bool> busy{false};
     // waiters spin for about one launch, then park here until the leader hands off (an
@@ -208,14 +223,13 @@ struct tsg_ctx {
       cv.notify_all();
     }
   };
-  std::mutex comu;
-  std::unordered_map<const void *, std::unique_ptr<Coalescer>> coal;  // per DeviceCtx
+  // one per device, created at tsg_init (read without a lock afterwards)
+  std::vector<std::pair<const void *, std::unique_ptr<Coalescer>>> coal;
   std::atomic<int> approaching{0};  // searches that have not reached their device stage yet
   Coalescer &coalescer(const void *dc) {
-    std::lock_guard<std::mutex> lk(comu);
-    auto &c = coal[dc];
-    if (!c) c = std::make_unique<Coalescer>();
-    return *c;
+    for (auto &x : coal)
+      if (x.first == dc) return *x.second;
+    throw std::logic_error("coalescer: unknown device");
   }
 };
 // A search on its way to the device stage (tsg_ctx::approaching), until leave().
@@ -426,7 +440,7 @@ static_assert(offsetof(ResultHolder, pub) == 0, "pub first");
 // Result holders are recycled (a query per ~60 us allocates a dozen arrays and a name
 // arena; reusing them keeps allocation and first-touch page faults off the step)
 struct HolderPool {
-  std::mutex mu;
+  SpinLock mu;
   std::vector<ResultHolder *> free;
   ~HolderPool() {
     for (auto *h : free) delete h;
@@ -439,7 +453,7 @@ static HolderPool &holder_pool() {
 static ResultHolder *acquire_holder() {
   HolderPool &hp = holder_pool();
   {
-    std::lock_guard<std::mutex> lk(hp.mu);
+    std::lock_guard<SpinLock> lk(hp.mu);
     if (!hp.free.empty()) {
       ResultHolder *h = hp.free.back();
       hp.free.pop_back();
@@ -453,7 +467,7 @@ static void release_holder(ResultHolder *h) {
   HolderPool &hp = holder_pool();
   if (h->arena_cap <= (64u << 20) && h->start.capacity() <= (1u << 20)) {
     h->clear();
-    std::lock_guard<std::mutex> lk(hp.mu);
+    std::lock_guard<SpinLock> lk(hp.mu);
     if (hp.free.size() < 16) {
       hp.free.push_back(h);
       return;
@@ -536,6 +550,7 @@ int tsg_init(const tsg_options *opts, tsg_ctx **out) {
     auto *c = new tsg_ctx();
     try {
       ctx_init(c->c, opts);
+      for (auto *dc : c->c.devs) c->coal.emplace_back(dc, std::make_unique<tsg_ctx::Coalescer>());
     } catch (...) {
       ctx_shutdown(c->c);
       delete c;
@@ -845,7 +860,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
   r.flags = flags;
   r.out = &out;
   {
-    std::lock_guard<std::mutex> lk(c.m);
+    std::lock_guard<SpinLock> lk(c.m);
     c.pending.push_back(&r);
   }
   ap.leave();
@@ -894,7 +909,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
     blist.clear();
     owner.clear();
     {
-      std::lock_guard<std::mutex> lk(c.m);
+      std::lock_guard<SpinLock> lk(c.m);
       size_t nb = 0;
       auto take = [&](size_t k) {
         tsg_ctx::CoalReq *x = c.pending[k];
