@@ -109,6 +109,17 @@ if has hostprof; then  # host phase times (TSG_PROF): the main line + limit-20, 
   rc=$?; echo "hostprof shim rc=$rc"; tail -30 gpurun_out/hostprof_shim.err
   [ $rc -eq 0 ] || exit $rc
 fi
+if has sweep; then  # pool-kernel knobs on the main line (blocks generated once, reused)
+  W=/tmp/tsg_sweep; mkdir -p $W
+  for cfg in "20 4" "30 4" "30 3" "40 3" "20 3"; do
+    set -- $cfg
+    TSG_POOL_DYN=$1 TSG_POOL_CHUNK=$2 timeout -k 10 300 python bench.py --steps 400 --cpu-baseline 0 --concurrent-steps 0 \
+      --cfg3 0 --cfg4 0 --mall-steps 0 --shim-steps 0 --limit-steps 0 --workdir $W --events 2 > gpurun_out/sweep_$1_$2.json 2> gpurun_out/sweep_$1_$2.err
+    rc=$?; echo "sweep dyn=$1 chunk=$2 rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+    python3 -c "import json; d=json.load(open('gpurun_out/sweep_$1_$2.json')); print('  value', round(d['value']/1e9,1), 'frac', round(d['roofline']['frac'],3), 'kernel', d['latency_us']['kernel'])"
+  done
+fi
 if has quick; then
   timeout -k 10 600 python bench.py --steps 200 --cpu-baseline 0 --cfg3 0 --concurrent-steps 0 ${BENCH_ARGS:-} \
     > gpurun_out/quick.json 2> gpurun_out/quick.err
