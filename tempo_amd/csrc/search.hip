@@ -229,6 +229,8 @@ constexpr uint32_t kStreamMaxNeedle = 1024;     // the 2 KiB window holds any ma
 constexpr uint64_t kStreamMinBytes = 1u << 20;  // smaller dictionaries: prep_kernel (lane per value)
 constexpr uint32_t kStreamOffs = 128;           // value offsets staged per reload
 constexpr int kStreamAhead = 4;                 // KiB loaded ahead of the window, per wave
+constexpr int kWaitVm0 = 0x0F70;                // s_waitcnt vmcnt(0) (expcnt, lgkmcnt untouched)
+constexpr uint32_t kStreamHits = 2048;          // LDS list of matched values per wave
 struct StreamJob {
   const uint8_t *base;  // 16-byte aligned: the dictionary bytes start at base + lead
   const uint32_t *off;  // value offsets, nvals + 1
@@ -249,12 +251,21 @@ __device__ __forceinline__ uint32_t value_at(const uint32_t *off, uint32_t lo, u
   while (hi - lo > 1) {
     const uint32_t step = (hi - lo + 63) / 64;
     const uint32_t idx = lo + uint32_t(lane) * step;
-    const bool le = idx < hi && uint64_t(off[idx]) <= p;
+    const bool le = idx < hi && uint64_t(G(off)[idx]) <= p;  // (global: flat loads make every wait drain LDS too)
     const uint32_t c = uint32_t(__popcll(__ballot(le)));  // lanes 0..c-1 (monotone offsets)
     lo = lo + (c - 1) * step;
     hi = min(hi, lo + step);
   }
   return lo;
+}
+
+// The dictionary stream kernel runs one wave per workgroup: its LDS hand-offs between lanes
+// need no s_barrier, and __syncthreads()' fence would also wait for every global load in
+// flight (s_waitcnt vmcnt(0)), draining the read-ahead ring at each step. A single wave's LDS
+// operations execute in order; the asm keeps the compiler from moving memory accesses across.
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
 }
 
 extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const StreamJob *jobs, uint32_t njobs,
@@ -263,6 +274,8 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
   __shared__ __attribute__((aligned(16))) uint8_t s_win[2048 + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_nd[kStreamMaxNeedle];
   __shared__ uint32_t s_off[kStreamOffs + 1];
+  __shared__ uint32_t s_hit[kStreamHits];  // matched values not yet marked in vmatch
+  __shared__ uint32_t s_nhit;
   const int lane = threadIdx.x;
   const uint32_t w = blockIdx.x;
   uint32_t j = 0;
@@ -280,7 +293,7 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
   const uint32_t n0 = uint32_t(needles[J.needle_off]) * 0x01010101u;
   const uint32_t n1 = nl > 1 ? uint32_t(needles[J.needle_off + 1]) * 0x01010101u : 0u;
   auto load16 = [&](uint64_t a) -> u32x4 {  // a: aligned coordinate of this lane's 16 bytes
-    if (a < end) return *reinterpret_cast<const u32x4 *>(J.base + a);
+    if (a < end) return *G<u32x4>(J.base + a);
     return u32x4{0u, 0u, 0u, 0u};
   };
   // value offsets of the values around the window: s_off[i] = off[vb + i]
@@ -289,36 +302,53 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
   auto stage_offs = [&](uint32_t v) {
     vb = v;
     kv = min<uint32_t>(kStreamOffs, J.nvals - v);
-    for (uint32_t i = lane; i <= kv; i += 64) s_off[i] = J.off[v + i];
-    cover = kv == J.nvals - v ? ~0ull : uint64_t(J.off[v + kv]);
+    for (uint32_t i = lane; i <= kv; i += 64) s_off[i] = G(J.off)[v + i];
+    cover = kv == J.nvals - v ? ~0ull : uint64_t(G(J.off)[v + kv]);
   };
   stage_offs(vb);
   uint64_t cq = s0;
-  // the next kStreamAhead KiB after the window stay in flight (registers): one 1 KiB load
-  // per step in flight kept the pass latency-bound at ~2.3 TB/s (bench cfg4, r03)
-  u32x4 ring[kStreamAhead + 2];  // ring[0] = the window's first KiB, ring[1] its second
+  // ring slots: the window's two KiB + kStreamAhead KiB in flight (one 1 KiB load per step
+  // in flight kept the pass latency-bound at ~2.3 TB/s, bench cfg4 r03). The step loop is
+  // unrolled over the slots so each slot keeps its register (a rotation by moves would wait
+  // for every in-flight load it moves), and a slot is reloaded right after its step used it.
+  constexpr int kRing = kStreamAhead + 2;
+  u32x4 ring[kRing];
 #pragma unroll
-  for (int k = 0; k < kStreamAhead + 2; k++) ring[k] = load16(cq + uint64_t(k) * 1024 + lane * 16);
+  for (int k = 0; k < kRing; k++) ring[k] = load16(cq + uint64_t(k) * 1024 + lane * 16);
   uint32_t last_v = 0xffffffffu;  // this lane's last marked value (skips repeats)
-  for (; cq < qhi; cq += 1024) {
-    const u32x4 nn = load16(cq + uint64_t(kStreamAhead + 2) * 1024 + lane * 16);
-    const u32x4 cur = ring[0], nxt = ring[1];
-    __syncthreads();  // (previous window's readers done)
+  if (lane == 0) s_nhit = 0;
+  wave_sync();
+  // the matched values to vmatch (rare: every kStreamHits - 1024 matches, and at the end);
+  // the wait leaves no store in flight, so the ring's wait counts stay exact past it
+  auto flush_hits = [&]() {
+    const uint32_t n = s_nhit;
+    for (uint32_t i = lane; i < n; i += 64) vmatch[J.vmatch_base + s_hit[i]] = 1;
+    wave_sync();
+    if (lane == 0) s_nhit = 0;
+    wave_sync();
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);
+  };
+  // one 1 KiB step of start positions [c, c + 1024): cur = its bytes, nxt = the next KiB
+  auto step = [&](const uint64_t c, const u32x4 cur, const u32x4 nxt) {
+    wave_sync();  // (previous window's readers done)
     reinterpret_cast<u32x4 *>(s_win)[lane] = cur;
     reinterpret_cast<u32x4 *>(s_win)[64 + lane] = nxt;
     // the offsets must cover every start of this window
-    const uint64_t wlast = min<uint64_t>(cq + 1024, qhi) - 1 - J.lead;
+    const uint64_t wlast = min<uint64_t>(c + 1024, qhi) - 1 - J.lead;
     if (cover != ~0ull && wlast >= cover) {
-      const uint64_t pfirst = max<uint64_t>(cq, qlo) - J.lead;
+      const uint64_t pfirst = max<uint64_t>(c, qlo) - J.lead;
       // staged values [vb, vb + kv) that start at or before pfirst
-      const uint32_t c = uint32_t(__popcll(__ballot(uint32_t(lane) < kv && uint64_t(s_off[lane]) <= pfirst))) +
-                         uint32_t(__popcll(__ballot(uint32_t(lane) + 64 < kv && uint64_t(s_off[64 + lane]) <= pfirst)));
-      const bool beyond = c == kv && uint64_t(s_off[kv]) <= pfirst;
-      __syncthreads();
-      const uint32_t v = beyond ? value_at(J.off, vb + kv, J.nvals + 1, pfirst, lane) : vb + c - 1;
+      const uint32_t k1 = uint32_t(__popcll(__ballot(uint32_t(lane) < kv && uint64_t(s_off[lane]) <= pfirst))) +
+                          uint32_t(__popcll(__ballot(uint32_t(lane) + 64 < kv && uint64_t(s_off[64 + lane]) <= pfirst)));
+      const bool beyond = k1 == kv && uint64_t(s_off[kv]) <= pfirst;
+      wave_sync();
+      const uint32_t v = beyond ? value_at(J.off, vb + kv, J.nvals + 1, pfirst, lane) : vb + k1 - 1;
       stage_offs(v);
+      // (rare: every ~kStreamOffs values) leave no load of this branch in flight, so that the
+      // compiler's wait counts for the ring's slots stay exact past the branch
+      __builtin_amdgcn_s_waitcnt(kWaitVm0);
     }
-    __syncthreads();
+    wave_sync();
     const uint32_t nxw = reinterpret_cast<const uint32_t *>(s_win)[(lane + 1) * 4];  // the next lane's first dword
     const uint32_t d[5] = {cur.x, cur.y, cur.z, cur.w, nxw};
     uint32_t cm = 0;
@@ -328,51 +358,77 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
       if (nl > 1) nz |= nz_bytes(__builtin_amdgcn_alignbyte(d[k + 1], d[k], 1) ^ n1);
       cm |= pack_hi_bits(nz ^ 0x80808080u) << (4 * k);
     }
-    while (cm) {
-      const uint32_t jb = uint32_t(__builtin_ctz(cm));
-      cm &= cm - 1;
-      const uint32_t wo = uint32_t(lane) * 16 + jb;  // window offset of the start
-      const uint64_t q = cq + wo;
-      if (q < qlo || q >= qhi) continue;
-      bool ok = true;
-      for (uint32_t i = 2; i < nl && ok; i++) ok = s_win[wo + i] == s_nd[i];
-      if (!ok) continue;
-      const uint64_t p = q - J.lead;
-      uint32_t v;
-      if (p < cover) {  // in the staged offsets: s_off[lo] <= p < s_off[hi]
-        uint32_t lo = 0, hi = kv;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (uint64_t(s_off[mid]) <= p) lo = mid;
-          else hi = mid;
+    // candidates: verify from LDS, map the start to its value, mark the value. When the
+    // staged offsets cover every start of the window (the usual case: a uniform branch) the
+    // loop touches LDS only — a global load here would make every wait drain the ring's
+    // loads in flight; a window past the staged values (a run of tiny values) searches the
+    // global offsets instead.
+    auto candidates = [&](auto global_tag) {
+      constexpr bool kGlobal = decltype(global_tag)::value;
+      while (cm) {
+        const uint32_t jb = uint32_t(__builtin_ctz(cm));
+        cm &= cm - 1;
+        const uint32_t wo = uint32_t(lane) * 16 + jb;  // window offset of the start
+        const uint64_t q = c + wo;
+        if (q < qlo || q >= qhi) continue;
+        bool ok = true;
+        for (uint32_t i = 2; i < nl && ok; i++) ok = s_win[wo + i] == s_nd[i];
+        if (!ok) continue;
+        const uint64_t p = q - J.lead;
+        uint32_t v;
+        uint64_t vend;
+        if (!kGlobal || p < cover) {  // in the staged offsets: s_off[lo] <= p < s_off[lo + 1]
+          uint32_t lo = 0, hi = kv;
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (uint64_t(s_off[mid]) <= p) lo = mid;
+            else hi = mid;
+          }
+          v = vb + lo;
+          vend = s_off[lo + 1];
+        } else {
+          uint32_t lo = vb, hi = J.nvals;
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (uint64_t(G(J.off)[mid]) <= p) lo = mid;
+            else hi = mid;
+          }
+          v = lo;
+          vend = G(J.off)[v + 1];
         }
-        v = vb + lo;
-      } else {  // (a run of tiny values past the staged ones: search the global offsets)
-        uint32_t lo = vb, hi = J.nvals;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (uint64_t(J.off[mid]) <= p) lo = mid;
-          else hi = mid;
+        if (p + nl > vend) continue;  // the match runs into the next value
+        if (v != last_v) {  // (marked through the LDS list: no global store in the step loop)
+          const uint32_t k = atomicAdd(&s_nhit, 1u);
+          s_hit[k] = v;
+          last_v = v;
         }
-        v = lo;
+        // the rest of this lane's starts inside the same value add nothing
+        const uint64_t skip = vend + J.lead;  // aligned coordinate of the value's end
+        if (skip > q + 1) {
+          const uint64_t rel = skip - (c + uint64_t(lane) * 16);
+          cm &= rel >= 16 ? 0u : ~((1u << uint32_t(rel)) - 1u);
+        }
       }
-      const uint64_t vend = J.off[v + 1];
-      if (p + nl > vend) continue;  // the match runs into the next value
-      if (v != last_v) {
-        vmatch[J.vmatch_base + v] = 1;
-        last_v = v;
-      }
-      // the rest of this lane's starts inside the same value add nothing
-      const uint64_t skip = vend + J.lead;  // aligned coordinate of the value's end
-      if (skip > q + 1) {
-        const uint64_t rel = skip - (cq + uint64_t(lane) * 16);
-        cm &= rel >= 16 ? 0u : ~((1u << uint32_t(rel)) - 1u);
-      }
+    };
+    if (cover == ~0ull || wlast < cover) {
+      candidates(std::false_type{});
+    } else {
+      candidates(std::true_type{});
+      __builtin_amdgcn_s_waitcnt(kWaitVm0);
     }
+    wave_sync();
+    if (s_nhit >= kStreamHits - 1024) flush_hits();  // (a step adds fewer than 1024: unique values)
+  };
+  for (; cq < qhi; cq += uint64_t(kRing) * 1024) {
 #pragma unroll
-    for (int k = 0; k < kStreamAhead + 1; k++) ring[k] = ring[k + 1];
-    ring[kStreamAhead + 1] = nn;
+    for (int st = 0; st < kRing; st++) {
+      const uint64_t c = cq + uint64_t(st) * 1024;
+      if (c >= qhi) break;
+      step(c, ring[st], ring[(st + 1) % kRing]);
+      ring[st] = load16(c + uint64_t(kRing) * 1024 + lane * 16);  // (the KiB kRing steps ahead)
+    }
   }
+  flush_hits();
 }
 
 // ------------------------------------------------------------------------------------
