@@ -120,6 +120,26 @@ if has sweep; then  # pool-kernel knobs on the main line (blocks generated once,
     python3 -c "import json; d=json.load(open('gpurun_out/sweep_$1_$2.json')); print('  value', round(d['value']/1e9,1), 'frac', round(d['roofline']['frac'],3), 'kernel', d['latency_us']['kernel'])"
   done
 fi
+if has cfg4; then  # dictionary-stream parity, then the config-4 leg alone
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_dict_stream.py tests/test_gpu_configs.py -k "stream or cfg4" -x -q \
+    --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_cfg4.log 2>&1
+  rc=$?; echo "pytest cfg4 rc=$rc"; tail -2 gpurun_out/pytest_cfg4.log
+  [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 400 python bench.py --steps 20 --cpu-baseline 0 --concurrent-steps 0 --cfg3 0 --cfg4 1 --mall-steps 0 \
+    --shim-steps 0 --limit-steps 0 > gpurun_out/cfg4.json 2> gpurun_out/cfg4.err
+  rc=$?; echo "cfg4 bench rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+  python3 -c "import json; d=json.load(open('gpurun_out/cfg4.json'))['cfg4']['queries']; [print(k, v['dict_pass_us']['p50'], round(v['dict_frac'],3), v['scan_us']['p50']) for k,v in d.items()]"
+fi
+if has limprof; then  # the limit-20 leg alone under TSG_PROF: static-run vs pool kernel for the waves
+  for su in 32 0; do
+    TSG_PROF=1 TSG_POOL_STATIC_UNITS=$su timeout -k 10 300 python bench.py --steps 20 --cpu-baseline 0 --concurrent-steps 0 \
+      --cfg3 0 --cfg4 0 --mall-steps 0 --shim-steps 0 --limit-steps 300 > gpurun_out/limprof_$su.json 2> gpurun_out/limprof_$su.err
+    rc=$?; echo "limprof units=$su rc=$rc"; grep "prof p50" gpurun_out/limprof_$su.err
+    [ $rc -eq 0 ] || exit $rc
+    python3 -c "import json; d=json.load(open('gpurun_out/limprof_$su.json'))['limit20']; print(' step', d['step_us'], 'kernel', d['kernel_us']['p50'])"
+  done
+fi
 if has quick; then
   timeout -k 10 600 python bench.py --steps 200 --cpu-baseline 0 --cfg3 0 --concurrent-steps 0 ${BENCH_ARGS:-} \
     > gpurun_out/quick.json 2> gpurun_out/quick.err
