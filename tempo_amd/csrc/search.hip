@@ -230,7 +230,6 @@ constexpr uint64_t kStreamMinBytes = 1u << 20;  // smaller dictionaries: prep_ke
 constexpr uint32_t kStreamOffs = 128;           // value offsets staged per reload
 constexpr int kStreamAhead = 4;                 // KiB loaded ahead of the window, per wave
 constexpr int kWaitVm0 = 0x0F70;                // s_waitcnt vmcnt(0) (expcnt, lgkmcnt untouched)
-constexpr uint32_t kStreamHits = 2048;          // LDS list of matched values per wave
 struct StreamJob {
   const uint8_t *base;  // 16-byte aligned: the dictionary bytes start at base + lead
   const uint32_t *off;  // value offsets, nvals + 1
@@ -274,8 +273,6 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
   __shared__ __attribute__((aligned(16))) uint8_t s_win[2048 + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_nd[kStreamMaxNeedle];
   __shared__ uint32_t s_off[kStreamOffs + 1];
-  __shared__ uint32_t s_hit[kStreamHits];  // matched values not yet marked in vmatch
-  __shared__ uint32_t s_nhit;
   const int lane = threadIdx.x;
   const uint32_t w = blockIdx.x;
   uint32_t j = 0;
@@ -292,10 +289,12 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
   for (uint32_t i = lane; i < nl; i += 64) s_nd[i] = needles[J.needle_off + i];
   const uint32_t n0 = uint32_t(needles[J.needle_off]) * 0x01010101u;
   const uint32_t n1 = nl > 1 ? uint32_t(needles[J.needle_off + 1]) * 0x01010101u : 0u;
-  auto load16 = [&](uint64_t a) -> u32x4 {  // a: aligned coordinate of this lane's 16 bytes
-    if (a < end) return *G<u32x4>(J.base + a);
-    return u32x4{0u, 0u, 0u, 0u};
-  };
+  // a: aligned coordinate of this lane's 16 bytes. Past the stream's last 16-byte chunk
+  // the load repeats that chunk: bytes past `end` only ever form starts >= qhi (dropped) and
+  // are never compared, and an unconditional load keeps the compiler's waits exact (a
+  // conditional one makes the zero on the other path wait for the load in flight).
+  const uint64_t last16 = (end - 1) & ~uint64_t(15);
+  auto load16 = [&](uint64_t a) -> u32x4 { return *G<u32x4>(J.base + min(a, last16)); };
   // value offsets of the values around the window: s_off[i] = off[vb + i]
   uint32_t vb = value_at(J.off, 0, J.nvals + 1, qlo - J.lead, lane), kv = 0;
   uint64_t cover = 0;  // starts p < cover map through s_off
@@ -306,30 +305,38 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
     cover = kv == J.nvals - v ? ~0ull : uint64_t(G(J.off)[v + kv]);
   };
   stage_offs(vb);
+  __builtin_amdgcn_s_waitcnt(kWaitVm0);
   uint64_t cq = s0;
-  // ring slots: the window's two KiB + kStreamAhead KiB in flight (one 1 KiB load per step
-  // in flight kept the pass latency-bound at ~2.3 TB/s, bench cfg4 r03). The step loop is
-  // unrolled over the slots so each slot keeps its register (a rotation by moves would wait
-  // for every in-flight load it moves), and a slot is reloaded right after its step used it.
+  // Ring slots: the window's two KiB + kStreamAhead KiB in flight. The step loop is unrolled
+  // over the slots so each slot keeps its register (a rotation by moves waits for every
+  // in-flight load it moves), and a slot is reloaded right after its step used it.
   constexpr int kRing = kStreamAhead + 2;
   u32x4 ring[kRing];
 #pragma unroll
   for (int k = 0; k < kRing; k++) ring[k] = load16(cq + uint64_t(k) * 1024 + lane * 16);
   uint32_t last_v = 0xffffffffu;  // this lane's last marked value (skips repeats)
-  if (lane == 0) s_nhit = 0;
-  wave_sync();
-  // the matched values to vmatch (rare: every kStreamHits - 1024 matches, and at the end);
-  // the wait leaves no store in flight, so the ring's wait counts stay exact past it
-  auto flush_hits = [&]() {
-    const uint32_t n = s_nhit;
-    for (uint32_t i = lane; i < n; i += 64) vmatch[J.vmatch_base + s_hit[i]] = 1;
-    wave_sync();
-    if (lane == 0) s_nhit = 0;
-    wave_sync();
-    __builtin_amdgcn_s_waitcnt(kWaitVm0);
-  };
   // one 1 KiB step of start positions [c, c + 1024): cur = its bytes, nxt = the next KiB
   auto step = [&](const uint64_t c, const u32x4 cur, const u32x4 nxt) {
+    // the needle's first two bytes at all 16 start positions of this lane, in registers:
+    // the dword after the lane's 16 bytes is the next lane's first (DPP shift; lane 63: the
+    // next KiB's first dword)
+    const uint32_t nx0 = __builtin_amdgcn_readlane(nxt.x, 0);
+    uint32_t nxw = uint32_t(__builtin_amdgcn_update_dpp(0, int(cur.x), 0x130, 0xf, 0xf, false));  // wave_shl:1
+    if (lane == 63) nxw = nx0;
+    const uint32_t d[5] = {cur.x, cur.y, cur.z, cur.w, nxw};
+    uint32_t cw[4], any = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t nz = nz_bytes(d[k] ^ n0);
+      if (nl > 1) nz |= nz_bytes(__builtin_amdgcn_alignbyte(d[k + 1], d[k], 1) ^ n1);
+      cw[k] = nz ^ 0x80808080u;  // bit 7 of a byte: a candidate start
+      any |= cw[k];
+    }
+    // most steps hold no candidate in any lane: nothing else to do (a wave-uniform branch)
+    if (__ballot(any != 0) == 0) return;
+    uint32_t cm = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) cm |= pack_hi_bits(cw[k]) << (4 * k);
     wave_sync();  // (previous window's readers done)
     reinterpret_cast<u32x4 *>(s_win)[lane] = cur;
     reinterpret_cast<u32x4 *>(s_win)[64 + lane] = nxt;
@@ -349,20 +356,11 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
       __builtin_amdgcn_s_waitcnt(kWaitVm0);
     }
     wave_sync();
-    const uint32_t nxw = reinterpret_cast<const uint32_t *>(s_win)[(lane + 1) * 4];  // the next lane's first dword
-    const uint32_t d[5] = {cur.x, cur.y, cur.z, cur.w, nxw};
-    uint32_t cm = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      uint32_t nz = nz_bytes(d[k] ^ n0);
-      if (nl > 1) nz |= nz_bytes(__builtin_amdgcn_alignbyte(d[k + 1], d[k], 1) ^ n1);
-      cm |= pack_hi_bits(nz ^ 0x80808080u) << (4 * k);
-    }
     // candidates: verify from LDS, map the start to its value, mark the value. When the
     // staged offsets cover every start of the window (the usual case: a uniform branch) the
-    // loop touches LDS only — a global load here would make every wait drain the ring's
-    // loads in flight; a window past the staged values (a run of tiny values) searches the
-    // global offsets instead.
+    // loop touches LDS only — a global load here would make the waits for the ring's slots
+    // drain every load in flight; a window past the staged values (a run of tiny values)
+    // searches the global offsets instead.
     auto candidates = [&](auto global_tag) {
       constexpr bool kGlobal = decltype(global_tag)::value;
       while (cm) {
@@ -397,9 +395,8 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
           vend = G(J.off)[v + 1];
         }
         if (p + nl > vend) continue;  // the match runs into the next value
-        if (v != last_v) {  // (marked through the LDS list: no global store in the step loop)
-          const uint32_t k = atomicAdd(&s_nhit, 1u);
-          s_hit[k] = v;
+        if (v != last_v) {
+          vmatch[J.vmatch_base + v] = 1;
           last_v = v;
         }
         // the rest of this lane's starts inside the same value add nothing
@@ -416,8 +413,6 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
       candidates(std::true_type{});
       __builtin_amdgcn_s_waitcnt(kWaitVm0);
     }
-    wave_sync();
-    if (s_nhit >= kStreamHits - 1024) flush_hits();  // (a step adds fewer than 1024: unique values)
   };
   for (; cq < qhi; cq += uint64_t(kRing) * 1024) {
 #pragma unroll
@@ -428,7 +423,6 @@ extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const Stream
       ring[st] = load16(c + uint64_t(kRing) * 1024 + lane * 16);  // (the KiB kRing steps ahead)
     }
   }
-  flush_hits();
 }
 
 // ------------------------------------------------------------------------------------
