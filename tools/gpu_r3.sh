@@ -131,6 +131,25 @@ if has cfg4; then  # dictionary-stream parity, then the config-4 leg alone
   [ $rc -eq 0 ] || exit $rc
   python3 -c "import json; d=json.load(open('gpurun_out/cfg4.json'))['cfg4']['queries']; [print(k, v['dict_pass_us']['p50'], round(v['dict_frac'],3), v['scan_us']['p50']) for k,v in d.items()]"
 fi
+if has cfg4prof; then  # per-kernel times of the config-4 leg
+  export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/c4prof -o run --output-format csv -- \
+    python3 bench.py --steps 20 --cpu-baseline 0 --concurrent-steps 0 --cfg3 0 --cfg4 1 --mall-steps 0 \
+    --shim-steps 0 --limit-steps 0 > gpurun_out/c4prof.json 2> gpurun_out/c4prof.err
+  rc=$?; echo "cfg4 rocprof rc=$rc"; head -12 gpurun_out/c4prof/run_kernel_stats.csv
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has sweep2; then
+  W=/tmp/tsg_sweep; mkdir -p $W
+  for cfg in "20 4" "30 4" "30 5" "40 4" "50 4" "30 4" "20 4"; do
+    set -- $cfg
+    TSG_POOL_DYN=$1 TSG_POOL_CHUNK=$2 timeout -k 10 300 python bench.py --steps 400 --cpu-baseline 0 --concurrent-steps 0 \
+      --cfg3 0 --cfg4 0 --mall-steps 0 --shim-steps 0 --limit-steps 0 --workdir $W --events 4 > gpurun_out/sweep_$1_$2.json 2> gpurun_out/sweep_$1_$2.err
+    rc=$?; echo "sweep dyn=$1 chunk=$2 rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+    python3 -c "import json; d=json.load(open('gpurun_out/sweep_$1_$2.json')); print('  value', round(d['value']/1e9,1), 'frac', round(d['roofline']['frac'],3), 'kernel', d['latency_us']['kernel'])"
+  done
+fi
 if has limprof; then  # the limit-20 leg alone under TSG_PROF: static-run vs pool kernel for the waves
   for su in 32 0; do
     TSG_PROF=1 TSG_POOL_STATIC_UNITS=$su timeout -k 10 300 python bench.py --steps 20 --cpu-baseline 0 --concurrent-steps 0 \
