@@ -155,7 +155,7 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the columnar CPU baseline (0 = this process's CPU share, at most 16)")
-    ap.add_argument("--events", type=int, default=8,
+    ap.add_argument("--events", type=int, default=4,
                     help="HIP events around the search kernel of every N-th timed step (roofline.achieved: "
                          "the average over those launches); 0 = off")
     ap.add_argument("--limit-steps", type=int, default=20,
@@ -406,7 +406,7 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, gen_thread=Non
     GPU): one generated 5 M-entry block and device clones of it (tsg_block_clone: the
     clones share the host side), 125 M entries resident. Full scan: --cfg3-steps
     back-to-back queries (SURVEY.md 8(d)'s batched mode over a >= 100 M-entry resident
-    set), kernel HIP events on every 8th; limit=20: the deterministic early exit."""
+    set), kernel HIP events (dispatch-stamped) on every 8th; limit=20: the deterministic early exit."""
     import torch
     import tempo_amd as T
     t0 = time.time()
@@ -433,7 +433,7 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, gen_thread=Non
     step = []
     for i in range(args.cfg3_steps):
         ts = time.perf_counter()
-        eng.search_raw(blocks, pipe, flags=sflags if i % 8 == 0 else 0)
+        eng.search_raw(blocks, pipe, flags=sflags if i % 8 == 4 else 0)
         step.append(time.perf_counter() - ts)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -658,20 +658,19 @@ def main():
         g2, _ = eng.search(s, pipe)
         assert [(m.block_idx, m.entry_idx, m.trace_id) for m in g2] == [(m.block_idx, m.entry_idx, m.trace_id)
                                                                         for m in got], "clone differs"
-    # HIP events around the search kernel of every --events-th timed step, on the
-    # library's stream; read after the timed region (the search does not wait for them).
-    # A pair of event records costs the host ~10 us, so not every step carries one.
+    # HIP events on the search kernel of every --events-th timed step, on the library's
+    # stream, stamped from the kernel's own dispatch packet (hipExtLaunchKernel: what
+    # rocprofv3's kernel trace measures); read after the timed region (the search does not
+    # wait for them). Not every step carries a pair: recording one costs the host time.
     sflags = T.SEARCH_TIME_DEFER if args.events else 0
-    for i in range(max(args.warmup, len(sets))):
-        eng.search_raw(sets[i % len(sets)], pipe, flags=0)
-    eng.kernel_times()  # (drain)
+    ev_phase = args.events // 2  # (sampled steps: i % events == events // 2, never the first step)
 
     def timed(nsteps, rot):
         step_s = []
         t0 = time.perf_counter()
         for i in range(nsteps):  # (tsg_search is synchronous: results are on the host when it returns)
             ts = time.perf_counter()
-            eng.search_raw(sets[i % rot], pipe, flags=sflags if args.events and i % args.events == 0 else 0,
+            eng.search_raw(sets[i % rot], pipe, flags=sflags if args.events and i % args.events == ev_phase else 0,
                            metrics=False)
             step_s.append(time.perf_counter() - ts)
         torch.cuda.synchronize()
@@ -679,9 +678,14 @@ def main():
 
     # Python's cyclic GC stays off through the timed legs (re-enabled before the CPU
     # baselines): a collection pass over this process's heap is host noise that the
-    # library's real caller, a Go querier, does not have
+    # library's real caller, a Go querier, does not have. Collected BEFORE the warmup, so
+    # that the warmup steps run right before the timed ones (a GPU left idle for the tens of
+    # milliseconds a collection takes runs its next kernel ~2x slower)
     gc.collect()
     gc.disable()
+    eng.kernel_times()  # (drain)
+    for i in range(max(args.warmup, len(sets))):
+        eng.search_raw(sets[i % len(sets)], pipe, flags=0)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -763,7 +767,7 @@ def main():
         for i in range(args.limit_steps):
             ts = time.perf_counter()
             nl, metl = eng.search_raw(sets[i % len(sets)], pipe, limit=20,
-                                      flags=sflags if args.events and i % args.events == 0 else 0)
+                                      flags=sflags if args.events and i % args.events == ev_phase else 0)
             ls.append(time.perf_counter() - ts)
         lk = eng.kernel_times() if args.events else []
         out["limit20"] = {"steps": args.limit_steps, "matches": nl, "traces_inspected": metl.inspected_traces,

@@ -229,6 +229,7 @@ constexpr uint32_t kStreamMaxNeedle = 1024;     // the 2 KiB window holds any ma
 constexpr uint64_t kStreamMinBytes = 1u << 20;  // smaller dictionaries: prep_kernel (lane per value)
 constexpr uint32_t kStreamOffs = 128;           // value offsets staged per reload
 constexpr int kStreamAhead = 4;                 // KiB loaded ahead of the window, per wave
+constexpr uint32_t kStreamWg = 4;               // waves (independent spans) per workgroup
 constexpr int kWaitVm0 = 0x0F70;                // s_waitcnt vmcnt(0) (expcnt, lgkmcnt untouched)
 struct StreamJob {
   const uint8_t *base;  // 16-byte aligned: the dictionary bytes start at base + lead
@@ -267,14 +268,21 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-extern "C" __global__ void __launch_bounds__(64) dict_stream_kernel(const StreamJob *jobs, uint32_t njobs,
-                                                                    const uint8_t *needles, uint8_t *vmatch,
-                                                                    uint32_t span) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_win[2048 + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_nd[kStreamMaxNeedle];
-  __shared__ uint32_t s_off[kStreamOffs + 1];
-  const int lane = threadIdx.x;
-  const uint32_t w = blockIdx.x;
+// kStreamWg waves per workgroup, each on its own span with its own LDS (no barriers: a
+// one-wave workgroup per span would cap a CU at its workgroup slots, half the wave slots)
+extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(const StreamJob *jobs, uint32_t njobs,
+                                                                                 const uint8_t *needles, uint8_t *vmatch,
+                                                                                 uint32_t span, uint32_t nwaves) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win_all[kStreamWg][2048 + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_nd_all[kStreamWg][kStreamMaxNeedle];
+  __shared__ uint32_t s_off_all[kStreamWg][kStreamOffs + 1];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wid = uint32_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  uint8_t *const s_win = s_win_all[wid];
+  uint8_t *const s_nd = s_nd_all[wid];
+  uint32_t *const s_off = s_off_all[wid];
+  const uint32_t w = blockIdx.x * kStreamWg + wid;
+  if (w >= nwaves) return;
   uint32_t j = 0;
   for (uint32_t k = 1; k < njobs; k++)
     if (jobs[k].wave0 <= w) j = k;
@@ -2139,9 +2147,9 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
         uint32_t(o_nd), uint32_t(needles.size()), static_cast<uint8_t *>(dc.vmatch.p),
         static_cast<uint32_t *>(dc.bitmaps.p));
     if (!stream_jobs.empty())
-      dict_stream_kernel<<<stream_waves, 64, 0, s>>>(reinterpret_cast<const StreamJob *>(dd + o_stj),
-                                                     uint32_t(stream_jobs.size()), dd + o_nd,
-                                                     static_cast<uint8_t *>(dc.vmatch.p), stream_span);
+      dict_stream_kernel<<<(stream_waves + kStreamWg - 1) / kStreamWg, 64 * kStreamWg, 0, s>>>(
+          reinterpret_cast<const StreamJob *>(dd + o_stj), uint32_t(stream_jobs.size()), dd + o_nd,
+          static_cast<uint8_t *>(dc.vmatch.p), stream_span, stream_waves);
     if (set_items.back())
       dict_sets_kernel<<<(set_items.back() + 255) / 256, 256, 0, s>>>(
           reinterpret_cast<const DictJob *>(dd + o_jobs), reinterpret_cast<const uint32_t *>(dd + o_sj),
