@@ -165,6 +165,12 @@ if has quick; then
   rc=$?; echo "quick rc=$rc"; tail -2 gpurun_out/quick.err; cat gpurun_out/quick.json
   [ $rc -eq 0 ] || exit $rc
 fi
+if has driver; then  # the driver's own bench command
+  timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/driver.json 2> gpurun_out/driver.err
+  rc=$?; echo "driver bench rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+  python3 -c "import json; d=json.load(open('gpurun_out/driver.json')); print('  value', round(d['value']/1e9,1), 'frac', round(d['roofline']['frac'],3), 'kernel', d['latency_us']['kernel'], 'step', d['latency_us']['step']['p50'])"
+fi
 if has bench; then
   timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
   rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.err; cat gpurun_out/bench.json
