@@ -60,7 +60,7 @@ struct LkParams {
   const uint32_t *direct;    // block ordinals probed one by one (ascending)
   const uint8_t *ids;
   uint64_t nids;
-  uint32_t pair, pad0;  // slab probes two at a time (TSG_LK_PAIR, default 1)
+  uint32_t pair, pad0;  // slab probes two at a time (TSG_LK_PAIR=1; default one at a time)
   unsigned long long epoch, ticket_base;
   unsigned long long *ticket, *gran;
   uint64_t *offsets;  // per id: first output slot
@@ -812,7 +812,7 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
   P.nids = nids;
   static const uint32_t pair = [] {
     const char *e = std::getenv("TSG_LK_PAIR");
-    return e ? uint32_t(std::atoi(e) != 0) : 1u;
+    return e ? uint32_t(std::atoi(e) != 0) : 0u;  // (pairs: 2.18 vs 2.15 ms per config-5 step, profiles/r03_lookup)
   }();
   P.pair = pair;
   P.epoch = dc.epoch;
