@@ -46,6 +46,37 @@ bool fb_contains_tag(const FbTable &t, uint16_t tags_vto, std::string_view k, st
   return false;
 }
 
+// The header's tag table as views (the same walk fb_contains_tag does per query).
+void index_header(HostBlock &hb) {
+  hb.hdr_keys.clear();
+  hb.hdr_vals.clear();
+  hb.hdr_val0.assign(1, 0);
+  hb.hdr_index = false;
+  try {
+    FbTable t = FbTable::root(hb.header.data(), hb.header.size());
+    const uint16_t o = t.field(kHdrTags);
+    const uint32_t n = o ? t.vector_len(o) : 0;
+    const uint32_t start = o ? t.vector_start(o) : 0;
+    FbTable kv{t.b, t.n, 0};
+    for (uint32_t h = 0; h < n; h++) {
+      kv.pos = t.indirect(start + 4 * h);
+      const uint16_t ko = kv.field(kKvKey);
+      hb.hdr_keys.push_back(ko ? kv.byte_vector(kv.pos + ko) : std::string_view());
+      const uint16_t vo = kv.field(kKvValue);
+      if (vo) {
+        const uint32_t vn = kv.vector_len(vo), vs = kv.vector_start(vo);
+        for (uint32_t q = 0; q < vn; q++) hb.hdr_vals.push_back(kv.byte_vector(vs + 4 * q));
+      }
+      hb.hdr_val0.push_back(uint32_t(hb.hdr_vals.size()));
+    }
+    hb.hdr_index = true;
+  } catch (...) {
+    hb.hdr_keys.clear();
+    hb.hdr_vals.clear();
+    hb.hdr_val0.assign(1, 0);
+  }
+}
+
 // ---- meta ---------------------------------------------------------------------------
 static bool json_field(std::string_view js, const char *name, std::string_view &val) {
   std::string pat = std::string("\"") + name + "\"";
@@ -427,6 +458,7 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
     hb.min_dur = h.u64(kHdrMin);
     hb.max_dur = h.u64(kHdrMax);
   }
+  index_header(hb);
   std::vector<IndexRecord> recs =
       read_index(index, index_len, hb.meta.index_page_size, hb.meta.index_records, &hb.index_truncated);
   if (nthreads <= 0) nthreads = int(std::max(1u, std::thread::hardware_concurrency()));

@@ -78,6 +78,8 @@ enum : uint16_t {
 
 // FindTag + ContainsTag over any [KeyValues] vector (pkg/tempofb/searchdata_util.go:47-100).
 bool fb_contains_tag(const FbTable &t, uint16_t tags_vto, std::string_view k, std::string_view v);
+struct HostBlock;
+void index_header(HostBlock &hb);  // fills hdr_keys / hdr_vals / hdr_val0 (block.cpp)
 
 // ---- search.meta.json (tempodb/search/block_meta.go:11-43) ----------------------
 struct SearchMeta {
@@ -151,6 +153,13 @@ struct HostBlock {
   SearchMeta meta;
   std::vector<uint8_t> header;  // raw search-header flatbuffer (kept for MatchesBlock/Tags)
   uint64_t min_dur = 0, max_dur = 0;
+  // the header's tag table walked once at open (MatchesBlock per query without decoding
+  // the flatbuffer again): keys in the header's own order, each key's values (CSR), views
+  // into `header`. hdr_index false: a header that did not walk cleanly (the per-query
+  // flatbuffer path then fails the search exactly where the reference's reader would)
+  std::vector<std::string_view> hdr_keys, hdr_vals;
+  std::vector<uint32_t> hdr_val0;
+  bool hdr_index = false;
   uint64_t n = 0;
   std::vector<uint32_t> page_entries;  // EntriesLength per page
   std::vector<uint64_t> page_fb_bytes; // flatbuffer bytes per page (bytesInspected)

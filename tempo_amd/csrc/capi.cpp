@@ -257,6 +257,7 @@ struct tsg_v2block {
 namespace tsg {
 tsg_pipeline *pipeline_new(const tsg_request &req);
 bool pipeline_matches_block(const tsg_query &q, const uint8_t *hdr, size_t len);
+bool pipeline_matches_block_indexed(const tsg_query &q, const HostBlock &h);
 bool pipeline_matches_stream_header(const tsg_query &q, uint64_t min_dur, uint64_t max_dur,
                                     const std::map<std::string, std::set<std::string>> &tags);
 
@@ -1086,7 +1087,8 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       }
       bool ok = b.host->streaming
                     ? pipeline_matches_stream_header(*q, b.host->min_dur, b.host->max_dur, b.host->stream_tags)
-                    : pipeline_matches_block(*q, b.host->header.data(), b.host->header.size());
+                    : b.host->hdr_index ? pipeline_matches_block_indexed(*q, *b.host)
+                                        : pipeline_matches_block(*q, b.host->header.data(), b.host->header.size());
       state[i] = ok ? 2 : 1;
     }
     // Blocks [b0, b1) on their devices, one device_search per device (concurrently).

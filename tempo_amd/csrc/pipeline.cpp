@@ -79,6 +79,38 @@ bool pipeline_matches_block(const tsg_query &q, const uint8_t *hdr, size_t len) 
   return true;
 }
 
+// The same predicate over the header walked at open (HostBlock::hdr_*): the same binary
+// search over the keys in the header's order (searchdata_util.go:63-100, reversed
+// comparator) and the same bytes.Contains over the found key's values.
+bool pipeline_matches_block_indexed(const tsg_query &q, const HostBlock &h) {
+  if (q.has_min && !(h.max_dur >= q.min_ns)) return false;  // pipeline.go:38-41
+  if (q.has_max && !(h.min_dur <= q.max_ns)) return false;  // :53-56
+  const uint32_t n = uint32_t(h.hdr_keys.size());
+  for (uint32_t t = 0; t < q.nterms; t++) {
+    const uint8_t *k = q.keys[t];
+    const size_t kl = q.key_lens[t];
+    std::string_view v(reinterpret_cast<const char *>(q.values[t]), q.value_lens[t]);
+    uint32_t i = 0, j = n, at = n;
+    while (i < j) {
+      const uint32_t m = (i + j) >> 1;
+      const std::string_view key = h.hdr_keys[m];
+      const int c = bytes_compare(reinterpret_cast<const uint8_t *>(key.data()), key.size(), k, kl);
+      if (c == 0) {
+        at = m;
+        break;
+      }
+      if (c < 0) j = m;
+      else i = m + 1;
+    }
+    if (at == n) return false;
+    bool any = false;
+    for (uint32_t x = h.hdr_val0[at]; x < h.hdr_val0[at + 1] && !any; x++)
+      any = v.empty() || h.hdr_vals[x].find(v) != std::string_view::npos;  // bytes.Contains
+    if (!any) return false;
+  }
+  return true;
+}
+
 // MatchesBlock on a StreamingSearchBlock's SearchBlockHeaderMutable
 // (streaming_search_block.go:127-134): the same duration filters, but the tag filter is
 // SearchDataMap.Contains (searchdatamap.go:43-49): the EXACT value must be present,
