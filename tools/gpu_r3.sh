@@ -71,6 +71,9 @@ if has scanprobe; then
   timeout -k 10 180 gpurun_out/scan_probe > gpurun_out/scan_probe.json 2>&1
   rc=$?; echo "scan probe rc=$rc"; cat gpurun_out/scan_probe.json
   [ $rc -eq 0 ] || exit $rc
+  PROBE_RAND=1 timeout -k 10 180 gpurun_out/scan_probe > gpurun_out/scan_probe_rand.json 2>&1
+  rc=$?; echo "scan probe rand rc=$rc"; cat gpurun_out/scan_probe_rand.json
+  [ $rc -eq 0 ] || exit $rc
 fi
 if has stamps; then
   TSG_STAMPS=1 timeout -k 10 600 python bench.py --steps 6 --warmup 2 --cpu-baseline 0 --cfg3 0 --concurrent-steps 0 \

@@ -203,6 +203,7 @@ struct Stat {
 };
 
 int main() {
+  const bool rand_data = std::getenv("PROBE_RAND") != nullptr;
   int cu = 0;
   CK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
   std::vector<Args> sets(4);
@@ -216,6 +217,21 @@ int main() {
       CK(hipMalloc(&ncol, size_t(kSlots) * kNpad));
       CK(hipMemset(scan, 0x11, size_t(3) * kNpad * 4));
       CK(hipMemset(ncol, 0x03, size_t(kSlots) * kNpad));
+      if (rand_data) {  // PROBE_RAND=1: config-2-like values (varied durations, times, value-set ids)
+        static std::vector<uint32_t> hs(size_t(3) * kNpad);
+        static std::vector<uint8_t> hc(size_t(kSlots) * kNpad);
+        uint64_t x = 0x9e3779b97f4a7c15ull * uint64_t(b + 1);
+        auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return uint32_t(x); };
+        for (uint32_t e = 0; e < kNpad; e++) {
+          const uint32_t st = 1700000000u + rnd() % 3600u;
+          hs[e] = rnd() % 2000000000u;                 // dur32 (ns)
+          hs[kNpad + e] = st;                          // start_s
+          hs[2 * kNpad + e] = st + rnd() % 3u;         // end_s
+        }
+        for (size_t i = 0; i < hc.size(); i++) hc[i] = uint8_t(rnd() % 16u);
+        CK(hipMemcpy(scan, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(ncol, hc.data(), hc.size(), hipMemcpyHostToDevice));
+      }
       A.s.scan[b] = scan;
       A.s.col[b][0] = ncol;
       A.s.col[b][1] = ncol + size_t(7) * kNpad;
@@ -226,7 +242,7 @@ int main() {
     A.start_s = 100;
     A.end_s = 200;
     for (int q = 0; q < 3; q++)
-      for (int w = 0; w < 8; w++) A.bm[q][w] = 0;
+      for (int w = 0; w < 8; w++) A.bm[q][w] = rand_data && w == 0 ? (q == 0 ? 0x80u : q == 1 ? 0x3u : 0x4u) : 0u;
     A.sink = sink;
   }
   const double bytes = double(kBlocks) * kN * 15;
@@ -270,6 +286,12 @@ int main() {
     ev.print(name, "events", bytes);
     ext.print(name, "ext_events", bytes);
   };
+  if (rand_data) {
+    for (auto &A : sets) { A.min32 = 10000000; A.max32 = 1000000000; A.start_s = 1700000900; A.end_s = 1700002700; }
+    run("rand_static1024_nt", reinterpret_cast<const void *>(static1024<true>), cu, 1024);
+    run("rand_static1024_nt_mall", reinterpret_cast<const void *>(static1024<true>), cu, 1024, false, 0, 1);
+    return 0;
+  }
   run("static1024_nt", reinterpret_cast<const void *>(static1024<true>), cu, 1024);
   run("static1024_nt_mall", reinterpret_cast<const void *>(static1024<true>), cu, 1024, false, 0, 1);
   run("big_nt", reinterpret_cast<const void *>(static_big<true, false, false>), cu, 1024, true);
