@@ -92,6 +92,42 @@ __device__ __forceinline__ uint32_t stream1(const uint8_t *p, uint64_t e) {
   else return *G<uint32_t>(p + e);
 }
 
+// The predicates of one unit (8 entries per lane) as a 32-bit lane mask, branch-free: every
+// test is evaluated for every entry and combined with bitwise ands (short-circuit tests
+// compiled to ~130 exec-mask branches per unit; with real, mixed values the lanes diverge
+// and the 150 MB scan ran 8 us longer than with uniform data, profiles/r03_launch).
+// lo/hi: the duration bounds (0 / 2^32-1 when a side is absent); bm: the LDS bitmaps.
+template <int NT, bool DUR, bool RANGE>
+__device__ __forceinline__ uint32_t unit_mask(const u32x4 (&d)[kSteps], const u32x4 (&sv4)[kSteps],
+                                              const u32x4 (&ev4)[kSteps], const uint32_t (&tv)[NT > 0 ? NT : 1][kSteps],
+                                              uint32_t e0, uint32_t n, uint32_t lo, uint32_t hi, uint32_t start_s,
+                                              uint32_t end_s, uint32_t bmi4, uint32_t ns4, const uint32_t *s_bm,
+                                              int lane) {
+  uint32_t mask = 0;
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) {
+    const uint32_t dv[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+    const uint32_t sv[4] = {sv4[k].x, sv4[k].y, sv4[k].z, sv4[k].w};
+    const uint32_t ev[4] = {ev4[k].x, ev4[k].y, ev4[k].z, ev4[k].w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint32_t ok = uint32_t(e0 + uint32_t(k) * 256 + uint32_t(lane) * 4 + uint32_t(j) < n);
+      if (DUR) ok &= uint32_t(dv[j] >= lo) & uint32_t(dv[j] <= hi);
+      // req.Start <= endSeconds && req.End >= startSeconds (pipeline.go:62-63)
+      if (RANGE) ok &= uint32_t(start_s <= ev[j]) & uint32_t(end_s >= sv[j]);
+#pragma unroll
+      for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
+        if (NT <= 0) break;
+        const uint32_t x = (tv[q][k] >> (8 * j)) & 0xffu;
+        const uint32_t wd = s_bm[((bmi4 >> (8 * q)) & 0xffu) * 8 + (x >> 5)];  // (x < 256: in the 256-bit map)
+        ok &= uint32_t(x < ((ns4 >> (8 * q)) & 0xffu)) & (wd >> (x & 31));
+      }
+      mask |= (ok & 1u) << (4 * k + j);
+    }
+  }
+  return mask;
+}
+
 template <int NT, bool DUR, bool RANGE, bool NTL>
 __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A) {
   const unsigned long long t_start = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -128,6 +164,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
   }
   const uint32_t S = A.static_per_wg, L = A.lookahead, cs = A.chunk_shift;
   const uint32_t rec_cap = A.rec_cap;
+  const uint32_t dlo = A.has_min ? A.min32 : 0u, dhi = A.has_max ? A.max32 : 0xffffffffu;
   // An LDS chunk slot once its answer is in. Bounded: never reached unless the protocol
   // is broken, and then the query fails on the host instead of the GPU hanging.
   auto poll_chunk = [&](uint32_t k) -> uint32_t {
@@ -211,32 +248,8 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     const PoolBlk &B = s_blk[R.blk];
     const uint32_t n = __builtin_amdgcn_readfirstlane(B.nent);
     const uint32_t bmi4 = __builtin_amdgcn_readfirstlane(B.bmi4), ns4 = __builtin_amdgcn_readfirstlane(B.nsets4);
-    uint32_t mask = 0;
-#pragma unroll
-    for (int k = 0; k < kSteps; k++)
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (R.e0 + uint32_t(k) * 256 + uint32_t(lane) * 4 + j < n) mask |= 1u << (4 * k + j);
-#pragma unroll
-    for (int k = 0; k < kSteps; k++) {
-      const uint32_t dv[4] = {R.d[k].x, R.d[k].y, R.d[k].z, R.d[k].w};
-      const uint32_t sv[4] = {R.s[k].x, R.s[k].y, R.s[k].z, R.s[k].w};
-      const uint32_t ev[4] = {R.e[k].x, R.e[k].y, R.e[k].z, R.e[k].w};
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        bool ok = true;
-        if (DUR) ok = (!A.has_min || dv[j] >= A.min32) && (!A.has_max || dv[j] <= A.max32);
-        if (RANGE) ok = ok && A.start_s <= ev[j] && A.end_s >= sv[j];  // req.Start <= endSeconds && req.End >= startSeconds
-#pragma unroll
-        for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
-          if (NT <= 0) break;
-          const uint32_t x = (R.tv[q][k] >> (8 * j)) & 0xffu;
-          const uint32_t wd = s_bm[((bmi4 >> (8 * q)) & 0xffu) * 8 + (x >> 5)];
-          ok = ok && (x < ((ns4 >> (8 * q)) & 0xffu)) && ((wd >> (x & 31)) & 1u);
-        }
-        if (!ok) mask &= ~(1u << (4 * k + j));
-      }
-    }
+    const uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, R.e, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
+                                                     ns4, s_bm, lane);
     if (__ballot(mask != 0) == 0) return;
     // matches: slots in the workgroup's LDS record buffer, record fields gathered now
     const DevBlockDesc *D = A.desc[R.blk];
@@ -379,36 +392,13 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
     }
   };
   const uint32_t rec_cap = A.rec_cap;
+  const uint32_t dlo = A.has_min ? A.min32 : 0u, dhi = A.has_max ? A.max32 : 0xffffffffu;
   // (evaluated right after the unit's load, while the block state still describes it)
   auto eval = [&](const Regs &R, uint32_t bslot) {
     const PoolBlk &P = A.blk[bslot];
     const uint32_t n = P.nent, bmi4 = P.bmi4, ns4 = P.nsets4;
-    uint32_t mask = 0;
-#pragma unroll
-    for (int k = 0; k < kSteps; k++)
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (R.e0 + uint32_t(k) * 256 + uint32_t(lane) * 4 + j < n) mask |= 1u << (4 * k + j);
-#pragma unroll
-    for (int k = 0; k < kSteps; k++) {
-      const uint32_t dv[4] = {R.d[k].x, R.d[k].y, R.d[k].z, R.d[k].w};
-      const uint32_t sv[4] = {R.s[k].x, R.s[k].y, R.s[k].z, R.s[k].w};
-      const uint32_t ev[4] = {R.e[k].x, R.e[k].y, R.e[k].z, R.e[k].w};
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        bool ok = true;
-        if (DUR) ok = (!A.has_min || dv[j] >= A.min32) && (!A.has_max || dv[j] <= A.max32);
-        if (RANGE) ok = ok && A.start_s <= ev[j] && A.end_s >= sv[j];
-#pragma unroll
-        for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
-          if (NT <= 0) break;
-          const uint32_t x = (R.tv[q][k] >> (8 * j)) & 0xffu;
-          const uint32_t wd = s_bm[((bmi4 >> (8 * q)) & 0xffu) * 8 + (x >> 5)];
-          ok = ok && (x < ((ns4 >> (8 * q)) & 0xffu)) && ((wd >> (x & 31)) & 1u);
-        }
-        if (!ok) mask &= ~(1u << (4 * k + j));
-      }
-    }
+    const uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, R.e, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
+                                                     ns4, s_bm, lane);
     if (__ballot(mask != 0) == 0) return;
     const DevBlockDesc *D = A.desc[bslot];
     const auto *Dc = K4(D);
