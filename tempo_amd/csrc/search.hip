@@ -458,10 +458,16 @@ __device__ __forceinline__ uint32_t col_at(u32x4 r, uint32_t width, int j) {
   if (width == 2) return ((j < 2 ? r.x : r.y) >> (16 * (j & 1))) & 0xffffu;
   return j == 0 ? r.x : j == 1 ? r.y : j == 2 ? r.z : r.w;
 }
-__device__ __forceinline__ bool term_ok(const ScanTerm &T, const uint32_t *lds_bm, uint32_t x) {
-  if (x >= T.nsets) return false;  // all-ones sentinel = key absent (FindTag fails)
-  uint32_t w = T.lds_off != kNoLds ? lds_bm[T.lds_off + (x >> 5)] : G(T.bm)[x >> 5];
-  return (w >> (x & 31)) & 1u;
+// Bit 0: value set x matches the term (x >= nsets: the all-ones sentinel, key absent, FindTag
+// fails). Branch-free over x: the sentinel reads word 0 and is masked off (an early return
+// became an exec-mask branch per entry that diverges on real data); the LDS / global choice is
+// per term (wave-uniform).
+__device__ __forceinline__ uint32_t term_bit(const ScanTerm &T, const uint32_t *lds_bm, uint32_t x) {
+  const uint32_t in = uint32_t(x < T.nsets);
+  const uint32_t xi = in ? x : 0u;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(T.lds_off);
+  const uint32_t w = lo != kNoLds ? lds_bm[lo + (xi >> 5)] : G(T.bm)[xi >> 5];
+  return in & (w >> (xi & 31));
 }
 
 // One tile's filter-column registers for this thread: entries
@@ -560,15 +566,15 @@ __device__ __forceinline__ uint32_t eval_tile(const TileRegs<NT, W1> &R, const S
       for (int q = 0; q < (NT > 0 ? NT : 1); q++)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          bool ok;
+          uint32_t ok;
           if constexpr (W1) {  // u8 column, bitmap in LDS padded to 8 words: branch-free lookup
             const uint32_t x = (R.tv[q][k] >> (8 * j)) & 0xffu;
             const uint32_t w = lds_bm[T[q].lds_off + (x >> 5)];
-            ok = (x < T[q].nsets) & ((w >> (x & 31)) & 1u);
+            ok = uint32_t(x < T[q].nsets) & (w >> (x & 31));
           } else {
-            ok = term_ok(T[q], lds_bm, col_at(R.tv[q][k], T[q].width, j));
+            ok = term_bit(T[q], lds_bm, col_at(R.tv[q][k], T[q].width, j));
           }
-          if (!ok) mask &= ~(1u << (4 * k + j));
+          mask &= ~((~ok & 1u) << (4 * k + j));
         }
     }
   }
@@ -582,7 +588,7 @@ __device__ __forceinline__ uint32_t eval_tile(const TileRegs<NT, W1> &R, const S
       for (int k = 0; k < kSteps; k++)
 #pragma unroll
         for (int j = 0; j < 4; j++)
-          if (!term_ok(Tq, lds_bm, col_at(c[k], Tq.width, j))) mask &= ~(1u << (4 * k + j));
+          mask &= ~((~term_bit(Tq, lds_bm, col_at(c[k], Tq.width, j)) & 1u) << (4 * k + j));
     }
   }
   return mask;
