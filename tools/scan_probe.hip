@@ -88,13 +88,14 @@ __device__ __forceinline__ uint32_t eval_unit(const Regs &R, const Args &A, cons
     const uint32_t ev[4] = {R.e[k].x, R.e[k].y, R.e[k].z, R.e[k].w};
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      bool ok = dv[j] >= A.min32 && dv[j] <= A.max32 && A.start_s <= ev[j] && A.end_s >= sv[j];
+      uint32_t ok = uint32_t(dv[j] >= A.min32) & uint32_t(dv[j] <= A.max32) & uint32_t(A.start_s <= ev[j]) &
+                    uint32_t(A.end_s >= sv[j]);  // (branch-free, as the engine's unit_mask)
 #pragma unroll
       for (int q = 0; q < 3; q++) {
         const uint32_t x = (R.t[q][k] >> (8 * j)) & 0xffu;
-        ok = ok && ((bm[q * 8 + (x >> 5)] >> (x & 31)) & 1u);
+        ok &= bm[q * 8 + (x >> 5)] >> (x & 31);
       }
-      if (ok) mask |= 1u << (4 * k + j);
+      mask |= (ok & 1u) << (4 * k + j);
     }
   }
   return mask;
