@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(1024, 1) static_big(BigArgs BA) {
   }
 }
 
-template <bool NT>
+template <bool NT, bool SPREAD = false>
 __global__ void __launch_bounds__(1024, 1) static1024(Args A) {
   __shared__ uint32_t bm[24];
   if (threadIdx.x < 24) bm[threadIdx.x] = A.bm[threadIdx.x / 8][threadIdx.x % 8];
@@ -161,7 +161,9 @@ __global__ void __launch_bounds__(1024, 1) static1024(Args A) {
     if (u + 2 < u1) load_unit<NT>(ra, A, u + 2, lane);
     if (u + 1 < u1) cnt += __popc(eval_unit(rb, A, bm));
   }
-  if (cnt) atomicAdd(A.sink, cnt);
+  if (SPREAD) {  // one word per wave: no same-address atomics at the end
+    if (cnt == 0x7fffffffu) A.sink[gw & 15] = cnt;
+  } else if (cnt) atomicAdd(A.sink, cnt);
 }
 
 // one workgroup per TILES x 2048 entries (tiles never straddle blocks: a block is 977 tiles
@@ -291,6 +293,7 @@ int main() {
     for (auto &A : sets) { A.min32 = 10000000; A.max32 = 1000000000; A.start_s = 1700000900; A.end_s = 1700002700; }
     run("rand_static1024_nt", reinterpret_cast<const void *>(static1024<true>), cu, 1024);
     run("rand_static1024_nt_mall", reinterpret_cast<const void *>(static1024<true>), cu, 1024, false, 0, 1);
+    run("rand_static1024_nt_noatomic", reinterpret_cast<const void *>(static1024<true, true>), cu, 1024);
     return 0;
   }
   run("static1024_nt", reinterpret_cast<const void *>(static1024<true>), cu, 1024);
