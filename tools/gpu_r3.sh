@@ -182,7 +182,7 @@ fi
 if has prof; then
   export TMPDIR=/tmp
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-    python3 bench.py --steps 40 --warmup 3 --cpu-baseline 0 --limit-steps 0 --cfg3 0 --concurrent-steps 0 \
+    python3 bench.py --steps 40 --warmup 3 --cpu-baseline 0 --limit-steps 0 --cfg3 0 --concurrent-steps 0 --shim-steps 0 --cfg4 0 \
     --mall-steps 0 ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
   rc=$?; echo "rocprof rc=$rc"; cat gpurun_out/prof/run_kernel_stats.csv
   [ $rc -eq 0 ] || exit $rc
@@ -191,7 +191,7 @@ if has pmc; then
   export TMPDIR=/tmp
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 -s KILL 600 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv -- \
-      python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 --limit-steps 0 --cfg3 0 --concurrent-steps 0 \
+      python3 bench.py --steps 10 --warmup 2 --cpu-baseline 0 --limit-steps 0 --cfg3 0 --concurrent-steps 0 --shim-steps 0 --cfg4 0 \
       --mall-steps 0 ${BENCH_ARGS:-} > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err
     rc=$?; echo "pmc $c rc=$rc"
     [ $rc -eq 0 ] || exit $rc
