@@ -274,12 +274,12 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
                                                                                  const uint8_t *needles, uint8_t *vmatch,
                                                                                  uint32_t span, uint32_t nwaves) {
   __shared__ __attribute__((aligned(16))) uint8_t s_win_all[kStreamWg][2048 + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_nd_all[kStreamWg][kStreamMaxNeedle];
+  __shared__ uint32_t s_ndw_all[kStreamWg][kStreamMaxNeedle / 4 + 1];  // needle bytes 2.. as words
   __shared__ uint32_t s_off_all[kStreamWg][kStreamOffs + 1];
   const int lane = threadIdx.x & 63;
   const uint32_t wid = uint32_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   uint8_t *const s_win = s_win_all[wid];
-  uint8_t *const s_nd = s_nd_all[wid];
+  uint32_t *const s_ndw = s_ndw_all[wid];
   uint32_t *const s_off = s_off_all[wid];
   const uint32_t w = blockIdx.x * kStreamWg + wid;
   if (w >= nwaves) return;
@@ -294,7 +294,14 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
   const uint64_t qlo = max<uint64_t>(s0, J.lead);
   const uint64_t qhi = min<uint64_t>(s0 + span, end >= nl ? end - nl + 1 : 0);
   if (qlo >= qhi) return;
-  for (uint32_t i = lane; i < nl; i += 64) s_nd[i] = needles[J.needle_off + i];
+  // the needle past its first two bytes as little-endian words (zero past its end): a
+  // candidate is verified 4 bytes per LDS round trip instead of 1
+  for (uint32_t i = lane; 4 * i + 2 < nl; i += 64) {
+    uint32_t x = 0;
+    for (uint32_t b = 0; b < 4; b++)
+      if (4 * i + 2 + b < nl) x |= uint32_t(needles[J.needle_off + 4 * i + 2 + b]) << (8 * b);
+    s_ndw[i] = x;
+  }
   const uint32_t n0 = uint32_t(needles[J.needle_off]) * 0x01010101u;
   const uint32_t n1 = nl > 1 ? uint32_t(needles[J.needle_off + 1]) * 0x01010101u : 0u;
   // a: aligned coordinate of this lane's 16 bytes. Past the stream's last 16-byte chunk
@@ -378,7 +385,14 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
         const uint64_t q = c + wo;
         if (q < qlo || q >= qhi) continue;
         bool ok = true;
-        for (uint32_t i = 2; i < nl && ok; i++) ok = s_win[wo + i] == s_nd[i];
+        const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
+        for (uint32_t k = 0; ok && 4 * k + 2 < nl; k++) {
+          const uint32_t off = wo + 2 + 4 * k;  // (< 2048: wo < 1024, nl <= 1024; the next word is padding)
+          const uint32_t x = __builtin_amdgcn_alignbyte(w32[(off >> 2) + 1], w32[off >> 2], off & 3);
+          const uint32_t rem = nl - 2 - 4 * k;
+          const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
+          ok = ((x ^ s_ndw[k]) & m) == 0;
+        }
         if (!ok) continue;
         const uint64_t p = q - J.lead;
         uint32_t v;
