@@ -162,6 +162,12 @@ if has limprof; then  # the limit-20 leg alone under TSG_PROF: static-run vs poo
     python3 -c "import json; d=json.load(open('gpurun_out/limprof_$su.json'))['limit20']; print(' step', d['step_us'], 'kernel', d['kernel_us']['p50'])"
   done
 fi
+if has mainstamps; then  # workgroup stamps of the main line's pool kernel only
+  TSG_STAMPS=1 timeout -k 10 300 python bench.py --steps 8 --warmup 2 --cpu-baseline 0 --cfg3 0 --cfg4 0 --concurrent-steps 0 \
+    --mall-steps 0 --shim-steps 0 --limit-steps 0 > gpurun_out/mainstamps.json 2> gpurun_out/mainstamps.err
+  rc=$?; echo "main stamps rc=$rc"; grep "stamps" gpurun_out/mainstamps.err | tail -6
+  [ $rc -eq 0 ] || exit $rc
+fi
 if has quick; then
   timeout -k 10 600 python bench.py --steps 200 --cpu-baseline 0 --cfg3 0 --concurrent-steps 0 ${BENCH_ARGS:-} \
     > gpurun_out/quick.json 2> gpurun_out/quick.err
