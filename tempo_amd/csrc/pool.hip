@@ -22,13 +22,12 @@ namespace tsg {
 // workgroups per CU finished as a ladder 22/25/28/33 us, profiles/r02_prio). The last
 // units of the launch are claimed in chunks from one device counter (dequeue: one
 // returning atomic per chunk, issued `lookahead` claims before the chunk is needed), so
-// CUs that the fabric serves faster take more of them. A match is written as it is found,
-// by its lane, into the workgroup's segment of pinned host memory (gathered from the cold
-// columns right away, system-scope write-through stores, slot from an LDS counter; record
+// CUs that the fabric serves faster take more of them. Matches go to the workgroup's LDS
+// record buffer as they are found (gathered from the cold columns right away; record
 // order inside a workgroup is claim order — the host sorts each block's records by scan
-// position, which is the reference order); at the end the workgroup waits for those stores
-// and stores its count. Matches beyond the segment are counted, not kept: the host then
-// reruns with larger segments, or on the segment/look-back path when they exceed rec_cap.
+// position, which is the reference order), then to the workgroup's segment of pinned
+// host memory with write-through stores, then its count. Records beyond the LDS capacity
+// are counted, not kept: the host then reruns the query on the segment/look-back path.
 constexpr int kPoolWaves = 16;
 constexpr int kPoolThreads = kPoolWaves * 64;
 constexpr uint32_t kPoolTile = 512;       // entries per unit (wave tile)
@@ -56,7 +55,7 @@ struct PoolArgs {
   uint32_t chunk_shift, lookahead, rec_cap, seg_cap, has_min, has_max, min32, max32, start_s, end_s;
   unsigned *head;       // this launch's dynamic-chunk counter (zero at launch)
   unsigned *head_next;  // the next launch's counter: zeroed by this one
-  uint8_t *recs;        // pinned host: workgroup w's first seg_cap records at w * seg_cap (rec_cap: the host's bound on seg_cap)
+  uint8_t *recs;        // pinned host: workgroup w's first seg_cap records at w * seg_cap (rec_cap: LDS records)
   uint32_t *counts;     // pinned host: workgroup w's match count, stored after its records
   unsigned long long *stamps;
   uint32_t *err;        // pinned host: set when an LDS poll ran past its bound (the host fails the query)
@@ -91,25 +90,6 @@ template <bool NTL>
 __device__ __forceinline__ uint32_t stream1(const uint8_t *p, uint64_t e) {
   if constexpr (NTL) return __builtin_nontemporal_load(G<uint32_t>(p + e));
   else return *G<uint32_t>(p + e);
-}
-
-// One match record into the workgroup's segment of pinned host memory, written through at
-// system scope by the lane that found it (48 B: id, start, end, entry | block | id length,
-// root name ids; MatchRec). Issued during the scan, so by the workgroup's end most of these
-// stores are already acknowledged.
-__device__ __forceinline__ void put_record(unsigned long long *d, const uint8_t *ids, const uint64_t *st_ns,
-                                           const uint64_t *en_ns, const uint32_t *names, const uint8_t *id_len,
-                                           uint32_t ei, uint32_t bidx) {
-  const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
-  const uint64_t st = G(st_ns)[ei], en = G(en_ns)[ei];
-  const uint64_t nm = G(reinterpret_cast<const uint64_t *>(names))[ei];
-  const uint32_t il = G(id_len)[ei];
-  host_store(d + 0, (unsigned long long)id.x | (unsigned long long)id.y << 32);
-  host_store(d + 1, (unsigned long long)id.z | (unsigned long long)id.w << 32);
-  host_store(d + 2, (unsigned long long)st);
-  host_store(d + 3, (unsigned long long)en);
-  host_store(d + 4, (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32);
-  host_store(d + 5, (unsigned long long)nm);
 }
 
 // The predicates of one unit (8 entries per lane) as a 32-bit lane mask, branch-free: every
@@ -156,6 +136,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
   __shared__ uint32_t s_bm[kArgBms * 8];
   __shared__ uint32_t s_chunk[kPoolChunks];
   __shared__ uint32_t s_next, s_nrec;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long s_rec[];  // rec_cap x 6 words
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = blockIdx.x, nsegs = A.nsegs, units = A.units;
   // ---- stage the launch's tables (one vector round trip from the kernel arguments)
@@ -182,8 +163,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     stamps[uint64_t(w) * kStampSlots + 8] = (xcc << 32) | hw;
   }
   const uint32_t S = A.static_per_wg, L = A.lookahead, cs = A.chunk_shift;
-  const uint32_t seg_cap = A.seg_cap;  // (<= rec_cap: the host sizes segments within the record budget)
-  unsigned long long *const seg = reinterpret_cast<unsigned long long *>(A.recs) + uint64_t(w) * seg_cap * 6;
+  const uint32_t rec_cap = A.rec_cap;
   const uint32_t dlo = A.has_min ? A.min32 : 0u, dhi = A.has_max ? A.max32 : 0xffffffffu;
   // An LDS chunk slot once its answer is in. Bounded: never reached unless the protocol
   // is broken, and then the query fails on the host instead of the GPU hanging.
@@ -285,9 +265,19 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     for (int b = 0; b < 4 * kSteps; b++) {
       if (!(mask & (1u << b))) continue;
       const uint32_t r = slot++;
-      if (r >= seg_cap) continue;  // (counted only: the host reruns with larger segments)
+      if (r >= rec_cap) continue;
       const uint32_t ei = R.e0 + uint32_t(b >> 2) * 256 + uint32_t(lane) * 4 + uint32_t(b & 3);
-      put_record(seg + uint64_t(r) * 6, ids, st_ns, en_ns, names, id_len, ei, bidx);
+      const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
+      const uint64_t st = G(st_ns)[ei], en = G(en_ns)[ei];
+      const uint64_t nm = G(reinterpret_cast<const uint64_t *>(names))[ei];
+      const uint32_t il = G(id_len)[ei];
+      unsigned long long *d = s_rec + uint64_t(r) * 6;
+      d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
+      d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
+      d[2] = st;
+      d[3] = en;
+      d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
+      d[5] = nm;
     }
   };
   // ---- scan: two units in flight per wave
@@ -313,10 +303,12 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     stamps[uint64_t(w) * kStampSlots + 2] = __builtin_amdgcn_s_memrealtime();
     stamps[uint64_t(w) * kStampSlots + 3] = __builtin_amdgcn_s_memrealtime();
   }
-  // ---- the count, once every record store of the workgroup is acknowledged (each lane
-  // stored its records into the workgroup's host segment as it found them)
+  // ---- records to the workgroup's host segment (write-through), then the count
   const uint32_t total = s_nrec;
-  if (total) {
+  const uint32_t nw = min(total, min(rec_cap, A.seg_cap)) * 6;
+  if (nw) {
+    auto *dst = reinterpret_cast<unsigned long long *>(A.recs) + uint64_t(w) * A.seg_cap * 6;
+    for (uint32_t i = tid; i < nw; i += blockDim.x) host_store(dst + i, s_rec[i]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -340,6 +332,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
   const unsigned long long t_start = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   __shared__ uint32_t s_bm[kArgBms * 8];
   __shared__ uint32_t s_nrec;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long s_rec[];  // rec_cap x 6 words
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = blockIdx.x, nsegs = A.nsegs, units = A.units;
   const uint32_t nwv = blockDim.x >> 6;
@@ -398,8 +391,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
         R.tv[q][k] = stream1<NTL>(B.col[q], uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
     }
   };
-  const uint32_t seg_cap = A.seg_cap;  // (<= rec_cap: the host sizes segments within the record budget)
-  unsigned long long *const seg = reinterpret_cast<unsigned long long *>(A.recs) + uint64_t(w) * seg_cap * 6;
+  const uint32_t rec_cap = A.rec_cap;
   const uint32_t dlo = A.has_min ? A.min32 : 0u, dhi = A.has_max ? A.max32 : 0xffffffffu;
   // (evaluated right after the unit's load, while the block state still describes it)
   auto eval = [&](const Regs &R, uint32_t bslot) {
@@ -421,9 +413,19 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
     for (int bit = 0; bit < 4 * kSteps; bit++) {
       if (!(mask & (1u << bit))) continue;
       const uint32_t r = slot++;
-      if (r >= seg_cap) continue;  // (counted only: the host reruns with larger segments)
+      if (r >= rec_cap) continue;
       const uint32_t ei = R.e0 + uint32_t(bit >> 2) * 256 + uint32_t(lane) * 4 + uint32_t(bit & 3);
-      put_record(seg + uint64_t(r) * 6, ids, st_ns, en_ns, names, id_len, ei, bidx);
+      const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
+      const uint64_t st = G(st_ns)[ei], en = G(en_ns)[ei];
+      const uint64_t nm = G(reinterpret_cast<const uint64_t *>(names))[ei];
+      const uint32_t il = G(id_len)[ei];
+      unsigned long long *d = s_rec + uint64_t(r) * 6;
+      d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
+      d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
+      d[2] = st;
+      d[3] = en;
+      d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
+      d[5] = nm;
     }
   };
   // the first unit's loads go out before anything is staged
@@ -466,10 +468,12 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
     stamps[uint64_t(w) * kStampSlots + 2] = __builtin_amdgcn_s_memrealtime();
     stamps[uint64_t(w) * kStampSlots + 3] = __builtin_amdgcn_s_memrealtime();
   }
-  // ---- the count, once every record store of the workgroup is acknowledged (each lane
-  // stored its records into the workgroup's host segment as it found them)
+  // ---- records to the workgroup's host segment (write-through), then the count
   const uint32_t total = s_nrec;
-  if (total) {
+  const uint32_t nw = min(total, min(rec_cap, A.seg_cap)) * 6;
+  if (nw) {
+    auto *dst = reinterpret_cast<unsigned long long *>(A.recs) + uint64_t(w) * A.seg_cap * 6;
+    for (uint32_t i = tid; i < nw; i += blockDim.x) host_store(dst + i, s_rec[i]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -583,10 +587,9 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   PA.max32 = uint32_t(q.max_ns);
   PA.start_s = q.start_s;
   PA.end_s = q.end_s;
-  // LDS: a 96 KiB dynamic request (unused by the kernels) keeps a second workgroup off the
-  // CU. Host segments: dc.pool_seg records per workgroup, adaptive (the records of a sparse
-  // query stay on a few pages of pinned memory), at most rec_cap (2048: beyond it the query
-  // is dense and takes the other paths)
+  // LDS: the record buffer is sized so that one workgroup takes more than half a CU. The
+  // host segments are smaller (dc.pool_seg records per workgroup, adaptive): the records
+  // of a sparse query stay on a few pages of pinned memory
   constexpr size_t kPoolLds = 96 << 10;
   const uint32_t rec_cap = std::min(dc.pool_rec, uint32_t(kPoolLds / sizeof(MatchRec)));
   if (uint64_t(W) * rec_cap > (1u << 20)) return false;  // (record slots are 20-bit in the host's sort keys)
