@@ -371,20 +371,6 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
       __builtin_amdgcn_s_waitcnt(kWaitVm0);
     }
     wave_sync();
-    // the staged values whose starts can hold this window's candidates: [w0, w1] (relative
-    // to vb; counts of staged offsets <= the window's first / last start position, both
-    // wave-wide ballots), so a candidate's value search spans the window's few values
-    // instead of every staged one
-    uint32_t w0 = 0, w1 = kv > 0 ? kv - 1 : 0;
-    if (cover == ~0ull || wlast < cover) {
-      const uint64_t pf = max<uint64_t>(c, qlo) - J.lead;
-      const uint32_t o0 = uint32_t(lane) < kv ? s_off[lane] : 0xffffffffu;
-      const uint32_t o1 = uint32_t(lane) + 64 < kv ? s_off[64 + lane] : 0xffffffffu;
-      const uint32_t a = uint32_t(__popcll(__ballot(uint64_t(o0) <= pf))) + uint32_t(__popcll(__ballot(uint64_t(o1) <= pf)));
-      const uint32_t b = uint32_t(__popcll(__ballot(uint64_t(o0) <= wlast))) + uint32_t(__popcll(__ballot(uint64_t(o1) <= wlast)));
-      w0 = a > 0 ? a - 1 : 0;
-      w1 = b > 0 ? b - 1 : 0;
-    }
     // candidates: verify from LDS, map the start to its value, mark the value. When the
     // staged offsets cover every start of the window (the usual case: a uniform branch) the
     // loop touches LDS only — a global load here would make the waits for the ring's slots
@@ -412,7 +398,7 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
         uint32_t v;
         uint64_t vend;
         if (!kGlobal || p < cover) {  // in the staged offsets: s_off[lo] <= p < s_off[lo + 1]
-          uint32_t lo = kGlobal ? 0 : w0, hi = kGlobal ? kv : w1 + 1;
+          uint32_t lo = 0, hi = kv;
           while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (uint64_t(s_off[mid]) <= p) lo = mid;
