@@ -139,6 +139,48 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
   extern __shared__ __attribute__((aligned(16))) unsigned long long s_rec[];  // rec_cap x 6 words
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = blockIdx.x, nsegs = A.nsegs, units = A.units;
+  const uint32_t S = A.static_per_wg, L = A.lookahead, cs = A.chunk_shift;
+  const uint32_t wv = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6)), nwv = blockDim.x >> 6;
+  // ---- the first two units of a wave, before anything is staged: a wave's first two claims
+  // are wv and wv + nwv (claims below S map to the workgroup's static run in order), so their
+  // loads go out with the block found by a scalar walk over the kernel arguments (the claims'
+  // bookkeeping, a chunk request they may trigger, runs after the staging)
+  PoolRegs<NT> ra, rb;
+  auto load_arg = [&](PoolRegs<NT> &R, uint32_t u) {
+    uint32_t b = 0;
+    while (b + 1 < nsegs && u >= A.ubase[b + 1]) b++;
+    R.blk = b;
+    const PoolBlk &B = A.blk[b];
+    const uint32_t npad = B.npad;
+    const uint32_t *scan = B.scan;
+    R.e0 = A.ebase[b] + (u - A.ubase[b]) * kPoolTile;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) {
+      const uint64_t e = uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
+      if (DUR) R.d[k] = stream4<NTL>(scan, e);
+      if (RANGE) {
+        R.s[k] = stream4<NTL>(scan + npad, e);
+        R.e[k] = stream4<NTL>(scan + 2ull * npad, e);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
+      if (NT <= 0) break;
+#pragma unroll
+      for (int k = 0; k < kSteps; k++)
+        R.tv[q][k] = stream1<NTL>(B.col[q], uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
+    }
+  };
+  const bool pre0 = wv < S, pre1 = wv + nwv < S;
+  uint32_t ua = kPoolNone, ub = kPoolNone;
+  if (pre0 && uint64_t(w) * S + wv < units) {
+    ua = w * S + wv;
+    load_arg(ra, ua);
+  }
+  if (pre1 && uint64_t(w) * S + wv + nwv < units) {
+    ub = w * S + wv + nwv;
+    load_arg(rb, ub);
+  }
   // ---- stage the launch's tables (one vector round trip from the kernel arguments)
   {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(A.blk);
@@ -148,7 +190,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     if (tid < kArgBms * 8) s_bm[tid] = reinterpret_cast<const uint32_t *>(A.bms)[tid];
     for (uint32_t i = tid; i < kPoolChunks; i += blockDim.x) s_chunk[i] = kPoolPending;
     if (tid == 0) {
-      s_next = 0;
+      s_next = min(2 * nwv, S);  // (the claims below it are the waves' first two)
       s_nrec = 0;
       if (w == 0) __hip_atomic_store(A.head_next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -162,7 +204,6 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     const unsigned long long xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
     stamps[uint64_t(w) * kStampSlots + 8] = (xcc << 32) | hw;
   }
-  const uint32_t S = A.static_per_wg, L = A.lookahead, cs = A.chunk_shift;
   const uint32_t rec_cap = A.rec_cap;
   const uint32_t dlo = A.has_min ? A.min32 : 0u, dhi = A.has_max ? A.max32 : 0xffffffffu;
   // An LDS chunk slot once its answer is in. Bounded: never reached unless the protocol
@@ -181,10 +222,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
   // claim -> unit (or kPoolNone): claims below S are this workgroup's static run; claim
   // S + k*C + off is unit `off` of its k-th dynamic chunk, which the claim L before the
   // chunk's first one requested from the device counter (so a wave rarely waits for it)
-  auto claim = [&]() -> uint32_t {
-    uint32_t c = 0;
-    if (lane == 0) c = atomicAdd(&s_next, 1u);
-    c = __builtin_amdgcn_readfirstlane(c);
+  auto trigger = [&](uint32_t c) {
     if (c + L >= S) {
       const uint32_t t = c + L - S;
       const uint32_t k = t >> cs;
@@ -205,6 +243,12 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
         }
       }
     }
+  };
+  auto claim = [&]() -> uint32_t {
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(&s_next, 1u);
+    c = __builtin_amdgcn_readfirstlane(c);
+    trigger(c);
     if (c < S) {  // (a small search's last static runs end at `units`: past it, no work)
       const uint32_t u = w * S + c;
       return u < units ? u : kPoolNone;
@@ -280,13 +324,20 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
       d[5] = nm;
     }
   };
-  // ---- scan: two units in flight per wave
-  PoolRegs<NT> ra, rb;
-  uint32_t ua = claim();
+  // ---- scan: two units in flight per wave (the first two loaded above when static). Every
+  // claim index is triggered exactly once, by the wave that holds it, whether or not it
+  // maps to a unit: a chunk request it owes is polled by later claims
+  if (pre0) trigger(wv);
+  if (pre1) trigger(wv + nwv);
+  if (!pre0) {
+    ua = claim();
+    if (ua != kPoolNone) load(ra, ua);
+  }
   if (ua != kPoolNone) {
-    load(ra, ua);
-    uint32_t ub = claim();
-    if (ub != kPoolNone) load(rb, ub);
+    if (!pre1) {
+      ub = claim();
+      if (ub != kPoolNone) load(rb, ub);
+    }
     for (;;) {
       eval(ra);
       if (ub == kPoolNone) break;
