@@ -616,6 +616,12 @@ def main():
     t0 = time.time()
     paths = gen_blocks(workdir, rank, args.blocks, args.entries, threads)
     log(f"rank {rank}: generated {args.blocks} x {args.entries} entries in {time.time() - t0:.1f}s")
+    # The config-3/4 generator threads (started at bench start, beside this set's synthesis)
+    # finish here, before the engine opens anything: no load or timed leg shares the host's
+    # CPUs with them, and the GPU is not left idle between the warmup and the timed steps.
+    for th in (cfg3_thread, cfg4_thread):
+        if th is not None:
+            th.join()
 
     streams = max(1, args.streams) if args.concurrent_steps else 1
     eng = T.Engine(devices=[local])
