@@ -14,10 +14,20 @@ and step i searches copy i % 4, so 4 x 150 MB of filter columns rotate through t
 256 MiB Infinity Cache and every step streams from HBM (roofline.regime "hbm").
 The same-copy-every-step number (round 1's, MALL-resident) is reported as "mall".
 
-Multi-GPU: one process per GPU (torchrun); blocks are sharded by block, each
-rank holds its own 10 M entries (weak scaling). Rank timings are bracketed by a
-barrier + device sync and the max over ranks is reported. No data-path
-collective: the ranks' ordered match lists are independent per block.
+Multi-GPU: one process per GPU. `--gpus N` under torchrun (WORLD_SIZE set) runs as
+one rank; `--gpus N` without it starts the N ranks itself (torch.distributed.run as a
+child process, before anything touches a GPU) and exits with their status, failing
+if fewer than N devices are visible. Blocks are sharded by block, each rank holds its
+own 10 M entries (weak scaling). Rank timings are bracketed by a barrier + device
+sync and the max over ranks is reported. No data-path collective in the main line:
+the ranks' ordered match lists are independent per block (the `merge` leg gathers
+them the way the frontend does, over gloo and over RCCL).
+
+Legs beside the main line: mall, limit20, shim (limit 0 and 20), concurrent, cfg3
+(config 3's per-GPU share: limit-20 early exit vs full scan), cfg4 (config 4 at 10 M
+entries), cfg5 (config 5: 10 M probes x 200 v2 blocks, ids sharded over the ranks),
+merge (N > 1). Every leg that searches is checked against the oracle after the timed
+legs (`parity`), on the host, untimed.
 
 Prints ONE JSON line (rank 0).
 """
@@ -26,6 +36,7 @@ import gc
 import json
 import os
 import shutil
+import subprocess
 import sys
 import tempfile
 import threading
@@ -175,12 +186,19 @@ def parse():
     ap.add_argument("--merge-steps", type=int, default=20,
                     help="N > 1: distributed full-scan queries with the frontend merge on rank 0 (0 = off)")
     ap.add_argument("--cfg4", type=int, default=None, help="config-4 leg (default: on at N=1)")
-    ap.add_argument("--cfg4-blocks", type=int, default=10)
-    ap.add_argument("--cfg4-entries", type=int, default=100_000)
-    ap.add_argument("--cfg4-steps", type=int, default=20)
+    ap.add_argument("--cfg4-blocks", type=int, default=10,
+                    help="config-4 blocks: one generated block of --cfg4-entries + device clones")
+    ap.add_argument("--cfg4-entries", type=int, default=1_000_000)
+    ap.add_argument("--cfg4-steps", type=int, default=10)
     ap.add_argument("--cfg3-blocks", type=int, default=25)
     ap.add_argument("--cfg3-entries", type=int, default=5_000_000)
     ap.add_argument("--cfg3-steps", type=int, default=64)
+    ap.add_argument("--cfg5", type=int, default=1, help="config-5 leg: batched trace-ID lookup (0 = skip)")
+    ap.add_argument("--cfg5-blocks", type=int, default=200)
+    ap.add_argument("--cfg5-objects", type=int, default=100_000)
+    ap.add_argument("--cfg5-probes", type=int, default=10_000_000, help="probes over all ranks (sharded by id)")
+    ap.add_argument("--cfg5-steps", type=int, default=5)
+    ap.add_argument("--parity", type=int, default=1, help="oracle parity of the cfg3/cfg4/cfg5 legs (untimed)")
     ap.add_argument("--pin", default="auto", choices=["auto", "none"],
                     help="auto: keep this process on the CPUs of its GPU's NUMA node (tsg_device_numa_node)")
     ap.add_argument("--workdir", default=None)
@@ -190,6 +208,110 @@ def parse():
 
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(argv, n, port):
+    """The torch.distributed.run command that starts `n` ranks of this script (one per GPU,
+    rendezvous on 127.0.0.1) with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def rank_env(args, env=None):
+    """(rank, world, local rank) of this process, or None when `--gpus N` asks this process
+    to start the ranks itself (N > 1 and no torchrun environment). A torchrun world that
+    differs from --gpus is an error."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if args.gpus not in (1, world):  # (--gpus 1 under an outer torchrun: the world decides)
+            raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return int(env.get("RANK", "0")), world, int(env.get("LOCAL_RANK", "0"))
+    if args.gpus <= 1:
+        return 0, 1, 0
+    return None
+
+
+def launch_ranks(args, argv, device_count=None):
+    """`--gpus N` without torchrun: start N ranks as a child process group and return
+    their exit status. Runs before anything touches a GPU (no HIP call in this process:
+    torch.cuda.device_count() does not initialise the device on this image)."""
+    if device_count is None:
+        import torch
+        device_count = torch.cuda.device_count()
+    if device_count < args.gpus:
+        print(f"bench: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {device_count}",
+              file=sys.stderr, flush=True)
+        return 2
+    cmd = launch_cmd(argv, args.gpus, free_port())
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log("starting %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.call(cmd, env=env)
+
+
+def columns_vs_oracle(cols, gmet, exp, omet, nrep):
+    """GPU result (Engine.search_columns) over `nrep` byte-identical device copies of one block
+    vs the oracle's result on that block: copy r must hold exactly the oracle's matches, in
+    order, with block index r, every field equal (id, scan position, start, end, DurationMs,
+    root names); the metrics are nrep times the oracle's."""
+    import numpy as np
+    keys = ("traces_inspected", "bytes_inspected", "blocks_inspected", "blocks_skipped")
+    got_m = (gmet.inspected_traces, gmet.inspected_bytes, gmet.inspected_blocks, gmet.skipped_blocks)
+    if got_m != tuple(nrep * omet[k] for k in keys):
+        return False
+    n1 = len(exp)
+    if len(cols["start_ns"]) != n1 * nrep:
+        return False
+    if n1 == 0:
+        return True
+    eid = np.frombuffer(b"".join(m["id"] for m in exp), np.uint8).reshape(n1, 16)
+    col = lambda f, dt: np.fromiter((m[f] for m in exp), dt, n1)  # noqa: E731
+    e_entry, e_start, e_end = col("entry_idx", np.uint64), col("start_ns", np.uint64), col("end_ns", np.uint64)
+    e_dur = col("duration_ms", np.uint32)
+    nidx = {s: i for i, s in enumerate(cols["names"])}
+    e_svc = np.fromiter((nidx.get(m["root_service"], -1) for m in exp), np.int64, n1)
+    e_nm = np.fromiter((nidx.get(m["root_name"], -1) for m in exp), np.int64, n1)
+    for r in range(nrep):
+        s = slice(r * n1, (r + 1) * n1)
+        if not ((cols["block_idx"][s] == r).all() and (cols["entry_idx"][s] == e_entry).all()
+                and (cols["trace_id"][s] == eid).all() and (cols["start_ns"][s] == e_start).all()
+                and (cols["end_ns"][s] == e_end).all() and (cols["duration_ms"][s] == e_dur).all()
+                and (cols["root_service"][s] == e_svc).all() and (cols["root_name"][s] == e_nm).all()):
+            return False
+    return True
+
+
+def oracle_query(q):
+    """A bench query (SearchRequest fields) as oracle.search keyword arguments."""
+    return dict(tags=q.get("tags", {}), min_ms=q.get("min_duration_ms", 0), max_ms=q.get("max_duration_ms", 0),
+                start=q.get("start", 0), end=q.get("end", 0))
+
+
+def run_parity(jobs):
+    """Run the legs' oracle checks (name -> callable) concurrently on the host (the oracle's
+    C calls release the GIL); returns name -> result (or the error)."""
+    res = {}
+
+    def one(item):
+        name, fn = item
+        t0 = time.time()
+        try:
+            r = fn()
+        except Exception as e:  # noqa: BLE001  (reported, not raised: the timed figures stand)
+            r = {"ok": False, "error": repr(e)}
+        r["oracle_s"] = time.time() - t0
+        res[name] = r
+
+    parallel(one, list(jobs.items()))
+    return res
 
 
 def gen_blocks(workdir, rank, nblocks, n, threads):
@@ -369,22 +491,31 @@ def shim_leg(args, eng, sets, pipe, entries, nmatch, batched, dist, all_cpus):
     cpus = node_cpus(node) & all_cpus if node >= 0 else set()
     if len(cpus) > len(sets[0]) + 2:
         cpus = set(idlest(sorted(cpus), len(sets[0]) + 2))
+    # limit 20 (the ingester's default): each block's call keeps its first 20 records; the
+    # record count per query is the per-block searches' (one block per call)
+    n20 = sum(eng.search_raw([b], pipe, limit=20)[0] for b in sets[0])
     try:
         if cpus and len(cpus) > len(mask):
             os.sched_setaffinity(0, cpus)
         eng.shim_pattern(sets, pipe, 16)  # warm (threads, per-thread scratch, pinned buffers)
+        eng.shim_pattern(sets, pipe, 16, limit=20)
         if dist:
             dist.barrier()
         ns, nm = eng.shim_pattern(sets, pipe, args.shim_steps)
+        ns20, nm20 = eng.shim_pattern(sets, pipe, args.shim_steps, limit=20)
     finally:
         os.sched_setaffinity(0, mask)
     assert all(x == nmatch for x in nm), "shim-pattern record count differs from the batched search"
+    assert all(x == n20 for x in nm20), "shim-pattern limit-20 record count differs from the per-block searches"
     rate = entries * len(ns) / (sum(ns) / 1e9)
     return {"threads": len(sets[0]), "queries": len(ns), "entries_per_s": rate,
             "vs_batched": rate / batched if batched else None,
             "query_us": pct([x / 1e3 for x in ns]),
-            "note": "one C thread per block, each a tsg_search over its block (limit 0), per query; "
-                    "concurrent calls coalesced into one launch; per-GPU rate"}
+            "limit20": {"query_us": pct([x / 1e3 for x in ns20]), "records_per_query": n20,
+                        "entries_per_s": entries * len(ns20) / (sum(ns20) / 1e9)},
+            "note": "one C thread per block, each a tsg_search over its block (limit 0, and limit 20 "
+                    "passed per block as Pipeline.Query carries it), per query; concurrent calls "
+                    "coalesced into one launch (per-block caps under a limit); per-GPU rate"}
 
 
 def cfg3_path(workdir, rank):
@@ -452,6 +583,29 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, gen_thread=Non
         nl, metl = eng.search_raw(blocks, pipe, limit=20)
         if i >= 3:
             lim.append(time.perf_counter() - ts)
+    # results kept for the oracle check after the timed legs (every copy is the same block)
+    full_cols, full_met = eng.search_columns(blocks, pipe)
+    lim_cols, lim_met = eng.search_columns(blocks, pipe, limit=20)
+    nrep = len(blocks)
+
+    def parity():
+        from oracle import oracle as O
+        q = oracle_query(QUERY)
+        ob = O.Block(p)
+        exp, omet, st = O.search([ob], **q)
+        full_ok = st == 0 and columns_vs_oracle(full_cols, full_met, exp, omet, nrep)
+        # limit 20 over the 25 copies: the sequential consumer (blocks in order) on the oracle
+        lexp, lomet, lst = O.search([ob] * nrep, limit=20, **q)
+        lim_ok = lst == 0 and len(lim_cols["start_ns"]) == len(lexp) and all(
+            (int(lim_cols["block_idx"][i]), int(lim_cols["entry_idx"][i]), bytes(lim_cols["trace_id"][i]),
+             int(lim_cols["start_ns"][i]), int(lim_cols["end_ns"][i]))
+            == (m["block_idx"], m["entry_idx"], m["id"], m["start_ns"], m["end_ns"]) for i, m in enumerate(lexp)) and (
+            lim_met.inspected_traces, lim_met.inspected_bytes, lim_met.inspected_blocks) == (
+            lomet["traces_inspected"], lomet["bytes_inspected"], lomet["blocks_inspected"])
+        return {"ok": bool(full_ok and lim_ok), "full_scan": bool(full_ok), "limit20": bool(lim_ok),
+                "checked": f"full scan: all {len(full_cols['start_ns'])} matches of the {nrep} copies "
+                           f"(every field, in order) + metrics vs the oracle on the block; limit 20: "
+                           f"the oracle's sequential consumer over the {nrep} copies"}
     res = {
         "workload": f"config 3 per-GPU share: {len(blocks)} blocks x {args.cfg3_entries} entries "
                     f"(1 generated + {len(blocks) - 1} device clones), config-2 query",
@@ -466,39 +620,42 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, gen_thread=Non
     }
     for b in blocks:
         b.close()
-    return res
+    return res, parity
 
 
-def cfg4_paths(args, workdir, rank):
-    return [os.path.join(workdir, f"r{rank}cfg4_{i}") for i in range(args.cfg4_blocks)]
+def cfg4_path(workdir, rank):
+    return os.path.join(workdir, f"r{rank}cfg4")
 
 
 def cfg4_generate(args, workdir, rank):
-    """Config-4 blocks (the high-cardinality profile: ~unique http.url, 100-2000 B
-    db.statement values), written in parallel in a thread at bench start."""
+    """The config-4 block (the high-cardinality profile: ~unique http.url, 100-2000 B
+    db.statement values; one block of --cfg4-entries), written in a thread at bench start."""
     import tempo_amd as T
-
-    def one(i_p):
-        i, p = i_p
-        if not os.path.exists(os.path.join(p, "search.meta.json")):
-            T.synth_search_block(p, args.cfg4_entries, seed=4000 + 97 * rank + i, profile=1,
-                                 encoding=T.ENC_SNAPPY, page_size=1024 * 1024)
-    parallel(one, list(enumerate(cfg4_paths(args, workdir, rank))))
+    p = cfg4_path(workdir, rank)
+    if not os.path.exists(os.path.join(p, "search.meta.json")):
+        T.synth_search_block(p, args.cfg4_entries, seed=4000 + 97 * rank, profile=1, encoding=T.ENC_SNAPPY,
+                             page_size=1024 * 1024)
 
 
 CFG4_QUERIES = [
     ("statement+url", dict(tags={"db.statement": "from orders", "http.url": "/carts/"}, min_duration_ms=1)),
     ("statement_id_range", dict(tags={"db.statement": "where id = 77"}, start=QUERY["start"], end=QUERY["end"])),
     ("url_prefix", dict(tags={"http.url": "/api/v1/users/12"})),
+    # a needle no value holds: MatchesBlock skips every block (blocksSkipped), from the
+    # device dictionary pass (the host scan of the header's values took 24 ms, VERDICT r3)
+    ("statement_absent", dict(tags={"db.statement": "qqzz"})),
 ]
 
 
 def cfg4_leg(args, eng, workdir, rank, gen_thread=None):
-    """BASELINE config 4: high-cardinality tags (http.url, db.statement) with long values,
-    ContainsTag semantics. Per query: the dictionary pass (every value of the searched keys
-    tested for the needle: dict_stream_kernel over the value bytes, then the value-set
-    bitmaps) and the scan. B_dict = the searched keys' dictionary bytes + offsets; the
-    dictionary pass time = device sequence time (TIME_ALL events) - scan kernel time."""
+    """BASELINE config 4 as config 2's size: --cfg4-blocks blocks of --cfg4-entries (10 x
+    1 M = 10 M entries: one generated block and device clones of it, tsg_block_clone),
+    high-cardinality tags (http.url, db.statement) with long values, ContainsTag semantics.
+    Per query: the dictionary pass (every value of the searched keys tested for the needle:
+    dict_stream_kernel over the value bytes, then the value-set bitmaps) and the scan; the
+    block filter's tag half comes from the same pass. B_dict = the searched keys' dictionary
+    bytes + offsets; the dictionary pass time = device sequence time (TIME_ALL events) - scan
+    kernel time. step_over_device = step p50 / device p50 (host share of a query)."""
     import tempo_amd as T
     t0 = time.time()
     if gen_thread is not None:
@@ -506,14 +663,20 @@ def cfg4_leg(args, eng, workdir, rank, gen_thread=None):
     cfg4_generate(args, workdir, rank)
     gen_s = time.time() - t0
     t0 = time.time()
-    blocks = parallel(eng.open_block, cfg4_paths(args, workdir, rank))
+    p = cfg4_path(workdir, rank)
+    b0 = eng.open_block(p)
+    load1_s = time.time() - t0
+    fb_gb = b0.info()["fb_bytes"] / 1e9
+    blocks = [b0] + [b0.clone(eng) for _ in range(args.cfg4_blocks - 1)]
     load_s = time.time() - t0
     entries = sum(b.info()["entries"] for b in blocks)
     log(f"rank {rank}: cfg4 {len(blocks)} x {args.cfg4_entries} entries resident (gen wait {gen_s:.1f}s, "
-        f"load {load_s:.1f}s)")
-    res = {"workload": f"config 4: {len(blocks)} blocks x {args.cfg4_entries} entries, high-cardinality profile "
-                       f"(~unique http.url, 100-2000 B db.statement)", "entries": entries, "load_s": load_s,
-           "queries": {}}
+        f"load {load1_s:.1f}s + clones {load_s - load1_s:.1f}s)")
+    res = {"workload": f"config 4: {len(blocks)} blocks x {args.cfg4_entries} entries (1 generated + "
+                       f"{len(blocks) - 1} device clones), high-cardinality profile (~unique http.url, "
+                       f"100-2000 B db.statement)", "entries": entries, "load_s": load_s,
+           "load_one_block_s": load1_s, "load_gb_per_s": fb_gb / load1_s if load1_s else None, "queries": {}}
+    kept = {}
     for name, q in CFG4_QUERIES:
         pipe = T.Pipeline(T.SearchRequest(**q))
         n0, _ = eng.search_raw(blocks, pipe)
@@ -530,19 +693,162 @@ def cfg4_leg(args, eng, workdir, rank, gen_thread=None):
         b_dict = met.device_bytes_read - met.scan_bytes
         dmed = sorted(dict_ns)[len(dict_ns) // 2]
         smed = sorted(scan_ns)[len(scan_ns) // 2]
+        amed = sorted(ts_all)[len(ts_all) // 2]
+        spmed = sorted(steps)[len(steps) // 2]
         res["queries"][name] = {
-            "query": q, "matches": n0,
+            "query": q, "matches": n0, "blocks_inspected": met.inspected_blocks, "blocks_skipped": met.skipped_blocks,
             "step_us": pct([x * 1e6 for x in steps]),
-            "entries_per_s": entries / (sorted(steps)[len(steps) // 2]),
+            "entries_per_s": entries / spmed,
+            "device_us": pct([x / 1e3 for x in ts_all]),
+            "step_over_device": spmed * 1e9 / amed if amed else None,
             "dict_pass_us": pct([x / 1e3 for x in dict_ns]), "scan_us": pct([x / 1e3 for x in scan_ns]),
             "b_dict": b_dict, "scan_bytes": met.scan_bytes,
             "dict_gbps": b_dict / dmed if dmed else None,
             "dict_frac": b_dict / dmed / PEAK_HBM_GBPS if dmed else None,
             "scan_gbps": met.scan_bytes / smed if smed else None,
         }
+        if args.parity:
+            kept[name] = (q, eng.search_columns(blocks, pipe))
+    nrep = len(blocks)
     for b in blocks:
         b.close()
-    return res
+
+    def parity():
+        from oracle import oracle as O
+        ob = O.Block(p)
+        out = {}
+
+        def one(name):
+            q, (cols, gmet) = kept[name]
+            exp, omet, st = O.search([ob], **oracle_query(q))
+            out[name] = bool(st == 0 and columns_vs_oracle(cols, gmet, exp, omet, nrep))
+        parallel(one, list(kept))
+        return {"ok": all(out.values()), "queries": out,
+                "checked": f"every query: all matches of the {nrep} copies (every field, in order) and the "
+                           f"metrics (blocks skipped / inspected, traces, bytes) vs the oracle on the block"}
+    return res, parity if args.parity else None
+
+
+def cfg5_dir(shared):
+    return os.path.join(shared, "cfg5")
+
+
+def cfg5_generate(args, shared, rank, world):
+    """Config-5 v2 blocks (synthetic ids, bloom fp 0.01 with 100 KiB shards, index over
+    1 MiB data pages), written into a directory every rank of this node reads: rank r
+    writes blocks i = r mod world (each with its ids beside it as ids.npy)."""
+    import numpy as np
+    import tempo_amd as T
+    d = cfg5_dir(shared)
+    os.makedirs(d, exist_ok=True)
+
+    def one(i):
+        p = os.path.join(d, f"v2_{i:03d}")
+        if not os.path.exists(os.path.join(p, "ids.npy")):
+            ids = T.synth_v2_block(p, args.cfg5_objects, seed=9000 + i)
+            np.save(os.path.join(p, "ids.tmp.npy"), ids)
+            os.replace(os.path.join(p, "ids.tmp.npy"), os.path.join(p, "ids.npy"))
+    mine = [i for i in range(args.cfg5_blocks) if i % world == rank]
+    nth = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    for k in range(0, len(mine), nth):
+        parallel(one, mine[k:k + nth])
+
+
+def cfg5_leg(args, eng, shared, rank, world, dist, gen_thread=None):
+    """BASELINE config 5: batched trace-ID lookup, --cfg5-probes ids (half present in some
+    block, half random) against --cfg5-blocks v2 blocks (bloom + sorted index; every block on
+    every rank), the ids sharded over the ranks (shard.shard_ids: no exchange on the data
+    path). value = probes over all ranks / the slowest rank's device time (tsg_lookup_ids'
+    event pair around slab build + count + write: ids resident, hits in HBM); host_e2e adds
+    moving ids in and hits out (PCIe). N > 1: the per-rank hit tables gathered to rank 0 over
+    RCCL (shard.distributed_lookup on cuda) once, timed."""
+    import numpy as np
+    import torch
+    import tempo_amd as T
+    from tempo_amd import shard
+    if gen_thread is not None:
+        gen_thread.join()
+    cfg5_generate(args, shared, rank, world)
+    if dist:
+        dist.barrier()
+    d = cfg5_dir(shared)
+    paths = [os.path.join(d, f"v2_{i:03d}") for i in range(args.cfg5_blocks)]
+    present = np.concatenate([np.load(os.path.join(p, "ids.npy")) for p in paths])
+    rng = np.random.default_rng(5)
+    half = args.cfg5_probes // 2
+    probes = np.concatenate([present[rng.integers(0, len(present), half)],
+                             rng.integers(0, 256, (args.cfg5_probes - half, 16), dtype=np.uint8)])
+    probes = np.ascontiguousarray(probes[rng.permutation(len(probes))])
+    del present
+    sl = shard.shard_ids(len(probes), world, rank)
+    mine = np.ascontiguousarray(probes[sl.start:sl.stop])
+    old = os.environ.get("TSG_V2_NO_DATA")
+    os.environ["TSG_V2_NO_DATA"] = "1"  # (the lookup reads bloom + index only)
+    t0 = time.time()
+    try:
+        blocks = parallel(eng.open_v2block, paths)
+    finally:
+        if old is None:
+            os.environ.pop("TSG_V2_NO_DATA", None)
+        else:
+            os.environ["TSG_V2_NO_DATA"] = old
+    load_s = time.time() - t0
+    hits, _ = eng.lookup(blocks, mine)  # warm
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    walls, kns = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.cfg5_steps):
+        ts = time.perf_counter()
+        hits, kns_i = eng.lookup(blocks, mine)
+        walls.append(time.perf_counter() - ts)
+        kns.append(kns_i)
+    elapsed = time.perf_counter() - t0
+    kmed = sorted(kns)[len(kns) // 2]
+    if dist:
+        t = torch.tensor([elapsed, float(kmed)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kmed = float(t[0].item()), float(t[1].item())
+    res = {"workload": f"config 5: {args.cfg5_probes} probe ids (50 % present) x {args.cfg5_blocks} v2 blocks "
+                       f"of {args.cfg5_objects} objects, ids sharded over {world} rank(s)",
+           "probes_per_rank": len(mine), "steps": args.cfg5_steps, "load_s": load_s,
+           "value": args.cfg5_probes / (kmed / 1e9), "unit": "probes/s",
+           "device_ms": kmed / 1e6, "probe_block_pairs_per_s": args.cfg5_probes * args.cfg5_blocks / (kmed / 1e9),
+           "host_e2e": {"probes_per_s": args.cfg5_probes * args.cfg5_steps / elapsed,
+                        "step_ms": pct([x * 1e3 for x in walls])},
+           "hits_rank0": int(len(hits)),
+           "requests_per_probe": "6.3 random 64-B slab reads (PMC FETCH_SIZE, profiles/r03_lookup)"}
+    if dist:
+        t0 = time.perf_counter()
+        allhits = shard.distributed_lookup(lambda x: eng.lookup(blocks, x)[0], probes, device="cuda")
+        torch.cuda.synchronize()
+        res["rccl_gather"] = {"s": time.perf_counter() - t0,
+                              "hits": int(len(allhits)) if allhits is not None else None,
+                              "note": "lookup of every rank's slice + dist.gather of the hit tables "
+                                      "to rank 0 over RCCL (nccl backend, cuda tensors)"}
+    for b in blocks:
+        b.close()
+    check = probes[:20_000] if rank == 0 else None
+    got_check = hits[hits[:, 0] < 20_000] if rank == 0 else None
+
+    def parity():
+        from oracle import oracle as O
+        ob = [O.V2Block(p) for p in paths]
+        nthr = max(1, min(16, len(os.sched_getaffinity(0))))
+        rc, exp = O.lookup(ob, check, nthreads=nthr)
+        ok = rc == 0 and np.array_equal(got_check, np.array(exp, dtype=np.int64).reshape(-1, 5))
+        # the CPU baseline on the same host: the oracle's lookup (pthreads over probes)
+        cs = probes[:200_000]
+        t0 = time.perf_counter()
+        O.lookup(ob, cs, nthreads=nthr)
+        dt = time.perf_counter() - t0
+        return {"ok": bool(ok), "checked": f"every hit (id, block, record, start, length) of the first "
+                                           f"{len(check)} probes vs the oracle's lookup",
+                "cpu_baseline": {"value": len(cs) / dt, "unit": "probes/s", "cores": nthr, "kind": "port",
+                                 "sample": f"first {len(cs)} probes x all {len(paths)} blocks, oracle lookup "
+                                           f"(oracle/tsg_oracle.c, {nthr} threads), {dt:.2f} s"}}
+    return res, parity if (args.parity and rank == 0) else None
 
 
 def merge_leg(args, eng, base, pipe, rank, world, dist):
@@ -578,6 +884,19 @@ def merge_leg(args, eng, base, pipe, rank, world, dist):
             res["merged_traces"] = len(merged)
             res["inspected_traces"] = merged.metrics.inspected_traces
             res["block_errors"] = sum(1 for x in merged.block_status if x)
+        # the same gather as cuda byte tensors over the default (nccl = RCCL over xGMI) group
+        m2 = shard.distributed_search_packed(local, everything, nb, device="cuda", columns=True)
+        dist.barrier()
+        ts2 = []
+        for _ in range(args.merge_steps):
+            t0 = time.perf_counter()
+            m2 = shard.distributed_search_packed(local, everything, nb, device="cuda", columns=True)
+            dist.barrier()
+            ts2.append(time.perf_counter() - t0)
+        res["rccl"] = {"step_us": pct([x * 1e6 for x in ts2]),
+                       "transport": "RCCL gather of the packed records (cuda uint8 tensors) to rank 0, then merge"}
+        if rank == 0:
+            res["rccl"]["same_as_gloo"] = bool(len(m2) == len(merged) and (m2.recs == merged.recs).all())
         return res
     except Exception as e:  # (the main line above is already measured; report, do not fail)
         return {"error": repr(e)}
@@ -585,11 +904,12 @@ def merge_leg(args, eng, base, pipe, rank, world, dist):
 
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    re = rank_env(args)
+    if re is None:  # --gpus N, no torchrun around us: start the ranks (nothing has touched a GPU)
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    rank, world, local = re
     if args.cfg3 is None:
-        args.cfg3 = 1 if world == 1 else 0
+        args.cfg3 = 1  # (config 3 is an 8-GPU config: every rank runs its share)
     if args.cfg4 is None:
         args.cfg4 = 1 if world == 1 else 0
     import torch
@@ -604,24 +924,31 @@ def main():
 
     workdir = args.workdir or tempfile.mkdtemp(prefix="tsg_bench_", dir="/tmp")
     os.makedirs(workdir, exist_ok=True)
+    # files every rank of the node reads (config 5's replicated v2 blocks): one directory per run
+    shared = os.path.join(args.workdir, "shared") if args.workdir else os.path.join(
+        "/tmp", "tsg_bench_shared_%s_%s" % (os.environ.get("MASTER_PORT", "solo"), os.environ.get(
+            "TORCHELASTIC_RUN_ID", os.getppid() if world > 1 else os.getpid())))
+    os.makedirs(shared, exist_ok=True)
     threads = min(args.blocks, max(1, min(16, (os.cpu_count() or 8)) // max(1, min(world, 8))))
-    cfg3_thread = None
+    gens = {}
     if args.cfg3:
-        cfg3_thread = threading.Thread(target=cfg3_generate, args=(args, workdir, rank), daemon=True)
-        cfg3_thread.start()
-    cfg4_thread = None
+        gens["cfg3"] = threading.Thread(target=cfg3_generate, args=(args, workdir, rank), daemon=True)
     if args.cfg4:
-        cfg4_thread = threading.Thread(target=cfg4_generate, args=(args, workdir, rank), daemon=True)
-        cfg4_thread.start()
+        gens["cfg4"] = threading.Thread(target=cfg4_generate, args=(args, workdir, rank), daemon=True)
+    if args.cfg5:
+        gens["cfg5"] = threading.Thread(target=cfg5_generate, args=(args, shared, rank, world), daemon=True)
+    for th in gens.values():
+        th.start()
     t0 = time.time()
     paths = gen_blocks(workdir, rank, args.blocks, args.entries, threads)
     log(f"rank {rank}: generated {args.blocks} x {args.entries} entries in {time.time() - t0:.1f}s")
-    # The config-3/4 generator threads (started at bench start, beside this set's synthesis)
+    # The config-3/4/5 generator threads (started at bench start, beside this set's synthesis)
     # finish here, before the engine opens anything: no load or timed leg shares the host's
     # CPUs with them, and the GPU is not left idle between the warmup and the timed steps.
-    for th in (cfg3_thread, cfg4_thread):
-        if th is not None:
-            th.join()
+    t0 = time.time()
+    for th in gens.values():
+        th.join()
+    log(f"rank {rank}: waited {time.time() - t0:.1f}s for the cfg3/4/5 generators")
 
     streams = max(1, args.streams) if args.concurrent_steps else 1
     eng = T.Engine(devices=[local])
@@ -786,28 +1113,50 @@ def main():
     if args.concurrent_steps and streams > 1:
         out["concurrent"] = concurrent_leg(args, base, pipe, streams, entries, dist, world, local)
 
+    checks = {}
     if args.cfg3:
-        out["cfg3"] = cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, cfg3_thread)
+        out["cfg3"], checks["cfg3"] = cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags)
 
     if args.cfg4:
-        out["cfg4"] = cfg4_leg(args, eng, workdir, rank, cfg4_thread)
+        out["cfg4"], checks["cfg4"] = cfg4_leg(args, eng, workdir, rank)
+
+    if args.cfg5:
+        out["cfg5"], checks["cfg5"] = cfg5_leg(args, eng, shared, rank, world, dist)
 
     if world > 1 and args.merge_steps:
         out["merge"] = merge_leg(args, eng, base, pipe, rank, world, dist)
 
-    gc.enable()
-    if rank == 0 and world == 1 and args.cpu_baseline:
-        os.sched_setaffinity(0, all_cpus)  # (the CPU baselines get the whole host share back)
-        out["cpu_baseline"] = cpu_baselines(paths, got, cpu_threads)
-
-    if rank == 0:
-        print(json.dumps(out), flush=True)
     for s in sets:
         for b in s:
             b.close()
     eng.close()
+    gc.enable()
+    os.sched_setaffinity(0, all_cpus)  # (the host checks and CPU baselines get the whole host share back)
+    if args.parity:
+        # the oracle checks of the cfg3/cfg4/cfg5 legs (rank 0 reports; every rank checks its own share)
+        jobs = {k: v for k, v in checks.items() if v is not None}
+        t0 = time.time()
+        par = run_parity(jobs)
+        log(f"rank {rank}: parity {', '.join('%s=%s' % (k, v.get('ok')) for k, v in par.items())} "
+            f"in {time.time() - t0:.1f}s")
+        for k, v in par.items():
+            if k == "cfg5" and "cpu_baseline" in v:
+                out[k]["cpu_baseline"] = v.pop("cpu_baseline")
+            out[k]["parity"] = v
+        if dist:
+            ok = torch.tensor([int(all(v.get("ok") for v in par.values()))], dtype=torch.int32)
+            g = dist.new_group(backend="gloo")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=g)
+            out["parity_all_ranks"] = bool(ok.item())
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        out["cpu_baseline"] = cpu_baselines(paths, got, cpu_threads)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     if not args.keep and not args.workdir:
         shutil.rmtree(workdir, ignore_errors=True)
+        if rank == 0:
+            shutil.rmtree(shared, ignore_errors=True)
     if dist:
         dist.destroy_process_group()
 

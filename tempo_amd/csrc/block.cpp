@@ -506,6 +506,88 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
   }
   for (auto &kc : hb.keys) kc.col.resize(hb.n, kNone);
   canonicalize_narrow_keys(hb);
+  verify_header_dicts(hb, nthreads);
+}
+
+// ---- header values == dictionary (hdr_defer) -------------------------------------------
+namespace {
+inline uint64_t fmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+// Two independent 64-bit lanes over the value's bytes (length folded in), avalanched.
+struct H128 {
+  uint64_t a = 0, b = 0;
+  void add(const uint8_t *p, size_t n) {
+    uint64_t x = 0x9E3779B97F4A7C15ULL ^ n, y = 0xC2B2AE3D27D4EB4FULL + n;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      uint64_t w;
+      std::memcpy(&w, p + i, 8);
+      x = rotl64((x ^ w) * 0x87c37b91114253d5ULL, 31);
+      y = rotl64((y + w) * 0x4cf5ad432745937fULL, 27) ^ x;
+    }
+    if (i < n) {
+      uint64_t w = 0;
+      std::memcpy(&w, p + i, n - i);
+      x = rotl64((x ^ w) * 0x87c37b91114253d5ULL, 31);
+      y = rotl64((y + w) * 0x4cf5ad432745937fULL, 27) ^ x;
+    }
+    a += fmix64(x ^ (y >> 1));  // multiset: a sum, so the order of the values does not matter
+    b += fmix64(y + rotl64(x, 17));
+  }
+};
+// sum of H128 over items [0, n) (value(i) -> string_view), on up to nthreads threads
+template <class Value>
+H128 multiset_hash(size_t n, int nthreads, Value &&value) {
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(size_t(std::max(1, nthreads)), n / 16384));
+  std::vector<H128> part(nt);
+  auto run = [&](size_t t) {
+    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    for (size_t i = lo; i < hi; i++) {
+      const std::string_view v = value(i);
+      part[t].add(reinterpret_cast<const uint8_t *>(v.data()), v.size());
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; t++) th.emplace_back(run, t);
+  run(0);
+  for (auto &x : th) x.join();
+  H128 s;
+  for (auto &p : part) {
+    s.a += p.a;
+    s.b += p.b;
+  }
+  return s;
+}
+}  // namespace
+
+void verify_header_dicts(HostBlock &hb, int nthreads) {
+  hb.hdr_defer.assign(hb.hdr_keys.size(), 0);
+  if (!hb.hdr_index) return;
+  if (nthreads <= 0) nthreads = int(std::max(1u, std::thread::hardware_concurrency()));
+  nthreads = std::min(nthreads, 32);
+  for (size_t hk = 0; hk < hb.hdr_keys.size(); hk++) {
+    auto it = hb.key_index.find(std::string(hb.hdr_keys[hk]));
+    if (it == hb.key_index.end()) continue;
+    const KeyColumn &kc = hb.keys[size_t(it->second)];
+    if (kc.dict_bytes.size() <= kDeferMinBytes) continue;
+    const uint32_t v0 = hb.hdr_val0[hk], v1 = hb.hdr_val0[hk + 1];
+    if (v1 - v0 != kc.nvals()) continue;
+    // (the dictionary's values are distinct (interned): equal counts and equal multiset hashes
+    // mean the header lists exactly those values, each once)
+    const H128 h = multiset_hash(v1 - v0, nthreads, [&](size_t i) { return hb.hdr_vals[v0 + i]; });
+    const H128 d = multiset_hash(kc.nvals(), nthreads, [&](size_t i) {
+      return std::string_view(reinterpret_cast<const char *>(kc.dict_bytes.data() + kc.dict_off[i]),
+                              kc.dict_off[i + 1] - kc.dict_off[i]);
+    });
+    hb.hdr_defer[hk] = h.a == d.a && h.b == d.b;
+  }
 }
 
 }  // namespace tsg

@@ -257,7 +257,7 @@ struct tsg_v2block {
 namespace tsg {
 tsg_pipeline *pipeline_new(const tsg_request &req);
 bool pipeline_matches_block(const tsg_query &q, const uint8_t *hdr, size_t len);
-bool pipeline_matches_block_indexed(const tsg_query &q, const HostBlock &h);
+bool pipeline_matches_block_indexed(const tsg_query &q, const HostBlock &h, uint32_t *defer = nullptr);
 bool pipeline_matches_stream_header(const tsg_query &q, uint64_t min_dur, uint64_t max_dur,
                                     const std::map<std::string, std::set<std::string>> &tags);
 
@@ -972,15 +972,21 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
       o.scan_ns = bout.scan_ns;
       o.reruns = batch[k] == &r ? bout.reruns : 0;
       o.pool = bout.pool;
+      o.term_any.clear();
       batch[k]->err = err;
     }
-    if (!err)
+    if (!err) {
       for (const auto &rec : bout.recs) {
         const auto &ow = owner[rec.block_il & 0xffffffu];
         SearchOut::Rec x = rec;
         x.block_il = (rec.block_il & 0xff000000u) | ow.second;
         batch[ow.first]->out->recs.push_back(x);
       }
+      for (const auto &ta : bout.term_any) {
+        const auto &ow = owner[ta.first];
+        batch[ow.first]->out->term_any.push_back({ow.second, ta.second});
+      }
+    }
     for (auto *x : batch) x->done.store(true, std::memory_order_release);
     c.busy.store(false, std::memory_order_release);
     c.wake();
@@ -1076,6 +1082,13 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     // (per-query scratch kept per thread: no allocations once warm)
     thread_local std::vector<int> state;
     state.assign(nblocks, 0);  // 0 no meta, 1 skipped, 2 inspected
+    // MatchesBlock terms left to the device dictionary pass (HostBlock::hdr_defer) per block,
+    // and what the pass found (term_any: -1 = not reported); resolved when the consumer
+    // reaches the block
+    thread_local std::vector<uint32_t> defer;
+    thread_local std::vector<int64_t> anym;
+    defer.assign(nblocks, 0);
+    anym.assign(nblocks, -1);
     bool any_live = false;
     for (size_t i = 0; i < nblocks; i++) {
       Block &b = blocks[i]->b;
@@ -1087,10 +1100,14 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       }
       bool ok = b.host->streaming
                     ? pipeline_matches_stream_header(*q, b.host->min_dur, b.host->max_dur, b.host->stream_tags)
-                    : b.host->hdr_index ? pipeline_matches_block_indexed(*q, *b.host)
+                    : b.host->hdr_index ? pipeline_matches_block_indexed(*q, *b.host, &defer[i])
                                         : pipeline_matches_block(*q, b.host->header.data(), b.host->header.size());
       state[i] = ok ? 2 : 1;
     }
+    auto note_any = [&](const SearchOut &o) {
+      for (const auto &ta : o.term_any)
+        if (ta.first < nblocks) anym[ta.first] = int64_t(ta.second);
+    };
     // Blocks [b0, b1) on their devices, one device_search per device (concurrently).
     // device outputs: a deque keeps them in place (per_block points into their records);
     // entries are reused across queries, their record vectors keep their capacity
@@ -1099,15 +1116,15 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     thread_local std::vector<std::pair<const SearchOut::Rec *, size_t>> per_block;
     per_block.assign(nblocks, {nullptr, 0});
     size_t nrec = 0;
-    // live blocks: a trace's result combines all its matching segments, so their rows are
-    // not capped per block; a launch holding one runs without per-block caps (the others'
-    // extra records are never consumed: ids are unique within a non-live block)
-    const uint32_t dlimit = any_live ? 0u : limit;
-    auto search_range = [&](size_t b0, size_t b1) {
+    // Blocks [b0, b1) (live_only: just the live ones) searched whole, each block capped at
+    // dlimit records. Live blocks are never capped: a trace's result combines all its
+    // matching segments (a limit search runs them on their own, below)
+    auto search_range = [&](size_t b0, size_t b1, bool live_only, uint32_t dlimit) {
       // blocks per device, in first-seen device order (a handful of devices: linear search)
       std::vector<std::pair<DeviceCtx *, std::vector<std::pair<uint32_t, Block *>>>> per_dev;
       for (size_t i = b0; i < b1; i++) {
         if (state[i] != 2 || !blocks[i]->b.dc) continue;
+        if (live_only && !blocks[i]->b.host->live) continue;
         DeviceCtx *dc = blocks[i]->b.dc;
         size_t d = 0;
         while (d < per_dev.size() && per_dev[d].first != dc) d++;
@@ -1144,6 +1161,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
           SearchOut more;
           device_search(*dc, part, *q, dlimit, flags, more);
           o.recs.insert(o.recs.end(), more.recs.begin(), more.recs.end());
+          o.term_any.insert(o.term_any.end(), more.term_any.begin(), more.term_any.end());
           o.device_bytes += more.device_bytes;
           o.kernel_ns += more.kernel_ns;
           o.scan_ns += more.scan_ns;
@@ -1156,6 +1174,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       // per block match lists in scan order (each device's records are grouped by block already)
       uint64_t wave_k = 0, wave_s = 0;  // devices run concurrently: a wave takes its slowest
       for (SearchOut *o : slots) {
+        note_any(*o);
         m.device_bytes_read += o->device_bytes;
         m.reruns += o->reruns;
         wave_k = std::max<uint64_t>(wave_k, o->kernel_ns);
@@ -1192,12 +1211,12 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       if (h.svc_key >= 0 && r->svc != kNone) sv = h.dict_value(h.svc_key, r->svc);
       if (h.name_key >= 0 && r->name != kNone) nm = h.dict_value(h.name_key, r->name);
     };
-    auto combine_live = [&](size_t i) {
+    auto combine_live = [&](size_t i, const SearchOut::Rec *recs, size_t nr) {
       live_recs.clear();
       const HostBlock &h = *blocks[i]->b.host;
       static const uint8_t zero[16] = {};
-      for (size_t ri = 0; ri < per_block[i].second; ri++) {
-        const SearchOut::Rec *r = per_block[i].first + ri;
+      for (size_t ri = 0; ri < nr; ri++) {
+        const SearchOut::Rec *r = recs + ri;
         const uint32_t t = h.row_trace[r->entry];
         std::string_view sv, nm;
         rec_names(h, r, sv, nm);
@@ -1241,11 +1260,25 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       const char *e = std::getenv("TSG_LIMIT_WAVE0");
       return e ? std::max<uint64_t>(512, uint64_t(std::atoll(e))) : uint64_t(1) << 21;
     }();
-    if (limit && !any_live) {
-      approach.leave();
+    // A limit search whose blocks hold at most one first wave's entries is one launch with
+    // per-block caps (concurrent callers coalesce: the shim's per-block calls); larger ones,
+    // and any with a live block, take the waves.
+    uint64_t inspect_entries = 0;
+    for (size_t i = 0; i < nblocks; i++)
+      if (state[i] == 2 && blocks[i]->b.dc && !blocks[i]->b.host->live) inspect_entries += blocks[i]->b.host->n;
+    if (limit && (any_live || inspect_entries > kWave0)) {
       thread_local std::vector<std::vector<SearchOut::Rec>> acc;  // per block: its records so far
       if (acc.size() < nblocks) acc.resize(nblocks);
       for (size_t i = 0; i < nblocks; i++) acc[i].clear();
+      // live blocks first, whole and uncapped (a trace's result combines all its segments;
+      // one live block no longer lifts the other blocks' caps or the waves)
+      if (any_live) {
+        search_range(0, nblocks, true, 0);
+        for (size_t i = 0; i < nblocks; i++)
+          if (blocks[i]->b.host->live) acc[i].assign(per_block[i].first, per_block[i].first + per_block[i].second);
+        nrec = 0;
+      }
+      approach.leave();
       thread_local IdSet distinct_w;
       distinct_w.clear();
       bool stop = false, cut_ok = true;
@@ -1254,7 +1287,8 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       uint64_t wave = kWave0, scanned = 0, matched = 0;
       thread_local std::deque<SearchOut> wouts;
       while (!stop) {
-        while (cb < nblocks && (state[cb] != 2 || !blocks[cb]->b.dc || ce >= blocks[cb]->b.host->n)) {
+        while (cb < nblocks && (state[cb] != 2 || !blocks[cb]->b.dc ||
+                                (!blocks[cb]->b.host->live && ce >= blocks[cb]->b.host->n))) {
           cb++;
           ce = 0;
         }
@@ -1268,6 +1302,12 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         uint64_t want = wave;
         while (want > 0 && cb < nblocks) {
           if (state[cb] != 2 || !blocks[cb]->b.dc) {
+            cb++;
+            ce = 0;
+            continue;
+          }
+          if (blocks[cb]->b.host->live) {  // (searched above: its place in the sequence)
+            order.push_back({cb, UINT64_MAX});
             cb++;
             ce = 0;
             continue;
@@ -1297,10 +1337,12 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         }
         while (wouts.size() < devs.size()) wouts.emplace_back();
         std::vector<uint8_t> used_pool(devs.size(), 0);
+        if (!devs.empty())
         ctx->fan_out(devs.size(), [&](size_t i) { return devs[i]; },
                      [&](size_t i) {
                        SearchOut &o = wouts[i];
                        o.recs.clear();
+                       o.term_any.clear();
                        // (a part list longer than one launch's 32 blocks: whole blocks by chunks)
                        const size_t nl = lists[i].size(), step = kChunk ? kChunk : nl;
                        for (size_t c0 = 0; c0 < nl; c0 += step) {
@@ -1309,8 +1351,11 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
                                                                               lists[i].begin() + c1);
                          const EntryRanges pr(rngs[i].begin() + c0, rngs[i].begin() + c1);
                          SearchOut more;
-                         device_search(*devs[i], part, *q, 0, flags, more, &pr);
+                         // (each part keeps its first `limit` records: ids are unique within a
+                         // block, so the consumer takes at most that many from a block)
+                         device_search(*devs[i], part, *q, limit, flags, more, &pr);
                          o.recs.insert(o.recs.end(), more.recs.begin(), more.recs.end());
+                         o.term_any.insert(o.term_any.end(), more.term_any.begin(), more.term_any.end());
                          o.device_bytes += more.device_bytes;
                          o.kernel_ns += more.kernel_ns;
                          o.scan_ns += more.scan_ns;
@@ -1322,6 +1367,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         uint64_t wk = 0, ws = 0;
         for (size_t i = 0; i < devs.size(); i++) {
           SearchOut &o = wouts[i];
+          note_any(o);
           m.device_bytes_read += o.device_bytes;
           m.scan_bytes += o.scan_bytes;
           m.reruns += o.reruns;
@@ -1338,6 +1384,12 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         for (size_t k = 0; k < order.size() && !stop; k++) {
           const size_t bi = order[k].first;
           const auto &v = acc[bi];
+          if (blocks[bi]->b.host->live) {  // its per-trace results, as the final consumer counts them
+            combine_live(bi, v.data(), v.size());
+            for (size_t x = 0; x < live_recs.size() && !stop; x++)
+              if (distinct_w.insert(live_recs[x].id) && distinct_w.size() >= limit) stop = true;
+            continue;
+          }
           for (size_t ri = 0; ri < v.size() && !stop; ri++) {
             if (v[ri].entry >= order[k].second) break;
             if (distinct_w.insert(v[ri].id) && distinct_w.size() >= limit)
@@ -1361,7 +1413,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         nrec += acc[i].size();
       }
     } else {
-      search_range(0, nblocks);
+      search_range(0, nblocks, false, limit);  // (limit > 0 here: no live block)
       check_cancel();
     }
     const clk::time_point t_dev = trace ? clk::now() : clk::time_point();
@@ -1376,7 +1428,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       const HostBlock &h = *blocks[i]->b.host;
       if (state[i] == 0) continue;  // meta missing: no-op (backend_search_block.go:191-203)
       if (h.live) {  // searchLiveTraces (instance_search.go:99-128)
-        combine_live(i);
+        combine_live(i, per_block[i].first, per_block[i].second);
         uint64_t stop_trace = UINT64_MAX;
         for (const LiveRec &x : live_recs) {
           res->set(nout, x.id, x.il, x.start, x.end, uint32_t(i), x.trace, x.sv.data(), x.sv.size(), x.nm.data(),
@@ -1399,6 +1451,13 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         continue;
       }
       m.bytes_inspected += h.header.size();
+      if (state[i] == 2 && defer[i]) {
+        // MatchesBlock's deferred terms: a key whose values all miss the needle skips the
+        // block (its scan found nothing: the term's bitmap is empty). Not reported (the block
+        // never reached a dictionary pass): the host scans the header's values itself.
+        if (anym[i] >= 0) state[i] = (defer[i] & ~uint32_t(anym[i])) ? 1 : 2;
+        else state[i] = pipeline_matches_block_indexed(*q, h) ? 2 : 1;
+      }
       if (state[i] == 1) {
         m.blocks_skipped++;
         continue;

@@ -133,6 +133,10 @@ struct SearchOut {
   uint64_t scan_ns = 0, scan_bytes = 0;
   uint32_t reruns = 0;  // extra launches after a record overflow (timed into scan_ns / kernel_ns when timing)
   bool pool = false;    // served by the pool kernels (they search entry ranges on the device)
+  // (block index, term mask) for the blocks whose dictionaries the device pass matched
+  // (prep / dict_stream / dict_sets): bit t clear = no value of the block's key for term t
+  // contains the needle. MatchesBlock's tag half for keys with HostBlock::hdr_defer.
+  std::vector<std::pair<uint32_t, uint32_t>> term_any;
 };
 // Runs the device pipeline for a set of (block index, block) pairs that share
 // one device. limit 0 = every match; limit L = each block's first L matches.

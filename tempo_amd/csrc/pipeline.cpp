@@ -82,7 +82,11 @@ bool pipeline_matches_block(const tsg_query &q, const uint8_t *hdr, size_t len) 
 // The same predicate over the header walked at open (HostBlock::hdr_*): the same binary
 // search over the keys in the header's order (searchdata_util.go:63-100, reversed
 // comparator) and the same bytes.Contains over the found key's values.
-bool pipeline_matches_block_indexed(const tsg_query &q, const HostBlock &h) {
+// defer != nullptr: a term whose key's header values are the block's (large) dictionary
+// (HostBlock::hdr_defer) is not scanned here; its bit is set in *defer and the caller takes
+// "some value contains the needle" from the device dictionary pass (tsg_search).
+bool pipeline_matches_block_indexed(const tsg_query &q, const HostBlock &h, uint32_t *defer) {
+  if (defer) *defer = 0;
   if (q.has_min && !(h.max_dur >= q.min_ns)) return false;  // pipeline.go:38-41
   if (q.has_max && !(h.min_dur <= q.max_ns)) return false;  // :53-56
   const uint32_t n = uint32_t(h.hdr_keys.size());
@@ -103,6 +107,10 @@ bool pipeline_matches_block_indexed(const tsg_query &q, const HostBlock &h) {
       else i = m + 1;
     }
     if (at == n) return false;
+    if (defer && t < 32 && !q.exhaustive && at < h.hdr_defer.size() && h.hdr_defer[at]) {
+      *defer |= 1u << t;
+      continue;
+    }
     bool any = false;
     for (uint32_t x = h.hdr_val0[at]; x < h.hdr_val0[at + 1] && !any; x++)
       any = v.empty() || h.hdr_vals[x].find(v) != std::string_view::npos;  // bytes.Contains

@@ -59,8 +59,37 @@ struct PoolArgs {
   uint32_t *counts;     // pinned host: workgroup w's match count, stored after its records
   unsigned long long *stamps;
   uint32_t *err;        // pinned host: set when an LDS poll ran past its bound (the host fails the query)
+  // limit L > 0: a unit keeps its first L matches in scan order (a block's first L records lie
+  // in the first L of each of its units; the host cuts each block to L): a dense limit query
+  // hands over at most L records per unit instead of every match
+  uint32_t unit_cap, pad0;
 };
 static_assert(sizeof(PoolArgs) <= 4096, "kernel arguments");
+
+// The unit's matches (mask bit 4k + j of lane l = entry e0 + 256k + 4l + j) cut to the first
+// `cap` in scan order (k, then lane, then j): each match's rank from per-step ballots.
+__device__ __forceinline__ uint32_t cap_unit_mask(uint32_t mask, uint32_t cap, int lane) {
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t out = 0, before = 0;
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) {
+    const uint32_t nib = (mask >> (4 * k)) & 0xfu;
+    uint32_t lower = 0, tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint64_t b = __ballot((nib >> j) & 1u);
+      lower += uint32_t(__popcll(b & below));
+      tot += uint32_t(__popcll(b));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t rank = before + lower + uint32_t(__popc(nib & ((1u << j) - 1u)));
+      if (((nib >> j) & 1u) && rank < cap) out |= 1u << (4 * k + j);
+    }
+    before += tot;
+  }
+  return out;
+}
 
 // A pointer read from LDS by every lane (same value), moved to SGPRs. (readfirstlane
 // returns int: each half goes through uint32_t, or the low half sign-extends.)
@@ -292,9 +321,10 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     const PoolBlk &B = s_blk[R.blk];
     const uint32_t n = __builtin_amdgcn_readfirstlane(B.nent);
     const uint32_t bmi4 = __builtin_amdgcn_readfirstlane(B.bmi4), ns4 = __builtin_amdgcn_readfirstlane(B.nsets4);
-    const uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, R.e, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
-                                                     ns4, s_bm, lane);
+    uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, R.e, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
+                                               ns4, s_bm, lane);
     if (__ballot(mask != 0) == 0) return;
+    if (A.unit_cap) mask = cap_unit_mask(mask, A.unit_cap, lane);
     // matches: slots in the workgroup's LDS record buffer, record fields gathered now
     const DevBlockDesc *D = A.desc[R.blk];
     const auto *Dc = K4(D);
@@ -448,9 +478,10 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
   auto eval = [&](const Regs &R, uint32_t bslot) {
     const PoolBlk &P = A.blk[bslot];
     const uint32_t n = P.nent, bmi4 = P.bmi4, ns4 = P.nsets4;
-    const uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, R.e, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
-                                                     ns4, s_bm, lane);
+    uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, R.e, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
+                                               ns4, s_bm, lane);
     if (__ballot(mask != 0) == 0) return;
+    if (A.unit_cap) mask = cap_unit_mask(mask, A.unit_cap, lane);
     const DevBlockDesc *D = A.desc[bslot];
     const auto *Dc = K4(D);
     const uint8_t *ids = Dc->ids;
@@ -583,14 +614,20 @@ static PoolFn pick_static(uint32_t nterms, bool dur, bool range, bool ntl) {
 // nothing written to `out`, when a workgroup found more matches than its record buffer
 // holds: the caller then runs the segment / look-back path.
 bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
-                        uint32_t flags, const std::vector<ScanSeg> &segs, const std::vector<NarrowSeg> &nsegv,
-                        const std::vector<std::array<uint32_t, 8>> &nbms,
-                        const std::vector<std::array<uint8_t, kArgTerms>> &nbmi,
-                        const std::vector<const DevBlockDesc *> &seg_desc, bool has_dur, Tracer &tr, SearchOut &out) {
+                 uint32_t limit, uint32_t flags, const std::vector<ScanSeg> &segs, const std::vector<NarrowSeg> &nsegv,
+                 const std::vector<std::array<uint32_t, 8>> &nbms,
+                 const std::vector<std::array<uint8_t, kArgTerms>> &nbmi,
+                 const std::vector<const DevBlockDesc *> &seg_desc, bool has_dur, Tracer &tr, SearchOut &out) {
   hipStream_t s = dc.stream;
   const uint32_t nsegs = uint32_t(segs.size()), W = uint32_t(dc.num_cu);
   PoolArgs PA;
   std::memset(&PA, 0, sizeof PA);
+  // limit L: each block's part needs its first L records only (ids are unique within a
+  // block: the consumer takes at most L from it), so units keep their first L (parts start
+  // on unit boundaries)
+  PA.unit_cap = limit;
+  for (const auto &sg : segs)
+    if (sg.e0 % kPoolTile) PA.unit_cap = 0;
   uint32_t U = 0;
   for (uint32_t i = 0; i < nsegs; i++) {
     PoolBlk &b = PA.blk[i];
@@ -853,24 +890,26 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       sorted[j] = k;
     }
   }
-  // limit L (segs[i].cap = min(L, n)): each block's first L matches in scan order, as the
-  // one-launch kernel's per-block caps keep them; the sorted records of a block are
-  // contiguous, so the cut keeps a prefix of each block's run
+  // limit L: each block's part keeps its first L matches in scan order (the records of a
+  // part all lie in its range [e0, e1)); the sorted records of a block are contiguous, so
+  // the cut keeps a prefix of each block's run
+  auto cut = [&](uint64_t i) { return limit ? std::min<uint64_t>(limit, segs[i].cap) : segs[i].cap; };
   out.recs.resize(total);
   uint64_t kept = 0;
-  for (uint64_t i = 0, run = 0, ps = ~0ull; i < total; i++) {
+  for (uint64_t i = 0, run = 0, ps = ~0ull, c = 0; i < total; i++) {
     const SearchOut::Rec &r = prec[sorted[i] & 0xfffffu];
     const uint32_t bi = r.block_il & 0xffffffu;
     const uint64_t seg_i = bi <= max_idx ? pos[bi] : 0;
     if (seg_i != ps) {
       ps = seg_i;
       run = 0;
+      c = cut(seg_i);
     }
-    if (run++ < segs[seg_i].cap) out.recs[kept++] = r;
+    if (run++ < c) out.recs[kept++] = r;
   }
   out.recs.resize(kept);
   for (uint32_t i = 0; i < nsegs; i++) {
-    per[i] = std::min<uint64_t>(per[i], segs[i].cap);
+    per[i] = std::min<uint64_t>(per[i], cut(i));
     for (size_t bi = 0; bi < blocks.size(); bi++)
       if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = per[i];
   }

@@ -121,7 +121,7 @@ static_assert(sizeof(DictJob) % 16 == 0, "DictJob staged as 16-byte words");
 extern "C" __global__ void __launch_bounds__(256) prep_kernel(const uint8_t *src, uint8_t *dst, uint32_t copy16,
                                                               uint32_t o_jobs, uint32_t o_jb, uint32_t njobs,
                                                               uint32_t total, uint32_t o_nd, uint32_t nd_bytes,
-                                                              uint8_t *vmatch, uint32_t *bitmaps) {
+                                                              uint8_t *vmatch, uint32_t *bitmaps, uint32_t *anyf) {
   __shared__ __attribute__((aligned(16))) DictJob s_jobs[kPrepLdsJobs];
   __shared__ __attribute__((aligned(16))) uint8_t s_nd[kPrepLdsNeedle];
   const int tid = threadIdx.x;
@@ -167,6 +167,7 @@ extern "C" __global__ void __launch_bounds__(256) prep_kernel(const uint8_t *src
     const uint32_t words = (jb.nsets + 31) >> 5;
     if (lane == 0 && w0 < words) bitmaps[jb.bm_base + w0] = uint32_t(b);
     if (lane == 32 && w0 + 1 < words) bitmaps[jb.bm_base + w0 + 1] = uint32_t(b >> 32);
+    if (lane == 0 && b != 0) host_store(anyf + lo, 1u);  // (some value of the job matched)
   } else if (v < jb.nvals) {
     vmatch[jb.vmatch_base + v] = m ? 1 : 0;
   }
@@ -176,7 +177,7 @@ extern "C" __global__ void __launch_bounds__(256) prep_kernel(const uint8_t *src
 extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob *jobs, const uint32_t *set_jobs,
                                                                    const uint32_t *prefix, uint32_t nsj,
                                                                    uint32_t total, const uint8_t *vmatch,
-                                                                   uint32_t *bitmaps) {
+                                                                   uint32_t *bitmaps, uint32_t *anyf) {
   uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= total) return;
   uint32_t lo = 0, hi = nsj;
@@ -198,6 +199,7 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
       word |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
     }
     bitmaps[jb.bm_base + w] = word;
+    if (word) host_store(anyf + set_jobs[lo], 1u);
     return;
   }
   for (uint32_t b = 0; b < 32; b++) {
@@ -210,6 +212,7 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
       }
   }
   bitmaps[jb.bm_base + w] = word;
+  if (word) host_store(anyf + set_jobs[lo], 1u);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1855,12 +1858,17 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     }
     sg.nunits = uint32_t((e1 + kUnit - 1) / kUnit);
     units += sg.nunits;
-    sg.cap = limit ? std::min<uint64_t>(limit, e1) : e1;
+    // limit L: the block's first L records (ids are unique within a block: the consumer takes
+    // at most L). The segment / look-back paths count records from position 0, so a part cut
+    // at e0 > 0 keeps everything there (drop_before_ranges removes what precedes it); the pool
+    // kernels scan [e0, e1) and cut each part to L themselves
+    sg.cap = limit && e0 == 0 ? std::min<uint64_t>(limit, e1) : e1;
     scan_bytes += (e1 - e0) * per;
     n_all += e1;
     segs.push_back(sg);
   }
   out.recs.clear();
+  out.term_any.clear();
   out.block_counts.assign(blocks.size(), 0);
   out.device_bytes = scan_bytes + dict_bytes;
   out.kernel_ns = out.scan_ns = 0;
@@ -1927,13 +1935,19 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     return fast && !dc.seg_off && c > 0 && c <= kSegMax &&
            uint64_t(dc.num_cu) * std::max(8, dc.per_cu_override) * c * sizeof(MatchRec) <= kSegBudget;
   };
-  uint32_t seg = limit ? limit : dc.seg_cap;
+  // the segment / look-back paths' limit mode (segments of L records per workgroup, no rerun
+  // on overflow) counts from position 0: a search with a part cut at e0 > 0 runs them in full
+  // mode (its e0 = 0 parts keep their caps); the pool kernels take `limit` as it is
+  bool cut_parts = false;
+  for (const auto &sg : segs) cut_parts = cut_parts || sg.e0 > 0;
+  const uint32_t climit = cut_parts ? 0u : limit;
+  uint32_t seg = climit ? climit : dc.seg_cap;
   if (!seg_fits(seg)) seg = 0;
   // ---- pool path: narrow searches (search_pool_kernel); falls through to the
   // segment / look-back paths below when a workgroup's matches overflow its LDS buffer
   if (fast && narrow && !dc.seg_off && !dc.pool_off) {
     if (dc.pool_skip) dc.pool_skip--;
-    else if (pool_search(dc, blocks, q, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out)) {
+    else if (pool_search(dc, blocks, q, limit, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out)) {
       if (ranges) drop_before_ranges(blocks, *ranges, out);
       out.pool = true;
       return;
@@ -2019,7 +2033,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   //    has (>= 2^16 records) and a larger match count re-runs into a grown buffer
   auto lb_cap = [&]() -> uint64_t {
     const uint64_t have = dc.hres.cap > hdr_bytes ? (dc.hres.cap - hdr_bytes) / sizeof(MatchRec) : 0;
-    return limit ? cap_total : std::min<uint64_t>(n_total, std::max<uint64_t>(have, 1u << 16));
+    return climit ? cap_total : std::min<uint64_t>(n_total, std::max<uint64_t>(have, 1u << 16));
   };
   const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
   const bool time_defer = flags & TSG_SEARCH_TIME_DEFER;
@@ -2031,7 +2045,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   P.has_min = q.has_min;
   P.has_max = q.has_max;
   P.need64 = (q.has_min && q.min_ns >= 0xffffffffULL) || (q.has_max && q.max_ns >= 0xffffffffULL);
-  P.limit_mode = limit ? 1 : 0;
+  P.limit_mode = climit ? 1 : 0;
   P.min_ns = q.min_ns;
   P.max_ns = q.max_ns;
   P.start_s = q.start_s;
@@ -2162,10 +2176,14 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     tr.mark("desc");
     if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
     if (!stream_jobs.empty()) HIP_OK(hipMemsetAsync(dc.vmatch.p, 0, vmatch_total, s));
+    // (no kernel of this device is in flight: device_search returns after its stream drained)
+    dc.hany.ensure(std::max<size_t>(jobs.size(), 1) * 4);
+    std::memset(dc.hany.p, 0, jobs.size() * 4);
+    auto *anyf = static_cast<uint32_t *>(dc.hany.p);
     prep_kernel<<<std::max<uint32_t>(1, (items + 255) / 256), 256, 0, s>>>(
         src, dd, uint32_t(total_desc / 16), uint32_t(o_jobs), uint32_t(o_jb), uint32_t(jobs.size()), items,
         uint32_t(o_nd), uint32_t(needles.size()), static_cast<uint8_t *>(dc.vmatch.p),
-        static_cast<uint32_t *>(dc.bitmaps.p));
+        static_cast<uint32_t *>(dc.bitmaps.p), anyf);
     if (!stream_jobs.empty())
       dict_stream_kernel<<<(stream_waves + kStreamWg - 1) / kStreamWg, 64 * kStreamWg, 0, s>>>(
           reinterpret_cast<const StreamJob *>(dd + o_stj), uint32_t(stream_jobs.size()), dd + o_nd,
@@ -2174,7 +2192,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       dict_sets_kernel<<<(set_items.back() + 255) / 256, 256, 0, s>>>(
           reinterpret_cast<const DictJob *>(dd + o_jobs), reinterpret_cast<const uint32_t *>(dd + o_sj),
           reinterpret_cast<const uint32_t *>(dd + o_sp), uint32_t(set_jobs.size()), set_items.back(),
-          static_cast<const uint8_t *>(dc.vmatch.p), static_cast<uint32_t *>(dc.bitmaps.p));
+          static_cast<const uint8_t *>(dc.vmatch.p), static_cast<uint32_t *>(dc.bitmaps.p), anyf);
     P.segs = reinterpret_cast<const ScanSeg *>(dd + o_segs);
     P.terms = reinterpret_cast<const ScanTerm *>(dd + o_terms);
     P.wg_seg = reinterpret_cast<const uint16_t *>(dd + o_ws);
@@ -2327,6 +2345,15 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   wait();
   tr.mark("sync");
   check();
+  if (!fast) {  // per block: which terms some dictionary value matched (job = segment x term)
+    const auto *anyf = static_cast<const volatile uint32_t *>(dc.hany.p);
+    for (uint32_t i = 0; i < nsegs; i++) {
+      uint32_t m = 0;
+      for (uint32_t t = 0; t < q.nterms; t++)
+        if (t >= 32 || anyf[size_t(i) * q.nterms + t]) m |= t < 32 ? 1u << t : 0u;
+      out.term_any.push_back({segs[i].block_idx, m});
+    }
+  }
   if (want_stamps) print_stamps(dc, nwg, fast);
   float ms = 0, sms = 0;
   if (time_all) {
@@ -2366,7 +2393,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       total += cnt[w];
     }
     tr.mark("counts");
-    if (!limit && maxc > P.seg_cap) {
+    if (!climit && maxc > P.seg_cap) {
       // a workgroup overflowed its segment: remember the size and run again with
       // larger segments, or in look-back mode
       uint32_t want = 16;
@@ -2419,12 +2446,12 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     out.scan_bytes += uint64_t(nwg) * 4 + nrec * 32;  // + workgroup counts, + id/start/end of each record
   } else {
     uint64_t total = *reinterpret_cast<volatile uint64_t *>(P.out);
-    if (!limit && total > P.out_cap) {
+    if (!climit && total > P.out_cap) {
       // more matches than the result buffer holds: grow it and run the launch again
       configure(0, total);
       rerun_timed();
     }
-    if (!limit && fast && total <= 64) dc.seg_cap = 16;  // sparse again: back to segment mode
+    if (!climit && fast && total <= 64) dc.seg_cap = 16;  // sparse again: back to segment mode
     nrec = total;
     out.recs.resize(total);
     if (total) std::memcpy(out.recs.data(), P.out + P.hdr_bytes, total * sizeof(MatchRec));

@@ -132,10 +132,11 @@ struct NarrowSeg {
 
 void print_stamps(DeviceCtx &dc, uint32_t nwg, bool fast);
 
-// pool.hip: one search_pool_kernel launch for a narrow full scan (limit 0); false (and
-// nothing written to `out`) when the caller should run the segment / look-back path
+// pool.hip: one search_pool_kernel (or search_static_kernel) launch for a narrow search;
+// limit L > 0 keeps each block part's first L records. false (and nothing written to
+// `out`) when the caller should run the segment / look-back path
 bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
-                 uint32_t flags, const std::vector<ScanSeg> &segs, const std::vector<NarrowSeg> &nsegv,
+                 uint32_t limit, uint32_t flags, const std::vector<ScanSeg> &segs, const std::vector<NarrowSeg> &nsegv,
                  const std::vector<std::array<uint32_t, 8>> &nbms,
                  const std::vector<std::array<uint8_t, kArgTerms>> &nbmi,
                  const std::vector<const DevBlockDesc *> &seg_desc, bool has_dur, Tracer &tr, SearchOut &out);

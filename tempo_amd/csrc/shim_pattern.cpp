@@ -3,8 +3,8 @@
 //
 // instance.searchLocalBlocks starts one goroutine per block and each calls
 // BackendSearchBlock.Search on its own (modules/ingester/instance_search.go:164-185); the
-// shim turns each into one tsg_search over that block with limit 0 and a
-// tsg_result_free. Goroutines run on OS threads without a global lock, so the pattern is
+// shim turns each into one tsg_search over that block with the request's
+// limit (Pipeline.Query carries it) and a tsg_result_free. Goroutines run on OS threads without a global lock, so the pattern is
 // driven from C threads here (Python threads would serialise on the GIL between calls).
 // One thread per block, kept across queries (Go reuses its OS threads); a query ends when
 // every block's call has returned.
@@ -19,10 +19,12 @@
 extern "C" {
 // rounds queries over nsets block sets of nblocks blocks each (blocks[s * nblocks + i]);
 // query r searches set r % nsets. round_ns[r] = wall time of query r (all calls issued at
-// once, until the last returned); matches[r] = records over all blocks of query r. Returns
-// the first non-zero tsg_search code (the round's other calls still complete).
+// once, until the last returned); matches[r] = records over all blocks of query r. limit: the
+// request's limit passed per block (tsg_search_opts.limit; the ingester's default is 20, 0 =
+// every match). Returns the first non-zero tsg_search code (the round's other calls still
+// complete).
 int tsgx_shim_pattern(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, size_t nsets, const tsg_query *q,
-                      uint32_t rounds, uint64_t *round_ns, uint64_t *matches) {
+                      uint32_t limit, uint32_t rounds, uint64_t *round_ns, uint64_t *matches) {
   if (!ctx || !q || !blocks || !nblocks || !nsets || !round_ns || !matches) return TSG_E_INVALID;
   std::atomic<uint32_t> gen{0};
   std::atomic<size_t> left{0};
@@ -41,6 +43,7 @@ int tsgx_shim_pattern(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, si
         if (stop.load(std::memory_order_acquire)) return;
         seen = g;
         tsg_search_opts o{};
+        o.limit = limit;
         tsg_result *r = nullptr;
         const int rc = tsg_search(ctx, &blocks[((g - 1) % nsets) * nblocks + i], 1, q, &o, &r);
         if (rc == TSG_OK) {

@@ -238,7 +238,7 @@ def shim_pattern_lib():
         S = C.CDLL(path)
         vp = C.c_void_p
         S.tsgx_shim_pattern.argtypes = [vp, C.POINTER(vp), C.c_size_t, C.c_size_t, C.POINTER(_Query), C.c_uint32,
-                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+                                        C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         _shim = S
     return _shim
 
@@ -352,6 +352,7 @@ class SearchMetrics:
     block_status: List[int] = field(default_factory=list)
     block_errors: List[Optional[str]] = field(default_factory=list)
     skipped_traces: int = 0  # SearchMetrics.SkippedTraces (the proto path's MaxBytes skips; 0 here)
+    reruns: int = 0  # extra launches after a record overflow (tsg_metrics.reruns)
 
 
 def _unpack(rp) -> (List[TraceSearchMetadata], SearchMetrics):
@@ -371,7 +372,8 @@ def _unpack(rp) -> (List[TraceSearchMetadata], SearchMetrics):
     st = [r.block_status[i] for i in range(r.nblocks)]
     errs = [r.block_error[i].decode(errors="replace") if st[i] else None for i in range(r.nblocks)]
     return out, SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,
-                              m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes, st, errs)
+                              m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes, st, errs,
+                              reruns=m.reruns)
 
 
 # ---------------------------------------------------------------------------
@@ -470,6 +472,55 @@ class Engine:
         free(rp)
         return n, met
 
+    def search_columns(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0):
+        """tsg_search with the ordered matches as numpy columns (large results: no per-record
+        Python): dict of trace_id (n, 16) uint8, trace_id_len, start_ns, end_ns, duration_ms,
+        block_idx, entry_idx, and root_service / root_name as index arrays into the
+        `names` list (distinct strings); plus SearchMetrics."""
+        import numpy as np
+        arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+        opts = _SearchOpts(limit=limit)
+        rp = C.POINTER(_Result)()
+        _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
+        try:
+            r = rp.contents
+            n = r.n
+            cols = {}
+
+            def col(ptr, dt, shape):
+                return np.ctypeslib.as_array(ptr, shape).astype(dt) if n else np.zeros(shape, dt)
+
+            cols["trace_id"] = col(r.trace_id, np.uint8, (n, 16)) if n else np.zeros((0, 16), np.uint8)
+            cols["trace_id_len"] = col(r.trace_id_len, np.uint8, (n,))
+            cols["start_ns"] = col(r.start_ns, np.uint64, (n,))
+            cols["end_ns"] = col(r.end_ns, np.uint64, (n,))
+            cols["duration_ms"] = col(r.duration_ms, np.uint32, (n,))
+            cols["block_idx"] = col(r.block_idx, np.uint32, (n,))
+            cols["entry_idx"] = col(r.entry_idx, np.uint64, (n,))
+            names, index = [], {}
+            arena = C.string_at(r.names, r.names_len) if r.names_len else b""
+            for which, off_p, len_p in (("root_service", r.root_service_off, r.root_service_len),
+                                        ("root_name", r.root_name_off, r.root_name_len)):
+                off = col(off_p, np.uint64, (n,))
+                ln = col(len_p, np.uint32, (n,))
+                key = (off << np.uint64(32)) | ln.astype(np.uint64)
+                uk, inv = np.unique(key, return_inverse=True)
+                ids = np.empty(len(uk), np.int64)
+                for j, k in enumerate(uk.tolist()):
+                    o, l = k >> 32, k & 0xffffffff
+                    s = arena[o:o + l] if l else b""
+                    ids[j] = index.setdefault(s, len(names))
+                    if ids[j] == len(names):
+                        names.append(s)
+                cols[which] = ids[inv] if n else np.zeros(0, np.int64)
+            cols["names"] = names
+            m = r.metrics
+            met = SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,
+                                m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
+            return cols, met
+        finally:
+            lib().tsg_result_free(rp)
+
     def search_wire(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0,
                     combine: Optional[int] = None, flags: int = 0):
         """tsg_search (+ tsg_results_combine when `combine` is set: instance.Search's
@@ -505,10 +556,11 @@ class Engine:
         chunk boundary with TSG_E_CANCELLED (the Go shim maps ctx.Done() to this)."""
         _check(lib().tsg_cancel(self.h, query_id))
 
-    def shim_pattern(self, sets: Sequence[Sequence["BackendSearchBlock"]], pipeline: Pipeline, rounds: int):
+    def shim_pattern(self, sets: Sequence[Sequence["BackendSearchBlock"]], pipeline: Pipeline, rounds: int,
+                     limit: int = 0):
         """The Go shim's ingester call pattern (instance_search.go:164-185) driven from C
-        threads (libtsg_shim_pattern.so): per query, one thread per block, each a limit-0
-        tsg_search over its one block; query r searches sets[r % len(sets)] (equal-sized
+        threads (libtsg_shim_pattern.so): per query, one thread per block, each a tsg_search
+        over its one block with `limit`; query r searches sets[r % len(sets)] (equal-sized
         sets). Returns (per-query wall ns, per-query record counts)."""
         sp = shim_pattern_lib()
         nb = len(sets[0])
@@ -516,7 +568,7 @@ class Engine:
         arr = (C.c_void_p * (nb * len(sets)))(*[b.h for s in sets for b in s])
         ns = (C.c_uint64 * rounds)()
         nm = (C.c_uint64 * rounds)()
-        _check(sp.tsgx_shim_pattern(self.h, arr, nb, len(sets), pipeline.query, rounds, ns, nm))
+        _check(sp.tsgx_shim_pattern(self.h, arr, nb, len(sets), pipeline.query, limit, rounds, ns, nm))
         return list(ns), list(nm)
 
     def kernel_times(self, cap: int = 65536) -> List[int]:

@@ -153,6 +153,41 @@ def test_equal_query_from_distinct_pipelines(engine, blockset):
             b.close()
 
 
+@pytest.mark.parametrize("q", [QA, dict(tags={"service.name": "svc-07"}), dict(tags={"status.code": ""})])
+def test_concurrent_single_block_limit20(engine, blockset, q):
+    """The shim with the request's limit passed per block (Pipeline.Query): each caller's
+    one-block limit-20 search runs in a coalesced launch with per-block caps and still gets
+    exactly its block's first 20 matches and the metrics of a search stopped there
+    (backend_search_block.go:247, instance_search.go:57-59)."""
+    blocks = [engine.open_block(p) for p in blockset]
+    try:
+        pipe = T.Pipeline(request(q))
+        exp = [expected([p], q, 20) for p in blockset]
+        for rnd in range(4):
+            got = [None] * len(blocks)
+            errs = []
+            go = threading.Barrier(len(blocks))
+
+            def worker(i):
+                try:
+                    go.wait()
+                    got[i] = key(engine.search([blocks[i]], pipe, limit=20))
+                except Exception as e:  # noqa: BLE001
+                    errs.append(e)
+
+            ths = [threading.Thread(target=worker, args=(i,)) for i in range(len(blocks))]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            assert not errs, errs
+            for i in range(len(blocks)):
+                assert got[i] == exp[i], (rnd, i)
+    finally:
+        for b in blocks:
+            b.close()
+
+
 def test_shim_pattern_driver(engine, blockset):
     """libtsg_shim_pattern.so (C threads, the bench's shim leg): every query's record count
     equals the per-block oracle's, over two rotating sets."""
@@ -164,6 +199,9 @@ def test_shim_pattern_driver(engine, blockset):
         ns, nm = engine.shim_pattern([a, b], pipe, 40)
         assert nm == [per] * 40
         assert all(x > 0 for x in ns)
+        per20 = sum(len(expected([p], QA, 20)[0]) for p in blockset[:10])
+        ns, nm = engine.shim_pattern([a, b], pipe, 40, limit=20)
+        assert nm == [per20] * 40
     finally:
         for x in a + b:
             x.close()

@@ -72,6 +72,27 @@ def test_cfg2_query_three_handles(engine, bench_block):
         check(engine, [bench_block] * 3, limit=lim, **CFG2)
 
 
+@pytest.mark.parametrize("tags,min_ms", [({"status.code": ""}, 0),   # every entry with the key: dense
+                                         ({"service.name": "svc-07"}, 1)])
+def test_dense_limit_waves(engine, bench_block, tags, min_ms):
+    """A dense query with a limit over 3 M entries (waves cut the second block): every part
+    hands over at most its first L records (units keep their first L on the device, ADVICE
+    r3), no rerun, and the ordered result and metrics are the oracle's; the pool path is
+    still taken afterwards (a full scan right after matches the oracle too)."""
+    for lim in (20, 300):
+        got, met = check(engine, [bench_block] * 3, limit=lim, tags=tags, min_ms=min_ms)
+        assert len(got) == lim
+    req = T.SearchRequest(tags=tags, min_duration_ms=min_ms)
+    blocks = [engine.open_block(bench_block) for _ in range(3)]
+    try:
+        got, met = engine.search(blocks, T.Pipeline(req), limit=20)
+        assert met.reruns == 0
+    finally:
+        for b in blocks:
+            b.close()
+    check(engine, [bench_block], **CFG2)
+
+
 @pytest.fixture(scope="module")
 def cfg3_blocks(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("cfg3"))
@@ -103,6 +124,11 @@ def test_cfg4_high_cardinality_200k(engine, tmp_path):
         got, met = check(engine, [p], **q)
         assert len(got) > 0
     check(engine, [p], limit=20, tags={"db.statement": "from orders"})
+    # an absent needle: MatchesBlock skips the block (blocksSkipped from the device pass)
+    got, met = check(engine, [p, p], tags={"db.statement": "qqzz"})
+    assert not got and met.skipped_blocks == 2
+    got, met = check(engine, [p], tags={"http.url": "/carts/", "db.statement": "qqzz"}, min_ms=1)
+    assert not got and met.skipped_blocks == 1
 
 
 def test_cfg5_lookup_1m_probes_200_blocks(engine, tmp_path):

@@ -68,3 +68,50 @@ def test_rank_contexts_pack_and_merge(world, limit):
             [_oracle_response([paths[i] for i in shard.shard_range(len(paths), world, r)], limit)
              for r in range(world)], limit, len(paths)))
         assert got == exp and len(got[0]) > 0
+
+
+def test_rccl_gather_world1(engine):
+    """The packed gather on cuda tensors through the nccl backend (RCCL) — the transport
+    bench.py's merge / cfg5 legs use at N > 1 — in a world of one: the merged response equals
+    the host merge of the same wire, and the id-sharded lookup's gathered hit table equals the
+    local one."""
+    import socket
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        with tempfile.TemporaryDirectory() as td:
+            paths = []
+            for i in range(3):
+                p = os.path.join(td, "b%d" % i)
+                T.synth_search_block(p, 40_000, seed=800 + i, page_size=64 << 10)
+                paths.append(p)
+            blocks = [engine.open_block(p) for p in paths]
+            req = T.SearchRequest(tags=QUERY["tags"], min_duration_ms=QUERY["min_ms"],
+                                  max_duration_ms=QUERY["max_ms"], start=QUERY["start"], end=QUERY["end"])
+            wire = engine.search_wire(blocks, T.Pipeline(req))
+            merged = shard.distributed_search_packed(lambda: wire, 1 << 30, len(paths), device="cuda", columns=True)
+            host = shard.merge_wires([wire], 1 << 30, len(paths))
+            assert len(merged) == len(host) > 0 and (merged.recs == host.recs).all()
+            assert merged.metrics.inspected_traces == host.metrics.inspected_traces
+            for b in blocks:
+                b.close()
+            v2 = []
+            for i in range(4):
+                p = os.path.join(td, "v%d" % i)
+                v2.append((p, T.synth_v2_block(p, 3000, seed=60 + i)))
+            vb = [engine.open_v2block(p) for p, _ in v2]
+            ids = np.concatenate([x[::7] for _, x in v2] + [np.arange(16 * 500, dtype=np.uint8).reshape(500, 16)])
+            local, _ = engine.lookup(vb, ids)
+            got = shard.distributed_lookup(lambda x: engine.lookup(vb, x)[0], ids, device="cuda")
+            np.testing.assert_array_equal(got, local)
+            for b in vb:
+                b.close()
+    finally:
+        dist.destroy_process_group()
