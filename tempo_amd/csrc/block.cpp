@@ -9,6 +9,9 @@
 
 #include "writer.hpp"
 #include <atomic>
+#include <chrono>
+#include <exception>
+#include <mutex>
 #include <thread>
 
 namespace tsg {
@@ -440,6 +443,729 @@ static void canonicalize_narrow_keys(HostBlock &hb) {
   }
 }
 
+// ---- the columnar loader of a backend block: three parallel phases -------------------
+// A. per page (threads over pages): decompress, walk the entries once, collect the page's
+//    distinct KeyValues tables (the writer shares a table between the entries of a page,
+//    searchdata.go:115-128) with their values' hashes, resolve each entry's FindTag target.
+// B. per key (threads over keys): intern the key's values and value sets over the pages in
+//    order (first-seen ids), no allocation per value: values are views into the page buffers.
+// C. per page again: the entries' columns (ids, times, value-set id per key, root names).
+// Keys are numbered in name order. Values, sets and entries keep the scan order (pages
+// ascending, entry index ascending); the first damaged page ends the block as in
+// BackendSearchBlock.Search (backend_search_block.go:258-266).
+namespace {
+inline uint64_t hash_bytes(const void *p, size_t n) { return xxhash64(static_cast<const uint8_t *>(p), n); }
+inline uint64_t mix_set(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+struct KeyNames {  // provisional key ids, shared by the page workers (a handful of keys)
+  std::mutex mu;
+  std::vector<std::string> names;
+  std::unordered_map<std::string, uint32_t> ids;
+  uint32_t get(std::string_view k) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = ids.find(std::string(k));
+    if (it != ids.end()) return it->second;
+    const uint32_t id = uint32_t(names.size());
+    names.emplace_back(k);
+    ids.emplace(names.back(), id);
+    return id;
+  }
+};
+struct KeyCache {  // per worker: key bytes -> provisional id, no lock once seen
+  struct E {
+    uint64_t h;
+    std::string k;
+    uint32_t id;
+  };
+  std::vector<E> e;
+  uint32_t get(KeyNames &kn, std::string_view k) {
+    const uint64_t h = hash_bytes(k.data(), k.size());
+    for (const auto &x : e)
+      if (x.h == h && x.k == k) return x.id;
+    const uint32_t id = kn.get(k);
+    e.push_back({h, std::string(k), id});
+    return id;
+  }
+};
+
+struct LPage {
+  std::vector<uint8_t> buf;
+  uint64_t fb_bytes = 0;
+  uint32_t n = 0;
+  int err = 0;
+  std::string msg;
+  std::vector<uint32_t> id_off;
+  std::vector<uint8_t> id_len;
+  std::vector<uint64_t> start, end;
+  std::vector<uint32_t> tag0;     // n + 1: entry j's tag references [tag0[j], tag0[j+1])
+  std::vector<uint32_t> tag_kv;   // per reference: its own table (SearchEntry.Get walks these)
+  std::vector<uint32_t> tag_res;  // per reference: the table FindTag lands on for its key, or kNone
+  std::vector<uint32_t> kv_key;   // per distinct table: provisional key id
+  std::vector<uint32_t> kv_v0;    // tables + 1: its values [kv_v0[t], kv_v0[t+1]) in vals
+  std::vector<std::string_view> vals;
+  std::vector<uint64_t> vhash;
+  std::vector<uint32_t> vloc;     // phase B: per value reference, its id in its hash shard
+  std::vector<uint32_t> kv_sid;   // phase B: the table's value set id within its key
+  std::vector<uint32_t> bykey, bykey0;  // tables grouped by provisional key (CSR)
+};
+
+// open addressing: table position -> page-local table index (reset per page)
+struct PosMap {
+  std::vector<uint64_t> slot;  // pos << 32 | (index + 1); 0 = empty
+  size_t used = 0;
+  void reset(size_t expect) {
+    size_t cap = 1024;
+    while (cap < 2 * expect) cap <<= 1;
+    if (slot.size() != cap) slot.assign(cap, 0);
+    else std::fill(slot.begin(), slot.end(), 0);
+    used = 0;
+  }
+  // index of `pos`, or inserts `fresh` and returns kNone
+  uint32_t find_or_put(uint32_t pos, uint32_t fresh) {
+    if (2 * (used + 1) > slot.size()) {
+      std::vector<uint64_t> old;
+      old.swap(slot);
+      slot.assign(old.size() * 2, 0);
+      used = 0;
+      for (uint64_t x : old)
+        if (x) find_or_put(uint32_t(x >> 32), uint32_t(x) - 1);
+    }
+    const size_t mask = slot.size() - 1;
+    for (size_t h = (uint64_t(pos) * 0x9E3779B97F4A7C15ull) >> 20;; h++) {
+      uint64_t &x = slot[h & mask];
+      if (!x) {
+        x = (uint64_t(pos) << 32) | (uint64_t(fresh) + 1);
+        used++;
+        return kNone;
+      }
+      if (uint32_t(x >> 32) == pos) return uint32_t(x) - 1;
+    }
+  }
+};
+
+void parse_lpage(const uint8_t *data, size_t dlen, int enc, const IndexRecord &rec, KeyNames &kn, KeyCache &kc,
+                 PosMap &pm, LPage &pp) {
+  read_data_page(data, dlen, rec, enc, pp.buf);
+  // object.UnmarshalAndAdvanceBuffer (object.go:82-113): [u32 total][u32 idLen][id][obj]
+  if (pp.buf.size() < 8) fail(TSG_E_CORRUPT, "object header truncated");
+  const uint32_t total = le32(pp.buf.data()), il = le32(pp.buf.data() + 4);
+  if (total < 8 || pp.buf.size() - 8 < total - 8 || il > total - 8) fail(TSG_E_CORRUPT, "object out of bounds");
+  const uint8_t *fb = pp.buf.data() + 8 + il;
+  const size_t fbn = total - 8 - il;
+  const uint32_t fb_base = uint32_t(fb - pp.buf.data());
+  pp.fb_bytes = fbn;
+  FbTable page = FbTable::root(fb, fbn);
+  const uint16_t eo = page.field(kPageEntries);
+  pp.n = eo ? page.vector_len(eo) : 0;
+  const uint32_t es = eo ? page.vector_start(eo) : 0;
+  pp.id_off.resize(pp.n);
+  pp.id_len.resize(pp.n);
+  pp.start.resize(pp.n);
+  pp.end.resize(pp.n);
+  pp.tag0.assign(1, 0);
+  pp.tag0.reserve(pp.n + 1);
+  pp.tag_kv.reserve(size_t(pp.n) * 20);
+  pp.tag_res.reserve(size_t(pp.n) * 20);
+  pp.kv_v0.assign(1, 0);
+  pm.reset(size_t(pp.n) * 8);
+  std::vector<std::pair<uint32_t, uint32_t>> kpos_ids;  // key string position -> key id
+  FbTable e{fb, fbn, 0}, kv{fb, fbn, 0};
+  for (uint32_t j = 0; j < pp.n; j++) {
+    e.pos = page.indirect(es + 4 * j);
+    const uint16_t io = e.field(kEntryId);
+    const std::string_view id = io ? e.byte_vector(e.pos + io) : std::string_view();
+    if (id.size() > 16) fail(TSG_E_UNSUPPORTED, "trace id longer than 16 bytes");
+    pp.id_off[j] = uint32_t(reinterpret_cast<const uint8_t *>(id.data()) - fb) + fb_base;
+    pp.id_len[j] = uint8_t(id.size());
+    pp.start[j] = e.u64(kEntryStart);
+    pp.end[j] = e.u64(kEntryEnd);
+    const uint16_t to = e.field(kEntryTags);
+    const uint32_t nt = to ? e.vector_len(to) : 0, ts = to ? e.vector_start(to) : 0;
+    const size_t t0 = pp.tag_kv.size();
+    bool ordered = true;
+    std::string_view prev;
+    for (uint32_t t = 0; t < nt; t++) {
+      const uint32_t pos = e.indirect(ts + 4 * t);
+      uint32_t idx = pm.find_or_put(pos, uint32_t(pp.kv_key.size()));
+      std::string_view key;
+      if (idx == kNone) {  // a table not seen in this page yet
+        idx = uint32_t(pp.kv_key.size());
+        kv.pos = pos;
+        const uint16_t ko = kv.field(kKvKey);
+        key = ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
+        // the page's strings are shared (one copy of a key per page): key id by string position
+        const uint32_t kpos = ko ? kv.indirect(kv.pos + ko) : 0u;
+        uint32_t kid = kNone;
+        for (const auto &x : kpos_ids)
+          if (x.first == kpos) {
+            kid = x.second;
+            break;
+          }
+        if (kid == kNone) {
+          kid = kc.get(kn, key);
+          kpos_ids.push_back({kpos, kid});
+        }
+        pp.kv_key.push_back(kid);
+        const uint16_t vo = kv.field(kKvValue);
+        const uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
+        for (uint32_t q = 0; q < vn; q++) {
+          const std::string_view v = kv.byte_vector(vs + 4 * q);
+          pp.vals.push_back(v);
+          pp.vhash.push_back(hash_bytes(v.data(), v.size()));
+        }
+        pp.kv_v0.push_back(uint32_t(pp.vals.size()));
+      } else {
+        kv.pos = pos;
+        const uint16_t ko = kv.field(kKvKey);
+        key = ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
+      }
+      // backend blocks hold keys unique and strictly descending (pitfall P3); otherwise
+      // FindTag's binary search is emulated below
+      if (t > 0 && !(prev > key)) ordered = false;
+      prev = key;
+      pp.tag_kv.push_back(idx);
+    }
+    if (ordered) {
+      pp.tag_res.insert(pp.tag_res.end(), pp.tag_kv.begin() + long(t0), pp.tag_kv.end());
+    } else {
+      auto key_of = [&](uint32_t x) {
+        kv.pos = e.indirect(ts + 4 * x);
+        const uint16_t ko = kv.field(kKvKey);
+        return ko ? kv.byte_vector(kv.pos + ko) : std::string_view();
+      };
+      for (uint32_t t = 0; t < nt; t++) {
+        const std::string_view k = key_of(t);
+        uint32_t i = 0, jj = nt, found = kNone;
+        while (i < jj) {  // binarySearch, reversed comparator (searchdata_util.go:63-100)
+          const uint32_t h = (i + jj) >> 1;
+          const std::string_view hk = key_of(h);
+          const int c = bytes_compare(reinterpret_cast<const uint8_t *>(hk.data()), hk.size(),
+                                      reinterpret_cast<const uint8_t *>(k.data()), k.size());
+          if (c == 0) {
+            found = pp.tag_kv[t0 + h];
+            break;
+          }
+          if (c < 0) jj = h;
+          else i = h + 1;
+        }
+        pp.tag_res.push_back(found);
+      }
+    }
+    pp.tag0.push_back(uint32_t(pp.tag_kv.size()));
+  }
+  pp.kv_sid.assign(pp.kv_key.size(), kNone);
+}
+
+// Phase B tables. A key's values are interned in hash shards (shard = top hash bits), each
+// by its own thread in page order; a value's id is its shard's base + its index there.
+struct ValueShard {
+  std::vector<uint8_t> bytes;
+  std::vector<uint32_t> off{0};
+  std::vector<uint64_t> slot;  // (hash high 32) << 32 | (local + 1)
+  std::vector<uint64_t> vh;    // per local id: its hash
+  size_t used = 0;
+  static size_t probe0(uint64_t h, size_t mask) { return size_t(h ^ (h >> 29)) & mask; }
+  void reserve(size_t nv, size_t nb) {
+    size_t c = 256;
+    while (c < 2 * nv + 2) c <<= 1;
+    slot.assign(c, 0);
+    vh.reserve(nv);
+    off.reserve(nv + 1);
+    bytes.reserve(nb);
+  }
+  uint32_t get(std::string_view v, uint64_t h) {
+    if (2 * (used + 1) > slot.size()) grow();
+    const size_t mask = slot.size() - 1;
+    for (size_t i = probe0(h, mask);; i = (i + 1) & mask) {
+      const uint64_t x = slot[i];
+      if (!x) {
+        const uint32_t id = uint32_t(off.size() - 1);
+        bytes.insert(bytes.end(), v.begin(), v.end());
+        off.push_back(uint32_t(bytes.size()));
+        vh.push_back(h);
+        slot[i] = (h & 0xffffffff00000000ull) | (uint64_t(id) + 1);
+        used++;
+        return id;
+      }
+      if ((x >> 32) == (h >> 32)) {
+        const uint32_t id = uint32_t(x) - 1;
+        if (vh[id] == h && off[id + 1] - off[id] == v.size() && std::memcmp(bytes.data() + off[id], v.data(), v.size()) == 0)
+          return id;
+      }
+    }
+  }
+  void grow() {
+    std::vector<uint64_t> old;
+    old.swap(slot);
+    slot.assign(std::max<size_t>(256, old.size() * 2), 0);
+    const size_t mask = slot.size() - 1;
+    for (uint64_t x : old) {
+      if (!x) continue;
+      size_t i = probe0(vh[uint32_t(x) - 1], mask);
+      while (slot[i]) i = (i + 1) & mask;
+      slot[i] = x;
+    }
+  }
+};
+// A multi-valued key's value sets (vectors of value ids), interned in page order.
+struct SetIntern {
+  KeyColumn *kc;
+  std::vector<uint64_t> slot, sh;
+  size_t used = 0;
+  void reserve(size_t ns) {
+    size_t c = 256;
+    while (c < 2 * ns + 2) c <<= 1;
+    slot.assign(c, 0);
+    sh.reserve(ns);
+  }
+  uint32_t get(const uint32_t *vids, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    for (size_t i = 0; i < n; i++) {
+      h = (h ^ vids[i]) * 0xff51afd7ed558ccdull;
+      h ^= h >> 32;
+    }
+    if (2 * (used + 1) > slot.size()) grow();
+    const size_t mask = slot.size() - 1;
+    for (size_t i = ValueShard::probe0(h, mask);; i = (i + 1) & mask) {
+      const uint64_t x = slot[i];
+      if (!x) {
+        const uint32_t sid = kc->nsets();
+        kc->set_vals.insert(kc->set_vals.end(), vids, vids + n);
+        kc->set_off.push_back(uint32_t(kc->set_vals.size()));
+        if (n != 1 || sid != vids[0]) kc->identity = false;
+        sh.push_back(h);
+        slot[i] = (h & 0xffffffff00000000ull) | (uint64_t(sid) + 1);
+        used++;
+        return sid;
+      }
+      if ((x >> 32) == (h >> 32)) {
+        const uint32_t sid = uint32_t(x) - 1;
+        if (sh[sid] == h && kc->set_off[sid + 1] - kc->set_off[sid] == n &&
+            std::equal(vids, vids + n, kc->set_vals.begin() + kc->set_off[sid]))
+          return sid;
+      }
+    }
+  }
+  void grow() {
+    std::vector<uint64_t> old;
+    old.swap(slot);
+    slot.assign(std::max<size_t>(256, old.size() * 2), 0);
+    const size_t mask = slot.size() - 1;
+    for (uint64_t x : old) {
+      if (!x) continue;
+      size_t i = ValueShard::probe0(sh[uint32_t(x) - 1], mask);
+      while (slot[i]) i = (i + 1) & mask;
+      slot[i] = x;
+    }
+  }
+};
+
+// runs f(i) for i in [0, n) on up to nthreads threads, items taken in order from a counter
+template <class F>
+void for_each_index(size_t n, int nthreads, F &&f) {
+  std::atomic<size_t> next{0};
+  std::mutex emu;
+  std::exception_ptr err;
+  auto work = [&] {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) break;
+      try {
+        f(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(emu);
+        if (!err) err = std::current_exception();
+        next.store(n);
+      }
+    }
+  };
+  const size_t nt = std::min<size_t>(size_t(std::max(1, nthreads)), n);
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; t++) th.emplace_back(work);
+  work();
+  for (auto &x : th) x.join();
+  if (err) std::rethrow_exception(err);
+}
+}  // namespace
+
+static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, const uint8_t *data, size_t data_len,
+                       int nthreads) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  // ---- A: pages
+  std::vector<LPage> pages(recs.size());
+  KeyNames kn;
+  std::vector<KeyCache> caches(size_t(std::max(1, nthreads)));
+  std::atomic<size_t> next{0};
+  {
+    auto work = [&](size_t w) {
+      PosMap pm;
+      for (;;) {
+        const size_t i = next.fetch_add(1);
+        if (i >= pages.size()) break;
+        LPage &pp = pages[i];
+        try {
+          parse_lpage(data, data_len, hb.meta.encoding, recs[i], kn, caches[w], pm, pp);
+        } catch (const Error &e) {
+          pp.err = e.code;
+          pp.msg = e.what();
+        }
+      }
+    };
+    const size_t nt = std::min<size_t>(size_t(std::max(1, nthreads)), std::max<size_t>(1, pages.size()));
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+  }
+  // the first damaged page ends the block: the pages before it stay, and its error is what
+  // Search returns once it gets there
+  size_t np = pages.size();
+  for (size_t i = 0; i < pages.size(); i++)
+    if (pages[i].err) {
+      hb.stop_status = pages[i].err;
+      hb.stop_msg = pages[i].msg;
+      np = i;
+      break;
+    }
+  const auto t1 = clk::now();
+  // keys (only those of the kept pages) in name order; tables grouped per key
+  const size_t nk0 = kn.names.size();
+  std::vector<uint8_t> used(nk0, 0);
+  for (size_t i = 0; i < np; i++)
+    for (uint32_t k : pages[i].kv_key) used[k] = 1;
+  std::vector<uint32_t> ord;
+  for (uint32_t k = 0; k < nk0; k++)
+    if (used[k]) ord.push_back(k);
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return kn.names[a] < kn.names[b]; });
+  std::vector<uint32_t> final_of(nk0, kNone);
+  hb.keys.clear();
+  hb.key_index.clear();
+  hb.keys.resize(ord.size());
+  for (size_t f = 0; f < ord.size(); f++) {
+    final_of[ord[f]] = uint32_t(f);
+    KeyColumn &kc = hb.keys[f];
+    kc.name = kn.names[ord[f]];
+    kc.dict_off.assign(1, 0);
+    kc.set_off.assign(1, 0);
+    hb.key_index.emplace(kc.name, int(f));
+    if (kc.name == "root.service.name") hb.svc_key = int(f);
+    if (kc.name == "root.name") hb.name_key = int(f);
+  }
+  const size_t nk = ord.size();
+  for_each_index(np, nthreads, [&](size_t i) {
+    LPage &pp = pages[i];
+    for (auto &k : pp.kv_key) k = final_of[k];
+    pp.bykey0.assign(nk + 1, 0);
+    for (uint32_t k : pp.kv_key) pp.bykey0[k + 1]++;
+    for (size_t k = 0; k < nk; k++) pp.bykey0[k + 1] += pp.bykey0[k];
+    pp.bykey.resize(pp.kv_key.size());
+    std::vector<uint32_t> at(pp.bykey0.begin(), pp.bykey0.end() - 1);
+    for (uint32_t t = 0; t < pp.kv_key.size(); t++) pp.bykey[at[pp.kv_key[t]]++] = t;
+  });
+  const auto t2 = clk::now();
+  // ---- B: values (hash shards, parallel) and value sets per key
+  {
+    struct KInfo {
+      uint64_t tables = 0, refs = 0, bytes = 0;
+      bool single = true;  // every table of the key holds exactly one value: set id = value id
+      uint32_t P = 1;      // value shards
+    };
+    std::vector<KInfo> kin(nk);
+    for_each_index(nk, nthreads, [&](size_t k) {
+      KInfo &I = kin[k];
+      for (size_t i = 0; i < np; i++) {
+        const LPage &pp = pages[i];
+        for (uint32_t b = pp.bykey0[k]; b < pp.bykey0[k + 1]; b++) {
+          const uint32_t t = pp.bykey[b];
+          const uint32_t nv = pp.kv_v0[t + 1] - pp.kv_v0[t];
+          I.tables++;
+          I.refs += nv;
+          I.single = I.single && nv == 1;
+          for (uint32_t v = pp.kv_v0[t]; v < pp.kv_v0[t + 1]; v++) I.bytes += pp.vals[v].size();
+        }
+      }
+      while (I.P < 16 && I.refs / I.P > 65536) I.P <<= 1;
+    });
+    auto shard_of = [](uint64_t h, uint32_t P) { return uint32_t(h >> 48) & (P - 1); };
+    // each shard's value references (page << 32 | value), in page order: one pass per key
+    std::vector<std::vector<std::vector<uint64_t>>> refs(nk);
+    for_each_index(nk, nthreads, [&](size_t k) {
+      const uint32_t P = kin[k].P;
+      refs[k].resize(P);
+      for (auto &r : refs[k]) r.reserve(size_t(kin[k].refs / P + kin[k].refs / (4 * P) + 16));
+      for (size_t i = 0; i < np; i++) {
+        const LPage &pp = pages[i];
+        for (uint32_t b = pp.bykey0[k]; b < pp.bykey0[k + 1]; b++) {
+          const uint32_t t = pp.bykey[b];
+          for (uint32_t v = pp.kv_v0[t]; v < pp.kv_v0[t + 1]; v++)
+            refs[k][shard_of(pp.vhash[v], P)].push_back((uint64_t(i) << 32) | v);
+        }
+      }
+    });
+    for_each_index(np, nthreads, [&](size_t i) { pages[i].vloc.resize(pages[i].vals.size()); });
+    const auto tb1 = clk::now();
+    std::vector<std::vector<ValueShard>> shards(nk);
+    std::vector<std::pair<uint32_t, uint32_t>> jobs;  // (key, shard), heaviest first
+    for (uint32_t k = 0; k < nk; k++) {
+      shards[k].resize(kin[k].P);
+      for (uint32_t x = 0; x < kin[k].P; x++) jobs.push_back({k, x});
+    }
+    std::sort(jobs.begin(), jobs.end(), [&](const auto &a, const auto &b) {
+      return kin[a.first].refs / kin[a.first].P > kin[b.first].refs / kin[b.first].P;
+    });
+    for_each_index(jobs.size(), nthreads, [&](size_t j) {
+      const uint32_t k = jobs[j].first, x = jobs[j].second, P = kin[k].P;
+      ValueShard &S = shards[k][x];
+      const auto &R = refs[k][x];
+      S.reserve(R.size(), size_t(kin[k].bytes / P + kin[k].bytes / (4 * P)));
+      for (const uint64_t r : R) {
+        LPage &pp = pages[size_t(r >> 32)];
+        const uint32_t v = uint32_t(r);
+        pp.vloc[v] = S.get(pp.vals[v], pp.vhash[v]);
+      }
+      S.slot = std::vector<uint64_t>();
+      std::vector<uint64_t>().swap(refs[k][x]);
+    });
+    const auto tb2 = clk::now();
+    // each key's dictionary: its shards one after another
+    std::vector<std::vector<uint32_t>> vbase(nk);
+    for_each_index(nk, nthreads, [&](size_t k) {
+      KeyColumn &kc = hb.keys[k];
+      uint64_t nv = 0, nb = 0;
+      vbase[k].resize(kin[k].P);
+      for (uint32_t x = 0; x < kin[k].P; x++) {
+        vbase[k][x] = uint32_t(nv);
+        nv += shards[k][x].off.size() - 1;
+        nb += shards[k][x].bytes.size();
+      }
+      if (nb > 0xF0000000u) fail(TSG_E_UNSUPPORTED, "dictionary too large");
+      kc.dict_bytes.resize(nb);
+      kc.dict_off.resize(nv + 1);
+      kc.dict_off[nv] = uint32_t(nb);
+    });
+    for_each_index(jobs.size(), nthreads, [&](size_t j) {
+      const uint32_t k = jobs[j].first, x = jobs[j].second;
+      const ValueShard &S = shards[k][x];
+      KeyColumn &kc = hb.keys[k];
+      uint64_t b0 = 0;
+      for (uint32_t y = 0; y < x; y++) b0 += shards[k][y].bytes.size();
+      if (!S.bytes.empty()) std::memcpy(kc.dict_bytes.data() + b0, S.bytes.data(), S.bytes.size());
+      for (size_t i = 0; i + 1 < S.off.size(); i++) kc.dict_off[vbase[k][x] + i] = uint32_t(b0 + S.off[i]);
+    });
+    shards.clear();
+    const auto tb3 = clk::now();
+    // value sets: a single-valued key's set of value v is v (identity); other keys intern
+    // their value-id vectors in page order
+    for_each_index(nk, nthreads, [&](size_t k) {
+      KeyColumn &kc = hb.keys[k];
+      const uint32_t P = kin[k].P;
+      const std::vector<uint32_t> &vb = vbase[k];
+      if (kin[k].single) {
+        const uint32_t nv = kc.nvals();
+        kc.identity = true;
+        kc.set_off.resize(size_t(nv) + 1);
+        kc.set_vals.resize(nv);
+        for (uint32_t v = 0; v <= nv; v++) kc.set_off[v] = v;
+        for (uint32_t v = 0; v < nv; v++) kc.set_vals[v] = v;
+        for (size_t i = 0; i < np; i++) {
+          LPage &pp = pages[i];
+          for (uint32_t b = pp.bykey0[k]; b < pp.bykey0[k + 1]; b++) {
+            const uint32_t t = pp.bykey[b], v = pp.kv_v0[t];
+            pp.kv_sid[t] = vb[shard_of(pp.vhash[v], P)] + pp.vloc[v];
+          }
+        }
+        return;
+      }
+      kc.identity = false;  // (some table holds no value or several)
+    });
+    // multi-valued keys: the value-id vectors interned in hash shards as well
+    auto vid_of = [&](const LPage &pp, uint32_t k, uint32_t v) {
+      return vbase[k][shard_of(pp.vhash[v], kin[k].P)] + pp.vloc[v];
+    };
+    auto set_hash = [&](const LPage &pp, uint32_t k, uint32_t t) {
+      const uint32_t n = pp.kv_v0[t + 1] - pp.kv_v0[t];
+      uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+      for (uint32_t v = pp.kv_v0[t]; v < pp.kv_v0[t + 1]; v++) {
+        h = (h ^ vid_of(pp, k, v)) * 0xff51afd7ed558ccdull;
+        h ^= h >> 32;
+      }
+      return mix_set(h);
+    };
+    std::vector<uint32_t> SP(nk, 1);
+    std::vector<std::vector<std::vector<uint64_t>>> srefs(nk);  // per set shard: page << 32 | table
+    for_each_index(nk, nthreads, [&](size_t k) {
+      if (kin[k].single) return;
+      while (SP[k] < 16 && kin[k].tables / SP[k] > 65536) SP[k] <<= 1;
+      srefs[k].resize(SP[k]);
+      for (auto &r : srefs[k]) r.reserve(size_t(kin[k].tables / SP[k] + kin[k].tables / (4 * SP[k]) + 16));
+      for (size_t i = 0; i < np; i++) {
+        LPage &pp = pages[i];
+        for (uint32_t b = pp.bykey0[k]; b < pp.bykey0[k + 1]; b++) {
+          const uint32_t t = pp.bykey[b];
+          const uint64_t h = set_hash(pp, uint32_t(k), t);
+          pp.kv_sid[t] = uint32_t(h >> 32);  // (the set hash's top half until the set id is known)
+          srefs[k][shard_of(h, SP[k])].push_back((uint64_t(i) << 32) | t);
+        }
+      }
+    });
+    struct SetShard {
+      std::vector<uint32_t> vals, off{0};
+      std::vector<uint64_t> slot, sh;
+      size_t used = 0;
+    };
+    std::vector<std::vector<SetShard>> sshards(nk);
+    std::vector<std::pair<uint32_t, uint32_t>> sjobs;
+    for (uint32_t k = 0; k < nk; k++) {
+      if (kin[k].single) continue;
+      sshards[k].resize(SP[k]);
+      for (uint32_t x = 0; x < SP[k]; x++) sjobs.push_back({k, x});
+    }
+    for_each_index(sjobs.size(), nthreads, [&](size_t j) {
+      const uint32_t k = sjobs[j].first, x = sjobs[j].second;
+      SetShard &S = sshards[k][x];
+      const auto &R = srefs[k][x];
+      size_t c = 256;
+      while (c < 2 * R.size() + 2) c <<= 1;
+      S.slot.assign(c, 0);
+      const size_t mask = c - 1;
+      std::vector<uint32_t> tmp;
+      for (const uint64_t r : R) {
+        LPage &pp = pages[size_t(r >> 32)];
+        const uint32_t t = uint32_t(r);
+        tmp.clear();
+        for (uint32_t v = pp.kv_v0[t]; v < pp.kv_v0[t + 1]; v++) tmp.push_back(vid_of(pp, k, v));
+        const uint64_t h = set_hash(pp, k, t);
+        uint32_t sid = kNone;
+        for (size_t i = ValueShard::probe0(h, mask);; i = (i + 1) & mask) {
+          const uint64_t xs = S.slot[i];
+          if (!xs) {
+            sid = uint32_t(S.off.size() - 1);
+            S.vals.insert(S.vals.end(), tmp.begin(), tmp.end());
+            S.off.push_back(uint32_t(S.vals.size()));
+            S.sh.push_back(h);
+            S.slot[i] = (h & 0xffffffff00000000ull) | (uint64_t(sid) + 1);
+            break;
+          }
+          if ((xs >> 32) == (h >> 32)) {
+            const uint32_t y = uint32_t(xs) - 1;
+            if (S.sh[y] == h && S.off[y + 1] - S.off[y] == tmp.size() &&
+                std::equal(tmp.begin(), tmp.end(), S.vals.begin() + S.off[y])) {
+              sid = y;
+              break;
+            }
+          }
+        }
+        pp.kv_sid[t] = sid;  // (local to the shard until the bases are added)
+      }
+      S.slot = std::vector<uint64_t>();
+    });
+    // each multi-valued key's sets: its shards one after another; table set ids shifted
+    std::vector<std::vector<uint32_t>> sbase(nk);
+    for_each_index(nk, nthreads, [&](size_t k) {
+      if (kin[k].single) return;
+      KeyColumn &kc = hb.keys[k];
+      uint64_t ns = 0, nvals = 0;
+      sbase[k].resize(SP[k]);
+      for (uint32_t x = 0; x < SP[k]; x++) {
+        sbase[k][x] = uint32_t(ns);
+        ns += sshards[k][x].off.size() - 1;
+        nvals += sshards[k][x].vals.size();
+      }
+      kc.set_vals.resize(nvals);
+      kc.set_off.resize(ns + 1);
+      uint64_t vo = 0;
+      for (uint32_t x = 0; x < SP[k]; x++) {
+        const SetShard &S = sshards[k][x];
+        std::copy(S.vals.begin(), S.vals.end(), kc.set_vals.begin() + long(vo));
+        for (size_t i = 0; i + 1 < S.off.size(); i++) kc.set_off[sbase[k][x] + i] = uint32_t(vo + S.off[i]);
+        vo += S.vals.size();
+      }
+      kc.set_off[ns] = uint32_t(vo);
+      for (size_t i = 0; i < np; i++) {
+        LPage &pp = pages[i];
+        for (uint32_t b = pp.bykey0[k]; b < pp.bykey0[k + 1]; b++) {
+          const uint32_t t = pp.bykey[b];
+          pp.kv_sid[t] += sbase[k][shard_of(set_hash(pp, uint32_t(k), t), SP[k])];
+        }
+      }
+    });
+    if (prof_on()) {
+      const auto tb4 = clk::now();
+      prof_add("load.b.stats", std::chrono::duration<double, std::micro>(tb1 - t2).count());
+      prof_add("load.b.values", std::chrono::duration<double, std::micro>(tb2 - tb1).count());
+      prof_add("load.b.dict", std::chrono::duration<double, std::micro>(tb3 - tb2).count());
+      prof_add("load.b.sets", std::chrono::duration<double, std::micro>(tb4 - tb3).count());
+    }
+  }
+  const auto t3 = clk::now();
+  // ---- C: entry columns
+  std::vector<uint64_t> base(np + 1, 0);
+  for (size_t i = 0; i < np; i++) {
+    base[i + 1] = base[i] + pages[i].n;
+    hb.page_entries.push_back(pages[i].n);
+    hb.page_fb_bytes.push_back(pages[i].fb_bytes);
+    hb.page_first.push_back(base[i]);
+    hb.fb_bytes += pages[i].fb_bytes;
+  }
+  const uint64_t n = base[np];
+  hb.n = n;
+  hb.ids.assign(n * 16, 0);
+  hb.id_len.resize(n);
+  hb.start.resize(n);
+  hb.end.resize(n);
+  hb.svc_vid.assign(n, kNone);
+  hb.name_vid.assign(n, kNone);
+  for_each_index(nk, nthreads, [&](size_t k) { hb.keys[k].col.assign(n, kNone); });
+  for_each_index(np, nthreads, [&](size_t i) {
+    const LPage &pp = pages[i];
+    for (uint32_t j = 0; j < pp.n; j++) {
+      const uint64_t e = base[i] + j;
+      const uint8_t il = pp.id_len[j];
+      std::memcpy(&hb.ids[e * 16 + 16 - il], pp.buf.data() + pp.id_off[j], il);
+      hb.id_len[e] = il;
+      hb.start[e] = pp.start[j];
+      hb.end[e] = pp.end[j];
+      bool svc_done = false, name_done = false;
+      for (uint32_t r = pp.tag0[j]; r < pp.tag0[j + 1]; r++) {
+        const uint32_t t = pp.tag_kv[r];
+        const uint32_t k = pp.kv_key[t];
+        if (pp.tag_res[r] != kNone) hb.keys[k].col[e] = pp.kv_sid[pp.tag_res[r]];
+        // SearchEntry.Get: the first table of the key in vector order, Value(0)
+        // (searchdata_util.go:10-23)
+        if (int(k) == hb.svc_key && !svc_done) {
+          svc_done = true;
+          if (pp.kv_v0[t + 1] > pp.kv_v0[t]) {
+            const KeyColumn &kc = hb.keys[k];
+            hb.svc_vid[e] = kc.set_vals[kc.set_off[pp.kv_sid[t]]];
+          }
+        }
+        if (int(k) == hb.name_key && !name_done) {
+          name_done = true;
+          if (pp.kv_v0[t + 1] > pp.kv_v0[t]) {
+            const KeyColumn &kc = hb.keys[k];
+            hb.name_vid[e] = kc.set_vals[kc.set_off[pp.kv_sid[t]]];
+          }
+        }
+      }
+    }
+  });
+  if (prof_on()) {
+    const auto t4 = clk::now();
+    prof_add("load.pages", std::chrono::duration<double, std::micro>(t1 - t0).count());
+    prof_add("load.group", std::chrono::duration<double, std::micro>(t2 - t1).count());
+    prof_add("load.intern", std::chrono::duration<double, std::micro>(t3 - t2).count());
+    prof_add("load.columns", std::chrono::duration<double, std::micro>(t4 - t3).count());
+  }
+}
+
 void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
                          const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
                          HostBlock &hb) {
@@ -461,52 +1187,20 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
   index_header(hb);
   std::vector<IndexRecord> recs =
       read_index(index, index_len, hb.meta.index_page_size, hb.meta.index_records, &hb.index_truncated);
-  if (nthreads <= 0) nthreads = int(std::max(1u, std::thread::hardware_concurrency()));
+  if (nthreads <= 0) nthreads = host_threads();
   nthreads = std::min<int>(nthreads, 64);
 
-  std::vector<KeyBuild> kb;
-  size_t batch = size_t(nthreads) * 4;
-  std::vector<PageParse> pages;
-  bool stopped = false;
-  for (size_t b0 = 0; b0 < recs.size() && !stopped; b0 += batch) {
-    size_t b1 = std::min(recs.size(), b0 + batch);
-    pages.clear();
-    pages.resize(b1 - b0);
-    std::atomic<size_t> next{b0};
-    auto work = [&]() {
-      for (;;) {
-        size_t i = next.fetch_add(1);
-        if (i >= b1) break;
-        PageParse &pp = pages[i - b0];
-        try {
-          parse_page(data, data_len, hb.meta.encoding, recs[i], pp);
-        } catch (const Error &e) {
-          pp.err = e.code;
-          pp.msg = e.what();
-        }
-      }
-    };
-    std::vector<std::thread> th;
-    int nt = int(std::min<size_t>(size_t(nthreads), b1 - b0));
-    for (int t = 1; t < nt; t++) th.emplace_back(work);
-    work();
-    for (auto &t : th) t.join();
-    // merge pages in order (scan order = pages ascending, entry index ascending); the
-    // first damaged page ends the block: the pages before it stay, and its error is
-    // what Search returns once it gets there (backend_search_block.go:258-266)
-    for (auto &pp : pages) {
-      if (pp.err) {
-        hb.stop_status = pp.err;
-        hb.stop_msg = pp.msg;
-        stopped = true;
-        break;
-      }
-      merge_page(hb, kb, pp);
-    }
-  }
-  for (auto &kc : hb.keys) kc.col.resize(hb.n, kNone);
+  using clk = std::chrono::steady_clock;
+  const bool prof = prof_on();
+  load_pages(hb, recs, data, data_len, nthreads);
+  const auto tc0 = clk::now();
   canonicalize_narrow_keys(hb);
+  const auto tc1 = clk::now();
   verify_header_dicts(hb, nthreads);
+  if (prof) {
+    prof_add("load.canon", std::chrono::duration<double, std::micro>(tc1 - tc0).count());
+    prof_add("load.verify", std::chrono::duration<double, std::micro>(clk::now() - tc1).count());
+  }
 }
 
 // ---- header values == dictionary (hdr_defer) -------------------------------------------
@@ -570,7 +1264,7 @@ H128 multiset_hash(size_t n, int nthreads, Value &&value) {
 void verify_header_dicts(HostBlock &hb, int nthreads) {
   hb.hdr_defer.assign(hb.hdr_keys.size(), 0);
   if (!hb.hdr_index) return;
-  if (nthreads <= 0) nthreads = int(std::max(1u, std::thread::hardware_concurrency()));
+  if (nthreads <= 0) nthreads = host_threads();
   nthreads = std::min(nthreads, 32);
   for (size_t hk = 0; hk < hb.hdr_keys.size(); hk++) {
     auto it = hb.key_index.find(std::string(hb.hdr_keys[hk]));

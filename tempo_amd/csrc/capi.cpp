@@ -284,10 +284,11 @@ static int guard(F &&f) {
 // Holder behind tsg_result: owns the arrays the public struct points into.
 struct ResultHolder {
   tsg_result pub{};
-  std::vector<uint8_t> ids, id_len;
-  std::vector<uint64_t> start, end, entry;
-  std::vector<uint32_t> dur, block, svc_len, name_len;
-  std::vector<uint64_t> svc_off, name_off;  // into `arena` (one allocation for every name)
+  // (RawVec: a result of millions of records is written once, never zero-filled first)
+  RawVec<uint8_t> ids, id_len;
+  RawVec<uint64_t> start, end, entry;
+  RawVec<uint32_t> dur, block, svc_len, name_len;
+  RawVec<uint64_t> svc_off, name_off;  // into `arena` (one allocation for every name)
   char *arena = nullptr;  // (grown by hand: no zero-fill, no per-name insert)
   size_t arena_size = 0, arena_cap = 0;
   ResultHolder() = default;
@@ -301,7 +302,7 @@ struct ResultHolder {
     arena = p;
     arena_cap = cap;
   }
-  std::vector<const char *> svc_p, name_p;
+  RawVec<const char *> svc_p, name_p;
   std::vector<int32_t> bstatus;      // per caller block
   std::vector<std::string> berr_s;
   std::vector<const char *> berr;
@@ -359,7 +360,7 @@ struct ResultHolder {
     intern[h & mask] = InternSlot{p, l, off};
     intern_used++;
   }
-  void set_str(std::vector<uint64_t> &off, std::vector<uint32_t> &len, size_t i, const char *p, size_t l) {
+  void set_str(RawVec<uint64_t> &off, RawVec<uint32_t> &len, size_t i, const char *p, size_t l) {
     len[i] = uint32_t(l);
     off[i] = l ? intern_lookup(p, l) : 0;
   }
@@ -409,10 +410,12 @@ struct ResultHolder {
     const size_t n = start.size();
     svc_p.resize(n);
     name_p.resize(n);
-    for (size_t i = 0; i < n; i++) {
-      svc_p[i] = svc(i);
-      name_p[i] = name(i);
-    }
+    parallel_ranges(n, size_t(1) << 18, 16, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; i++) {
+        svc_p[i] = svc(i);
+        name_p[i] = name(i);
+      }
+    });
     pub.n = n;
     pub.trace_id = reinterpret_cast<const uint8_t(*)[16]>(ids.data());
     pub.trace_id_len = id_len.data();
@@ -466,10 +469,16 @@ static ResultHolder *acquire_holder() {
 static void release_holder(ResultHolder *h) {
   if (!h) return;
   HolderPool &hp = holder_pool();
-  if (h->arena_cap <= (64u << 20) && h->start.capacity() <= (1u << 20)) {
+  // large holders (a dense result of millions of records: their pages stay faulted in for
+  // the next such query) are kept too, at most 2 of them
+  constexpr size_t kSmall = size_t(1) << 20, kBig = size_t(1) << 25;
+  const size_t cap = h->start.capacity();
+  if (h->arena_cap <= (256u << 20) && cap <= kBig) {
     h->clear();
     std::lock_guard<SpinLock> lk(hp.mu);
-    if (hp.free.size() < 16) {
+    size_t big = 0;
+    for (auto *x : hp.free) big += x->start.capacity() > kSmall;
+    if (hp.free.size() < 16 && (cap <= kSmall || big < 2)) {
       hp.free.push_back(h);
       return;
     }
@@ -1046,6 +1055,99 @@ struct IdSet {
   }
 };
 
+// Result arrays of a large full scan on several threads: output record o of block i is
+// per_block[i].first[o - obase[i]]. Each thread interns its names into an arena of its own
+// (a name = a block dictionary value, interned by address); the arenas are then placed one
+// after another and each thread's name offsets shifted by its arena's place.
+static void fill_records_parallel(ResultHolder &res, tsg_block *const *blocks,
+                                  const std::vector<std::pair<const SearchOut::Rec *, size_t>> &per_block,
+                                  const std::vector<size_t> &obase, size_t nout) {
+  const size_t hw = size_t(host_threads());
+  const size_t nt = std::max<size_t>(1, std::min<size_t>({16, hw, nout / 32768}));
+  struct Local {
+    std::vector<ResultHolder::InternSlot> tab;
+    size_t used = 0;
+    std::string arena;
+    uint64_t get(const char *p, size_t l) {
+      if (2 * (used + 1) > tab.size()) {  // grow: rehash
+        std::vector<ResultHolder::InternSlot> old;
+        old.swap(tab);
+        tab.assign(std::max<size_t>(256, 2 * old.size()), ResultHolder::InternSlot{nullptr, 0, 0});
+        used = 0;
+        for (const auto &x : old)
+          if (x.p) put(x);
+      }
+      const size_t mask = tab.size() - 1;
+      for (size_t h = (uintptr_t(p) * 0x9E3779B97F4A7C15ull ^ l) >> 7;; h++) {
+        auto &x = tab[h & mask];
+        if (!x.p) {
+          x = ResultHolder::InternSlot{p, uint32_t(l), arena.size()};
+          used++;
+          arena.append(p, l);
+          return x.off;
+        }
+        if (x.p == p && x.l == l) return x.off;
+      }
+    }
+    void put(const ResultHolder::InternSlot &s) {
+      const size_t mask = tab.size() - 1;
+      size_t h = (uintptr_t(s.p) * 0x9E3779B97F4A7C15ull ^ s.l) >> 7;
+      while (tab[h & mask].p) h++;
+      tab[h & mask] = s;
+      used++;
+    }
+  };
+  std::vector<Local> loc(nt);
+  auto range = [&](size_t t, size_t &o0, size_t &o1) {
+    o0 = nout * t / nt;
+    o1 = nout * (t + 1) / nt;
+  };
+  parallel_ranges(nt, 1, int(nt), [&](size_t t0, size_t t1) {
+    for (size_t t = t0; t < t1; t++) {
+      size_t o0, o1;
+      range(t, o0, o1);
+      if (o0 >= o1) continue;
+      Local &L = loc[t];
+      size_t i = size_t(std::upper_bound(obase.begin(), obase.end(), o0) - obase.begin()) - 1;
+      for (size_t o = o0; o < o1; o++) {
+        while (o >= obase[i + 1]) i++;
+        const HostBlock &h = *blocks[i]->b.host;
+        const SearchOut::Rec *r = per_block[i].first + (o - obase[i]);
+        std::memcpy(&res.ids[16 * o], r->id, 16);
+        res.id_len[o] = uint8_t(r->block_il >> 24);
+        res.start[o] = r->start;
+        res.end[o] = r->end;
+        res.dur[o] = uint32_t((r->end - r->start) / 1000000ULL);  // util.go:33
+        res.block[o] = uint32_t(i);
+        res.entry[o] = r->entry;
+        std::string_view sv, nm;
+        if (h.svc_key >= 0 && r->svc != kNone) sv = h.dict_value(h.svc_key, r->svc);
+        if (h.name_key >= 0 && r->name != kNone) nm = h.dict_value(h.name_key, r->name);
+        res.svc_len[o] = uint32_t(sv.size());
+        res.svc_off[o] = sv.empty() ? 0 : L.get(sv.data(), sv.size());
+        res.name_len[o] = uint32_t(nm.size());
+        res.name_off[o] = nm.empty() ? 0 : L.get(nm.data(), nm.size());
+      }
+    }
+  });
+  std::vector<uint64_t> base(nt + 1, 0);
+  for (size_t t = 0; t < nt; t++) base[t + 1] = base[t] + loc[t].arena.size();
+  if (base[nt] > res.arena_cap) res.arena_grow(base[nt]);
+  res.arena_size = base[nt];
+  parallel_ranges(nt, 1, int(nt), [&](size_t t0, size_t t1) {
+    for (size_t t = t0; t < t1; t++) {
+      if (!loc[t].arena.empty()) std::memcpy(res.arena + base[t], loc[t].arena.data(), loc[t].arena.size());
+      size_t o0, o1;
+      range(t, o0, o1);
+      if (!base[t]) continue;
+      for (size_t o = o0; o < o1; o++) {
+        if (res.svc_len[o]) res.svc_off[o] += base[t];
+        if (res.name_len[o]) res.name_off[o] += base[t];
+      }
+    }
+  });
+}
+
 int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
                const tsg_search_opts *opts, tsg_result **out) {
   if (!ctx || !q || !out || (nblocks && !blocks)) return TSG_E_INVALID;
@@ -1420,11 +1522,44 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     res->reserve(nrec);
     res->resize(nrec);
     size_t nout = 0;
+    // A large full scan (no limit, no live block: every record of every inspected block is
+    // kept, nothing to consume) is assembled on several threads; otherwise one thread
+    // consumes in caller block order (deterministic refinement of instance.Search)
+    const bool par = !limit && !any_live && nrec >= (size_t(1) << 16);
+    if (par) {
+      thread_local std::vector<size_t> obase;
+      obase.assign(nblocks + 1, 0);
+      for (size_t i = 0; i < nblocks; i++) {
+        const HostBlock &h = *blocks[i]->b.host;
+        size_t k = 0;
+        if (state[i] != 0) {
+          m.bytes_inspected += h.header.size();
+          if (state[i] == 2 && defer[i])  // (as below)
+            state[i] = anym[i] >= 0 ? ((defer[i] & ~uint32_t(anym[i])) ? 1 : 2)
+                                    : (pipeline_matches_block_indexed(*q, h) ? 2 : 1);
+          if (state[i] == 1) {
+            m.blocks_skipped++;
+          } else {
+            m.blocks_inspected++;
+            k = per_block[i].second;
+            m.traces_inspected += uint32_t(h.n);
+            m.bytes_inspected += h.fb_bytes;
+            if (h.stop_status) {
+              res->bstatus[i] = h.stop_status;
+              res->berr_s[i] = h.stop_msg;
+            }
+          }
+        }
+        obase[i + 1] = obase[i] + k;
+      }
+      nout = obase[nblocks];
+      fill_records_parallel(*res, blocks, per_block, obase, nout);
+    }
     // consume in caller block order (deterministic refinement of instance.Search)
     thread_local IdSet distinct;
     distinct.clear();
     bool stopped = false;
-    for (size_t i = 0; i < nblocks && !stopped; i++) {
+    for (size_t i = 0; i < nblocks && !stopped && !par; i++) {
       const HostBlock &h = *blocks[i]->b.host;
       if (state[i] == 0) continue;  // meta missing: no-op (backend_search_block.go:191-203)
       if (h.live) {  // searchLiveTraces (instance_search.go:99-128)

@@ -4,7 +4,10 @@
 #include <algorithm>
 #include <cerrno>
 #include <cstdio>
+#include <exception>
 #include <mutex>
+#include <thread>
+#include <sched.h>
 #include <sys/stat.h>
 #include <sys/types.h>
 #include <strings.h>
@@ -106,7 +109,24 @@ static void crc_init() {
   for (uint32_t i = 0; i < 256; i++)
     for (int t = 1; t < 8; t++) g_crc[t][i] = (g_crc[t - 1][i] >> 8) ^ g_crc[0][g_crc[t - 1][i] & 0xff];
 }
+// the host CPU's CRC32C instruction (SSE4.2), three independent streams over thirds of
+// the buffer combined by table-free shifts would be faster still; one stream is ~8 B/cycle/3
+__attribute__((target("sse4.2"))) static uint32_t crc32c_hw(const uint8_t *p, size_t n) {
+  uint64_t c = 0xFFFFFFFFu;
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    c = __builtin_ia32_crc32di(c, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = uint32_t(c);
+  while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+  return ~c32;
+}
 uint32_t crc32c(const uint8_t *p, size_t n) {
+  static const bool hw = __builtin_cpu_supports("sse4.2");
+  if (hw) return crc32c_hw(p, n);
   std::call_once(g_crc_once, crc_init);
   uint32_t c = 0xFFFFFFFFu;
   while (n >= 8) {  // slicing-by-8
@@ -134,6 +154,13 @@ static void snappy_block_decode(const uint8_t *src, size_t sl, uint8_t *dst, siz
       uint32_t x = src[s] >> 2;
       if (x < 60) {
         s += 1;
+        // a short literal with 16 bytes of slack on both sides: one fixed-size copy
+        if (x < 16 && sl - s >= 16 && dl - d >= 16) {
+          std::memcpy(dst + d, src + s, 16);
+          d += x + 1;
+          s += x + 1;
+          continue;
+        }
       } else {
         size_t nb = x - 59;
         s += 1 + nb;
@@ -165,7 +192,13 @@ static void snappy_block_decode(const uint8_t *src, size_t sl, uint8_t *dst, siz
       off = le32(src + s - 4);
     }
     if (off == 0 || d < off || len > dl - d) fail(TSG_E_CORRUPT, "snappy: bad copy");
-    if (off >= len) {
+    if (off >= 8 && dl - d >= ((len + 7) & ~size_t(7))) {
+      // 8 bytes at a time: every chunk reads bytes written before it (off >= 8); the last
+      // may write up to 7 bytes past the copy, inside the block, which later ops overwrite
+      uint8_t *o = dst + d;
+      const uint8_t *in = o - off;
+      for (size_t k = 0; k < len; k += 8) std::memcpy(o + k, in + k, 8);
+    } else if (off >= len) {
       std::memcpy(dst + d, dst + d - off, len);
     } else {
       for (size_t i = 0; i < len; i++) dst[d + i] = dst[d - off + i];
@@ -450,6 +483,13 @@ struct ProfTable {
       std::fprintf(stderr, " %s=%.2f", r.first.c_str(), r.second[r.second.size() / 2]);
     }
     std::fprintf(stderr, " (n=%zu)\n", rows[0].second.size());
+    std::fprintf(stderr, "[tsg] prof p90/p99/max us:");
+    for (auto &r : rows) {
+      const auto &v = r.second;
+      std::fprintf(stderr, " %s=%.1f/%.1f/%.1f(n=%zu)", r.first.c_str(), v[v.size() * 9 / 10], v[v.size() * 99 / 100],
+                   v.back(), v.size());
+    }
+    std::fprintf(stderr, "\n");
   }
 };
 ProfTable &prof_table() {
@@ -457,6 +497,54 @@ ProfTable &prof_table() {
   return t;
 }
 }  // namespace
+int host_threads() {
+  static const int n = [] {
+    int c = int(std::max(1u, std::thread::hardware_concurrency()));
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) c = std::max(1, std::min(c, CPU_COUNT(&set)));
+    // a cgroup CPU quota (cpu.max "quota period"): the CPUs' worth of time this job may use
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {};
+      long long period = 0;
+      if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+        c = std::max(1, std::min(c, int((std::atoll(q) + period - 1) / period)));
+      std::fclose(f);
+    }
+    return c;
+  }();
+  return n;
+}
+
+void parallel_ranges(size_t n, size_t grain, int max_threads, const std::function<void(size_t, size_t)> &f) {
+  if (n == 0) return;
+  const size_t hw = size_t(host_threads());
+  size_t nt = std::min<size_t>({size_t(std::max(1, max_threads)), hw, (n + std::max<size_t>(grain, 1) - 1) /
+                                                                        std::max<size_t>(grain, 1)});
+  if (nt <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::exception_ptr> errs(nt);
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (size_t t = 1; t < nt; t++)
+    th.emplace_back([&, t] {
+      try {
+        f(n * t / nt, n * (t + 1) / nt);
+      } catch (...) {
+        errs[t] = std::current_exception();
+      }
+    });
+  try {
+    f(0, n / nt);
+  } catch (...) {
+    errs[0] = std::current_exception();
+  }
+  for (auto &x : th) x.join();
+  for (auto &e : errs)
+    if (e) std::rethrow_exception(e);
+}
+
 bool prof_on() {
   static const bool on = std::getenv("TSG_PROF") != nullptr;
   return on;

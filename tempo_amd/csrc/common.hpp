@@ -1,10 +1,15 @@
 // common.hpp — shared host utilities of libtsg: byte order, status/errors,
 // hashes used by the on-disk formats, snappy framing (decode + encode).
 #pragma once
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <new>
 #include <stdexcept>
+#include <type_traits>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -91,6 +96,55 @@ std::string go_to_lower(std::string_view s);
 bool read_file(const std::string &path, std::vector<uint8_t> &out);  // false if missing
 void write_file(const std::string &path, const uint8_t *p, size_t n);
 void make_dirs(const std::string &path);
+
+// ---- host parallelism -----------------------------------------------------------
+// CPUs this process may use: its affinity mask, capped by a cgroup CPU quota (a GPU box's
+// job share); std::thread::hardware_concurrency counts the whole machine
+int host_threads();
+// f(lo, hi) over [0, n) split into contiguous ranges of at least `grain` items, on up to
+// max_threads threads (the caller runs the first range). Exceptions: the first is rethrown.
+void parallel_ranges(size_t n, size_t grain, int max_threads, const std::function<void(size_t, size_t)> &f);
+
+// A growable array of trivially copyable T without value-initialisation on resize (a result
+// of millions of records is written once; zero-filling it first would be a second pass).
+template <class T>
+struct RawVec {
+  static_assert(std::is_trivially_copyable<T>::value, "RawVec holds plain data");
+  T *p = nullptr;
+  size_t n = 0, cap = 0;
+  RawVec() = default;
+  RawVec(const RawVec &) = delete;
+  RawVec &operator=(const RawVec &) = delete;
+  ~RawVec() { std::free(p); }
+  void reserve(size_t c) {
+    if (c <= cap) return;
+    T *q = static_cast<T *>(std::realloc(p, c * sizeof(T)));
+    if (!q) throw std::bad_alloc();
+    p = q;
+    cap = c;
+  }
+  void resize(size_t m) {
+    if (m > cap) reserve(std::max(m, cap * 2));
+    n = m;
+  }
+  void assign(size_t m, const T &v) {
+    resize(m);
+    for (size_t i = 0; i < m; i++) p[i] = v;
+  }
+  void push_back(const T &v) {
+    if (n == cap) reserve(std::max<size_t>(16, cap * 2));
+    p[n++] = v;
+  }
+  void clear() { n = 0; }
+  size_t size() const { return n; }
+  size_t capacity() const { return cap; }
+  bool empty() const { return n == 0; }
+  T *data() { return p; }
+  const T *data() const { return p; }
+  T &operator[](size_t i) { return p[i]; }
+  const T &operator[](size_t i) const { return p[i]; }
+  T &back() { return p[n - 1]; }
+};
 
 // backend.Encoding names (tempodb/backend/encoding.go:40-62)
 int parse_encoding(std::string_view s);

@@ -121,6 +121,7 @@ void block_free(Block &b);
 
 struct SearchOut {
   struct Rec {
+    Rec() {}  // (not zero-filled: record arrays are resized to millions, then written once)
     uint8_t id[16];
     uint64_t start, end;
     uint32_t entry;

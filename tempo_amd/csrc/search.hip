@@ -2454,7 +2454,11 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     if (!climit && fast && total <= 64) dc.seg_cap = 16;  // sparse again: back to segment mode
     nrec = total;
     out.recs.resize(total);
-    if (total) std::memcpy(out.recs.data(), P.out + P.hdr_bytes, total * sizeof(MatchRec));
+    // (a dense result is tens of MB of pinned memory: copied on several threads)
+    if (total)
+      parallel_ranges(size_t(total) * sizeof(MatchRec), size_t(8) << 20, 16, [&](size_t lo, size_t hi) {
+        std::memcpy(reinterpret_cast<uint8_t *>(out.recs.data()) + lo, P.out + P.hdr_bytes + lo, hi - lo);
+      });
     for (size_t i = 0; i < segs.size(); i++) {
       uint64_t c;
       std::memcpy(&c, P.out + 64 + 8 * i, 8);
