@@ -1197,6 +1197,19 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
   canonicalize_narrow_keys(hb);
   const auto tc1 = clk::now();
   verify_header_dicts(hb, nthreads);
+  // byte-pair counts of the large dictionaries: 64 windows of 16 KiB spread over the bytes
+  for_each_index(hb.keys.size(), nthreads, [&](size_t k) {
+    KeyColumn &kc = hb.keys[k];
+    const size_t nb = kc.dict_bytes.size();
+    if (nb <= kDeferMinBytes) return;
+    kc.pair_freq.assign(65536, 0);
+    constexpr size_t kWin = 16384, kWins = 64;
+    for (size_t w = 0; w < kWins; w++) {
+      const size_t a = (nb - kWin) / (kWins - 1) * w;
+      const uint8_t *p = kc.dict_bytes.data() + a;
+      for (size_t i = 0; i + 1 < kWin; i++) kc.pair_freq[(uint32_t(p[i]) << 8) | p[i + 1]]++;
+    }
+  });
   if (prof) {
     prof_add("load.canon", std::chrono::duration<double, std::micro>(tc1 - tc0).count());
     prof_add("load.verify", std::chrono::duration<double, std::micro>(clk::now() - tc1).count());

@@ -120,6 +120,9 @@ struct KeyColumn {
   std::vector<uint32_t> set_vals;  // value ids, in vector order (descending bytes)
   bool identity = true;            // every set is {v} with set id == value id
   std::vector<uint32_t> col;       // per entry: set id or kNone (key absent)
+  // large dictionaries (> kDeferMinBytes): counts of each adjacent byte pair (b0 << 8 | b1) in
+  // a sample of the value bytes; the dictionary stream pass tests a needle's rarest pair
+  std::vector<uint32_t> pair_freq;
   uint32_t nvals() const { return uint32_t(dict_off.size() - 1); }
   uint32_t nsets() const { return uint32_t(set_off.size() - 1); }
   int width() const { return nsets() < 255 ? 1 : (nsets() < 65535 ? 2 : 4); }

@@ -1062,7 +1062,7 @@ struct IdSet {
 static void fill_records_parallel(ResultHolder &res, tsg_block *const *blocks,
                                   const std::vector<std::pair<const SearchOut::Rec *, size_t>> &per_block,
                                   const std::vector<size_t> &obase, size_t nout) {
-  const size_t hw = size_t(host_threads());
+  const size_t hw = size_t(host_threads_now());
   const size_t nt = std::max<size_t>(1, std::min<size_t>({16, hw, nout / 32768}));
   struct Local {
     std::vector<ResultHolder::InternSlot> tab;
@@ -1098,6 +1098,13 @@ static void fill_records_parallel(ResultHolder &res, tsg_block *const *blocks,
     }
   };
   std::vector<Local> loc(nt);
+  // a name's arena offset by its dictionary value id, per thread and block, where the block's
+  // names are few next to its records (an array index instead of a hash probe per name)
+  auto dense_ok = [&](size_t i, int key) {
+    if (key < 0) return false;
+    const uint64_t recs = obase[i + 1] - obase[i];
+    return uint64_t(blocks[i]->b.host->keys[size_t(key)].nvals()) * 4 <= recs / nt + 1024;
+  };
   auto range = [&](size_t t, size_t &o0, size_t &o1) {
     o0 = nout * t / nt;
     o1 = nout * (t + 1) / nt;
@@ -1109,9 +1116,25 @@ static void fill_records_parallel(ResultHolder &res, tsg_block *const *blocks,
       if (o0 >= o1) continue;
       Local &L = loc[t];
       size_t i = size_t(std::upper_bound(obase.begin(), obase.end(), o0) - obase.begin()) - 1;
+      std::vector<uint64_t> dsvc, dname;  // value id -> arena offset + 1 (0: not yet), this block
+      size_t dblock = ~size_t(0);
+      bool dsv = false, dnm = false;
+      auto name_off = [&](std::vector<uint64_t> &dense, bool use, uint32_t vid, std::string_view v) -> uint64_t {
+        if (!use) return L.get(v.data(), v.size());
+        uint64_t &x = dense[vid];
+        if (!x) x = L.get(v.data(), v.size()) + 1;
+        return x - 1;
+      };
       for (size_t o = o0; o < o1; o++) {
         while (o >= obase[i + 1]) i++;
         const HostBlock &h = *blocks[i]->b.host;
+        if (i != dblock) {
+          dblock = i;
+          dsv = dense_ok(i, h.svc_key);
+          dnm = dense_ok(i, h.name_key);
+          if (dsv) dsvc.assign(h.keys[size_t(h.svc_key)].nvals(), 0);
+          if (dnm) dname.assign(h.keys[size_t(h.name_key)].nvals(), 0);
+        }
         const SearchOut::Rec *r = per_block[i].first + (o - obase[i]);
         std::memcpy(&res.ids[16 * o], r->id, 16);
         res.id_len[o] = uint8_t(r->block_il >> 24);
@@ -1124,9 +1147,9 @@ static void fill_records_parallel(ResultHolder &res, tsg_block *const *blocks,
         if (h.svc_key >= 0 && r->svc != kNone) sv = h.dict_value(h.svc_key, r->svc);
         if (h.name_key >= 0 && r->name != kNone) nm = h.dict_value(h.name_key, r->name);
         res.svc_len[o] = uint32_t(sv.size());
-        res.svc_off[o] = sv.empty() ? 0 : L.get(sv.data(), sv.size());
+        res.svc_off[o] = sv.empty() ? 0 : name_off(dsvc, dsv, r->svc, sv);
         res.name_len[o] = uint32_t(nm.size());
-        res.name_off[o] = nm.empty() ? 0 : L.get(nm.data(), nm.size());
+        res.name_off[o] = nm.empty() ? 0 : name_off(dname, dnm, r->name, nm);
       }
     }
   });
@@ -1275,7 +1298,8 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       if (!per_dev.empty()) ctx->fan_out(per_dev.size(), [&](size_t i) { return per_dev[i].first; }, work);
       // per block match lists in scan order (each device's records are grouped by block already)
       uint64_t wave_k = 0, wave_s = 0;  // devices run concurrently: a wave takes its slowest
-      for (SearchOut *o : slots) {
+      for (size_t d = 0; d < slots.size(); d++) {
+        SearchOut *o = slots[d];
         note_any(*o);
         m.device_bytes_read += o->device_bytes;
         m.reruns += o->reruns;
@@ -1283,6 +1307,22 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         wave_s = std::max<uint64_t>(wave_s, o->scan_ns);
         m.scan_bytes += o->scan_bytes;
         const auto &recs = o->recs;
+        // the device's per-block counts (its list order = record order) when they describe
+        // these records; otherwise one pass over the records' block indices
+        const auto &list = per_dev[d].second;
+        if (o->block_counts.size() == list.size()) {
+          uint64_t sum = 0;
+          for (uint64_t c : o->block_counts) sum += c;
+          if (sum == recs.size()) {
+            size_t r = 0;
+            for (size_t x = 0; x < list.size(); x++) {
+              if (o->block_counts[x]) per_block[list[x].first] = {recs.data() + r, size_t(o->block_counts[x])};
+              r += size_t(o->block_counts[x]);
+            }
+            nrec += recs.size();
+            continue;
+          }
+        }
         for (size_t r = 0; r < recs.size();) {
           const uint32_t bi = recs[r].block_il & 0xffffffu;
           size_t e = r;

@@ -515,9 +515,15 @@ int host_threads() {
   return n;
 }
 
+int host_threads_now() {
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof set, &set) == 0) return std::max(1, std::min(host_threads(), CPU_COUNT(&set)));
+  return host_threads();
+}
+
 void parallel_ranges(size_t n, size_t grain, int max_threads, const std::function<void(size_t, size_t)> &f) {
   if (n == 0) return;
-  const size_t hw = size_t(host_threads());
+  const size_t hw = size_t(host_threads_now());
   size_t nt = std::min<size_t>({size_t(std::max(1, max_threads)), hw, (n + std::max<size_t>(grain, 1) - 1) /
                                                                         std::max<size_t>(grain, 1)});
   if (nt <= 1) {

@@ -101,6 +101,8 @@ void make_dirs(const std::string &path);
 // CPUs this process may use: its affinity mask, capped by a cgroup CPU quota (a GPU box's
 // job share); std::thread::hardware_concurrency counts the whole machine
 int host_threads();
+// the same, for the calling thread's current affinity (a caller pinned to a few CPUs)
+int host_threads_now();
 // f(lo, hi) over [0, n) split into contiguous ranges of at least `grain` items, on up to
 // max_threads threads (the caller runs the first range). Exceptions: the first is rethrown.
 void parallel_ranges(size_t n, size_t grain, int max_threads, const std::function<void(size_t, size_t)> &f);

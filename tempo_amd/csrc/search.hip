@@ -241,8 +241,13 @@ struct StreamJob {
   uint32_t lead, nvals;
   uint32_t needle_off, needle_len;
   uint32_t vmatch_base, wave0;  // match bytes (32-aligned); first wave of this job
+  // a second byte pair of the needle tested in registers beside its first two bytes: needle
+  // bytes [pj, pj + 1], 2 <= pj <= min(len - 2, kStreamPairMax); 0 = none (the host picks
+  // the pair that is rarest in the key's values: most steps then hold no candidate at all)
+  uint32_t pj, pad[3];
 };
-static_assert(sizeof(StreamJob) == 48, "StreamJob layout");
+static_assert(sizeof(StreamJob) == 64, "StreamJob layout");
+constexpr uint32_t kStreamPairMax = 11;  // its bytes of a lane's 16 starts lie in this lane's + the next lane's 16
 
 // bit 7 of each byte of the result: that byte of x is non-zero (exact, no carries across bytes)
 __device__ __forceinline__ uint32_t nz_bytes(uint32_t x) { return (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u; }
@@ -307,6 +312,10 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
   }
   const uint32_t n0 = uint32_t(needles[J.needle_off]) * 0x01010101u;
   const uint32_t n1 = nl > 1 ? uint32_t(needles[J.needle_off + 1]) * 0x01010101u : 0u;
+  const uint32_t pj = J.pj;  // (wave-uniform)
+  const uint32_t r0 = pj ? uint32_t(needles[J.needle_off + pj]) * 0x01010101u : 0u;
+  const uint32_t r1 = pj ? uint32_t(needles[J.needle_off + pj + 1]) * 0x01010101u : 0u;
+  const uint32_t pq = pj >> 2, ps = pj & 3u;
   // a: aligned coordinate of this lane's 16 bytes. Past the stream's last 16-byte chunk
   // the load repeats that chunk: bytes past `end` only ever form starts >= qhi (dropped) and
   // are never compared, and an unconditional load keeps the compiler's waits exact (a
@@ -342,12 +351,42 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     uint32_t nxw = uint32_t(__builtin_amdgcn_update_dpp(0, int(cur.x), 0x130, 0xf, 0xf, false));  // wave_shl:1
     if (lane == 63) nxw = nx0;
     const uint32_t d[5] = {cur.x, cur.y, cur.z, cur.w, nxw};
-    uint32_t cw[4], any = 0;
+    uint32_t nzs[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       uint32_t nz = nz_bytes(d[k] ^ n0);
       if (nl > 1) nz |= nz_bytes(__builtin_amdgcn_alignbyte(d[k + 1], d[k], 1) ^ n1);
-      cw[k] = nz ^ 0x80808080u;  // bit 7 of a byte: a candidate start
+      nzs[k] = nz;
+    }
+    if (pj) {
+      // the second pair: bytes pj, pj + 1 after each start, from this lane's 16 bytes and the
+      // next lane's (DPP; lane 63: the next KiB's first lane). V[m] = window bytes pj + 4m ..
+      const uint32_t ny = uint32_t(__builtin_amdgcn_update_dpp(0, int(cur.y), 0x130, 0xf, 0xf, false));
+      const uint32_t nzw = uint32_t(__builtin_amdgcn_update_dpp(0, int(cur.z), 0x130, 0xf, 0xf, false));
+      const uint32_t nww = uint32_t(__builtin_amdgcn_update_dpp(0, int(cur.w), 0x130, 0xf, 0xf, false));
+      const uint32_t W[8] = {cur.x, cur.y, cur.z, cur.w, nxw,
+                             lane == 63 ? __builtin_amdgcn_readlane(nxt.y, 0) : ny,
+                             lane == 63 ? __builtin_amdgcn_readlane(nxt.z, 0) : nzw,
+                             lane == 63 ? __builtin_amdgcn_readlane(nxt.w, 0) : nww};
+      uint32_t V[5];
+      if (pq == 0) {
+#pragma unroll
+        for (int m = 0; m < 5; m++) V[m] = __builtin_amdgcn_alignbyte(W[m + 1], W[m], ps);
+      } else if (pq == 1) {
+#pragma unroll
+        for (int m = 0; m < 5; m++) V[m] = __builtin_amdgcn_alignbyte(W[m + 2], W[m + 1], ps);
+      } else {
+#pragma unroll
+        for (int m = 0; m < 5; m++) V[m] = __builtin_amdgcn_alignbyte(W[m + 3], W[m + 2], ps);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        nzs[k] |= nz_bytes(V[k] ^ r0) | nz_bytes(__builtin_amdgcn_alignbyte(V[k + 1], V[k], 1) ^ r1);
+    }
+    uint32_t cw[4], any = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      cw[k] = nzs[k] ^ 0x80808080u;  // bit 7 of a byte: a candidate start
       any |= cw[k];
     }
     // most steps hold no candidate in any lane: nothing else to do (a wave-uniform branch)
@@ -1789,6 +1828,24 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
         sj.needle_off = needle_off[t];
         sj.needle_len = q.value_lens[t];
         sj.vmatch_base = jb.vmatch_base;
+        // the second byte pair tested in registers: the needle's rarest in the key's values
+        // (sampled at open), else its last pair within reach
+        if (q.value_lens[t] >= 4) {
+          const uint8_t *nd = q.values[t];
+          const uint32_t hi = std::min<uint32_t>(q.value_lens[t] - 2, kStreamPairMax);
+          const auto &pf = b.host->keys[size_t(kidx[t])].pair_freq;
+          sj.pj = hi;
+          if (pf.size() == 65536) {
+            uint32_t best = UINT32_MAX;
+            for (uint32_t j = 2; j <= hi; j++) {
+              const uint32_t f = pf[(uint32_t(nd[j]) << 8) | nd[j + 1]];
+              if (f < best) {
+                best = f;
+                sj.pj = j;
+              }
+            }
+          }
+        }
         stream_jobs.push_back(sj);  // (wave0: after the plan, once the span is known)
       } else if (!k.identity) {
         jb.vmatch_base = vmatch_total;
