@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define TSG_ABI_VERSION 4
+#define TSG_ABI_VERSION 5
 
 /* Status codes. */
 #define TSG_OK 0
@@ -173,6 +173,14 @@ typedef struct tsg_search_opts {
                         for an id whose search finished recently is ignored (it cannot fail a later
                         search that reuses the id); one for an id not seen yet waits up to 10 s for
                         its search to start. */
+  /* ABI 5: trace IDs the caller's consumer has already taken (16 bytes each, right-aligned
+     like tsg_result.trace_id), counted toward `limit` as if they had been consumed first:
+     the search stops where a consumer that saw them before this call's blocks stops. A
+     querier fanning blocks out over ranks (modules/frontend/searchsharding.go:88-106,
+     tempo_amd/shard.py distributed_search_limit) passes the distinct IDs of the blocks
+     before this rank's. NULL / 0 = none. */
+  const uint8_t (*seen_ids)[16];
+  uint64_t nseen;
 } tsg_search_opts;
 
 /* ---- context --------------------------------------------------------------- */

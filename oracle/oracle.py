@@ -67,6 +67,8 @@ def lib():
         L.orc_block_free.argtypes = [vp]
         L.orc_block_bytes.argtypes = [vp]
         L.orc_block_bytes.restype = C.c_uint64
+        L.orc_search_seeded.argtypes = [C.POINTER(vp), C.c_uint32, C.POINTER(Request), C.c_uint32, C.c_void_p,
+                                        C.c_uint64, C.POINTER(C.POINTER(Result))]
         L.orc_search.argtypes = [C.POINTER(vp), C.c_uint32, C.POINTER(Request), C.c_uint32, C.c_int,
                                  C.POINTER(C.POINTER(Result))]
         L.orc_combine.argtypes = [C.POINTER(Result), C.c_uint32, C.POINTER(C.POINTER(Result))]
@@ -239,12 +241,18 @@ def _unpack(res):
     return out, met, r.status
 
 
-def search(blocks, tags=None, min_ms=0, max_ms=0, start=0, end=0, limit=0, nthreads=1, combine=None):
-    """BackendSearchBlock.Search over blocks (oracle). Returns (matches, metrics, status)."""
+def search(blocks, tags=None, min_ms=0, max_ms=0, start=0, end=0, limit=0, nthreads=1, combine=None, seen=None):
+    """BackendSearchBlock.Search over blocks (oracle). Returns (matches, metrics, status).
+    seen: trace IDs ((n, 16) uint8) a consumer took before these blocks (orc_search_seeded)."""
     req = make_request(tags, min_ms, max_ms, start, end, limit)
     arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
     res = C.POINTER(Result)()
-    lib().orc_search(arr, len(blocks), C.byref(req), limit, nthreads, C.byref(res))
+    if seen is not None and len(seen):
+        import numpy as np
+        sa = np.ascontiguousarray(seen, dtype=np.uint8).reshape(-1, 16)
+        lib().orc_search_seeded(arr, len(blocks), C.byref(req), limit, sa.ctypes.data, sa.shape[0], C.byref(res))
+    else:
+        lib().orc_search(arr, len(blocks), C.byref(req), limit, nthreads, C.byref(res))
     try:
         if combine is not None:
             fin = C.POINTER(Result)()

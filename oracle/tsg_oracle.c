@@ -1119,6 +1119,8 @@ static void finish(mlist *l, orc_result **out) {
   *out = r;
 }
 
+int orc_search_seeded(orc_block *const *blocks, uint32_t nblocks, const orc_request *req, uint32_t limit,
+                      const uint8_t (*seen)[16], uint64_t nseen, orc_result **out);
 int orc_search(orc_block *const *blocks, uint32_t nblocks, const orc_request *req, uint32_t limit,
                int nthreads, orc_result **out) {
   orc_pipeline p;
@@ -1174,6 +1176,36 @@ int orc_search(orc_block *const *blocks, uint32_t nblocks, const orc_request *re
     free(lc.ids.k);
     free(lc.ids.used);
   }
+  pipeline_free(&p);
+  finish(&all, out);
+  return ORC_OK;
+}
+
+/* The sequential consumer of instance.Search (instance_search.go:45-60) whose id map already
+ * holds `seen` (the distinct trace IDs a consumer took from blocks before these): it stops
+ * where that consumer, having taken them first, would stop. The rank fan-out of a limit
+ * search (tempo_amd/shard.py distributed_search_limit) is checked against it. */
+int orc_search_seeded(orc_block *const *blocks, uint32_t nblocks, const orc_request *req, uint32_t limit,
+                      const uint8_t (*seen)[16], uint64_t nseen, orc_result **out) {
+  orc_pipeline p;
+  pipeline_new(req, &p);
+  mlist all;
+  memset(&all, 0, sizeof all);
+  all.nb = nblocks;
+  all.bstat = (int32_t *)calloc(nblocks + 1, sizeof(int32_t));
+  limit_ctx lc;
+  memset(&lc, 0, sizeof lc);
+  lc.limit = limit;
+  for (uint64_t i = 0; i < nseen; i++)
+    if (idset_add(&lc.ids, seen[i])) lc.distinct++;
+  int quit = limit && lc.distinct >= limit;
+  for (uint32_t i = 0; i < nblocks && !quit; i++) {
+    int rc = block_search(blocks[i], i, &p, &all, limit ? limit_consume : NULL, &lc, &quit);
+    if (rc && !all.status) all.status = rc;
+    all.bstat[i] = rc;
+  }
+  free(lc.ids.k);
+  free(lc.ids.used);
   pipeline_free(&p);
   finish(&all, out);
   return ORC_OK;

@@ -89,6 +89,8 @@ uint64_t orc_block_bytes(const orc_block *b);
 /* BackendSearchBlock.Search over blocks in order, consumer = deterministic
  * refinement of instance.Search (limit 0 = every match). nthreads > 1 runs
  * one thread per block (only valid with limit 0; same result). */
+int orc_search_seeded(orc_block *const *blocks, uint32_t nblocks, const orc_request *req, uint32_t limit,
+                      const uint8_t (*seen)[16], uint64_t nseen, orc_result **out);
 int orc_search(orc_block *const *blocks, uint32_t nblocks, const orc_request *req, uint32_t limit,
                int nthreads, orc_result **out);
 int orc_combine(const orc_result *in, uint32_t max_results, orc_result **out);

@@ -1408,7 +1408,13 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     uint64_t inspect_entries = 0;
     for (size_t i = 0; i < nblocks; i++)
       if (state[i] == 2 && blocks[i]->b.dc && !blocks[i]->b.host->live) inspect_entries += blocks[i]->b.host->n;
-    if (limit && (any_live || inspect_entries > kWave0)) {
+    // IDs the caller's consumer took before these blocks (tsg_search_opts.seen_ids)
+    const uint8_t(*seen)[16] = opts && opts->nseen ? opts->seen_ids : nullptr;
+    const uint64_t nseen = seen ? opts->nseen : 0;
+    auto seed = [&](IdSet &ids) {
+      for (uint64_t i = 0; i < nseen; i++) ids.insert(seen[i]);
+    };
+    if (limit && (any_live || inspect_entries > kWave0 || nseen)) {
       thread_local std::vector<std::vector<SearchOut::Rec>> acc;  // per block: its records so far
       if (acc.size() < nblocks) acc.resize(nblocks);
       for (size_t i = 0; i < nblocks; i++) acc[i].clear();
@@ -1423,7 +1429,8 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       approach.leave();
       thread_local IdSet distinct_w;
       distinct_w.clear();
-      bool stop = false, cut_ok = true;
+      seed(distinct_w);
+      bool stop = distinct_w.size() >= limit, cut_ok = true;
       size_t cb = 0;     // cursor: next block ...
       uint64_t ce = 0;   // ... and its next scan position
       uint64_t wave = kWave0, scanned = 0, matched = 0;
@@ -1598,7 +1605,8 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     // consume in caller block order (deterministic refinement of instance.Search)
     thread_local IdSet distinct;
     distinct.clear();
-    bool stopped = false;
+    seed(distinct);
+    bool stopped = limit && distinct.size() >= limit;
     for (size_t i = 0; i < nblocks && !stopped && !par; i++) {
       const HostBlock &h = *blocks[i]->b.host;
       if (state[i] == 0) continue;  // meta missing: no-op (backend_search_block.go:191-203)

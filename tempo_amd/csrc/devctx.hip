@@ -54,12 +54,14 @@ void ctx_shutdown(Ctx &c) {
     (void)hipStreamSynchronize(dc->stream);
     for (DevBuf *b : {&dc->desc, &dc->vmatch, &dc->bitmaps, &dc->gran, &dc->ticket, &dc->out, &dc->regions,
                       &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps, &dc->gbm, &dc->lkhits,
-                      &dc->done, &dc->steal, &dc->fpages, &dc->fhits, &dc->fres, &dc->farena, &dc->fcrc, &dc->fdst, &dc->foff})
+                      &dc->done, &dc->steal, &dc->fpages, &dc->fhits, &dc->fres, &dc->farena, &dc->fcrc, &dc->fdst, &dc->foff,
+                      &dc->danyf, &dc->pool_head, &dc->lkslab, &dc->lkslabdesc, &dc->pbm, &dc->pout})
       b->release();
     for (hipEvent_t e : dc->tring) (void)hipEventDestroy(e);
     dc->hdesc.release();
     dc->hout.release();
     dc->hres.release();
+    dc->hany.release();
     (void)hipEventDestroy(dc->ev0);
     (void)hipEventDestroy(dc->ev1);
     (void)hipEventDestroy(dc->es0);

@@ -102,8 +102,9 @@ struct DeviceCtx {
   // stores go over the fabric, visible to the host once the stream is synchronised)
   HostBuf hres{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};
   // per dictionary job of a general-path search: 1 once some value of it matched (prep /
-  // dict_sets kernels, system-scope stores; read after the stream synchronises)
+  // dict_sets kernels set danyf in device memory; one copy here; read after the sync)
   HostBuf hany{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};
+  DevBuf danyf;  // (the device-side flags hany is copied from)
   unsigned long long epoch = 0, ticket_base = 0;  // lookup launches
   uint32_t search_epoch = 0;
   bool fast_off = std::getenv("TSG_NO_FAST") != nullptr;  // force the general (prep + search) path

@@ -167,7 +167,7 @@ extern "C" __global__ void __launch_bounds__(256) prep_kernel(const uint8_t *src
     const uint32_t words = (jb.nsets + 31) >> 5;
     if (lane == 0 && w0 < words) bitmaps[jb.bm_base + w0] = uint32_t(b);
     if (lane == 32 && w0 + 1 < words) bitmaps[jb.bm_base + w0 + 1] = uint32_t(b >> 32);
-    if (lane == 0 && b != 0) host_store(anyf + lo, 1u);  // (some value of the job matched)
+    if (lane == 0 && b != 0) anyf[lo] = 1u;  // (some value of the job matched; device memory)
   } else if (v < jb.nvals) {
     vmatch[jb.vmatch_base + v] = m ? 1 : 0;
   }
@@ -199,7 +199,7 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
       word |= ((x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u)) << (4 * k);
     }
     bitmaps[jb.bm_base + w] = word;
-    if (word) host_store(anyf + set_jobs[lo], 1u);
+    if (word) anyf[set_jobs[lo]] = 1u;
     return;
   }
   for (uint32_t b = 0; b < 32; b++) {
@@ -212,7 +212,7 @@ extern "C" __global__ void __launch_bounds__(256) dict_sets_kernel(const DictJob
       }
   }
   bitmaps[jb.bm_base + w] = word;
-  if (word) host_store(anyf + set_jobs[lo], 1u);
+  if (word) anyf[set_jobs[lo]] = 1u;
 }
 
 // ------------------------------------------------------------------------------------
@@ -351,12 +351,14 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     uint32_t nxw = uint32_t(__builtin_amdgcn_update_dpp(0, int(cur.x), 0x130, 0xf, 0xf, false));  // wave_shl:1
     if (lane == 63) nxw = nx0;
     const uint32_t d[5] = {cur.x, cur.y, cur.z, cur.w, nxw};
-    uint32_t nzs[4];
+    // x[k]: a byte is zero where every tested needle byte matches at that start (the xors of
+    // the pairs OR-ed together: one zero-byte test per dword for all of them)
+    uint32_t xs[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      uint32_t nz = nz_bytes(d[k] ^ n0);
-      if (nl > 1) nz |= nz_bytes(__builtin_amdgcn_alignbyte(d[k + 1], d[k], 1) ^ n1);
-      nzs[k] = nz;
+      uint32_t x = d[k] ^ n0;
+      if (nl > 1) x |= __builtin_amdgcn_alignbyte(d[k + 1], d[k], 1) ^ n1;
+      xs[k] = x;
     }
     if (pj) {
       // the second pair: bytes pj, pj + 1 after each start, from this lane's 16 bytes and the
@@ -380,13 +382,12 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
         for (int m = 0; m < 5; m++) V[m] = __builtin_amdgcn_alignbyte(W[m + 3], W[m + 2], ps);
       }
 #pragma unroll
-      for (int k = 0; k < 4; k++)
-        nzs[k] |= nz_bytes(V[k] ^ r0) | nz_bytes(__builtin_amdgcn_alignbyte(V[k + 1], V[k], 1) ^ r1);
+      for (int k = 0; k < 4; k++) xs[k] |= (V[k] ^ r0) | (__builtin_amdgcn_alignbyte(V[k + 1], V[k], 1) ^ r1);
     }
     uint32_t cw[4], any = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      cw[k] = nzs[k] ^ 0x80808080u;  // bit 7 of a byte: a candidate start
+      cw[k] = nz_bytes(xs[k]) ^ 0x80808080u;  // bit 7 of a byte: a candidate start
       any |= cw[k];
     }
     // most steps hold no candidate in any lane: nothing else to do (a wave-uniform branch)
@@ -2233,10 +2234,12 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     tr.mark("desc");
     if (time_all) HIP_OK(hipEventRecord(dc.ev0, s));
     if (!stream_jobs.empty()) HIP_OK(hipMemsetAsync(dc.vmatch.p, 0, vmatch_total, s));
-    // (no kernel of this device is in flight: device_search returns after its stream drained)
+    // per job: some value matched (device flags, zeroed here; copied to pinned host memory
+    // after the dictionary kernels: one small copy instead of a host store per matching word)
     dc.hany.ensure(std::max<size_t>(jobs.size(), 1) * 4);
-    std::memset(dc.hany.p, 0, jobs.size() * 4);
-    auto *anyf = static_cast<uint32_t *>(dc.hany.p);
+    dc.danyf.ensure(std::max<size_t>(jobs.size(), 1) * 4);
+    auto *anyf = static_cast<uint32_t *>(dc.danyf.p);
+    if (!jobs.empty()) HIP_OK(hipMemsetAsync(anyf, 0, jobs.size() * 4, s));
     prep_kernel<<<std::max<uint32_t>(1, (items + 255) / 256), 256, 0, s>>>(
         src, dd, uint32_t(total_desc / 16), uint32_t(o_jobs), uint32_t(o_jb), uint32_t(jobs.size()), items,
         uint32_t(o_nd), uint32_t(needles.size()), static_cast<uint8_t *>(dc.vmatch.p),
@@ -2250,6 +2253,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
           reinterpret_cast<const DictJob *>(dd + o_jobs), reinterpret_cast<const uint32_t *>(dd + o_sj),
           reinterpret_cast<const uint32_t *>(dd + o_sp), uint32_t(set_jobs.size()), set_items.back(),
           static_cast<const uint8_t *>(dc.vmatch.p), static_cast<uint32_t *>(dc.bitmaps.p), anyf);
+    if (!jobs.empty()) HIP_OK(hipMemcpyAsync(dc.hany.p, anyf, jobs.size() * 4, hipMemcpyDeviceToHost, s));
     P.segs = reinterpret_cast<const ScanSeg *>(dd + o_segs);
     P.terms = reinterpret_cast<const ScanTerm *>(dd + o_terms);
     P.wg_seg = reinterpret_cast<const uint16_t *>(dd + o_ws);

@@ -321,3 +321,194 @@ def distributed_lookup(lookup_local: Callable[[object], object], ids, device=Non
     if rank != dst:
         return None
     return np.concatenate([np.frombuffer(g[0].tobytes(), dtype=np.int64).reshape(-1, 5) for g in got])
+
+
+# ---------------------------------------------------------------------------
+# limit queries over ranks: the consumer's early exit across the block shards
+
+def _distinct_in_order(resp: Response) -> np.ndarray:
+    """The response's trace IDs, each once, in first-occurrence order ((k, 16) uint8)."""
+    if len(resp.recs) == 0:
+        return np.zeros((0, 16), np.uint8)
+    ids = np.ascontiguousarray(resp.recs["trace_id"]).view(np.uint8).reshape(-1, 16)
+    _, first = np.unique(ids, axis=0, return_index=True)
+    return ids[np.sort(first)]
+
+
+def concat_responses(resps: Sequence[Response]) -> Response:
+    """Responses of consecutive block ranges as one: records one after another (names
+    re-indexed into one table), metrics summed, block statuses concatenated."""
+    recs, offs, names, st, errs = [], [np.zeros(1, np.uint32)], [], [], []
+    nn = nb = 0
+    m = SearchMetrics(0, 0, 0, 0)
+    for r in resps:
+        x = np.array(r.recs, copy=True)
+        x["root_service"] += nn
+        x["root_name"] += nn
+        recs.append(x)
+        offs.append(np.asarray(r.name_off[1:], np.uint64) + nb)
+        names.append(r.names)
+        nn += len(r.name_off) - 1
+        nb += len(r.names)
+        m.inspected_traces += r.metrics.inspected_traces
+        m.inspected_bytes += r.metrics.inspected_bytes
+        m.inspected_blocks += r.metrics.inspected_blocks
+        m.skipped_blocks += r.metrics.skipped_blocks
+        m.skipped_traces += r.metrics.skipped_traces
+        st.append(np.asarray(r.block_status, np.int32))
+        errs.extend(r.block_errors)
+    status = np.concatenate(st) if st else np.zeros(0, np.int32)
+    m.block_status, m.block_errors = status.tolist(), errs
+    return Response(np.concatenate(recs) if recs else np.zeros(0, REC_DTYPE),
+                    np.concatenate(offs).astype(np.uint32), b"".join(names), m, status, errs)
+
+
+_CTRL_KEEP, _CTRL_SEEDED, _CTRL_DROP = 0, 1, 2
+
+
+def distributed_search_limit(search, cancel, limit: int, group=None, dst: int = 0,
+                             query_id: int = 0) -> Optional[Response]:
+    """A limit-L search over block shards (rank r holds the r-th range of the query's blocks,
+    in block order) that returns on `dst` exactly what one consumer over all blocks in order
+    returns — instance.Search's consumer (instance_search.go:45-60) stopping at the L-th
+    distinct trace ID, records in order, metrics of the blocks and pages it reached — while
+    later ranks stop early (ranks publish what they matched, the host finds
+    the prefix that holds L distinct IDs, the rest is cancelled; the frontend's shouldQuit,
+    modules/frontend/searchsharding.go:88-106).
+
+    search(seen, qid) -> wire: this rank's tsg_search over its blocks with limit L (e.g.
+    Engine.search_wire(blocks, pipe, limit=L, query_id=qid, seen=seen)); seen = trace IDs
+    taken before these blocks, or None. cancel(qid): Engine.cancel.
+
+    1. Every rank searches its shard with limit L at once (its own early exit).
+    2. `dst` takes the ranks' reports in rank order and runs the consumer over their
+       distinct IDs. Ranks before the one where it reaches L keep their result (they did not
+       reach L alone, so they hold every match); that rank (r*) searches again with the IDs
+       before it as `seen` (unless none), stopping exactly where the single consumer stops;
+       ranks after it are told to drop, cancelling a search still running (tsg_cancel).
+    3. The kept responses are gathered to `dst` and concatenated in rank order.
+    Messages are point-to-point over `group` (gloo: host tensors)."""
+    import threading
+
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    gdst = dst if group is None else dist.get_global_rank(group, dst)
+
+    def grank(r):
+        return r if group is None else dist.get_global_rank(group, r)
+
+    def send_ids(ids, to):
+        dist.send(torch.tensor([len(ids)], dtype=torch.int64), grank(to), group=group)
+        if len(ids):
+            dist.send(torch.from_numpy(np.ascontiguousarray(ids, np.uint8)), grank(to), group=group)
+
+    def recv_ids(frm):
+        n = torch.zeros(1, dtype=torch.int64)
+        dist.recv(n, grank(frm), group=group)
+        ids = torch.zeros((int(n.item()), 16), dtype=torch.uint8)
+        if int(n.item()):
+            dist.recv(ids, grank(frm), group=group)
+        return ids.numpy()
+
+    def send_wire(w, to):
+        a = np.ascontiguousarray(w, np.uint8) if w is not None else np.zeros(0, np.uint8)
+        dist.send(torch.tensor([a.size], dtype=torch.int64), grank(to), group=group)
+        if a.size:
+            dist.send(torch.from_numpy(a), grank(to), group=group)
+
+    def recv_wire(frm):
+        n = torch.zeros(1, dtype=torch.int64)
+        dist.recv(n, grank(frm), group=group)
+        if not int(n.item()):
+            return None
+        a = torch.zeros(int(n.item()), dtype=torch.uint8)
+        dist.recv(a, grank(frm), group=group)
+        return a.numpy()
+
+    # 1. this rank's speculative search (a worker thread, so a drop can cancel it)
+    box = {}
+
+    def work():
+        try:
+            box["wire"] = _wire_of(search(None, query_id))
+        except TsgError as e:
+            box["err"] = e
+
+    if rank != dst:
+        ctrl = torch.full((1,), -1, dtype=torch.int64)
+        creq = dist.irecv(ctrl, gdst, group=group)
+        th = threading.Thread(target=work, daemon=True)
+        th.start()
+        # the control message can come while the search runs: a drop cancels it
+        got_ctrl = threading.Event()
+
+        def watch():
+            creq.wait()
+            got_ctrl.set()
+            if int(ctrl.item()) == _CTRL_DROP and query_id and th.is_alive():
+                cancel(query_id)
+        wt = threading.Thread(target=watch, daemon=True)
+        wt.start()
+        th.join()
+        dropped = got_ctrl.is_set() and int(ctrl.item()) == _CTRL_DROP
+        if "err" in box and not (box["err"].code == 5 and dropped):  # (TSG_E_CANCELLED after a drop)
+            raise box["err"]
+        wire = box.get("wire")
+        # report: the distinct IDs of this rank's result, in order (empty after a drop)
+        send_ids(_distinct_in_order(from_wire(wire)) if wire is not None else np.zeros((0, 16), np.uint8), dst)
+        wt.join()
+        code = int(ctrl.item())
+        if code == _CTRL_SEEDED:
+            seen = recv_ids(dst)
+            wire = _wire_of(search(seen, 0))
+        send_wire(wire if code != _CTRL_DROP else None, dst)
+        return None
+
+    # dst: its own search first (its blocks come first when dst = 0), then the reports in order
+    work()
+    if "err" in box:
+        raise box["err"]
+    seen_ids, seen_set = [], set()
+    stop_at = None
+    codes = {}
+    for r in range(world):
+        ids = _distinct_in_order(from_wire(box["wire"])) if r == dst else recv_ids(r)
+        if stop_at is not None:
+            continue  # (a rank past the stop: its report is read and dropped)
+        before = np.array(seen_ids, np.uint8).reshape(-1, 16)
+        reached = False
+        for x in ids:
+            k = x.tobytes()
+            if k not in seen_set:
+                seen_set.add(k)
+                seen_ids.append(x)
+                if len(seen_set) >= limit:
+                    reached = True
+                    break
+        if reached:
+            stop_at = r
+            codes[r] = (_CTRL_SEEDED if len(before) else _CTRL_KEEP, before)
+            for q in range(r + 1, world):
+                codes[q] = (_CTRL_DROP, None)
+                if q != dst:
+                    dist.send(torch.tensor([_CTRL_DROP], dtype=torch.int64), grank(q), group=group)
+        else:
+            codes[r] = (_CTRL_KEEP, None)
+        if r != dst:
+            code = codes[r][0]
+            if code != _CTRL_DROP:
+                dist.send(torch.tensor([code], dtype=torch.int64), grank(r), group=group)
+                if code == _CTRL_SEEDED:
+                    send_ids(codes[r][1], r)
+    # 3. the kept responses, in rank order
+    parts = []
+    for r in range(world):
+        if r == dst:
+            code, before = codes[r]
+            w = box["wire"] if code == _CTRL_KEEP else (_wire_of(search(before, 0)) if code == _CTRL_SEEDED else None)
+        else:
+            w = recv_wire(r)
+        if w is not None:
+            parts.append(from_wire(w))
+    return concat_responses(parts)

@@ -91,7 +91,8 @@ class _Result(C.Structure):
 
 
 class _SearchOpts(C.Structure):
-    _fields_ = [("limit", C.c_uint32), ("flags", C.c_uint32), ("query_id", C.c_uint64)]
+    _fields_ = [("limit", C.c_uint32), ("flags", C.c_uint32), ("query_id", C.c_uint64),
+                ("seen_ids", C.c_void_p), ("nseen", C.c_uint64)]
 
 
 class _BlockInfo(C.Structure):
@@ -424,11 +425,14 @@ class Engine:
         return _packed(lib().tsg_search_tag_values, _handles(blocks), len(blocks), key, len(key), max_bytes)
 
     def search(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0, flags: int = 0,
-               query_id: int = 0):
+               query_id: int = 0, seen=None):
         """Ordered match sequence + metrics (tsg_search). flags: SEARCH_TIME_*; query_id
-        (non-zero) makes the search cancellable with Engine.cancel(query_id)."""
+        (non-zero) makes the search cancellable with Engine.cancel(query_id); seen: trace IDs
+        ((n, 16) uint8, right-aligned) a consumer took before these blocks (they count toward
+        the limit)."""
         arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
         opts = _SearchOpts(limit=limit, flags=flags, query_id=query_id)
+        seen_arr = _seen(opts, seen)  # noqa: F841  (kept alive across the call)
         rp = C.POINTER(_Result)()
         _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
         try:
@@ -522,13 +526,14 @@ class Engine:
             lib().tsg_result_free(rp)
 
     def search_wire(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0,
-                    combine: Optional[int] = None, flags: int = 0):
+                    combine: Optional[int] = None, flags: int = 0, query_id: int = 0, seen=None):
         """tsg_search (+ tsg_results_combine when `combine` is set: instance.Search's
         consumer) packed by tsg_result_pack into a wire buffer (numpy uint8): what a rank
         ships to the merging rank (tempo_amd.shard). No per-record Python."""
         import numpy as np
         arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
-        opts = _SearchOpts(limit=limit, flags=flags)
+        opts = _SearchOpts(limit=limit, flags=flags, query_id=query_id)
+        seen_arr = _seen(opts, seen)  # noqa: F841
         rp = C.POINTER(_Result)()
         _check(lib().tsg_search(self.h, arr, len(blocks), pipeline.query, C.byref(opts), C.byref(rp)))
         fin = None
@@ -693,6 +698,17 @@ class Engine:
         if getattr(self, "h", None):
             lib().tsg_shutdown(self.h)
             self.h = None
+
+
+def _seen(opts, seen):
+    """tsg_search_opts.seen_ids / nseen from an (n, 16) uint8 array (returned: keep it alive)."""
+    if seen is None or len(seen) == 0:
+        return None
+    import numpy as np
+    arr = np.ascontiguousarray(seen, dtype=np.uint8).reshape(-1, 16)
+    opts.seen_ids = arr.ctypes.data
+    opts.nseen = arr.shape[0]
+    return arr
 
 
 def _handles(blocks):

@@ -1,0 +1,55 @@
+"""Limit queries over ranks on the GPU: 3 rank processes (torch.distributed.run, gloo), each
+with its own libtsg context on the device and its range of the blocks; shard.
+distributed_search_limit (early exit across ranks: seeded search on the rank where the
+consumer stops, tsg_cancel for later ranks) must return exactly ONE tsg_search(limit=L)
+over all blocks in order — records and metrics (instance_search.go:45-60).
+The CPU version of the protocol (oracle stand-in) is tests/test_shard_limit.py."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+import tempo_amd as T
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def rank_blocks(tmp_path_factory):
+    d = tmp_path_factory.mktemp("lr")
+    paths = []
+    for i in range(6):
+        p = str(d / ("b%d" % i))
+        T.synth_search_block(p, 30_000 + 3_000 * i, seed=610 + i, page_size=64 << 10)
+        paths.append(p)
+    return paths
+
+
+@pytest.mark.parametrize("tags,min_ms,limit", [
+    ({"service.name": "svc-07"}, 0, 20),                                          # stop in rank 0
+    ({"service.name": "svc-07", "http.method": "get", "status.code": "error"}, 10, 60),  # stop in a later rank
+    ({"service.name": "svc-07", "http.method": "get", "status.code": "error"}, 10, 100000),  # no stop
+])
+def test_limit_over_three_ranks(rank_blocks, tmp_path, tags, min_ms, limit):
+    out = str(tmp_path / "r.json")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3", "--master-addr",
+           "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tools", "limit_ranks_check.py"),
+           "--limit", str(limit), "--tags", json.dumps(tags), "--min-ms", str(min_ms), "--out", out,
+           "--blocks", *rank_blocks]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run(cmd, env=env, timeout=150, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.load(open(out))
+    assert res["ok"], res
+    assert res["n"] > 0
