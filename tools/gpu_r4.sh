@@ -10,7 +10,7 @@ ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 0 pass, 1 test failures (no cr
 T="python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider"
 
 if has new; then  # this round's new / changed GPU tests first
-  timeout -k 10 600 $T -m gpu tests/test_gpu_block_filter.py tests/test_gpu_coalesce.py tests/test_gpu_multiproc.py \
+  timeout -k 10 600 $T -m gpu tests/test_gpu_limit_ranks.py tests/test_gpu_block_filter.py tests/test_gpu_coalesce.py tests/test_gpu_multiproc.py \
     tests/test_gpu_configs.py > gpurun_out/pytest_new.log 2>&1
   rc=$?; echo "pytest new rc=$rc"; tail -25 gpurun_out/pytest_new.log
   [ $rc -eq 0 ] || exit $rc

@@ -29,8 +29,7 @@ def main():
     eng = T.Engine(devices=[0])
     try:
         pipe = T.Pipeline(T.SearchRequest(tags=json.loads(a.tags), min_duration_ms=a.min_ms))
-        mine = [eng.open_block(p) for p in a.blocks[shard.shard_range(len(a.blocks), world, rank).start:
-                                                   shard.shard_range(len(a.blocks), world, rank).stop]]
+        mine = [eng.open_block(a.blocks[i]) for i in shard.shard_range(len(a.blocks), world, rank)]
         res = shard.distributed_search_limit(
             lambda seen, qid: eng.search_wire(mine, pipe, limit=a.limit, query_id=qid, seen=seen),
             eng.cancel, a.limit, query_id=7000 + rank)
