@@ -267,6 +267,20 @@ __device__ __forceinline__ uint32_t value_at(const uint32_t *off, uint32_t lo, u
   return lo;
 }
 
+// The ring of the stream kernel is loaded by inline asm and waited for by hand: the compiler's
+// wait insertion drained every load in flight twice per ring turn (at the loop head, and where
+// it copies a scalar through a VGPR whose load was still pending), so the read-ahead was
+// mostly idle. Loads return in issue order, so "all but the newest N" covers the two oldest
+// ring slots whatever other vector memory operations were issued after them.
+__device__ __forceinline__ u32x4 ring_load(const uint8_t *p) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+// slots a (the step's KiB) and b (the next) have arrived; kRing - 2 newer loads may be in flight
+__device__ __forceinline__ void ring_wait4(u32x4 &a, u32x4 &b) { asm volatile("s_waitcnt vmcnt(4)" : "+v"(a), "+v"(b)); }
+__device__ __forceinline__ void ring_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // The dictionary stream kernel runs one wave per workgroup: its LDS hand-offs between lanes
 // need no s_barrier, and __syncthreads()' fence would also wait for every global load in
 // flight (s_waitcnt vmcnt(0)), draining the read-ahead ring at each step. A single wave's LDS
@@ -321,7 +335,7 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
   // are never compared, and an unconditional load keeps the compiler's waits exact (a
   // conditional one makes the zero on the other path wait for the load in flight).
   const uint64_t last16 = (end - 1) & ~uint64_t(15);
-  auto load16 = [&](uint64_t a) -> u32x4 { return *G<u32x4>(J.base + min(a, last16)); };
+  auto load16 = [&](uint64_t a) -> u32x4 { return ring_load(J.base + min(a, last16)); };
   // value offsets of the values around the window: s_off[i] = off[vb + i]
   uint32_t vb = value_at(J.off, 0, J.nvals + 1, qlo - J.lead, lane), kv = 0;
   uint64_t cover = 0;  // starts p < cover map through s_off
@@ -338,6 +352,7 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
   // over the slots so each slot keeps its register (a rotation by moves waits for every
   // in-flight load it moves), and a slot is reloaded right after its step used it.
   constexpr int kRing = kStreamAhead + 2;
+  static_assert(kRing == 6, "ring_wait4: kRing - 2 loads newer than a step's two slots");
   u32x4 ring[kRing];
 #pragma unroll
   for (int k = 0; k < kRing; k++) ring[k] = load16(cq + uint64_t(k) * 1024 + lane * 16);
@@ -366,10 +381,11 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
       const uint32_t ny = uint32_t(__builtin_amdgcn_update_dpp(0, int(cur.y), 0x130, 0xf, 0xf, false));
       const uint32_t nzw = uint32_t(__builtin_amdgcn_update_dpp(0, int(cur.z), 0x130, 0xf, 0xf, false));
       const uint32_t nww = uint32_t(__builtin_amdgcn_update_dpp(0, int(cur.w), 0x130, 0xf, 0xf, false));
-      const uint32_t W[8] = {cur.x, cur.y, cur.z, cur.w, nxw,
-                             lane == 63 ? __builtin_amdgcn_readlane(nxt.y, 0) : ny,
-                             lane == 63 ? __builtin_amdgcn_readlane(nxt.z, 0) : nzw,
-                             lane == 63 ? __builtin_amdgcn_readlane(nxt.w, 0) : nww};
+      // (the readlanes unconditional: a select, not a branch around each)
+      const uint32_t n1y = __builtin_amdgcn_readlane(nxt.y, 0), n1z = __builtin_amdgcn_readlane(nxt.z, 0),
+                     n1w = __builtin_amdgcn_readlane(nxt.w, 0);
+      const bool l63 = lane == 63;
+      const uint32_t W[8] = {cur.x, cur.y, cur.z, cur.w, nxw, l63 ? n1y : ny, l63 ? n1z : nzw, l63 ? n1w : nww};
       uint32_t V[5];
       if (pq == 0) {
 #pragma unroll
@@ -484,10 +500,12 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     for (int st = 0; st < kRing; st++) {
       const uint64_t c = cq + uint64_t(st) * 1024;
       if (c >= qhi) break;
+      ring_wait4(ring[st], ring[(st + 1) % kRing]);
       step(c, ring[st], ring[(st + 1) % kRing]);
       ring[st] = load16(c + uint64_t(kRing) * 1024 + lane * 16);  // (the KiB kRing steps ahead)
     }
   }
+  ring_drain();  // (no load of the ring outlives the wave)
 }
 
 // ------------------------------------------------------------------------------------
