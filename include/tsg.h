@@ -345,9 +345,9 @@ int tsg_result_pack(const tsg_result *r, uint8_t **out, size_t *out_len);
  * InspectedBytes / SkippedBlocks / SkippedTraces; InspectedBlocks = total_blocks (set by the
  * sharder, :221); result sorts by start time descending (ties: first position, a deterministic
  * form of sort.Slice). Block statuses and errors of every response are carried in order. The
- * merged response is written as a wire buffer into the caller's `out` (cap bytes; the sum of
- * the input lengths always suffices): *out_len = its length; TSG_E_INVALID with *out_len = the
- * needed size when cap is too small. Host code, no device needed; parallel over host threads. */
+ * merged response is written as a wire buffer into the caller's `out` (cap bytes; for n >= 1
+ * the sum of the input lengths always suffices, n = 0 needs sizeof(tsg_wire_header) + 8):
+ * *out_len = its length; TSG_E_INVALID with *out_len = the needed size when cap is too small. Host code, no device needed; parallel over host threads. */
 int tsg_wire_merge(const uint8_t *const *wires, const size_t *lens, size_t n, uint64_t limit, uint64_t total_blocks,
                    uint8_t *out, size_t cap, size_t *out_len);
 

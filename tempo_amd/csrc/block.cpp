@@ -261,30 +261,6 @@ void parse_entry(const FbTable &e, const uint8_t *fb, uint32_t fb_base, PagePars
   pp.tag_begin.push_back(uint32_t(pp.tag_kv.size()));
 }
 
-void parse_page(const uint8_t *data, size_t dlen, int enc, const IndexRecord &rec, PageParse &pp) {
-  read_data_page(data, dlen, rec, enc, pp.buf);
-  // object.UnmarshalAndAdvanceBuffer (object.go:82-113): [u32 total][u32 idLen][id][obj]
-  if (pp.buf.size() < 8) fail(TSG_E_CORRUPT, "object header truncated");
-  uint32_t total = le32(pp.buf.data()), il = le32(pp.buf.data() + 4);
-  if (total < 8 || pp.buf.size() - 8 < total - 8 || il > total - 8) fail(TSG_E_CORRUPT, "object out of bounds");
-  const uint8_t *fb = pp.buf.data() + 8 + il;
-  size_t fbn = total - 8 - il;
-  pp.fb_bytes = fbn;
-  FbTable page = FbTable::root(fb, fbn);
-  uint16_t eo = page.field(kPageEntries);
-  pp.nentries = eo ? page.vector_len(eo) : 0;
-  uint32_t es = eo ? page.vector_start(eo) : 0;
-  std::unordered_map<uint32_t, uint32_t> memo;  // KeyValues table position -> kvs index
-  pp.tag_begin.reserve(pp.nentries + 1);
-  pp.tag_begin.push_back(0);
-  FbTable e{fb, fbn, 0};
-  const uint32_t fb_base = uint32_t(fb - pp.buf.data());
-  for (uint32_t j = 0; j < pp.nentries; j++) {
-    e.pos = page.indirect(es + 4 * j);
-    parse_entry(e, fb, fb_base, pp, memo);
-  }
-}
-
 struct KeyBuild {
   std::unordered_map<std::string, uint32_t> vmap;
   std::unordered_map<std::string, uint32_t> smap;

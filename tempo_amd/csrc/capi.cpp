@@ -133,17 +133,19 @@ struct tsg_ctx {
   }
   // tsg_cancel (cooperative, like BackendSearchBlock.Search's per-page sr.Quit()): a search
   // with a query id registers it while it runs and checks for a cancel between device
-  // chunks and waves. A cancel for a running id marks it; for an id that finished recently
-  // (the usual timeout race: the cancel lands just after the search returned) it is
-  // dropped, so it cannot fail a later search that reuses the id; for an id not seen yet it
-  // is kept for kPendingNs (a cancel that overtakes its search start) and then expires.
+  // chunks and waves. A cancel for a running id marks it; for an id whose search finished
+  // less than kLateNs ago (the usual timeout race: the cancel lands just after the search
+  // returned) it is dropped, so it cannot fail a later search that reuses the id; any other
+  // cancel is kept for kPendingNs (one that overtakes its search start, also for a reused id)
+  // and then expires.
   std::mutex cmu;
   std::unordered_map<uint64_t, int> active;        // id -> searches running with it
   std::unordered_set<uint64_t> cancelled;          // marks on running ids
   std::unordered_map<uint64_t, uint64_t> pending;  // id -> time of a cancel before its search
-  std::unordered_set<uint64_t> recent;             // ids of finished searches (FIFO, bounded)
+  std::unordered_map<uint64_t, uint64_t> recent;   // id -> when its last search finished (FIFO, bounded)
   std::deque<uint64_t> recent_order;
   static constexpr uint64_t kPendingNs = 10'000'000'000ull;
+  static constexpr uint64_t kLateNs = 1'000'000'000ull;
   static uint64_t now_ns() {
     return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
                         std::chrono::steady_clock::now().time_since_epoch())
@@ -153,7 +155,9 @@ struct tsg_ctx {
     std::lock_guard<std::mutex> lk(cmu);
     if (active.count(qid)) {
       cancelled.insert(qid);
-    } else if (!recent.count(qid)) {
+    } else {
+      auto r = recent.find(qid);
+      if (r != recent.end() && now_ns() - r->second < kLateNs) return;  // late cancel of a finished search
       if (pending.size() >= 4096) {  // expire, then bound
         const uint64_t t = now_ns();
         for (auto it = pending.begin(); it != pending.end();) it = t - it->second > kPendingNs ? pending.erase(it) : ++it;
@@ -185,9 +189,11 @@ struct tsg_ctx {
       active.erase(it);
       cancelled.erase(qid);
     }
-    if (recent.insert(qid).second) {
+    auto r = recent.emplace(qid, 0);
+    r.first->second = now_ns();
+    if (r.second) {
       recent_order.push_back(qid);
-      if (recent_order.size() > 4096) {
+      while (recent_order.size() > 4096) {
         recent.erase(recent_order.front());
         recent_order.pop_front();
       }
@@ -217,6 +223,9 @@ struct tsg_ctx {
     std::mutex wm;
     std::condition_variable cv;
     std::atomic<int> sleepers{0};
+    // searches with a block on this device that have not reached their device stage yet:
+    // the leader waits (bounded) for them to queue
+    std::atomic<int> approaching{0};
     void wake() {
       if (sleepers.load(std::memory_order_acquire) == 0) return;
       std::lock_guard<std::mutex> lk(wm);
@@ -225,20 +234,29 @@ struct tsg_ctx {
   };
   // one per device, created at tsg_init (read without a lock afterwards)
   std::vector<std::pair<const void *, std::unique_ptr<Coalescer>>> coal;
-  std::atomic<int> approaching{0};  // searches that have not reached their device stage yet
   Coalescer &coalescer(const void *dc) {
     for (auto &x : coal)
       if (x.first == dc) return *x.second;
     throw std::logic_error("coalescer: unknown device");
   }
 };
-// A search on its way to the device stage (tsg_ctx::approaching), until leave().
+// A search on its way to the device stage, counted on the coalescer of every device its
+// blocks are on (Coalescer::approaching), until leave().
 struct Approach {
-  std::atomic<int> *cnt;
+  static constexpr int kMaxDev = 16;
+  std::atomic<int> *cnt[kMaxDev];
+  int ncnt = 0;
   std::atomic<bool> left{false};
-  explicit Approach(std::atomic<int> *c) : cnt(c) { cnt->fetch_add(1, std::memory_order_acq_rel); }
+  void add(std::atomic<int> *c) {
+    for (int i = 0; i < ncnt; i++)
+      if (cnt[i] == c) return;
+    if (ncnt == kMaxDev) return;
+    cnt[ncnt++] = c;
+    c->fetch_add(1, std::memory_order_acq_rel);
+  }
   void leave() {
-    if (!left.exchange(true, std::memory_order_acq_rel)) cnt->fetch_sub(1, std::memory_order_acq_rel);
+    if (!left.exchange(true, std::memory_order_acq_rel))
+      for (int i = 0; i < ncnt; i++) cnt[i]->fetch_sub(1, std::memory_order_acq_rel);
   }
   ~Approach() { leave(); }
 };
@@ -905,7 +923,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
     if (prof) prof_add("coal.lead_after_us", std::chrono::duration<double, std::micro>(t_lead - t_wait).count());
     if (window_ns) {
       const auto t0 = std::chrono::steady_clock::now();
-      while (ctx->approaching.load(std::memory_order_acquire) > 0 &&
+      while (c.approaching.load(std::memory_order_acquire) > 0 &&
              uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
                           .count()) < window_ns)
         __builtin_ia32_pause();
@@ -964,6 +982,21 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
     } catch (...) {
       err = std::current_exception();
     }
+    if (err) {
+      // the batched launch failed (device memory, a device error): each caller's part runs
+      // on its own, so that one caller's failure is not every caller's
+      for (auto *x : batch) {
+        try {
+          device_search(*dc, *x->list, *x->q, limit, flags, *x->out);
+        } catch (...) {
+          x->err = std::current_exception();
+        }
+        x->done.store(true, std::memory_order_release);
+      }
+      c.busy.store(false, std::memory_order_release);
+      c.wake();
+      break;
+    }
     // each caller: its blocks' records (the batch's are grouped by position, in order), its
     // share of the algorithmic bytes (by entries), the launch's device time
     uint64_t n_all = 0;
@@ -982,19 +1015,16 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
       o.reruns = batch[k] == &r ? bout.reruns : 0;
       o.pool = bout.pool;
       o.term_any.clear();
-      batch[k]->err = err;
     }
-    if (!err) {
-      for (const auto &rec : bout.recs) {
-        const auto &ow = owner[rec.block_il & 0xffffffu];
-        SearchOut::Rec x = rec;
-        x.block_il = (rec.block_il & 0xff000000u) | ow.second;
-        batch[ow.first]->out->recs.push_back(x);
-      }
-      for (const auto &ta : bout.term_any) {
-        const auto &ow = owner[ta.first];
-        batch[ow.first]->out->term_any.push_back({ow.second, ta.second});
-      }
+    for (const auto &rec : bout.recs) {
+      const auto &ow = owner[rec.block_il & 0xffffffu];
+      SearchOut::Rec x = rec;
+      x.block_il = (rec.block_il & 0xff000000u) | ow.second;
+      batch[ow.first]->out->recs.push_back(x);
+    }
+    for (const auto &ta : bout.term_any) {
+      const auto &ow = owner[ta.first];
+      batch[ow.first]->out->term_any.push_back({ow.second, ta.second});
     }
     for (auto *x : batch) x->done.store(true, std::memory_order_release);
     c.busy.store(false, std::memory_order_release);
@@ -1185,7 +1215,9 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
   const clk::time_point t_in = trace ? clk::now() : clk::time_point();
   const uint64_t qid = opts ? opts->query_id : 0;
   ctx->begin(qid);
-  Approach approach(&ctx->approaching);
+  Approach approach;
+  for (size_t i = 0; i < nblocks; i++)
+    if (blocks && blocks[i] && blocks[i]->b.dc) approach.add(&ctx->coalescer(blocks[i]->b.dc).approaching);
   struct Forget {  // the id is done with once this search returns, cancelled or not
     tsg_ctx *c;
     uint64_t q;

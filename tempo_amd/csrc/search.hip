@@ -251,8 +251,13 @@ constexpr uint32_t kStreamPairMax = 11;  // its bytes of a lane's 16 starts lie 
 
 // bit 7 of each byte of the result: that byte of x is non-zero (exact, no carries across bytes)
 __device__ __forceinline__ uint32_t nz_bytes(uint32_t x) { return (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u; }
-// bits 7/15/23/31 -> bits 0..3
-__device__ __forceinline__ uint32_t pack_hi_bits(uint32_t c) { return (((c >> 7) * 0x204081u) >> 21) & 0xfu; }
+// bits 7/15/23/31 -> bits 0..3 (two rotations instead of a quarter-rate multiply)
+__device__ __forceinline__ uint32_t pack_hi_bits(uint32_t c) {
+  uint32_t x = c >> 7;                          // bits 0, 8, 16, 24
+  x |= __builtin_amdgcn_alignbit(x, x, 7);      // + 1 (<- 8), 17 (<- 24), ...
+  x |= __builtin_amdgcn_alignbit(x, x, 14);     // + 2 (<- 16), 3 (<- 17)
+  return x & 0xfu;
+}
 
 // largest v in [lo, hi) with off[v] <= p (off[lo] <= p < off[hi] or hi = nvals + 1): 64-ary search
 __device__ __forceinline__ uint32_t value_at(const uint32_t *off, uint32_t lo, uint32_t hi, uint64_t p, int lane) {
@@ -325,7 +330,7 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     s_ndw[i] = x;
   }
   const uint32_t n0 = uint32_t(needles[J.needle_off]) * 0x01010101u;
-  const uint32_t n1 = nl > 1 ? uint32_t(needles[J.needle_off + 1]) * 0x01010101u : 0u;
+  const uint32_t n1 = uint32_t(needles[J.needle_off + 1]) * 0x01010101u;  // (streamed needles: >= 2 bytes)
   const uint32_t pj = J.pj;  // (wave-uniform)
   const uint32_t r0 = pj ? uint32_t(needles[J.needle_off + pj]) * 0x01010101u : 0u;
   const uint32_t r1 = pj ? uint32_t(needles[J.needle_off + pj + 1]) * 0x01010101u : 0u;
@@ -357,6 +362,7 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
 #pragma unroll
   for (int k = 0; k < kRing; k++) ring[k] = load16(cq + uint64_t(k) * 1024 + lane * 16);
   uint32_t last_v = 0xffffffffu;  // this lane's last marked value (skips repeats)
+  uint64_t mdone = 0;  // (wave-uniform) starts below this lie in a value the wave has marked
   // one 1 KiB step of start positions [c, c + 1024): cur = its bytes, nxt = the next KiB
   auto step = [&](const uint64_t c, const u32x4 cur, const u32x4 nxt) {
     // the needle's first two bytes at all 16 start positions of this lane, in registers:
@@ -370,11 +376,7 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     // the pairs OR-ed together: one zero-byte test per dword for all of them)
     uint32_t xs[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      uint32_t x = d[k] ^ n0;
-      if (nl > 1) x |= __builtin_amdgcn_alignbyte(d[k + 1], d[k], 1) ^ n1;
-      xs[k] = x;
-    }
+    for (int k = 0; k < 4; k++) xs[k] = (d[k] ^ n0) | (__builtin_amdgcn_alignbyte(d[k + 1], d[k], 1) ^ n1);
     if (pj) {
       // the second pair: bytes pj, pj + 1 after each start, from this lane's 16 bytes and the
       // next lane's (DPP; lane 63: the next KiB's first lane). V[m] = window bytes pj + 4m ..
@@ -400,24 +402,27 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
 #pragma unroll
       for (int k = 0; k < 4; k++) xs[k] |= (V[k] ^ r0) | (__builtin_amdgcn_alignbyte(V[k + 1], V[k], 1) ^ r1);
     }
-    uint32_t cw[4], any = 0;
+    // a zero byte anywhere: (x - 0x01010101) & ~x & 0x80808080 is non-zero exactly when x has
+    // one (its false flags sit above a true zero: right for "any", not for "which")
+    uint32_t any = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      cw[k] = nz_bytes(xs[k]) ^ 0x80808080u;  // bit 7 of a byte: a candidate start
-      any |= cw[k];
-    }
+    for (int k = 0; k < 4; k++) any |= (xs[k] - 0x01010101u) & ~xs[k];
     // most steps hold no candidate in any lane: nothing else to do (a wave-uniform branch)
-    if (__ballot(any != 0) == 0) return;
-    uint32_t cm = 0;
+    if (__ballot((any & 0x80808080u) != 0) == 0) return;
+    uint32_t cm = 0;  // bit 4k + b: start 4k + b of this lane is a candidate (exact per byte)
 #pragma unroll
-    for (int k = 0; k < 4; k++) cm |= pack_hi_bits(cw[k]) << (4 * k);
+    for (int k = 0; k < 4; k++) cm |= pack_hi_bits(nz_bytes(xs[k]) ^ 0x80808080u) << (4 * k);
+    // starts inside a value this wave already marked add nothing
+    if (c + uint64_t(lane) * 16 + 16 <= mdone) cm = 0;
+    else if (c + uint64_t(lane) * 16 < mdone) cm &= ~0u << uint32_t(mdone - c - uint64_t(lane) * 16);
+    if (__ballot(cm != 0) == 0) return;
     wave_sync();  // (previous window's readers done)
     reinterpret_cast<u32x4 *>(s_win)[lane] = cur;
     reinterpret_cast<u32x4 *>(s_win)[64 + lane] = nxt;
     // the offsets must cover every start of this window
     const uint64_t wlast = min<uint64_t>(c + 1024, qhi) - 1 - J.lead;
+    const uint64_t pfirst = max<uint64_t>(c, qlo) - J.lead;
     if (cover != ~0ull && wlast >= cover) {
-      const uint64_t pfirst = max<uint64_t>(c, qlo) - J.lead;
       // staged values [vb, vb + kv) that start at or before pfirst
       const uint32_t k1 = uint32_t(__popcll(__ballot(uint32_t(lane) < kv && uint64_t(s_off[lane]) <= pfirst))) +
                           uint32_t(__popcll(__ballot(uint32_t(lane) + 64 < kv && uint64_t(s_off[64 + lane]) <= pfirst)));
@@ -425,39 +430,57 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
       wave_sync();
       const uint32_t v = beyond ? value_at(J.off, vb + kv, J.nvals + 1, pfirst, lane) : vb + k1 - 1;
       stage_offs(v);
-      // (rare: every ~kStreamOffs values) leave no load of this branch in flight, so that the
-      // compiler's wait counts for the ring's slots stay exact past the branch
+      // (rare: every ~kStreamOffs values) leave no load of this branch in flight
       __builtin_amdgcn_s_waitcnt(kWaitVm0);
     }
     wave_sync();
     // candidates: verify from LDS, map the start to its value, mark the value. When the
     // staged offsets cover every start of the window (the usual case: a uniform branch) the
-    // loop touches LDS only — a global load here would make the waits for the ring's slots
-    // drain every load in flight; a window past the staged values (a run of tiny values)
-    // searches the global offsets instead.
+    // loop touches LDS only; a window past the staged values (a run of tiny values) searches
+    // the global offsets instead.
+    uint64_t mend = 0;  // end (aligned coordinates) of the last value this lane marked
     auto candidates = [&](auto global_tag) {
       constexpr bool kGlobal = decltype(global_tag)::value;
+      // staged values that hold the window's starts: [wlo, whi) (a start maps by a binary
+      // search of those few, not of all kStreamOffs)
+      uint32_t wlo = 0, whi = kv;
+      if (!kGlobal) {
+        const uint32_t a = s_off[lane], b = s_off[64 + lane];
+        wlo = uint32_t(__popcll(__ballot(uint32_t(lane) < kv && uint64_t(a) <= pfirst))) +
+              uint32_t(__popcll(__ballot(uint32_t(lane) + 64 < kv && uint64_t(b) <= pfirst))) - 1;
+        whi = uint32_t(__popcll(__ballot(uint32_t(lane) < kv && uint64_t(a) <= wlast))) +
+              uint32_t(__popcll(__ballot(uint32_t(lane) + 64 < kv && uint64_t(b) <= wlast)));
+      }
+      const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
       while (cm) {
         const uint32_t jb = uint32_t(__builtin_ctz(cm));
         cm &= cm - 1;
         const uint32_t wo = uint32_t(lane) * 16 + jb;  // window offset of the start
         const uint64_t q = c + wo;
         if (q < qlo || q >= qhi) continue;
+        // needle bytes 2.. compared 4 words (16 bytes) per LDS round trip
         bool ok = true;
-        const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
-        for (uint32_t k = 0; ok && 4 * k + 2 < nl; k++) {
-          const uint32_t off = wo + 2 + 4 * k;  // (< 2048: wo < 1024, nl <= 1024; the next word is padding)
-          const uint32_t x = __builtin_amdgcn_alignbyte(w32[(off >> 2) + 1], w32[off >> 2], off & 3);
-          const uint32_t rem = nl - 2 - 4 * k;
-          const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
-          ok = ((x ^ s_ndw[k]) & m) == 0;
+        for (uint32_t k = 0; ok && 4 * k + 2 < nl; k += 4) {
+          uint32_t bad = 0;
+#pragma unroll
+          for (uint32_t u = 0; u < 4; u++) {
+            const uint32_t kk = k + u;
+            if (4 * kk + 2 < nl) {  // (nl wave-uniform)
+              const uint32_t off = wo + 2 + 4 * kk;  // (< 2048: wo < 1024, nl <= 1024; the next word is padding)
+              const uint32_t x = __builtin_amdgcn_alignbyte(w32[(off >> 2) + 1], w32[off >> 2], off & 3);
+              const uint32_t rem = nl - 2 - 4 * kk;
+              const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
+              bad |= (x ^ s_ndw[kk]) & m;
+            }
+          }
+          ok = bad == 0;
         }
         if (!ok) continue;
         const uint64_t p = q - J.lead;
         uint32_t v;
         uint64_t vend;
         if (!kGlobal || p < cover) {  // in the staged offsets: s_off[lo] <= p < s_off[lo + 1]
-          uint32_t lo = 0, hi = kv;
+          uint32_t lo = wlo, hi = whi;
           while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (uint64_t(s_off[mid]) <= p) lo = mid;
@@ -482,6 +505,7 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
         }
         // the rest of this lane's starts inside the same value add nothing
         const uint64_t skip = vend + J.lead;  // aligned coordinate of the value's end
+        mend = skip;
         if (skip > q + 1) {
           const uint64_t rel = skip - (c + uint64_t(lane) * 16);
           cm &= rel >= 16 ? 0u : ~((1u << uint32_t(rel)) - 1u);
@@ -493,6 +517,15 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     } else {
       candidates(std::true_type{});
       __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    }
+    // the highest lane that marked a value holds the furthest end: later starts before it
+    // are skipped (the values' ends increase with the lane)
+    const uint64_t marked = __ballot(mend != 0);
+    if (marked) {
+      const int hl = 63 - __builtin_clzll(marked);
+      const uint64_t e = (uint64_t(__builtin_amdgcn_readlane(uint32_t(mend >> 32), hl)) << 32) |
+                         __builtin_amdgcn_readlane(uint32_t(mend), hl);
+      mdone = max(mdone, e);
     }
   };
   for (; cq < qhi; cq += uint64_t(kRing) * 1024) {
@@ -1826,7 +1859,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       jb.item_base = items;
       // a large dictionary of values >= 16 B on average: one byte-stream pass
       // (dict_stream_kernel) instead of a lane per value
-      const bool stream = dc.dict_stream && k.dict_nbytes > kStreamMinBytes && q.value_lens[t] >= 1 &&
+      const bool stream = dc.dict_stream && k.dict_nbytes > kStreamMinBytes && q.value_lens[t] >= 2 &&
                           q.value_lens[t] <= kStreamMaxNeedle && k.dict_nbytes >= 16ull * k.nvals;
       if (!stream) items += uint32_t(align_up(std::max<uint32_t>(k.nvals, 1), 64));
       const uint32_t words = (k.nsets + 31) / 32;

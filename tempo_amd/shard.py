@@ -40,7 +40,7 @@ from typing import Callable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
-from .tsg import SearchMetrics, TraceSearchMetadata, TsgError, _check, lib
+from .tsg import TSG_E_INVALID, SearchMetrics, TraceSearchMetadata, TsgError, _check, lib
 
 WIRE_MAGIC = 0x57475354
 WIRE_VERSION = 1
@@ -171,12 +171,17 @@ def merge_wires(wires: Sequence, limit: int, total_blocks: int, out: Optional[np
     n = len(keep)
     ptrs = (C.POINTER(C.c_uint8) * max(n, 1))(*[p for _, p in keep])
     lens = (C.c_size_t * max(n, 1))(*[a.size for a, _ in keep])
-    need = max(_HDR.size, sum(a.size for a, _ in keep))  # the merged wire is never longer
+    # the merged wire is never longer than its inputs; with none it is the header + one name offset
+    need = max(_HDR.size + 8, sum(a.size for a, _ in keep))
     if out is None or out.size < need:
         out = np.empty(need, np.uint8)
     ln = C.c_size_t()
-    _check(lib().tsg_wire_merge(ptrs, lens, n, min(int(limit), 2**64 - 1), total_blocks, out.ctypes.data, out.size,
-                                C.byref(ln)))
+    lim = min(int(limit), 2**64 - 1)
+    rc = lib().tsg_wire_merge(ptrs, lens, n, lim, total_blocks, out.ctypes.data, out.size, C.byref(ln))
+    if rc == TSG_E_INVALID and ln.value > out.size:  # (short buffer: the library reports the size)
+        out = np.empty(ln.value, np.uint8)
+        rc = lib().tsg_wire_merge(ptrs, lens, n, lim, total_blocks, out.ctypes.data, out.size, C.byref(ln))
+    _check(rc)
     return from_wire(out[:ln.value])
 
 

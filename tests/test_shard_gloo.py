@@ -120,6 +120,15 @@ def test_shard_range_partitions():
         shard.shard_range(4, 2, 2)
 
 
+def test_merge_of_no_responses():
+    """A merge with no responses (the output was sized 8 bytes short): an empty
+    response whose InspectedBlocks is the sharder's total (searchsharding.go:221)."""
+    r = shard.merge_wires([], 20, 3)
+    assert len(r) == 0 and r.metrics.inspected_blocks == 3 and r.metrics.inspected_traces == 0
+    traces, met = shard.merge_responses([], 20, 0)
+    assert traces == [] and met.inspected_blocks == 0
+
+
 def test_wire_roundtrip():
     ts = [T.TraceSearchMetadata(trace_id=bytes(range(i, i + 16)), trace_id_len=16 - (i % 9),
                                 root_service_name="svc-%d" % (i % 4), root_trace_name="op\u00e9-%d" % i,
