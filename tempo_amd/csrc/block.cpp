@@ -926,6 +926,7 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
       kc.dict_bytes.resize(nb);
       kc.dict_off.resize(nv + 1);
       kc.dict_off[nv] = uint32_t(nb);
+      if (nb > kDeferMinBytes) kc.dict_vh.resize(nv);  // (kept for verify_header_dicts)
     });
     for_each_index(jobs.size(), nthreads, [&](size_t j) {
       const uint32_t k = jobs[j].first, x = jobs[j].second;
@@ -935,6 +936,7 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
       for (uint32_t y = 0; y < x; y++) b0 += shards[k][y].bytes.size();
       if (!S.bytes.empty()) std::memcpy(kc.dict_bytes.data() + b0, S.bytes.data(), S.bytes.size());
       for (size_t i = 0; i + 1 < S.off.size(); i++) kc.dict_off[vbase[k][x] + i] = uint32_t(b0 + S.off[i]);
+      if (!kc.dict_vh.empty()) std::copy(S.vh.begin(), S.vh.end(), kc.dict_vh.begin() + vbase[k][x]);
     });
     shards.clear();
     const auto tb3 = clk::now();
@@ -1203,39 +1205,23 @@ inline uint64_t fmix64(uint64_t x) {
   return x;
 }
 inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-// Two independent 64-bit lanes over the value's bytes (length folded in), avalanched.
+// A multiset of values as two sums of avalanched forms of each value's xxhash64 (the hash
+// the loader interned the value with: the dictionary side costs no second pass over its bytes)
 struct H128 {
   uint64_t a = 0, b = 0;
-  void add(const uint8_t *p, size_t n) {
-    uint64_t x = 0x9E3779B97F4A7C15ULL ^ n, y = 0xC2B2AE3D27D4EB4FULL + n;
-    size_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-      uint64_t w;
-      std::memcpy(&w, p + i, 8);
-      x = rotl64((x ^ w) * 0x87c37b91114253d5ULL, 31);
-      y = rotl64((y + w) * 0x4cf5ad432745937fULL, 27) ^ x;
-    }
-    if (i < n) {
-      uint64_t w = 0;
-      std::memcpy(&w, p + i, n - i);
-      x = rotl64((x ^ w) * 0x87c37b91114253d5ULL, 31);
-      y = rotl64((y + w) * 0x4cf5ad432745937fULL, 27) ^ x;
-    }
-    a += fmix64(x ^ (y >> 1));  // multiset: a sum, so the order of the values does not matter
-    b += fmix64(y + rotl64(x, 17));
+  void add_hash(uint64_t h) {
+    a += fmix64(h);  // multiset: a sum, so the order of the values does not matter
+    b += fmix64(rotl64(h, 29) ^ 0x9E3779B97F4A7C15ULL);
   }
 };
-// sum of H128 over items [0, n) (value(i) -> string_view), on up to nthreads threads
-template <class Value>
-H128 multiset_hash(size_t n, int nthreads, Value &&value) {
+// sum of H128 over items [0, n) (hash(i) -> the value's xxhash64), on up to nthreads threads
+template <class Hash>
+H128 multiset_hash(size_t n, int nthreads, Hash &&hash) {
   const size_t nt = std::max<size_t>(1, std::min<size_t>(size_t(std::max(1, nthreads)), n / 16384));
   std::vector<H128> part(nt);
   auto run = [&](size_t t) {
     const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
-    for (size_t i = lo; i < hi; i++) {
-      const std::string_view v = value(i);
-      part[t].add(reinterpret_cast<const uint8_t *>(v.data()), v.size());
-    }
+    for (size_t i = lo; i < hi; i++) part[t].add_hash(hash(i));
   };
   std::vector<std::thread> th;
   for (size_t t = 1; t < nt; t++) th.emplace_back(run, t);
@@ -1261,16 +1247,17 @@ void verify_header_dicts(HostBlock &hb, int nthreads) {
     const KeyColumn &kc = hb.keys[size_t(it->second)];
     if (kc.dict_bytes.size() <= kDeferMinBytes) continue;
     const uint32_t v0 = hb.hdr_val0[hk], v1 = hb.hdr_val0[hk + 1];
-    if (v1 - v0 != kc.nvals()) continue;
+    if (v1 - v0 != kc.nvals() || kc.dict_vh.size() != kc.nvals()) continue;
     // (the dictionary's values are distinct (interned): equal counts and equal multiset hashes
     // mean the header lists exactly those values, each once)
-    const H128 h = multiset_hash(v1 - v0, nthreads, [&](size_t i) { return hb.hdr_vals[v0 + i]; });
-    const H128 d = multiset_hash(kc.nvals(), nthreads, [&](size_t i) {
-      return std::string_view(reinterpret_cast<const char *>(kc.dict_bytes.data() + kc.dict_off[i]),
-                              kc.dict_off[i + 1] - kc.dict_off[i]);
+    const H128 h = multiset_hash(v1 - v0, nthreads, [&](size_t i) {
+      const std::string_view v = hb.hdr_vals[v0 + i];
+      return xxhash64(reinterpret_cast<const uint8_t *>(v.data()), v.size());
     });
+    const H128 d = multiset_hash(kc.nvals(), nthreads, [&](size_t i) { return kc.dict_vh[i]; });
     hb.hdr_defer[hk] = h.a == d.a && h.b == d.b;
   }
+  for (auto &kc : hb.keys) std::vector<uint64_t>().swap(kc.dict_vh);
 }
 
 }  // namespace tsg

@@ -123,6 +123,8 @@ struct KeyColumn {
   // large dictionaries (> kDeferMinBytes): counts of each adjacent byte pair (b0 << 8 | b1) in
   // a sample of the value bytes; the dictionary stream pass tests a needle's rarest pair
   std::vector<uint32_t> pair_freq;
+  // during the load only (large dictionaries): each value's xxhash64, for verify_header_dicts
+  std::vector<uint64_t> dict_vh;
   uint32_t nvals() const { return uint32_t(dict_off.size() - 1); }
   uint32_t nsets() const { return uint32_t(set_off.size() - 1); }
   int width() const { return nsets() < 255 ? 1 : (nsets() < 65535 ? 2 : 4); }

@@ -208,8 +208,39 @@ static void snappy_block_decode(const uint8_t *src, size_t sl, uint8_t *dst, siz
   if (d != dl) fail(TSG_E_CORRUPT, "snappy: short block");
 }
 
+// Decoded size of a framed stream, from its chunk headers (no checks beyond what reading them
+// needs: stops at the first chunk it cannot read; the decode below does the checking)
+static size_t snappy_framed_size(const uint8_t *src, size_t n) {
+  size_t s = 0, total = 0;
+  while (n - s >= 4) {
+    const uint8_t ct = src[s];
+    const size_t cl = size_t(src[s + 1]) | (size_t(src[s + 2]) << 8) | (size_t(src[s + 3]) << 16);
+    s += 4;
+    if (cl > n - s) break;
+    const uint8_t *b = src + s;
+    s += cl;
+    if (ct == 0x00) {
+      uint64_t v = 0;
+      int shift = 0;
+      for (size_t i = 0; 4 + i < cl && i < 10; i++) {
+        v |= uint64_t(b[4 + i] & 0x7f) << shift;
+        if (b[4 + i] < 0x80) {
+          total += std::min<uint64_t>(v, kMaxBlock);
+          break;
+        }
+        shift += 7;
+      }
+    } else if (ct == 0x01 && cl >= 4) {
+      total += std::min<size_t>(cl - 4, kMaxBlock);
+    }
+  }
+  return total;
+}
+
 void snappy_framed_decode(const uint8_t *src, size_t n, std::vector<uint8_t> &out) {
   out.clear();
+  // one allocation (and one zero fill) for the whole stream instead of a growing vector
+  out.reserve(snappy_framed_size(src, n));
   size_t s = 0;
   bool hdr = false;
   while (s < n) {

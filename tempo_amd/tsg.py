@@ -22,7 +22,7 @@ from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtsg.so")
+LIB_PATH = os.environ.get("TSG_LIB_PATH") or os.path.join(HERE, "libtsg.so")  # (override: A/B runs of two builds)
 
 TSG_OK = 0
 TSG_E_NOT_FOUND = 1
