@@ -1041,7 +1041,8 @@ def main():
     scan_bytes = met.scan_bytes
     achieved = scan_bytes / scan_avg_ns if scan_avg_ns else None  # bytes/ns == GB/s
     regime = "hbm" if len(sets) * scan_bytes > 256 * 2**20 * 1.5 else "mall"
-    traffic, traffic_src = pmc_traffic(f"blocks={args.blocks},entries={args.entries},sets={len(sets)}")
+    # (the PMC figure of this layout: the pool kernels' 11 B/entry columns, round 4 on)
+    traffic, traffic_src = pmc_traffic(f"blocks={args.blocks},entries={args.entries},sets={len(sets)},layout=ds")
     out = {
         "metric": METRIC,
         "value": value,
@@ -1073,7 +1074,7 @@ def main():
                             "the same set every step: its filter columns stay in the 256 MiB Infinity Cache"),
             "traffic": traffic, "traffic_measured_in_run": False,
             "traffic_source": traffic_src, "bytes_per_launch": scan_bytes, "avg_launch_us": scan_avg_ns / 1e3,
-            "bytes_per_entry": 15,
+            "bytes_per_entry": round(scan_bytes / entries, 3),
         },
         "load_s": load_s,
         "load_gb_per_s": fb_bytes / load_s / 1e9 if load_s else None,

@@ -124,17 +124,27 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
   HIP_OK(hipSetDevice(dc.ordinal));
   hipStream_t s = dc.stream;
   size_t n = h.n;
-  // [dur32 | start_s | end_s], npad entries each (whole tiles: kColPad), one allocation
+  // [dur32 | start_s | end_s | ds], npad entries each (whole tiles: kColPad), one allocation.
+  // ds, the pool kernels' compact form of the other three (4 B where they read 12):
+  //   bits 0..15  D16 = 2 * floor(dur / 1 ms) + (dur % 1 ms != 0), saturated at 0xffff: for whole-
+  //               ms bounds m, M <= kDs16MaxMs, dur >= m ms <=> D16 >= 2m and dur <= M ms <=> D16 <= 2M
+  //               (a saturated entry has dur >= 32767 ms: above every such M, not below any m)
+  //   bits 16..31 end_s - start_s when it fits below 0xffff, else 0xffff (the kernel then reads end_s)
   const size_t npad = (std::max<size_t>(n, 1) + kColPad - 1) / kColPad * kColPad;
   d.npad = npad;
-  std::vector<uint32_t> scan(3 * npad, 0);
+  std::vector<uint32_t> scan(4 * npad, 0);
   std::vector<uint64_t> dur64(n);
   for (size_t i = 0; i < n; i++) {
     uint64_t dd = h.end[i] - h.start[i];  // uint64 wrap (pitfall P2)
     dur64[i] = dd;
     scan[i] = dd >= 0xffffffffULL ? 0xffffffffu : uint32_t(dd);
-    scan[npad + i] = uint32_t(h.start[i] / 1000000000ULL);
-    scan[2 * npad + i] = uint32_t(h.end[i] / 1000000000ULL);
+    const uint32_t ss = uint32_t(h.start[i] / 1000000000ULL), es = uint32_t(h.end[i] / 1000000000ULL);
+    scan[npad + i] = ss;
+    scan[2 * npad + i] = es;
+    const uint64_t q = dd / 1000000ULL;
+    const uint64_t d16 = q >= 0x8000ULL ? 0xffffULL : std::min<uint64_t>(2 * q + (dd % 1000000ULL != 0), 0xffffULL);
+    const uint32_t span = es - ss;  // (uint32: an end before the start wraps to a large value)
+    scan[3 * npad + i] = uint32_t(d16) | (span < 0xffffu ? span : 0xffffu) << 16;
   }
   d.dur32 = dev_upload(d, scan.data(), scan.size(), s);
   d.start_s = d.dur32 + npad;

@@ -37,7 +37,7 @@ constexpr uint32_t kPoolSpinMax = 1u << 24;  // LDS poll bound (~1 s of s_sleep 
 static_assert(kColPad % kPoolTile == 0, "column padding covers whole units");
 
 struct PoolBlk {           // 64 B, staged in LDS
-  const uint32_t *scan;    // dur32 | start_s | end_s, npad entries each
+  const uint32_t *scan;    // dur32 | start_s | end_s | ds, npad entries each (the pool reads ds, start_s)
   const uint8_t *col[4];   // one-byte term columns
   uint32_t npad, nent;
   uint32_t ubase;          // first unit of the block in the launch's unit space
@@ -103,7 +103,7 @@ __device__ __forceinline__ T *uniform_ptr(T *p) {
 
 template <int NT>
 struct PoolRegs {
-  u32x4 d[kSteps], s[kSteps], e[kSteps];
+  u32x4 d[kSteps], s[kSteps];  // ds (duration | span), start seconds
   uint32_t tv[NT > 0 ? NT : 1][kSteps];
   uint32_t blk, e0;  // wave-uniform: block slot, first entry of the unit in its block
 };
@@ -125,7 +125,9 @@ __device__ __forceinline__ uint32_t stream1(const uint8_t *p, uint64_t e) {
 // test is evaluated for every entry and combined with bitwise ands (short-circuit tests
 // compiled to ~130 exec-mask branches per unit; with real, mixed values the lanes diverge
 // and the 150 MB scan ran 8 us longer than with uniform data, profiles/r03_launch).
-// lo/hi: the duration bounds (0 / 2^32-1 when a side is absent); bm: the LDS bitmaps.
+// ds: the compact duration | span column (devctx.hip), sv / ev: start / end seconds;
+// lo/hi: the duration bounds in ds's units (0 / 2^32-1 when a side is absent); bm: the LDS
+// bitmaps.
 template <int NT, bool DUR, bool RANGE>
 __device__ __forceinline__ uint32_t unit_mask(const u32x4 (&d)[kSteps], const u32x4 (&sv4)[kSteps],
                                               const u32x4 (&ev4)[kSteps], const uint32_t (&tv)[NT > 0 ? NT : 1][kSteps],
@@ -135,7 +137,7 @@ __device__ __forceinline__ uint32_t unit_mask(const u32x4 (&d)[kSteps], const u3
   uint32_t mask = 0;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
-    const uint32_t dv[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+    const uint32_t dv[4] = {d[k].x & 0xffffu, d[k].y & 0xffffu, d[k].z & 0xffffu, d[k].w & 0xffffu};
     const uint32_t sv[4] = {sv4[k].x, sv4[k].y, sv4[k].z, sv4[k].w};
     const uint32_t ev[4] = {ev4[k].x, ev4[k].y, ev4[k].z, ev4[k].w};
 #pragma unroll
@@ -155,6 +157,63 @@ __device__ __forceinline__ uint32_t unit_mask(const u32x4 (&d)[kSteps], const u3
     }
   }
   return mask;
+}
+
+// A workgroup barrier that waits for this wave's LDS and scalar-memory operations only
+// (lgkmcnt), not for its vector loads in flight: __syncthreads()' fence also waits
+// vmcnt(0), which at the staging barrier drained the units each wave had already asked for
+// (the whole launch-wide burst: ~8-10 us before any wave evaluated its first unit). The
+// staging below reads the kernel arguments with scalar loads, so nothing it needs is
+// counted by vmcnt. (asm memory clobber: no LDS access moves across it)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// PoolBlk b of the kernel arguments into LDS, by scalar loads (wave-uniform b): lane j
+// writes word j
+__device__ __forceinline__ void stage_blk(const PoolBlk *src, PoolBlk *dst, uint32_t b, int lane) {
+  const uint32_t *sw = reinterpret_cast<const uint32_t *>(src + b);
+  uint32_t x = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t v = sw[j];
+    x = lane == j ? v : x;
+  }
+  if (lane < 16) reinterpret_cast<uint32_t *>(dst + b)[lane] = x;
+}
+// the launch's value-set bitmaps (kArgBms x 8 words) into LDS the same way, 8 bitmaps per
+// pass of a wave (lane 8i + j: word j of bitmap i)
+__device__ __forceinline__ void stage_bms(const uint32_t (*bms)[8], uint32_t *s_bm, uint32_t wv, uint32_t nwv, int lane) {
+  for (uint32_t g = wv; g < uint32_t(kArgBms) / 8; g += nwv) {
+    const uint32_t *sw = bms[8 * g];
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+      const uint32_t v = sw[j];
+      x = lane == j ? v : x;
+    }
+    s_bm[64 * g + uint32_t(lane)] = x;
+  }
+}
+
+// End seconds of a unit's entries: start + span from the ds column, or, in a unit where some
+// entry's span did not fit 16 bits (ends 18 h or more after the start, or before it: the
+// escape 0xffff), the exact end column for the whole unit (rare: a wave-uniform branch).
+template <bool NTL>
+__device__ __forceinline__ void unit_ends(const u32x4 (&ds)[kSteps], const u32x4 (&sv)[kSteps], u32x4 (&ev)[kSteps],
+                                          const uint32_t *scan, uint32_t npad, uint32_t e0, int lane) {
+  bool esc = false;
+#pragma unroll
+  for (int k = 0; k < kSteps; k++) {
+    const uint32_t sp[4] = {ds[k].x >> 16, ds[k].y >> 16, ds[k].z >> 16, ds[k].w >> 16};
+    esc = esc || sp[0] == 0xffffu || sp[1] == 0xffffu || sp[2] == 0xffffu || sp[3] == 0xffffu;
+    ev[k].x = sv[k].x + sp[0];
+    ev[k].y = sv[k].y + sp[1];
+    ev[k].z = sv[k].z + sp[2];
+    ev[k].w = sv[k].w + sp[3];
+  }
+  if (__ballot(esc)) {
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) ev[k] = stream4<NTL>(scan + 2ull * npad, uint64_t(e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
+  }
 }
 
 template <int NT, bool DUR, bool RANGE, bool NTL>
@@ -186,11 +245,8 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
 #pragma unroll
     for (int k = 0; k < kSteps; k++) {
       const uint64_t e = uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
-      if (DUR) R.d[k] = stream4<NTL>(scan, e);
-      if (RANGE) {
-        R.s[k] = stream4<NTL>(scan + npad, e);
-        R.e[k] = stream4<NTL>(scan + 2ull * npad, e);
-      }
+      if (DUR || RANGE) R.d[k] = stream4<NTL>(scan + 3ull * npad, e);
+      if (RANGE) R.s[k] = stream4<NTL>(scan + npad, e);
     }
 #pragma unroll
     for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
@@ -210,21 +266,23 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     ub = w * S + wv + nwv;
     load_arg(rb, ub);
   }
-  // ---- stage the launch's tables (one vector round trip from the kernel arguments)
+  // ---- stage the launch's tables (scalar loads of the kernel arguments; the barrier does not
+  // wait for the units' loads above)
   {
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(A.blk);
-    uint32_t *dst = reinterpret_cast<uint32_t *>(s_blk);
-    for (uint32_t i = tid; i < nsegs * 16; i += blockDim.x) dst[i] = src[i];
-    if (uint32_t(tid) <= nsegs) s_ub[tid] = uint32_t(tid) < nsegs ? A.blk[tid].ubase : units;
-    if (tid < kArgBms * 8) s_bm[tid] = reinterpret_cast<const uint32_t *>(A.bms)[tid];
+    for (uint32_t b = wv; b < nsegs; b += nwv) {
+      stage_blk(A.blk, s_blk, b, lane);
+      if (lane == 0) s_ub[b] = A.blk[b].ubase;
+    }
+    stage_bms(A.bms, s_bm, wv, nwv, lane);
     for (uint32_t i = tid; i < kPoolChunks; i += blockDim.x) s_chunk[i] = kPoolPending;
     if (tid == 0) {
+      s_ub[nsegs] = units;
       s_next = min(2 * nwv, S);  // (the claims below it are the waves' first two)
       s_nrec = 0;
       if (w == 0) __hip_atomic_store(A.head_next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  __syncthreads();
+  lds_barrier();
   unsigned long long *const stamps = A.stamps;
   if (stamps && tid == 0) {
     stamps[uint64_t(w) * kStampSlots] = t_start;
@@ -302,11 +360,8 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
 #pragma unroll
     for (int k = 0; k < kSteps; k++) {
       const uint64_t e = uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
-      if (DUR) R.d[k] = stream4<NTL>(scan, e);
-      if (RANGE) {
-        R.s[k] = stream4<NTL>(scan + npad, e);
-        R.e[k] = stream4<NTL>(scan + 2ull * npad, e);
-      }
+      if (DUR || RANGE) R.d[k] = stream4<NTL>(scan + 3ull * npad, e);
+      if (RANGE) R.s[k] = stream4<NTL>(scan + npad, e);
     }
 #pragma unroll
     for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
@@ -321,7 +376,9 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     const PoolBlk &B = s_blk[R.blk];
     const uint32_t n = __builtin_amdgcn_readfirstlane(B.nent);
     const uint32_t bmi4 = __builtin_amdgcn_readfirstlane(B.bmi4), ns4 = __builtin_amdgcn_readfirstlane(B.nsets4);
-    uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, R.e, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
+    u32x4 ev[kSteps];
+    if (RANGE) unit_ends<NTL>(R.d, R.s, ev, uniform_ptr(B.scan), __builtin_amdgcn_readfirstlane(B.npad), R.e0, lane);
+    uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, ev, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
                                                ns4, s_bm, lane);
     if (__ballot(mask != 0) == 0) return;
     if (A.unit_cap) mask = cap_unit_mask(mask, A.unit_cap, lane);
@@ -445,7 +502,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
   };
   set_block(b);
   struct Regs {
-    u32x4 d[kSteps], s[kSteps], e[kSteps];
+    u32x4 d[kSteps], s[kSteps];  // ds (duration | span), start seconds
     uint32_t tv[NT > 0 ? NT : 1][kSteps];
     uint32_t e0;
   };
@@ -458,11 +515,8 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
 #pragma unroll
     for (int k = 0; k < kSteps; k++) {
       const uint64_t e = uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
-      if (DUR) R.d[k] = stream4<NTL>(B.scan, e);
-      if (RANGE) {
-        R.s[k] = stream4<NTL>(B.scan + B.npad, e);
-        R.e[k] = stream4<NTL>(B.scan + 2ull * B.npad, e);
-      }
+      if (DUR || RANGE) R.d[k] = stream4<NTL>(B.scan + 3ull * B.npad, e);
+      if (RANGE) R.s[k] = stream4<NTL>(B.scan + B.npad, e);
     }
 #pragma unroll
     for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
@@ -478,7 +532,9 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
   auto eval = [&](const Regs &R, uint32_t bslot) {
     const PoolBlk &P = A.blk[bslot];
     const uint32_t n = P.nent, bmi4 = P.bmi4, ns4 = P.nsets4;
-    uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, R.e, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
+    u32x4 ev[kSteps];
+    if (RANGE) unit_ends<NTL>(R.d, R.s, ev, P.scan, P.npad, R.e0, lane);
+    uint32_t mask = unit_mask<NT, DUR, RANGE>(R.d, R.s, ev, R.tv, R.e0, n, dlo, dhi, A.start_s, A.end_s, bmi4,
                                                ns4, s_bm, lane);
     if (__ballot(mask != 0) == 0) return;
     if (A.unit_cap) mask = cap_unit_mask(mask, A.unit_cap, lane);
@@ -517,9 +573,9 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
     load(ra, u);
     ba = b;
   }
-  if (tid < kArgBms * 8) s_bm[tid] = reinterpret_cast<const uint32_t *>(A.bms)[tid];
+  stage_bms(A.bms, s_bm, wave, nwv, lane);
   if (tid == 0) s_nrec = 0;
-  __syncthreads();
+  lds_barrier();  // (not waiting for the first unit's loads)
   unsigned long long *const stamps = A.stamps;
   if (stamps && tid == 0) {
     stamps[uint64_t(w) * kStampSlots] = t_start;
@@ -671,8 +727,10 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   PA.lookahead = std::min(dc.pool_lookahead, S);
   PA.has_min = q.has_min;
   PA.has_max = q.has_max;
-  PA.min32 = uint32_t(q.min_ns);  // (narrow mode: thresholds below 2^32-1 ns)
-  PA.max32 = uint32_t(q.max_ns);
+  // duration bounds in the ds column's units (2 x whole ms + a remainder bit: devctx.hip):
+  // dur >= m ms <=> ds >= 2m, dur <= M ms <=> ds <= 2M (callers: m, M <= kDs16MaxMs)
+  PA.min32 = q.has_min ? uint32_t(2 * (q.min_ns / 1000000ull)) : 0u;
+  PA.max32 = q.has_max ? uint32_t(2 * (q.max_ns / 1000000ull)) : 0u;
   PA.start_s = q.start_s;
   PA.end_s = q.end_s;
   // LDS: the record buffer is sized so that one workgroup takes more than half a CU. The
@@ -914,6 +972,10 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = per[i];
   }
   out.scan_bytes += uint64_t(W) * 4 + kept * 32;  // + workgroup counts, + id/start/end of each record
+  // (the caller counted 4 B of duration + 8 B of start / end per entry; these kernels read
+  // the 4 B ds column (duration | span) + the 4 B start column when both filters are on)
+  if (has_dur && q.has_range)
+    for (const auto &sg : segs) out.scan_bytes -= 4ull * (sg.n - sg.e0);
   tr.mark("post");
   return true;
 }

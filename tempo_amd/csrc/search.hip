@@ -2054,7 +2054,8 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   if (!seg_fits(seg)) seg = 0;
   // ---- pool path: narrow searches (search_pool_kernel); falls through to the
   // segment / look-back paths below when a workgroup's matches overflow its LDS buffer
-  if (fast && narrow && !dc.seg_off && !dc.pool_off) {
+  const bool ds16 = (!q.has_min || q.min_ns <= kDs16MaxMs * 1000000ull) && (!q.has_max || q.max_ns <= kDs16MaxMs * 1000000ull);
+  if (fast && narrow && ds16 && !dc.seg_off && !dc.pool_off) {
     if (dc.pool_skip) dc.pool_skip--;
     else if (pool_search(dc, blocks, q, limit, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out)) {
       if (ranges) drop_before_ranges(blocks, *ranges, out);

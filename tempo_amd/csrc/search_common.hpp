@@ -60,6 +60,10 @@ __device__ __forceinline__ const __attribute__((address_space(1))) T *G(const vo
   return (const __attribute__((address_space(1))) T *)(p);
 }
 
+// The pool kernels' compact duration column (devctx.hip, ds = D16 | span16 << 16): D16 =
+// 2 x whole ms + (a sub-ms remainder), saturated at 0xffff, is exact for duration bounds up
+// to this many ms (larger bounds take the other search paths)
+constexpr uint64_t kDs16MaxMs = 32767;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // (tile registers are kept as 128-bit vectors, not 4 scalars: a quad returned by one

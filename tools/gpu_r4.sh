@@ -58,5 +58,5 @@ if has pmc; then
     [ $rc -eq 0 ] || exit $rc
   done
   python3 tools/pmc_summary.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE --out gpurun_out/pmc_traffic.json \
-    --workload "${PMC_WORKLOAD:-blocks=10,entries=1000000,sets=4}" --source "${PMC_SOURCE:-gpu_r4.sh pmc}" | tee gpurun_out/pmc_summary.txt
+    --workload "${PMC_WORKLOAD:-blocks=10,entries=1000000,sets=4,layout=ds}" --source "${PMC_SOURCE:-gpu_r4.sh pmc}" | tee gpurun_out/pmc_summary.txt
 fi

@@ -35,3 +35,14 @@ if has ab; then  # A/B of library builds on the main line: $AB_VARIANTS (dirs ho
   done
   unset TSG_LIB_PATH
 fi
+if has stamps; then  # workgroup stamps of the main-line kernel, per library variant
+  mkdir -p /tmp/abw
+  for v in ${AB_VARIANTS:-ab_old new}; do
+    if [ $v = new ]; then unset TSG_LIB_PATH; else export TSG_LIB_PATH=$PWD/$v/libtsg.so; fi
+    TSG_STAMPS=1 timeout -k 10 300 python -u bench.py --workdir /tmp/abw --steps 16 --warmup 8 --cfg3 0 --cfg4 0 --cfg5 0 \
+      --shim-steps 0 --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --parity 0 --limit-steps 0 ${BENCH_ARGS:-} > gpurun_out/st_$v.json 2> gpurun_out/st_$v.err
+    rc=$?; [ $rc -eq 0 ] || { echo "stamps $v rc=$rc"; tail -3 gpurun_out/st_$v.err; exit $rc; }
+    echo "== $v"; grep "\[tsg\]" gpurun_out/st_$v.err | tail -6
+  done
+  unset TSG_LIB_PATH
+fi
