@@ -167,33 +167,6 @@ __device__ __forceinline__ uint32_t unit_mask(const u32x4 (&d)[kSteps], const u3
 // counted by vmcnt. (asm memory clobber: no LDS access moves across it)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// PoolBlk b of the kernel arguments into LDS, by scalar loads (wave-uniform b): lane j
-// writes word j
-__device__ __forceinline__ void stage_blk(const PoolBlk *src, PoolBlk *dst, uint32_t b, int lane) {
-  const uint32_t *sw = reinterpret_cast<const uint32_t *>(src + b);
-  uint32_t x = 0;
-#pragma unroll
-  for (int j = 0; j < 16; j++) {
-    const uint32_t v = sw[j];
-    x = lane == j ? v : x;
-  }
-  if (lane < 16) reinterpret_cast<uint32_t *>(dst + b)[lane] = x;
-}
-// the launch's value-set bitmaps (kArgBms x 8 words) into LDS the same way, 8 bitmaps per
-// pass of a wave (lane 8i + j: word j of bitmap i)
-__device__ __forceinline__ void stage_bms(const uint32_t (*bms)[8], uint32_t *s_bm, uint32_t wv, uint32_t nwv, int lane) {
-  for (uint32_t g = wv; g < uint32_t(kArgBms) / 8; g += nwv) {
-    const uint32_t *sw = bms[8 * g];
-    uint32_t x = 0;
-#pragma unroll
-    for (int j = 0; j < 64; j++) {
-      const uint32_t v = sw[j];
-      x = lane == j ? v : x;
-    }
-    s_bm[64 * g + uint32_t(lane)] = x;
-  }
-}
-
 // End seconds of a unit's entries: start + span from the ds column, or, in a unit where some
 // entry's span did not fit 16 bits (ends 18 h or more after the start, or before it: the
 // escape 0xffff), the exact end column for the whole unit (rare: a wave-uniform branch).
@@ -256,27 +229,30 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
         R.tv[q][k] = stream1<NTL>(B.col[q], uint64_t(R.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
     }
   };
+  // the staging's kernel-argument words first, by vector loads issued ahead of the units'
+  // loads: vector loads complete in issue order, so the wait for these (before the LDS
+  // writes below) does not wait for the burst of unit loads behind them. The units' loads
+  // are unconditional (a wave without a unit reloads unit 0), so the compiler's count of the
+  // loads issued after these is the same on every path.
+  const uint32_t *blk_words = reinterpret_cast<const uint32_t *>(A.blk);
+  const uint32_t xblk = uint32_t(tid) < nsegs * 16 ? blk_words[tid] : 0u;
+  const uint32_t xub = uint32_t(tid) < nsegs ? A.blk[tid].ubase : units;
+  const uint32_t xbm = tid < kArgBms * 8 ? reinterpret_cast<const uint32_t *>(A.bms)[tid] : 0u;
   const bool pre0 = wv < S, pre1 = wv + nwv < S;
   uint32_t ua = kPoolNone, ub = kPoolNone;
-  if (pre0 && uint64_t(w) * S + wv < units) {
-    ua = w * S + wv;
-    load_arg(ra, ua);
-  }
-  if (pre1 && uint64_t(w) * S + wv + nwv < units) {
-    ub = w * S + wv + nwv;
-    load_arg(rb, ub);
-  }
+  if (pre0 && uint64_t(w) * S + wv < units) ua = w * S + wv;
+  if (pre1 && uint64_t(w) * S + wv + nwv < units) ub = w * S + wv + nwv;
+  load_arg(ra, ua != kPoolNone ? ua : 0u);
+  load_arg(rb, ub != kPoolNone ? ub : 0u);
   // ---- stage the launch's tables (scalar loads of the kernel arguments; the barrier does not
   // wait for the units' loads above)
   {
-    for (uint32_t b = wv; b < nsegs; b += nwv) {
-      stage_blk(A.blk, s_blk, b, lane);
-      if (lane == 0) s_ub[b] = A.blk[b].ubase;
-    }
-    stage_bms(A.bms, s_bm, wv, nwv, lane);
+    static_assert(kArgSegs * 16 <= kPoolThreads && kArgBms * 8 <= kPoolThreads, "one staging word per thread");
+    if (uint32_t(tid) < nsegs * 16) reinterpret_cast<uint32_t *>(s_blk)[tid] = xblk;
+    if (uint32_t(tid) <= nsegs) s_ub[tid] = xub;
+    if (tid < kArgBms * 8) s_bm[tid] = xbm;
     for (uint32_t i = tid; i < kPoolChunks; i += blockDim.x) s_chunk[i] = kPoolPending;
     if (tid == 0) {
-      s_ub[nsegs] = units;
       s_next = min(2 * nwv, S);  // (the claims below it are the waves' first two)
       s_nrec = 0;
       if (w == 0) __hip_atomic_store(A.head_next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -566,14 +542,16 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
       d[5] = nm;
     }
   };
-  // the first unit's loads go out before anything is staged
+  // the bitmap words by vector loads issued ahead of the first unit's loads (in-order
+  // completion: their wait does not wait for those); the first unit's loads are
+  // unconditional (a wave without units reloads the launch's last unit), so every path issues
+  // the same loads after these
+  const uint32_t xbm = tid < kArgBms * 8 ? reinterpret_cast<const uint32_t *>(A.bms)[tid] : 0u;
   Regs ra, rb;
   uint32_t u = u_begin, ba = b, bb = b;
-  if (u < u_end) {
-    load(ra, u);
-    ba = b;
-  }
-  stage_bms(A.bms, s_bm, wave, nwv, lane);
+  load(ra, u < u_end ? u : (units ? units - 1 : 0u));
+  ba = b;
+  if (tid < kArgBms * 8) s_bm[tid] = xbm;
   if (tid == 0) s_nrec = 0;
   lds_barrier();  // (not waiting for the first unit's loads)
   unsigned long long *const stamps = A.stamps;
