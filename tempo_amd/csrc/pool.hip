@@ -167,25 +167,23 @@ __device__ __forceinline__ uint32_t unit_mask(const u32x4 (&d)[kSteps], const u3
 // counted by vmcnt. (asm memory clobber: no LDS access moves across it)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// End seconds of a unit's entries: start + span from the ds column, or, in a unit where some
-// entry's span did not fit 16 bits (ends 18 h or more after the start, or before it: the
-// escape 0xffff), the exact end column for the whole unit (rare: a wave-uniform branch).
+// End seconds of a unit's entries: start + span from the ds column, or, for a lane's four
+// entries of a step where some span did not fit 16 bits (ends 18 h or more after the start,
+// or before it: the escape 0xffff, e.g. the end = 0 entries of pitfall P1), those four from
+// the exact end column (rare; only the lanes that need them load: a unit-wide reload moved
+// 16 MB more per config-2 query, the PMC count in profiles/r04_final).
 template <bool NTL>
 __device__ __forceinline__ void unit_ends(const u32x4 (&ds)[kSteps], const u32x4 (&sv)[kSteps], u32x4 (&ev)[kSteps],
                                           const uint32_t *scan, uint32_t npad, uint32_t e0, int lane) {
-  bool esc = false;
 #pragma unroll
   for (int k = 0; k < kSteps; k++) {
     const uint32_t sp[4] = {ds[k].x >> 16, ds[k].y >> 16, ds[k].z >> 16, ds[k].w >> 16};
-    esc = esc || sp[0] == 0xffffu || sp[1] == 0xffffu || sp[2] == 0xffffu || sp[3] == 0xffffu;
+    const bool esc = sp[0] == 0xffffu || sp[1] == 0xffffu || sp[2] == 0xffffu || sp[3] == 0xffffu;
     ev[k].x = sv[k].x + sp[0];
     ev[k].y = sv[k].y + sp[1];
     ev[k].z = sv[k].z + sp[2];
     ev[k].w = sv[k].w + sp[3];
-  }
-  if (__ballot(esc)) {
-#pragma unroll
-    for (int k = 0; k < kSteps; k++) ev[k] = stream4<NTL>(scan + 2ull * npad, uint64_t(e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
+    if (esc) ev[k] = stream4<NTL>(scan + 2ull * npad, uint64_t(e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
   }
 }
 

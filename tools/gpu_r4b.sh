@@ -46,3 +46,19 @@ if has stamps; then  # workgroup stamps of the main-line kernel, per library var
   done
   unset TSG_LIB_PATH
 fi
+if has wave0; then  # the limit-20 legs at several first-wave sizes (TSG_LIMIT_WAVE0)
+  mkdir -p /tmp/abw
+  for wz in ${WAVE0S:-2097152 1048576 524288}; do
+    TSG_LIMIT_WAVE0=$wz timeout -k 10 300 python -u bench.py --workdir /tmp/abw --steps 50 --warmup 10 --cfg4 0 --cfg5 0 \
+      --shim-steps 0 --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --parity 0 --limit-steps 200 ${BENCH_ARGS:-} > gpurun_out/w0_$wz.json 2> gpurun_out/w0_$wz.err
+    rc=$?; [ $rc -eq 0 ] || { echo "wave0 $wz rc=$rc"; tail -3 gpurun_out/w0_$wz.err; exit $rc; }
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); l=d['limit20']; c=d.get('cfg3',{}).get('limit20',{}); print('wave0', sys.argv[2], 'lim20 step mean %.1f p50 %.1f kernel mean %.2f' % (l['step_us']['mean'], l['step_us']['p50'], l['kernel_us']['mean']), 'cfg3 first20 p50 %.1f mean %.1f' % (c.get('time_to_first_20_us',{}).get('p50',0), c.get('time_to_first_20_us',{}).get('mean',0)))" gpurun_out/w0_$wz.json $wz
+  done
+fi
+if has limstamps; then  # workgroup stamps of the limit-20 first wave (static kernel)
+  mkdir -p /tmp/abw
+  TSG_STAMPS=1 timeout -k 10 300 python -u bench.py --workdir /tmp/abw --steps 2 --warmup 1 --cfg3 0 --cfg4 0 --cfg5 0 \
+    --shim-steps 0 --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --parity 0 --limit-steps 12 ${BENCH_ARGS:-} > gpurun_out/ls.json 2> gpurun_out/ls.err
+  rc=$?; [ $rc -eq 0 ] || { echo "limstamps rc=$rc"; tail -3 gpurun_out/ls.err; exit $rc; }
+  grep "\[tsg\]" gpurun_out/ls.err | tail -8
+fi
