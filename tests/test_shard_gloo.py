@@ -257,7 +257,7 @@ def test_gloo_merge_one_million_per_rank():
     """pack + gloo gather + merge of 1 M records per rank with no
     per-record Python (the rank's response is packed into one numpy wire buffer, gathered
     as one tensor, merged in libtsg). TSG_MERGE_BOUND_MS sets the bound: 100 when run on the
-    GPU box's host (a CPU-only pytest process there, profiles/r03_merge/), 2000 by default in
+    GPU box's host (a CPU-only pytest process there: profiles/r04_merge/), 2000 by default in
     the build container, whose 8 shared CPUs sort 2 M u64 in ~35 ms with numpy alone."""
     n = 1_000_000
     r = run_merge_perf(n)
