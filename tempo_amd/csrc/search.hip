@@ -297,15 +297,23 @@ __device__ __forceinline__ void wave_sync() {
 
 // kStreamWg waves per workgroup, each on its own span with its own LDS (no barriers: a
 // one-wave workgroup per span would cap a CU at its workgroup slots, half the wave slots)
+//
+// A step's candidates (starts where the tested needle bytes all match) are appended to the
+// wave's LDS list in scan order; the list is verified and mapped to values in batches of 64
+// (one candidate per lane: the needle compared from global memory, L2-resident after the
+// stream read it; the start's value found by a wave-wide 64-ary search plus the offsets
+// around it staged in LDS). Verifying inline cost a whole wave iteration per candidate with
+// one or two lanes active, on nearly every step of a dense needle (db.statement "from orders").
+constexpr uint32_t kCandMax = 512;  // >= half a step's 64 x 16 starts: a step always fits after a flush, in two halves at worst
 extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(const StreamJob *jobs, uint32_t njobs,
                                                                                  const uint8_t *needles, uint8_t *vmatch,
                                                                                  uint32_t span, uint32_t nwaves) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_win_all[kStreamWg][2048 + 16];
-  __shared__ uint32_t s_ndw_all[kStreamWg][kStreamMaxNeedle / 4 + 1];  // needle bytes 2.. as words
+  __shared__ uint32_t s_cand_all[kStreamWg][kCandMax];                  // candidate starts - s0, ascending
+  __shared__ uint32_t s_ndw_all[kStreamWg][kStreamMaxNeedle / 4 + 1];  // the needle as words
   __shared__ uint32_t s_off_all[kStreamWg][kStreamOffs + 1];
   const int lane = threadIdx.x & 63;
   const uint32_t wid = uint32_t(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
-  uint8_t *const s_win = s_win_all[wid];
+  uint32_t *const s_cand = s_cand_all[wid];
   uint32_t *const s_ndw = s_ndw_all[wid];
   uint32_t *const s_off = s_off_all[wid];
   const uint32_t w = blockIdx.x * kStreamWg + wid;
@@ -321,12 +329,11 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
   const uint64_t qlo = max<uint64_t>(s0, J.lead);
   const uint64_t qhi = min<uint64_t>(s0 + span, end >= nl ? end - nl + 1 : 0);
   if (qlo >= qhi) return;
-  // the needle past its first two bytes as little-endian words (zero past its end): a
-  // candidate is verified 4 bytes per LDS round trip instead of 1
-  for (uint32_t i = lane; 4 * i + 2 < nl; i += 64) {
+  // the needle as little-endian words (zero past its end)
+  for (uint32_t i = lane; 4 * i < nl; i += 64) {
     uint32_t x = 0;
     for (uint32_t b = 0; b < 4; b++)
-      if (4 * i + 2 + b < nl) x |= uint32_t(needles[J.needle_off + 4 * i + 2 + b]) << (8 * b);
+      if (4 * i + b < nl) x |= uint32_t(needles[J.needle_off + 4 * i + b]) << (8 * b);
     s_ndw[i] = x;
   }
   const uint32_t n0 = uint32_t(needles[J.needle_off]) * 0x01010101u;
@@ -337,21 +344,99 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
   const uint32_t pq = pj >> 2, ps = pj & 3u;
   // a: aligned coordinate of this lane's 16 bytes. Past the stream's last 16-byte chunk
   // the load repeats that chunk: bytes past `end` only ever form starts >= qhi (dropped) and
-  // are never compared, and an unconditional load keeps the compiler's waits exact (a
-  // conditional one makes the zero on the other path wait for the load in flight).
+  // are never compared.
   const uint64_t last16 = (end - 1) & ~uint64_t(15);
+  const uint64_t last4 = (end - 1) & ~uint64_t(3);  // (verification's dword loads stay inside the value bytes)
   auto load16 = [&](uint64_t a) -> u32x4 { return ring_load(J.base + min(a, last16)); };
-  // value offsets of the values around the window: s_off[i] = off[vb + i]
-  uint32_t vb = value_at(J.off, 0, J.nvals + 1, qlo - J.lead, lane), kv = 0;
-  uint64_t cover = 0;  // starts p < cover map through s_off
-  auto stage_offs = [&](uint32_t v) {
-    vb = v;
-    kv = min<uint32_t>(kStreamOffs, J.nvals - v);
-    for (uint32_t i = lane; i <= kv; i += 64) s_off[i] = G(J.off)[v + i];
-    cover = kv == J.nvals - v ? ~0ull : uint64_t(G(J.off)[v + kv]);
+  wave_sync();
+  uint32_t ncand = 0;   // (wave-uniform) candidates in the list
+  uint64_t mdone = 0;   // (wave-uniform) starts below this lie in a value the wave has marked
+  uint32_t vlo = 0;     // (wave-uniform) no value before it holds a start not yet verified
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // verify the list's candidates, map the matches to their values, mark them; empties the list
+  auto flush = [&]() {
+    // every ring load has arrived before anything here may move a ring register (a copy of a
+    // register whose load is still in flight would read the old bytes); flushes are rare
+    ring_drain();
+    wave_sync();
+    for (uint32_t b0 = 0; b0 < ncand; b0 += 64) {
+      const uint32_t nb = min(64u, ncand - b0);
+      const bool act = uint32_t(lane) < nb;
+      const uint64_t q = s0 + s_cand[b0 + (act ? uint32_t(lane) : 0u)];
+      bool ok = act && q >= qlo && q < qhi && q >= mdone;
+      // the needle from global memory, 16 bytes per round trip (five dword loads issued together)
+      const uint64_t qa = q & ~uint64_t(3);
+      const uint32_t sh = uint32_t(q & 3);
+      for (uint32_t k = 0; 4 * k < nl; k += 4) {
+        if (__ballot(ok) == 0) break;
+        uint32_t dw[5];
+#pragma unroll
+        for (uint32_t u = 0; u < 5; u++) dw[u] = *G<uint32_t>(J.base + min(qa + 4 * (k + u), last4));
+        uint32_t bad = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+          if (4 * (k + u) < nl) {  // (nl wave-uniform)
+            const uint32_t x = __builtin_amdgcn_alignbyte(dw[u + 1], dw[u], sh);
+            const uint32_t rem = nl - 4 * (k + u);
+            const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
+            bad |= (x ^ s_ndw[k + u]) & m;
+          }
+        }
+        ok = ok && bad == 0;
+      }
+      const uint64_t okb = __ballot(ok);
+      if (okb) {
+        // the values of the batch's verified starts: the first one's by a 64-ary search from vlo,
+        // then the offsets from there staged in LDS (a batch of a dense needle spans a few dozen
+        // values); a start past the staged ones searches the global offsets
+        const int f = __builtin_ctzll(okb);
+        const uint64_t pf = uint64_t(__builtin_amdgcn_readlane(uint32_t(q - J.lead), f)) |
+                            (uint64_t(__builtin_amdgcn_readlane(uint32_t((q - J.lead) >> 32), f)) << 32);
+        const uint32_t v0 = value_at(J.off, vlo, J.nvals + 1, pf, lane);
+        const uint32_t kv = min<uint32_t>(kStreamOffs, J.nvals - v0);
+        for (uint32_t i = lane; i <= kv; i += 64) s_off[i] = G(J.off)[v0 + i];
+        wave_sync();
+        const uint64_t p = q - J.lead;
+        uint32_t v = 0;
+        uint64_t vend = 0;
+        if (ok) {
+          if (p < uint64_t(s_off[kv]) || kv == J.nvals - v0) {
+            uint32_t lo = 0, hi = kv;
+            while (hi - lo > 1) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (uint64_t(s_off[mid]) <= p) lo = mid;
+              else hi = mid;
+            }
+            v = v0 + lo;
+            vend = s_off[lo + 1];
+          } else {
+            uint32_t lo = v0 + kv, hi = J.nvals;
+            while (hi - lo > 1) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (uint64_t(G(J.off)[mid]) <= p) lo = mid;
+              else hi = mid;
+            }
+            v = lo;
+            vend = G(J.off)[v + 1];
+          }
+          if (p + nl <= vend) vmatch[J.vmatch_base + v] = 1;  // (a match that runs into the next value does not count)
+          else ok = false;
+        }
+        // later starts inside the furthest marked value add nothing; no later start lies before v0
+        const uint64_t mb = __ballot(ok);
+        if (mb) {
+          const int hl = 63 - __builtin_clzll(mb);
+          const uint64_t e = vend + J.lead;
+          mdone = max(mdone, uint64_t(__builtin_amdgcn_readlane(uint32_t(e), hl)) |
+                                 (uint64_t(__builtin_amdgcn_readlane(uint32_t(e >> 32), hl)) << 32));
+        }
+        vlo = v0;
+        wave_sync();
+      }
+    }
+    ncand = 0;
+    wave_sync();
   };
-  stage_offs(vb);
-  __builtin_amdgcn_s_waitcnt(kWaitVm0);
   uint64_t cq = s0;
   // Ring slots: the window's two KiB + kStreamAhead KiB in flight. The step loop is unrolled
   // over the slots so each slot keeps its register (a rotation by moves waits for every
@@ -361,8 +446,6 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
   u32x4 ring[kRing];
 #pragma unroll
   for (int k = 0; k < kRing; k++) ring[k] = load16(cq + uint64_t(k) * 1024 + lane * 16);
-  uint32_t last_v = 0xffffffffu;  // this lane's last marked value (skips repeats)
-  uint64_t mdone = 0;  // (wave-uniform) starts below this lie in a value the wave has marked
   // one 1 KiB step of start positions [c, c + 1024): cur = its bytes, nxt = the next KiB
   auto step = [&](const uint64_t c, const u32x4 cur, const u32x4 nxt) {
     // the needle's first two bytes at all 16 start positions of this lane, in registers:
@@ -415,117 +498,33 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     // starts inside a value this wave already marked add nothing
     if (c + uint64_t(lane) * 16 + 16 <= mdone) cm = 0;
     else if (c + uint64_t(lane) * 16 < mdone) cm &= ~0u << uint32_t(mdone - c - uint64_t(lane) * 16);
-    if (__ballot(cm != 0) == 0) return;
-    wave_sync();  // (previous window's readers done)
-    reinterpret_cast<u32x4 *>(s_win)[lane] = cur;
-    reinterpret_cast<u32x4 *>(s_win)[64 + lane] = nxt;
-    // the offsets must cover every start of this window
-    const uint64_t wlast = min<uint64_t>(c + 1024, qhi) - 1 - J.lead;
-    const uint64_t pfirst = max<uint64_t>(c, qlo) - J.lead;
-    if (cover != ~0ull && wlast >= cover) {
-      // staged values [vb, vb + kv) that start at or before pfirst
-      const uint32_t k1 = uint32_t(__popcll(__ballot(uint32_t(lane) < kv && uint64_t(s_off[lane]) <= pfirst))) +
-                          uint32_t(__popcll(__ballot(uint32_t(lane) + 64 < kv && uint64_t(s_off[64 + lane]) <= pfirst)));
-      const bool beyond = k1 == kv && uint64_t(s_off[kv]) <= pfirst;
-      wave_sync();
-      const uint32_t v = beyond ? value_at(J.off, vb + kv, J.nvals + 1, pfirst, lane) : vb + k1 - 1;
-      stage_offs(v);
-      // (rare: every ~kStreamOffs values) leave no load of this branch in flight
-      __builtin_amdgcn_s_waitcnt(kWaitVm0);
-    }
-    wave_sync();
-    // candidates: verify from LDS, map the start to its value, mark the value. When the
-    // staged offsets cover every start of the window (the usual case: a uniform branch) the
-    // loop touches LDS only; a window past the staged values (a run of tiny values) searches
-    // the global offsets instead.
-    uint64_t mend = 0;  // end (aligned coordinates) of the last value this lane marked
-    auto candidates = [&](auto global_tag) {
-      constexpr bool kGlobal = decltype(global_tag)::value;
-      // staged values that hold the window's starts: [wlo, whi) (a start maps by a binary
-      // search of those few, not of all kStreamOffs)
-      uint32_t wlo = 0, whi = kv;
-      if (!kGlobal) {
-        const uint32_t a = s_off[lane], b = s_off[64 + lane];
-        wlo = uint32_t(__popcll(__ballot(uint32_t(lane) < kv && uint64_t(a) <= pfirst))) +
-              uint32_t(__popcll(__ballot(uint32_t(lane) + 64 < kv && uint64_t(b) <= pfirst))) - 1;
-        whi = uint32_t(__popcll(__ballot(uint32_t(lane) < kv && uint64_t(a) <= wlast))) +
-              uint32_t(__popcll(__ballot(uint32_t(lane) + 64 < kv && uint64_t(b) <= wlast)));
-      }
-      const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
-      while (cm) {
-        const uint32_t jb = uint32_t(__builtin_ctz(cm));
-        cm &= cm - 1;
-        const uint32_t wo = uint32_t(lane) * 16 + jb;  // window offset of the start
-        const uint64_t q = c + wo;
-        if (q < qlo || q >= qhi) continue;
-        // needle bytes 2.. compared 4 words (16 bytes) per LDS round trip
-        bool ok = true;
-        for (uint32_t k = 0; ok && 4 * k + 2 < nl; k += 4) {
-          uint32_t bad = 0;
+    // append the step's candidates to the list (a lane's in start order, lanes in order):
+    // each lane's place from the bit planes of the per-lane counts
+    const uint32_t mine = uint32_t(__popc(cm));
+    uint32_t pre = 0, tot = 0;
 #pragma unroll
-          for (uint32_t u = 0; u < 4; u++) {
-            const uint32_t kk = k + u;
-            if (4 * kk + 2 < nl) {  // (nl wave-uniform)
-              const uint32_t off = wo + 2 + 4 * kk;  // (< 2048: wo < 1024, nl <= 1024; the next word is padding)
-              const uint32_t x = __builtin_amdgcn_alignbyte(w32[(off >> 2) + 1], w32[off >> 2], off & 3);
-              const uint32_t rem = nl - 2 - 4 * kk;
-              const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
-              bad |= (x ^ s_ndw[kk]) & m;
-            }
-          }
-          ok = bad == 0;
-        }
-        if (!ok) continue;
-        const uint64_t p = q - J.lead;
-        uint32_t v;
-        uint64_t vend;
-        if (!kGlobal || p < cover) {  // in the staged offsets: s_off[lo] <= p < s_off[lo + 1]
-          uint32_t lo = wlo, hi = whi;
-          while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (uint64_t(s_off[mid]) <= p) lo = mid;
-            else hi = mid;
-          }
-          v = vb + lo;
-          vend = s_off[lo + 1];
-        } else {
-          uint32_t lo = vb, hi = J.nvals;
-          while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (uint64_t(G(J.off)[mid]) <= p) lo = mid;
-            else hi = mid;
-          }
-          v = lo;
-          vend = G(J.off)[v + 1];
-        }
-        if (p + nl > vend) continue;  // the match runs into the next value
-        if (v != last_v) {
-          vmatch[J.vmatch_base + v] = 1;
-          last_v = v;
-        }
-        // the rest of this lane's starts inside the same value add nothing
-        const uint64_t skip = vend + J.lead;  // aligned coordinate of the value's end
-        mend = skip;
-        if (skip > q + 1) {
-          const uint64_t rel = skip - (c + uint64_t(lane) * 16);
-          cm &= rel >= 16 ? 0u : ~((1u << uint32_t(rel)) - 1u);
-        }
-      }
-    };
-    if (cover == ~0ull || wlast < cover) {
-      candidates(std::false_type{});
-    } else {
-      candidates(std::true_type{});
-      __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    for (int b = 0; b < 5; b++) {
+      const uint64_t bal = __ballot((mine >> b) & 1u);
+      pre += uint32_t(__popcll(bal & below)) << b;
+      tot += uint32_t(__popcll(bal)) << b;
     }
-    // the highest lane that marked a value holds the furthest end: later starts before it
-    // are skipped (the values' ends increase with the lane)
-    const uint64_t marked = __ballot(mend != 0);
-    if (marked) {
-      const int hl = 63 - __builtin_clzll(marked);
-      const uint64_t e = (uint64_t(__builtin_amdgcn_readlane(uint32_t(mend >> 32), hl)) << 32) |
-                         __builtin_amdgcn_readlane(uint32_t(mend), hl);
-      mdone = max(mdone, e);
+    if (tot == 0) return;
+    if (ncand + tot > kCandMax) flush();
+    auto append = [&](bool mine_now, uint32_t base) {
+      uint32_t at = ncand + pre - base;
+      if (mine_now)
+        for (uint32_t m = cm; m; m &= m - 1) s_cand[at++] = uint32_t(c - s0) + uint32_t(lane) * 16 + uint32_t(__builtin_ctz(m));
+    };
+    if (tot <= kCandMax) {
+      append(true, 0);
+      ncand += tot;
+    } else {  // (more than kCandMax starts in one KiB, e.g. "aa" in a run of a's: lanes 0-31, then 32-63)
+      const uint32_t half = uint32_t(__builtin_amdgcn_readlane(pre, 32));
+      append(lane < 32, 0);
+      ncand += half;
+      flush();
+      append(lane >= 32, half);
+      ncand += tot - half;
     }
   };
   for (; cq < qhi; cq += uint64_t(kRing) * 1024) {
@@ -539,6 +538,7 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     }
   }
   ring_drain();  // (no load of the ring outlives the wave)
+  if (ncand) flush();
 }
 
 // ------------------------------------------------------------------------------------

@@ -107,3 +107,25 @@ def test_stream_two_terms_and_lane_path_agree(engine, dict_blocks):
         for b in ba + bb:
             b.close()
         lane.close()
+
+
+def test_stream_every_start_a_candidate(engine, tmp_path):
+    """Values that are long runs of one byte: with the needle "aa" every start of a KiB is a
+    candidate (1024 per step, more than the wave's candidate list takes at once: the step
+    appends in two halves around a flush), "aab" makes them all fail verification but the
+    last, and "ba" sits at run boundaries."""
+    rng = random.Random(5)
+    ents = []
+    ids = sorted({bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(1500)})
+    for i, tid in enumerate(ids):
+        n = rng.randrange(200, 3000)
+        st = "a" * n if i % 3 else "a" * (n // 2) + "b" + "a" * (n // 2)
+        start = 1_700_000_000 * 10**9 + rng.randrange(3600 * 10**9)
+        ents.append({"id": tid, "start": start, "end": start + 1000, "tags": {"db.statement": [st]}})
+    path = write_block(str(tmp_path), "runs", ents, page_size=256 << 10)
+    blk = engine.open_block(path)
+    try:
+        for nd in ("aa", "aaa", "aab", "ba", "aaaaaaaaaaaaaaaaaaaab", "a" * 300):
+            assert check(engine, [blk], [path], {"db.statement": nd})
+    finally:
+        blk.close()

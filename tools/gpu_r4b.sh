@@ -62,3 +62,9 @@ if has limstamps; then  # workgroup stamps of the limit-20 first wave (static ke
   rc=$?; [ $rc -eq 0 ] || { echo "limstamps rc=$rc"; tail -3 gpurun_out/ls.err; exit $rc; }
   grep "\[tsg\]" gpurun_out/ls.err | tail -8
 fi
+if has cfg4prof; then  # host phases of the config-4 leg (TSG_PROF)
+  mkdir -p /tmp/abw
+  TSG_PROF=1 timeout -k 10 400 python -u bench.py --workdir /tmp/abw --steps 3 --warmup 1 --cfg3 0 --cfg5 0 --shim-steps 0 \
+    --limit-steps 0 --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --parity 0 --cfg4-steps 10 > gpurun_out/c4p.json 2> gpurun_out/c4p.err
+  rc=$?; echo "cfg4prof rc=$rc"; grep -v "^\[bench\]" gpurun_out/c4p.err | tail -6; [ $rc -eq 0 ] || exit $rc
+fi
