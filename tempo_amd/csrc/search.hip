@@ -304,7 +304,7 @@ __device__ __forceinline__ void wave_sync() {
 // stream read it; the start's value found by a wave-wide 64-ary search plus the offsets
 // around it staged in LDS). Verifying inline cost a whole wave iteration per candidate with
 // one or two lanes active, on nearly every step of a dense needle (db.statement "from orders").
-constexpr uint32_t kCandMax = 512;  // >= half a step's 64 x 16 starts: a step always fits after a flush, in two halves at worst
+constexpr uint32_t kCandMax = 1024;  // >= the 64 x 16 starts of one step: a step always fits after a flush
 extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(const StreamJob *jobs, uint32_t njobs,
                                                                                  const uint8_t *needles, uint8_t *vmatch,
                                                                                  uint32_t span, uint32_t nwaves) {
@@ -364,25 +364,18 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
       const bool act = uint32_t(lane) < nb;
       const uint64_t q = s0 + s_cand[b0 + (act ? uint32_t(lane) : 0u)];
       bool ok = act && q >= qlo && q < qhi && q >= mdone;
-      // the needle from global memory, 16 bytes per round trip (five dword loads issued together)
-      const uint64_t qa = q & ~uint64_t(3);
-      const uint32_t sh = uint32_t(q & 3);
-      for (uint32_t k = 0; 4 * k < nl; k += 4) {
+      // the needle, 4 bytes per round trip, from global memory (issuing 16 bytes' loads at once
+      // measured slower: profiles/r04_final, `tools/gpu_r4b.sh abcfg4`)
+      for (uint32_t k = 0; 4 * k < nl; k++) {
         if (__ballot(ok) == 0) break;
-        uint32_t dw[5];
-#pragma unroll
-        for (uint32_t u = 0; u < 5; u++) dw[u] = *G<uint32_t>(J.base + min(qa + 4 * (k + u), last4));
-        uint32_t bad = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
-          if (4 * (k + u) < nl) {  // (nl wave-uniform)
-            const uint32_t x = __builtin_amdgcn_alignbyte(dw[u + 1], dw[u], sh);
-            const uint32_t rem = nl - 4 * (k + u);
-            const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
-            bad |= (x ^ s_ndw[k + u]) & m;
-          }
-        }
-        ok = ok && bad == 0;
+        const uint64_t a = q + 4 * k;
+        const uint64_t a4 = a & ~uint64_t(3);
+        const uint32_t lo4 = *G<uint32_t>(J.base + min(a4, last4));
+        const uint32_t hi4 = *G<uint32_t>(J.base + min(a4 + 4, last4));
+        const uint32_t x = __builtin_amdgcn_alignbyte(hi4, lo4, uint32_t(a & 3));
+        const uint32_t rem = nl - 4 * k;
+        const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
+        ok = ok && ((x ^ s_ndw[k]) & m) == 0;
       }
       const uint64_t okb = __ballot(ok);
       if (okb) {
@@ -510,22 +503,9 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     }
     if (tot == 0) return;
     if (ncand + tot > kCandMax) flush();
-    auto append = [&](bool mine_now, uint32_t base) {
-      uint32_t at = ncand + pre - base;
-      if (mine_now)
-        for (uint32_t m = cm; m; m &= m - 1) s_cand[at++] = uint32_t(c - s0) + uint32_t(lane) * 16 + uint32_t(__builtin_ctz(m));
-    };
-    if (tot <= kCandMax) {
-      append(true, 0);
-      ncand += tot;
-    } else {  // (more than kCandMax starts in one KiB, e.g. "aa" in a run of a's: lanes 0-31, then 32-63)
-      const uint32_t half = uint32_t(__builtin_amdgcn_readlane(pre, 32));
-      append(lane < 32, 0);
-      ncand += half;
-      flush();
-      append(lane >= 32, half);
-      ncand += tot - half;
-    }
+    uint32_t at = ncand + pre;
+    for (uint32_t m = cm; m; m &= m - 1) s_cand[at++] = uint32_t(c - s0) + uint32_t(lane) * 16 + uint32_t(__builtin_ctz(m));
+    ncand += tot;
   };
   for (; cq < qhi; cq += uint64_t(kRing) * 1024) {
 #pragma unroll

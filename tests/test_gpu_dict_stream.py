@@ -111,9 +111,9 @@ def test_stream_two_terms_and_lane_path_agree(engine, dict_blocks):
 
 def test_stream_every_start_a_candidate(engine, tmp_path):
     """Values that are long runs of one byte: with the needle "aa" every start of a KiB is a
-    candidate (1024 per step, more than the wave's candidate list takes at once: the step
-    appends in two halves around a flush), "aab" makes them all fail verification but the
-    last, and "ba" sits at run boundaries."""
+    candidate (1024 per step: the wave's whole candidate list, flushed before the next step
+    appends), "aab" makes them all fail verification but the last, and "ba" sits at run
+    boundaries."""
     rng = random.Random(5)
     ents = []
     ids = sorted({bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(1500)})

@@ -68,3 +68,16 @@ if has cfg4prof; then  # host phases of the config-4 leg (TSG_PROF)
     --limit-steps 0 --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --parity 0 --cfg4-steps 10 > gpurun_out/c4p.json 2> gpurun_out/c4p.err
   rc=$?; echo "cfg4prof rc=$rc"; grep -v "^\[bench\]" gpurun_out/c4p.err | tail -6; [ $rc -eq 0 ] || exit $rc
 fi
+if has abcfg4; then  # A/B of library builds on the config-4 leg, interleaved
+  mkdir -p /tmp/abw
+  for k in 1 2; do
+    for v in ${AB_VARIANTS:-ab_old new}; do
+      if [ $v = new ]; then unset TSG_LIB_PATH; else export TSG_LIB_PATH=$PWD/$v/libtsg.so; fi
+      timeout -k 10 400 python -u bench.py --workdir /tmp/abw --steps 3 --warmup 1 --cfg3 0 --cfg5 0 --shim-steps 0 --limit-steps 0 \
+        --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --parity 0 --cfg4-steps 10 > gpurun_out/a4_${v}_$k.json 2> gpurun_out/a4_${v}_$k.err
+      rc=$?; [ $rc -eq 0 ] || { echo "abcfg4 $v rc=$rc"; tail -3 gpurun_out/a4_${v}_$k.err; exit $rc; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); q=d['cfg4']['queries']; print(sys.argv[2], ' '.join('%s %.0f/%.3f' % (n[:9], v['dict_pass_us']['p50'], v['dict_frac']) for n, v in q.items()))" gpurun_out/a4_${v}_$k.json $v
+    done
+  done
+  unset TSG_LIB_PATH
+fi
