@@ -233,7 +233,6 @@ constexpr uint64_t kStreamMinBytes = 1u << 20;  // smaller dictionaries: prep_ke
 constexpr uint32_t kStreamOffs = 128;           // value offsets staged per reload
 constexpr int kStreamAhead = 4;                 // KiB loaded ahead of the window, per wave
 constexpr uint32_t kStreamWg = 4;               // waves (independent spans) per workgroup
-constexpr int kWaitVm0 = 0x0F70;                // s_waitcnt vmcnt(0) (expcnt, lgkmcnt untouched)
 struct StreamJob {
   const uint8_t *base;  // 16-byte aligned: the dictionary bytes start at base + lead
   const uint32_t *off;  // value offsets, nvals + 1
@@ -251,14 +250,6 @@ constexpr uint32_t kStreamPairMax = 11;  // its bytes of a lane's 16 starts lie 
 
 // bit 7 of each byte of the result: that byte of x is non-zero (exact, no carries across bytes)
 __device__ __forceinline__ uint32_t nz_bytes(uint32_t x) { return (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u; }
-// bits 7/15/23/31 -> bits 0..3 (two rotations instead of a quarter-rate multiply)
-__device__ __forceinline__ uint32_t pack_hi_bits(uint32_t c) {
-  uint32_t x = c >> 7;                          // bits 0, 8, 16, 24
-  x |= __builtin_amdgcn_alignbit(x, x, 7);      // + 1 (<- 8), 17 (<- 24), ...
-  x |= __builtin_amdgcn_alignbit(x, x, 14);     // + 2 (<- 16), 3 (<- 17)
-  return x & 0xfu;
-}
-
 // largest v in [lo, hi) with off[v] <= p (off[lo] <= p < off[hi] or hi = nvals + 1): 64-ary search
 __device__ __forceinline__ uint32_t value_at(const uint32_t *off, uint32_t lo, uint32_t hi, uint64_t p, int lane) {
   while (hi - lo > 1) {
@@ -485,26 +476,36 @@ extern "C" __global__ void __launch_bounds__(64 * kStreamWg) dict_stream_kernel(
     for (int k = 0; k < 4; k++) any |= (xs[k] - 0x01010101u) & ~xs[k];
     // most steps hold no candidate in any lane: nothing else to do (a wave-uniform branch)
     if (__ballot((any & 0x80808080u) != 0) == 0) return;
-    uint32_t cm = 0;  // bit 4k + b: start 4k + b of this lane is a candidate (exact per byte)
+    // bit 7 of byte b of f[k]: start 4k + b of this lane is a candidate (exact per byte); starts
+    // inside a value the wave already marked are dropped when the list is verified
+    uint32_t f[4], mine = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) cm |= pack_hi_bits(nz_bytes(xs[k]) ^ 0x80808080u) << (4 * k);
-    // starts inside a value this wave already marked add nothing
-    if (c + uint64_t(lane) * 16 + 16 <= mdone) cm = 0;
-    else if (c + uint64_t(lane) * 16 < mdone) cm &= ~0u << uint32_t(mdone - c - uint64_t(lane) * 16);
-    // append the step's candidates to the list (a lane's in start order, lanes in order):
-    // each lane's place from the bit planes of the per-lane counts
-    const uint32_t mine = uint32_t(__popc(cm));
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int b = 0; b < 5; b++) {
-      const uint64_t bal = __ballot((mine >> b) & 1u);
-      pre += uint32_t(__popcll(bal & below)) << b;
-      tot += uint32_t(__popcll(bal)) << b;
+    for (int k = 0; k < 4; k++) {
+      f[k] = nz_bytes(xs[k]) ^ 0x80808080u;
+      mine += uint32_t(__popc(f[k]));
     }
-    if (tot == 0) return;
+    // append the step's candidates to the list (a lane's in start order, lanes in order): a
+    // lane's place is the count of the lanes below it (one ballot when no lane has two)
+    uint32_t pre, tot;
+    if (__ballot(mine > 1u) == 0) {
+      const uint64_t one = __ballot(mine != 0u);
+      pre = uint32_t(__popcll(one & below));
+      tot = uint32_t(__popcll(one));
+    } else {
+      pre = tot = 0;
+#pragma unroll
+      for (int b = 0; b < 5; b++) {
+        const uint64_t bal = __ballot((mine >> b) & 1u);
+        pre += uint32_t(__popcll(bal & below)) << b;
+        tot += uint32_t(__popcll(bal)) << b;
+      }
+    }
     if (ncand + tot > kCandMax) flush();
     uint32_t at = ncand + pre;
-    for (uint32_t m = cm; m; m &= m - 1) s_cand[at++] = uint32_t(c - s0) + uint32_t(lane) * 16 + uint32_t(__builtin_ctz(m));
+    const uint32_t rel = uint32_t(c - s0) + uint32_t(lane) * 16;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      for (uint32_t m = f[k]; m; m &= m - 1) s_cand[at++] = rel + 4 * k + (uint32_t(__builtin_ctz(m)) >> 3);
     ncand += tot;
   };
   for (; cq < qhi; cq += uint64_t(kRing) * 1024) {
