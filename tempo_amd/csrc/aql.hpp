@@ -1,0 +1,36 @@
+// aql.hpp — kernel dispatch straight onto an HSA queue of our own (AQL packets), for the
+// narrow search kernels whose per-query launch is on the step's critical path.
+//
+// The HIP launch call costs ~3.1-3.6 us of host time per launch (tools/probe/launch_probe.hip:
+// <<<>>> and hipModuleLaunchKernel alike); writing the packet ourselves costs the copy of the
+// argument words into device memory plus a few stores. The kernels come from a code object
+// of pool.hip built beside libtsg.so (libtsg_pool.co) and read no implicit kernel argument.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+namespace tsg {
+
+struct Aql;
+struct AqlKernel {
+  uint64_t kobj = 0;  // 0: not available
+  uint32_t group = 0, priv = 0, kernarg = 0;
+};
+// The device's dispatcher (hip_ordinal = the HIP device), or nullptr when unavailable:
+// TSG_AQL=0, no code object, or any HSA call failing (then the caller launches through HIP).
+Aql *aql_open(int hip_ordinal);
+void aql_close(Aql *a);
+// a kernel of the code object by its symbol name (without ".kd")
+AqlKernel aql_kernel(Aql *a, const char *name);
+// One dispatch of grid x block threads with dyn_lds bytes of dynamic LDS. The kernel's
+// argument block is assembled in a device-memory slot from `parts` (offset, bytes) of `args`
+// (only the parts the kernel reads for this launch: the rest of the slot is stale).
+void aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uint32_t dyn_lds, const void *args,
+                  const std::vector<std::pair<uint32_t, uint32_t>> &parts);
+// true once the last dispatch has completed (its packet's completion signal; for a caller's
+// liveness check while it polls the kernel's own completion words)
+bool aql_done(Aql *a);
+
+}  // namespace tsg

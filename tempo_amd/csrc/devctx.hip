@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstring>
 
+#include "aql.hpp"
 #include "devctx.hpp"
 
 namespace tsg {
@@ -52,6 +53,8 @@ void ctx_shutdown(Ctx &c) {
   for (auto &dc : c.devs) {
     (void)hipSetDevice(dc->ordinal);
     (void)hipStreamSynchronize(dc->stream);
+    aql_close(dc->aql);  // (waits for its queue to drain)
+    dc->aql = nullptr;
     for (DevBuf *b : {&dc->desc, &dc->vmatch, &dc->bitmaps, &dc->gran, &dc->ticket, &dc->out, &dc->regions,
                       &dc->seg_counts, &dc->hdr, &dc->err, &dc->maskbits, &dc->agg, &dc->stamps, &dc->gbm, &dc->lkhits,
                       &dc->done, &dc->steal, &dc->fpages, &dc->fhits, &dc->fres, &dc->farena, &dc->fcrc, &dc->fdst, &dc->foff,

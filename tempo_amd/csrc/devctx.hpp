@@ -12,6 +12,7 @@
 #include "engine.hpp"
 
 namespace tsg {
+struct Aql;  // aql.hpp
 
 #define HIP_OK(x)                                                                                   \
   do {                                                                                              \
@@ -159,6 +160,10 @@ struct DeviceCtx {
   // large dictionaries matched as one byte stream (dict_stream_kernel); 0: a lane per value
   bool dict_stream = env_u32("TSG_DICT_STREAM", 1, 0, 1) != 0;
   DevBuf pool_head;  // two dynamic-chunk counters (128 B apart): a launch uses one, zeroes the other
+  // untimed narrow-search launches as AQL packets on a queue of our own (aql.hpp); opened at
+  // the first narrow search, nullptr when unavailable (TSG_AQL=0: always through HIP)
+  Aql *aql = nullptr;
+  bool aql_tried = false;
   uint32_t pool_parity = 0;
   std::set<const void *> pool_attr;  // pool kernels whose dynamic LDS limit has been raised
   // TSG_PER_CU=k (1..16): scan workgroups per CU in the grid plan instead of the

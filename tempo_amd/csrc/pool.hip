@@ -5,8 +5,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
+#include <cstdio>
+#include <string>
 #include <cstring>
 
+#include "aql.hpp"
 #include "search_common.hpp"
 
 namespace tsg {
@@ -62,7 +66,10 @@ struct PoolArgs {
   // limit L > 0: a unit keeps its first L matches in scan order (a block's first L records lie
   // in the first L of each of its units; the host cuts each block to L): a dense limit query
   // hands over at most L records per unit instead of every match
-  uint32_t unit_cap, pad0;
+  uint32_t unit_cap;
+  // the launch shape, passed explicitly: the kernels read no implicit kernel argument (blockDim /
+  // gridDim come from them), so an AQL packet of our own needs none (aql.cpp)
+  uint32_t nthreads, ngroups, pad1;
 };
 static_assert(sizeof(PoolArgs) <= 4096, "kernel arguments");
 
@@ -199,7 +206,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = blockIdx.x, nsegs = A.nsegs, units = A.units;
   const uint32_t S = A.static_per_wg, L = A.lookahead, cs = A.chunk_shift;
-  const uint32_t wv = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6)), nwv = blockDim.x >> 6;
+  const uint32_t wv = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6)), nwv = A.nthreads >> 6;
   // ---- the first two units of a wave, before anything is staged: a wave's first two claims
   // are wv and wv + nwv (claims below S map to the workgroup's static run in order), so their
   // loads go out with the block found by a scalar walk over the kernel arguments (the claims'
@@ -249,7 +256,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
     if (uint32_t(tid) < nsegs * 16) reinterpret_cast<uint32_t *>(s_blk)[tid] = xblk;
     if (uint32_t(tid) <= nsegs) s_ub[tid] = xub;
     if (tid < kArgBms * 8) s_bm[tid] = xbm;
-    for (uint32_t i = tid; i < kPoolChunks; i += blockDim.x) s_chunk[i] = kPoolPending;
+    for (uint32_t i = tid; i < kPoolChunks; i += A.nthreads) s_chunk[i] = kPoolPending;
     if (tid == 0) {
       s_next = min(2 * nwv, S);  // (the claims below it are the waves' first two)
       s_nrec = 0;
@@ -420,7 +427,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
   const uint32_t nw = min(total, min(rec_cap, A.seg_cap)) * 6;
   if (nw) {
     auto *dst = reinterpret_cast<unsigned long long *>(A.recs) + uint64_t(w) * A.seg_cap * 6;
-    for (uint32_t i = tid; i < nw; i += blockDim.x) host_store(dst + i, s_rec[i]);
+    for (uint32_t i = tid; i < nw; i += A.nthreads) host_store(dst + i, s_rec[i]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -447,9 +454,9 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
   extern __shared__ __attribute__((aligned(16))) unsigned long long s_rec[];  // rec_cap x 6 words
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = blockIdx.x, nsegs = A.nsegs, units = A.units;
-  const uint32_t nwv = blockDim.x >> 6;
+  const uint32_t nwv = A.nthreads >> 6;
   const uint32_t wave = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6));
-  const uint32_t NW = gridDim.x * nwv, gw = w * nwv + wave;
+  const uint32_t NW = A.ngroups * nwv, gw = w * nwv + wave;
   const uint32_t u_begin = uint32_t(uint64_t(units) * gw / NW), u_end = uint32_t(uint64_t(units) * (gw + 1) / NW);
   // the wave's current block (all scalar)
   uint32_t b = 0;
@@ -587,7 +594,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
   const uint32_t nw = min(total, min(rec_cap, A.seg_cap)) * 6;
   if (nw) {
     auto *dst = reinterpret_cast<unsigned long long *>(A.recs) + uint64_t(w) * A.seg_cap * 6;
-    for (uint32_t i = tid; i < nw; i += blockDim.x) host_store(dst + i, s_rec[i]);
+    for (uint32_t i = tid; i < nw; i += A.nthreads) host_store(dst + i, s_rec[i]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -639,6 +646,13 @@ static PoolFn pick_static_t(uint32_t nterms, bool dur, bool range) {
 }
 static PoolFn pick_static(uint32_t nterms, bool dur, bool range, bool ntl) {
   return ntl ? pick_static_t<true>(nterms, dur, range) : pick_static_t<false>(nterms, dur, range);
+}
+// the device symbol of pick_pool / pick_static's kernel (Itanium mangling of the template)
+static std::string kernel_symbol(bool is_static, uint32_t nterms, bool dur, bool range, bool ntl) {
+  char b[128];
+  std::snprintf(b, sizeof b, "_ZN3tsg%s_kernelILi%uELb%dELb%dELb%dEEEvNS_8PoolArgsE",
+                is_static ? "20search_static" : "18search_pool", std::min(nterms, 4u), int(dur), int(range), int(ntl));
+  return b;
 }
 
 // One search_pool_kernel launch for a narrow search (every block scanned whole; a limit
@@ -717,7 +731,14 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   if (uint64_t(W) * rec_cap > (1u << 20)) return false;  // (record slots are 20-bit in the host's sort keys)
   PA.rec_cap = rec_cap;
   const size_t hdr = 256, cntb = align_up(size_t(W) * 4, 256);
-  if (dc.pool_head.ensure(256)) HIP_OK(hipMemsetAsync(dc.pool_head.p, 0, dc.pool_head.cap, s));  // then self-resetting
+  if (dc.pool_head.ensure(256)) {  // then self-resetting
+    HIP_OK(hipMemsetAsync(dc.pool_head.p, 0, dc.pool_head.cap, s));
+    HIP_OK(hipStreamSynchronize(s));  // (launches may go to the AQL queue, which does not follow this stream)
+  }
+  if (!dc.aql_tried) {
+    dc.aql_tried = true;
+    dc.aql = aql_open(dc.ordinal);
+  }
   unsigned *heads = static_cast<unsigned *>(dc.pool_head.p);
   static const bool want_stamps = std::getenv("TSG_STAMPS") != nullptr;
   if (want_stamps) {
@@ -734,11 +755,14 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     dc.pool_attr.insert(reinterpret_cast<const void *>(fn));
   }
   const uint32_t threads = 64 * dc.pool_waves;
+  PA.nthreads = threads;
+  PA.ngroups = W;
   const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
   hipEvent_t e0 = dc.es0, e1 = dc.es1;
   const bool defer = !time_scan && (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
   uint32_t *counts = nullptr;
   const uint8_t *recs = nullptr;
+  bool via_aql = false;  // the launch being waited for went to the AQL queue
   auto launch = [&](bool first) {
     PA.seg_cap = dc.pool_seg;
     dc.hres.ensure(hdr + cntb + size_t(W) * PA.seg_cap * sizeof(MatchRec));
@@ -756,7 +780,22 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     // timing: the first launch on e0/e1 (scan time or a deferred pair), a rerun on er0/er1
     const bool timed = first ? (time_scan || defer) : time_scan;
     hipEvent_t t0 = first ? e0 : dc.er0, t1 = first ? e1 : dc.er1;
-    if (timed && dc.ext_events) {  // stamped from the dispatch packet itself
+    AqlKernel ak;
+    via_aql = false;
+    if (!timed && !want_stamps && dc.aql) ak = aql_kernel(dc.aql, kernel_symbol(use_static, q.nterms, has_dur, q.has_range, dc.pool_nt).c_str());
+    if (ak.kobj) {
+      // our own AQL packet (aql.hpp): only the argument words this launch's kernel reads
+      thread_local std::vector<std::pair<uint32_t, uint32_t>> parts;
+      parts.clear();
+      parts.push_back({uint32_t(offsetof(PoolArgs, blk)), uint32_t(nsegs * sizeof(PoolBlk))});
+      parts.push_back({uint32_t(offsetof(PoolArgs, desc)), uint32_t(nsegs * sizeof(PA.desc[0]))});
+      if (!nbms.empty()) parts.push_back({uint32_t(offsetof(PoolArgs, bms)), uint32_t(nbms.size() * sizeof(PA.bms[0]))});
+      parts.push_back({uint32_t(offsetof(PoolArgs, ubase)), uint32_t((nsegs + 1) * sizeof(PA.ubase[0]))});
+      parts.push_back({uint32_t(offsetof(PoolArgs, ebase)), uint32_t(nsegs * sizeof(PA.ebase[0]))});
+      parts.push_back({uint32_t(offsetof(PoolArgs, nsegs)), uint32_t(sizeof(PoolArgs) - offsetof(PoolArgs, nsegs))});
+      aql_dispatch(dc.aql, ak, W, threads, uint32_t(kPoolLds), &PA, parts);
+      via_aql = true;
+    } else if (timed && dc.ext_events) {  // stamped from the dispatch packet itself
       void *kargs[] = {&PA};
       HIP_OK(hipExtLaunchKernel(reinterpret_cast<const void *>(fn), dim3(W), dim3(threads), kargs, kPoolLds, s, t0,
                                 t1, 0));
@@ -792,7 +831,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       }
       if (lo == W) break;
       if ((it & 255u) == 0) {
-        const hipError_t e = hipStreamQuery(s);
+        const hipError_t e = via_aql ? (aql_done(dc.aql) ? hipSuccess : hipErrorNotReady) : hipStreamQuery(s);
         if (e == hipSuccess) {
           bool all = true;
           for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
