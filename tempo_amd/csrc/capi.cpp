@@ -344,24 +344,35 @@ struct ResultHolder {
     uint32_t l;
     uint64_t off;
   };
+  // slots of an earlier result (another generation) count as empty: a reused holder starts a
+  // result in O(1) instead of clearing the table (a query over 10 blocks interns ~1 000 names)
   std::vector<InternSlot> intern;
+  std::vector<uint32_t> intern_gen;
+  uint32_t gen = 1;
   size_t intern_used = 0;
   uint64_t intern_lookup(const char *p, size_t l) {
-    if (intern.empty()) intern.assign(1024, InternSlot{nullptr, 0, 0});
-    if (2 * (intern_used + 1) > intern.size()) {  // grow: rehash
+    if (intern.empty()) {
+      intern.assign(4096, InternSlot{nullptr, 0, 0});
+      intern_gen.assign(4096, 0);
+    }
+    if (2 * (intern_used + 1) > intern.size()) {  // grow: rehash this generation's slots
       std::vector<InternSlot> old;
+      std::vector<uint32_t> og;
       old.swap(intern);
+      og.swap(intern_gen);
       intern.assign(2 * old.size(), InternSlot{nullptr, 0, 0});
+      intern_gen.assign(2 * old.size(), 0);
       intern_used = 0;
-      for (const auto &x : old)
-        if (x.p) intern_insert(x.p, x.l, x.off);
+      for (size_t i = 0; i < old.size(); i++)
+        if (og[i] == gen) intern_insert(old[i].p, old[i].l, old[i].off);
     }
     const size_t mask = intern.size() - 1;
     size_t h = (uintptr_t(p) * 0x9E3779B97F4A7C15ull ^ l) >> 7;
     for (;; h++) {
       InternSlot &x = intern[h & mask];
-      if (!x.p) {
+      if (intern_gen[h & mask] != gen) {
         x = InternSlot{p, uint32_t(l), arena_size};
+        intern_gen[h & mask] = gen;
         intern_used++;
         if (arena_size + l > arena_cap) arena_grow(arena_size + l);
         std::memcpy(arena + arena_size, p, l);
@@ -374,8 +385,9 @@ struct ResultHolder {
   void intern_insert(const char *p, uint32_t l, uint64_t off) {
     const size_t mask = intern.size() - 1;
     size_t h = (uintptr_t(p) * 0x9E3779B97F4A7C15ull ^ l) >> 7;
-    while (intern[h & mask].p) h++;
+    while (intern_gen[h & mask] == gen) h++;
     intern[h & mask] = InternSlot{p, l, off};
+    intern_gen[h & mask] = gen;
     intern_used++;
   }
   void set_str(RawVec<uint64_t> &off, RawVec<uint32_t> &len, size_t i, const char *p, size_t l) {
@@ -414,7 +426,10 @@ struct ResultHolder {
     for (auto *v : {&start, &end, &entry, &svc_off, &name_off}) v->clear();
     for (auto *v : {&dur, &block, &svc_len, &name_len}) v->clear();
     arena_size = 0;
-    if (intern_used) std::fill(intern.begin(), intern.end(), InternSlot{nullptr, 0, 0});
+    if (intern_used && ++gen == 0) {  // (wrapped: clear once)
+      std::fill(intern_gen.begin(), intern_gen.end(), 0u);
+      gen = 1;
+    }
     intern_used = 0;
     svc_p.clear();
     name_p.clear();
