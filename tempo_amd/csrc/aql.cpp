@@ -25,7 +25,7 @@ struct Aql {
   std::string code;
   uint8_t *kargs = nullptr;  // kSlots x kSlotBytes of device memory the host writes through the BAR
   uint32_t next = 0;
-  hsa_signal_t done{0};  // completion signal of the last dispatch (1 while it runs)
+  hsa_signal_t done{0};  // completion signal: the number of dispatches not yet complete
   std::unordered_map<std::string, AqlKernel> kernels;
 };
 
@@ -190,7 +190,10 @@ void aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uin
   pk->kernel_object = k.kobj;
   pk->kernarg_address = slot;
   pk->reserved2 = 0;
-  hsa_signal_store_relaxed(a->done, 1);
+  // the signal counts the dispatches not yet complete (each completion decrements it): a
+  // shared signal reset to 1 here could be taken to 0 by the previous dispatch's late
+  // completion while this one still runs
+  hsa_signal_add_scacq_screl(a->done, 1);
   pk->completion_signal = a->done;
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
   // agent-scope fences: the argument slots are uncached device memory, the search kernels

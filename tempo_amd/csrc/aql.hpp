@@ -29,8 +29,8 @@ AqlKernel aql_kernel(Aql *a, const char *name);
 // (only the parts the kernel reads for this launch: the rest of the slot is stale).
 void aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uint32_t dyn_lds, const void *args,
                   const std::vector<std::pair<uint32_t, uint32_t>> &parts);
-// true once the last dispatch has completed (its packet's completion signal; for a caller's
-// liveness check while it polls the kernel's own completion words)
+// true once every dispatch so far has completed (the packets' shared completion signal; for a
+// caller's liveness check while it polls the kernel's own completion words)
 bool aql_done(Aql *a);
 
 }  // namespace tsg
