@@ -17,6 +17,7 @@
 
 namespace tsg {
 
+static constexpr uint32_t kSlotsDecl = 64;
 struct Aql {
   hsa_agent_t agent{};
   hsa_queue_t *queue = nullptr;
@@ -25,7 +26,13 @@ struct Aql {
   std::string code;
   uint8_t *kargs = nullptr;  // kSlots x kSlotBytes of device memory the host writes through the BAR
   uint32_t next = 0;
-  hsa_signal_t done{0};  // completion signal: the number of dispatches not yet complete
+  // completion signals: a ring for the plain dispatches (one per dispatch, set to 1 before it;
+  // reused kSlots dispatches later) and one per profiled dispatch until aql_time_reset
+  hsa_signal_t ring[kSlotsDecl]{};
+  std::vector<hsa_signal_t> prof;
+  size_t prof_used = 0;
+  hsa_signal_t last{0};
+  double ns_per_tick = 1.0;
   std::unordered_map<std::string, AqlKernel> kernels;
 };
 
@@ -106,7 +113,12 @@ Aql *aql_open(int hip_ordinal) {
   if (hsa_queue_create(a->agent, 1024, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &a->queue) !=
       HSA_STATUS_SUCCESS)
     return fail("queue");
-  if (hsa_signal_create(0, 0, nullptr, &a->done) != HSA_STATUS_SUCCESS) return fail("signal");
+  for (auto &sg : a->ring)
+    if (hsa_signal_create(0, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) return fail("signal");
+  if (hsa_amd_profiling_set_profiler_enabled(a->queue, 1) != HSA_STATUS_SUCCESS) return fail("queue profiling");
+  uint64_t freq = 0;
+  if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &freq) == HSA_STATUS_SUCCESS && freq)
+    a->ns_per_tick = 1e9 / double(freq);
   // argument slots in device memory (as HIP keeps kernel arguments), written through the BAR;
   // zeroed once (the kernels read only the parts a launch writes)
   void *p = nullptr;
@@ -128,7 +140,9 @@ void aql_close(Aql *a) {
     }
   }
   if (a->kargs) (void)hipFree(a->kargs);
-  if (a->done.handle) hsa_signal_destroy(a->done);
+  for (auto &sg : a->ring)
+    if (sg.handle) hsa_signal_destroy(sg);
+  for (auto &sg : a->prof) hsa_signal_destroy(sg);
   if (a->queue) hsa_queue_destroy(a->queue);
   if (a->exe.handle) hsa_executable_destroy(a->exe);
   if (a->reader.handle) hsa_code_object_reader_destroy(a->reader);
@@ -155,9 +169,24 @@ AqlKernel aql_kernel(Aql *a, const char *name) {
   return k;
 }
 
-void aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uint32_t dyn_lds, const void *args,
-                  const std::vector<std::pair<uint32_t, uint32_t>> &parts) {
-  uint8_t *slot = a->kargs + size_t(a->next++ % kSlots) * kSlotBytes;
+int aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uint32_t dyn_lds, const void *args,
+                 const std::vector<std::pair<uint32_t, uint32_t>> &parts, bool profiled) {
+  static_assert(kSlotsDecl == kSlots, "signal ring = argument slots");
+  const uint32_t si = a->next++ % kSlots;
+  uint8_t *slot = a->kargs + size_t(si) * kSlotBytes;
+  int pslot = -1;
+  hsa_signal_t sig = a->ring[si];
+  if (profiled) {
+    constexpr size_t kMaxProf = 4096;
+    if (a->prof_used == a->prof.size() && a->prof.size() < kMaxProf) {
+      hsa_signal_t x{};
+      if (hsa_signal_create(0, 0, nullptr, &x) == HSA_STATUS_SUCCESS) a->prof.push_back(x);
+    }
+    if (a->prof_used < a->prof.size()) {
+      pslot = int(a->prof_used++);
+      sig = a->prof[size_t(pslot)];
+    }
+  }
   const auto *src = static_cast<const uint8_t *>(args);
   uint32_t last = 0;
   for (const auto &pt : parts) {
@@ -190,11 +219,11 @@ void aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uin
   pk->kernel_object = k.kobj;
   pk->kernarg_address = slot;
   pk->reserved2 = 0;
-  // the signal counts the dispatches not yet complete (each completion decrements it): a
-  // shared signal reset to 1 here could be taken to 0 by the previous dispatch's late
-  // completion while this one still runs
-  hsa_signal_add_scacq_screl(a->done, 1);
-  pk->completion_signal = a->done;
+  // (a signal of this dispatch's own: one shared signal reset to 1 here could be taken to 0 by
+  // the previous dispatch's late completion while this one still runs)
+  hsa_signal_store_relaxed(sig, 1);
+  pk->completion_signal = sig;
+  a->last = sig;
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
   // agent-scope fences: the argument slots are uncached device memory, the search kernels
   // write their host results with system-scope stores of their own (a system-scope acquire
@@ -208,8 +237,22 @@ void aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uin
                        (scope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   __atomic_store_n(reinterpret_cast<uint32_t *>(pk), uint32_t(hdr) | (uint32_t(setup) << 16), __ATOMIC_RELEASE);
   hsa_signal_store_screlease(q->doorbell_signal, hsa_signal_value_t(idx));
+  return pslot;
 }
 
-bool aql_done(Aql *a) { return hsa_signal_load_scacquire(a->done) <= 0; }
+bool aql_done(Aql *a) { return !a->last.handle || hsa_signal_load_scacquire(a->last) <= 0; }
+
+uint64_t aql_time_ns(Aql *a, int slot) {
+  if (slot < 0 || size_t(slot) >= a->prof_used) return 0;
+  const hsa_signal_t sg = a->prof[size_t(slot)];
+  for (int i = 0; i < 1000000 && hsa_signal_load_scacquire(sg) > 0; i++) {
+    struct timespec ts{0, 1000};
+    nanosleep(&ts, nullptr);
+  }
+  hsa_amd_profiling_dispatch_time_t t{};
+  if (hsa_amd_profiling_get_dispatch_time(a->agent, sg, &t) != HSA_STATUS_SUCCESS || t.end < t.start) return 0;
+  return uint64_t(double(t.end - t.start) * a->ns_per_tick);
+}
+void aql_time_reset(Aql *a) { a->prof_used = 0; }
 
 }  // namespace tsg

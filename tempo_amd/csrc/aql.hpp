@@ -27,10 +27,16 @@ AqlKernel aql_kernel(Aql *a, const char *name);
 // One dispatch of grid x block threads with dyn_lds bytes of dynamic LDS. The kernel's
 // argument block is assembled in a device-memory slot from `parts` (offset, bytes) of `args`
 // (only the parts the kernel reads for this launch: the rest of the slot is stale).
-void aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uint32_t dyn_lds, const void *args,
-                  const std::vector<std::pair<uint32_t, uint32_t>> &parts);
-// true once every dispatch so far has completed (the packets' shared completion signal; for a
-// caller's liveness check while it polls the kernel's own completion words)
+// profiled = true: the dispatch's start / end are recorded (the queue's profiling timestamps,
+// what rocprofv3's kernel trace reports) and the return value names them for aql_time_ns
+// (-1 when no profiling slot is free); otherwise -1.
+int aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uint32_t dyn_lds, const void *args,
+                 const std::vector<std::pair<uint32_t, uint32_t>> &parts, bool profiled = false);
+// true once the last dispatch has completed (its own completion signal: dispatches on the
+// queue complete in order; for a caller's liveness check while it polls the kernel's words)
 bool aql_done(Aql *a);
+// a profiled dispatch's duration (ns; 0 if it has not completed); aql_time_reset frees the slots
+uint64_t aql_time_ns(Aql *a, int slot);
+void aql_time_reset(Aql *a);
 
 }  // namespace tsg

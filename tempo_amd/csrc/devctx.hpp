@@ -175,6 +175,7 @@ struct DeviceCtx {
   }();
   // TSG_SEARCH_TIME_DEFER: event pairs recorded around search kernels, read by tsg_kernel_times
   std::vector<hipEvent_t> tring;
+  std::vector<int> tring_aql;  // per deferred slot: its AQL profiling slot, or -1 (the event pair)
   size_t tring_used = 0;
   bool defer_slot(hipEvent_t &a, hipEvent_t &b) {
     constexpr size_t kMaxDeferred = 4096;
@@ -188,6 +189,8 @@ struct DeviceCtx {
     }
     a = tring[2 * tring_used];
     b = tring[2 * tring_used + 1];
+    if (tring_aql.size() <= tring_used) tring_aql.resize(tring_used + 1);
+    tring_aql[tring_used] = -1;
     tring_used++;
     return true;
   }

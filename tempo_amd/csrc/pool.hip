@@ -782,7 +782,11 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     hipEvent_t t0 = first ? e0 : dc.er0, t1 = first ? e1 : dc.er1;
     AqlKernel ak;
     via_aql = false;
-    if (!timed && !want_stamps && dc.aql) ak = aql_kernel(dc.aql, kernel_symbol(use_static, q.nterms, has_dur, q.has_range, dc.pool_nt).c_str());
+    // AQL for untimed launches and for deferred-timed first launches (timed by the queue's own
+    // dispatch timestamps, as the untimed ones run); explicit per-call timing stays on HIP events
+    const bool aql_timed = first && defer && !time_scan;
+    if ((!timed || aql_timed) && !want_stamps && dc.aql)
+      ak = aql_kernel(dc.aql, kernel_symbol(use_static, q.nterms, has_dur, q.has_range, dc.pool_nt).c_str());
     if (ak.kobj) {
       // our own AQL packet (aql.hpp): only the argument words this launch's kernel reads
       thread_local std::vector<std::pair<uint32_t, uint32_t>> parts;
@@ -793,7 +797,8 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       parts.push_back({uint32_t(offsetof(PoolArgs, ubase)), uint32_t((nsegs + 1) * sizeof(PA.ubase[0]))});
       parts.push_back({uint32_t(offsetof(PoolArgs, ebase)), uint32_t(nsegs * sizeof(PA.ebase[0]))});
       parts.push_back({uint32_t(offsetof(PoolArgs, nsegs)), uint32_t(sizeof(PoolArgs) - offsetof(PoolArgs, nsegs))});
-      aql_dispatch(dc.aql, ak, W, threads, uint32_t(kPoolLds), &PA, parts);
+      const int ps = aql_dispatch(dc.aql, ak, W, threads, uint32_t(kPoolLds), &PA, parts, aql_timed);
+      if (aql_timed) dc.tring_aql[dc.tring_used - 1] = ps >= 0 ? ps : -2;  // (the slot defer_slot took; -2: untimed)
       via_aql = true;
     } else if (timed && dc.ext_events) {  // stamped from the dispatch packet itself
       void *kargs[] = {&PA};

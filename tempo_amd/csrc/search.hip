@@ -26,6 +26,7 @@
 #include <cstring>
 #include <type_traits>
 
+#include "aql.hpp"
 #include "search_common.hpp"
 
 namespace tsg {
@@ -2570,11 +2571,17 @@ void device_kernel_times(DeviceCtx &dc, std::vector<uint64_t> &ns) {
   HIP_OK(hipSetDevice(dc.ordinal));
   HIP_OK(hipStreamSynchronize(dc.stream));
   for (size_t i = 0; i < dc.tring_used; i++) {
+    if (i < dc.tring_aql.size() && dc.tring_aql[i] == -2) continue;  // (an AQL dispatch left untimed)
+    if (i < dc.tring_aql.size() && dc.tring_aql[i] >= 0 && dc.aql) {  // an AQL dispatch: its queue's timestamps
+      ns.push_back(aql_time_ns(dc.aql, dc.tring_aql[i]));
+      continue;
+    }
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, dc.tring[2 * i], dc.tring[2 * i + 1]));
     ns.push_back(uint64_t(double(ms) * 1e6));
   }
   dc.tring_used = 0;
+  if (dc.aql) aql_time_reset(dc.aql);
 }
 
 }  // namespace tsg
