@@ -165,3 +165,17 @@ def test_pool_matches_segment_engine(engine, ragged):
             assert run(engine, ragged, q) == run(other, ragged, q)
     finally:
         other.close()
+
+
+def test_aql_and_hip_launches_agree(engine, ragged):
+    """The narrow kernels launched as AQL packets on libtsg's own queue (default) and through
+    HIP (TSG_AQL=0) return the same records and metrics, full scans and limit queries."""
+    os.environ["TSG_AQL"] = "0"
+    try:
+        hip = T.Engine()
+        for q in QUERIES:
+            for limit in (0, 20):
+                assert run(engine, ragged, q, limit) == run(hip, ragged, q, limit)
+    finally:
+        del os.environ["TSG_AQL"]
+        hip.close()
