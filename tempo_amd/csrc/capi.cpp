@@ -1438,8 +1438,9 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     // Early exit (limit > 0): the consumer stops at the L-th distinct id in
     // block order, so nothing behind that point is needed. The blocks' entries form one
     // sequence (blocks in caller order, scan order inside); progressive waves search its next
-    // stretch — the first TSG_LIMIT_WAVE0 entries (2^21: one 512-entry unit per wave of the
-    // chip), then a stretch sized by the selectivity seen so far (x1.5 the entries the missing
+    // stretch — the first TSG_LIMIT_WAVE0 entries (2^20: a 512-entry unit for every other wave
+    // of the chip; 2^21 took 1.3 us more of kernel and 3.7 us more of step on the limit-20 leg,
+    // profiles/r04_final), then a stretch sized by the selectivity seen so far (x1.5 the entries the missing
     // ids need at that rate, at least 4x the last wave) — cutting blocks on unit boundaries,
     // until the consumer stops inside what has been searched. A block's records over its
     // parts are its records in scan order, so the result is the one-wave result. Live blocks
@@ -1447,7 +1448,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     // (which take the cut ranges on the device) the waves cut at block boundaries only.
     static const uint64_t kWave0 = [] {
       const char *e = std::getenv("TSG_LIMIT_WAVE0");
-      return e ? std::max<uint64_t>(512, uint64_t(std::atoll(e))) : uint64_t(1) << 21;
+      return e ? std::max<uint64_t>(512, uint64_t(std::atoll(e))) : uint64_t(1) << 20;
     }();
     // A limit search whose blocks hold at most one first wave's entries is one launch with
     // per-block caps (concurrent callers coalesce: the shim's per-block calls); larger ones,
