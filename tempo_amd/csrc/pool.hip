@@ -69,7 +69,10 @@ struct PoolArgs {
   uint32_t unit_cap;
   // the launch shape, passed explicitly: the kernels read no implicit kernel argument (blockDim /
   // gridDim come from them), so an AQL packet of our own needs none (aql.cpp)
-  uint32_t nthreads, ngroups, pad1;
+  uint32_t nthreads, ngroups;
+  // static kernel: the launch's NW waves split the units as wave g -> [g*sq + min(g, sr), ...),
+  // the first sr waves one unit more (sq, sr = units / NW, units % NW: no division on the device)
+  uint32_t sq, sr;
 };
 static_assert(sizeof(PoolArgs) <= 4096, "kernel arguments");
 
@@ -440,7 +443,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_pool_kernel(PoolArgs A
 // ------------------------------------------------------------------------------------
 // static search: the pool kernel's loads, predicates and record hand-off without its
 // machinery. One 1024-thread workgroup per CU; wave g of the launch owns the contiguous
-// unit run [g * U / NW, (g + 1) * U / NW) of the launch's unit space (NW waves, runs differ
+// unit run [g * sq + min(g, sr), ...) of the launch's unit space (NW waves, runs differ
 // by at most one unit), two units in flight. The block of a unit comes from the wave's own
 // walk over the kernel arguments' unit bases (scalar loads, once per block boundary), not
 // from LDS: the first loads are issued before anything is staged, and nothing is claimed.
@@ -456,8 +459,8 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
   const uint32_t w = blockIdx.x, nsegs = A.nsegs, units = A.units;
   const uint32_t nwv = A.nthreads >> 6;
   const uint32_t wave = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6));
-  const uint32_t NW = A.ngroups * nwv, gw = w * nwv + wave;
-  const uint32_t u_begin = uint32_t(uint64_t(units) * gw / NW), u_end = uint32_t(uint64_t(units) * (gw + 1) / NW);
+  const uint32_t gw = w * nwv + wave;
+  const uint32_t u_begin = gw * A.sq + min(gw, A.sr), u_end = u_begin + A.sq + (gw < A.sr ? 1u : 0u);
   // the wave's current block (all scalar)
   uint32_t b = 0;
   while (b + 1 < nsegs && u_begin >= A.ubase[b + 1]) b++;
@@ -757,6 +760,8 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   const uint32_t threads = 64 * dc.pool_waves;
   PA.nthreads = threads;
   PA.ngroups = W;
+  PA.sq = U / (W * (threads / 64));
+  PA.sr = U % (W * (threads / 64));
   const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
   hipEvent_t e0 = dc.es0, e1 = dc.es1;
   const bool defer = !time_scan && (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
