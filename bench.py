@@ -431,7 +431,7 @@ def concurrent_leg(args, base, pipe, streams, entries, dist, world, local):
     import tempo_amd as T
     # (its own engine, created after the main legs: they run with one device context)
     eng = T.Engine(devices=[local] * streams)
-    csets = [[b.clone(eng, device=i) for b in base] for i in range(streams)]
+    csets = [tuple(b.clone(eng, device=i) for b in base) for i in range(streams)]
     for i, cs in enumerate(csets):  # warm every stream (plans, pinned buffers)
         for _ in range(3):
             eng.search_raw(cs, pipe)
@@ -962,7 +962,7 @@ def main():
     log(f"rank {rank}: loaded {entries} entries ({fb_bytes / 1e9:.2f} GB flatbuffer) in {load_s:.1f}s, "
         f"{dev_bytes / 1e9:.2f} GB resident")
     # disjoint resident copies of the set: the rotation's working set is sets x the set
-    sets = [base] + [[b.clone(eng) for b in base] for _ in range(max(1, args.sets) - 1)]
+    sets = [tuple(base)] + [tuple(b.clone(eng) for b in base) for _ in range(max(1, args.sets) - 1)]
     if len(sets) > 1:
         log(f"rank {rank}: {len(sets)} resident copies of the set ({len(sets) * dev_bytes / 1e9:.2f} GB)")
 

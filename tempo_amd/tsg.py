@@ -390,6 +390,7 @@ class Engine:
             o.num_devices, o.devices = len(devices), self._devs
         self.h = C.c_void_p()
         self._raw_calls = {}  # search_raw: prebuilt ctypes arguments (handle values only)
+        self._raw_ids = {}  # search_raw fast path for tuple block lists: id -> (tuple, close gen, call)
         # open blocks (weak): closed before tsg_shutdown frees the device contexts they use
         self._open = weakref.WeakSet()
         _check(lib().tsg_init(C.byref(o), C.byref(self.h)))
@@ -446,21 +447,23 @@ class Engine:
         (match count, SearchMetrics). The result arrays are assembled by libtsg as
         for any caller (what the Go shim would receive) and then freed. The ctypes
         argument objects are built once per (blocks, pipeline, limit, flags) and kept on
-        this Engine (bounded; they hold handle values, not the block objects)."""
-        key = (pipeline.query_addr, limit, flags) + tuple(b.h.value for b in blocks)
-        _cache = self._raw_calls
-        call = _cache.get(key)
-        if call is None:
-            if len(_cache) >= 64:
-                _cache.clear()
-            L = _raw_lib()  # its own function objects: no argtypes, arguments are prebuilt ctypes objects
-            fn, free = L.tsg_search, L.tsg_result_free
-            arr = (C.c_void_p * max(len(blocks), 1))(*[b.h.value for b in blocks])
-            opts = _SearchOpts(limit=limit, flags=flags)
-            rp = C.POINTER(_Result)()
-            args = (C.c_void_p(self.h.value), arr, C.c_size_t(len(blocks)), C.c_void_p(pipeline.query_addr),
-                    C.byref(opts), C.byref(rp))
-            call = _cache[key] = (fn, free, args, rp, arr, opts)
+        this Engine (bounded; they hold handle values, not the block objects). A tuple of
+        blocks is also looked up by identity (the entry keeps the tuple alive, and any block
+        close since the entry was made invalidates it), which skips the per-block key."""
+        fast = type(blocks) is tuple
+        if fast:
+            ik = (id(blocks), pipeline.query_addr, limit, flags)
+            ent = self._raw_ids.get(ik)
+            if ent is not None and ent[0] is blocks and ent[1] == _block_closes[0]:
+                call = ent[2]
+            else:
+                ent = None
+        if not fast or ent is None:
+            call = self._raw_call(blocks, pipeline, limit, flags)
+            if fast:
+                if len(self._raw_ids) >= 64:
+                    self._raw_ids.clear()
+                self._raw_ids[ik] = (blocks, _block_closes[0], call)
         fn, free, args, rp = call[0], call[1], call[2], call[3]
         rc = fn(*args)
         if rc:
@@ -475,6 +478,23 @@ class Engine:
                             m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
         free(rp)
         return n, met
+
+    def _raw_call(self, blocks, pipeline, limit, flags):
+        key = (pipeline.query_addr, limit, flags) + tuple(b.h.value for b in blocks)
+        _cache = self._raw_calls
+        call = _cache.get(key)
+        if call is None:
+            if len(_cache) >= 64:
+                _cache.clear()
+            L = _raw_lib()  # its own function objects: no argtypes, arguments are prebuilt ctypes objects
+            fn, free = L.tsg_search, L.tsg_result_free
+            arr = (C.c_void_p * max(len(blocks), 1))(*[b.h.value for b in blocks])
+            opts = _SearchOpts(limit=limit, flags=flags)
+            rp = C.POINTER(_Result)()
+            args = (C.c_void_p(self.h.value), arr, C.c_size_t(len(blocks)), C.c_void_p(pipeline.query_addr),
+                    C.byref(opts), C.byref(rp))
+            call = _cache[key] = (fn, free, args, rp, arr, opts)
+        return call
 
     def search_columns(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0):
         """tsg_search with the ordered matches as numpy columns (large results: no per-record
@@ -693,11 +713,15 @@ class Engine:
 
     def close(self):
         self._raw_calls = {}
+        self._raw_ids = {}
         for b in list(getattr(self, "_open", ())):
             b.close()
         if getattr(self, "h", None):
             lib().tsg_shutdown(self.h)
             self.h = None
+
+
+_block_closes = [0]  # BackendSearchBlock closes so far
 
 
 def _seen(opts, seen):
@@ -762,6 +786,7 @@ class BackendSearchBlock:
 
     def close(self):
         if getattr(self, "h", None) and _lib is not None:
+            _block_closes[0] += 1  # (search_raw's identity cache entries made before this are stale)
             _lib.tsg_block_close(self.h)
             self.h = None
 

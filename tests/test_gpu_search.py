@@ -429,3 +429,28 @@ def test_header_min_dur_quirk_skips_block(engine, tmp_path):
     got, met, exp, omet = both(engine, [pq, pp], tags={"k": "a"})
     assert met.skipped_blocks == 0 and ref_id(1) in [m.trace_id for m in got]
     assert_parity(got, met, exp, omet)
+
+
+def test_search_raw_tuple_identity_cache(engine, tmp_path):
+    """search_raw's identity fast path for tuple block lists: the same tuple gives the
+    same count as a list of the same blocks, and closing any block invalidates the entry
+    (the call then fails on the closed handle instead of using it)."""
+    p = os.path.join(str(tmp_path), "syn")
+    T.synth_search_block(p, 20_000, seed=9)
+    b = engine.open_block(p)
+    c = b.clone(engine)
+    pipe = T.Pipeline(T.SearchRequest(tags={"service.name": "svc-07"}))
+    try:
+        blocks = (b, c)
+        n_list, _ = engine.search_raw([b, c], pipe)
+        for _ in range(3):
+            n_tup, _ = engine.search_raw(blocks, pipe, metrics=False)
+            assert n_tup == n_list > 0
+        n_lim, _ = engine.search_raw(blocks, pipe, limit=5)
+        assert 0 < n_lim <= n_list
+        c.close()
+        with pytest.raises(Exception):
+            engine.search_raw(blocks, pipe)
+    finally:
+        c.close()
+        b.close()
