@@ -526,8 +526,14 @@ struct PosMap {
   }
 };
 
+// per worker: the sizes of its previous page (pages of a block are alike: reserving them up
+// front saves the vectors' regrowth copies)
+struct PageHint {
+  size_t tables = 0, vals = 0, refs = 0;
+};
+
 void parse_lpage(const uint8_t *data, size_t dlen, int enc, const IndexRecord &rec, KeyNames &kn, KeyCache &kc,
-                 PosMap &pm, LPage &pp) {
+                 PosMap &pm, PageHint &hint, LPage &pp) {
   read_data_page(data, dlen, rec, enc, pp.buf);
   // object.UnmarshalAndAdvanceBuffer (object.go:82-113): [u32 total][u32 idLen][id][obj]
   if (pp.buf.size() < 8) fail(TSG_E_CORRUPT, "object header truncated");
@@ -547,10 +553,17 @@ void parse_lpage(const uint8_t *data, size_t dlen, int enc, const IndexRecord &r
   pp.end.resize(pp.n);
   pp.tag0.assign(1, 0);
   pp.tag0.reserve(pp.n + 1);
-  pp.tag_kv.reserve(size_t(pp.n) * 20);
-  pp.tag_res.reserve(size_t(pp.n) * 20);
+  const size_t want_refs = hint.refs ? hint.refs + hint.refs / 4 : size_t(pp.n) * 20;
+  pp.tag_kv.reserve(want_refs);
+  pp.tag_res.reserve(want_refs);
   pp.kv_v0.assign(1, 0);
-  pm.reset(size_t(pp.n) * 8);
+  if (hint.tables) {
+    pp.kv_key.reserve(hint.tables + hint.tables / 4);
+    pp.kv_v0.reserve(hint.tables + hint.tables / 4 + 1);
+    pp.vals.reserve(hint.vals + hint.vals / 4);
+    pp.vhash.reserve(hint.vals + hint.vals / 4);
+  }
+  pm.reset(hint.tables ? hint.tables + hint.tables / 4 : size_t(pp.n) * 8);
   std::vector<std::pair<uint32_t, uint32_t>> kpos_ids;  // key string position -> key id
   FbTable e{fb, fbn, 0}, kv{fb, fbn, 0};
   for (uint32_t j = 0; j < pp.n; j++) {
@@ -637,6 +650,9 @@ void parse_lpage(const uint8_t *data, size_t dlen, int enc, const IndexRecord &r
     pp.tag0.push_back(uint32_t(pp.tag_kv.size()));
   }
   pp.kv_sid.assign(pp.kv_key.size(), kNone);
+  hint.tables = pp.kv_key.size();
+  hint.vals = pp.vals.size();
+  hint.refs = pp.tag_kv.size();
 }
 
 // Phase B tables. A key's values are interned in hash shards (shard = top hash bits), each
@@ -796,12 +812,13 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
   {
     auto work = [&](size_t w) {
       PosMap pm;
+      PageHint hint;
       for (;;) {
         const size_t i = next.fetch_add(1);
         if (i >= pages.size()) break;
         LPage &pp = pages[i];
         try {
-          parse_lpage(data, data_len, hb.meta.encoding, recs[i], kn, caches[w], pm, pp);
+          parse_lpage(data, data_len, hb.meta.encoding, recs[i], kn, caches[w], pm, hint, pp);
         } catch (const Error &e) {
           pp.err = e.code;
           pp.msg = e.what();

@@ -394,6 +394,44 @@ struct ResultHolder {
     len[i] = uint32_t(l);
     off[i] = l ? intern_lookup(p, l) : 0;
   }
+  // The record loop's names come from one block's root.service.name / root.name dictionaries
+  // at a time: a direct-indexed cache per column (value id -> arena offset and length) in
+  // front of the pointer-keyed intern table, started afresh for every block (vid_block)
+  static constexpr size_t kVcMax = 1 << 16;
+  struct VcSlot {
+    uint32_t gen, len;
+    uint64_t off;
+  };
+  std::vector<VcSlot> vc[2];
+  uint32_t vc_gen = 0;
+  void vid_block(size_t nsvc, size_t nname) {
+    if (++vc_gen == 0) {
+      for (auto &c : vc) std::fill(c.begin(), c.end(), VcSlot{0, 0, 0});
+      vc_gen = 1;
+    }
+    if (nsvc <= kVcMax && vc[0].size() < nsvc) vc[0].resize(nsvc, VcSlot{0, 0, 0});
+    if (nname <= kVcMax && vc[1].size() < nname) vc[1].resize(nname, VcSlot{0, 0, 0});
+  }
+  // record i's name of column c (0 root service, 1 root name): value `vid` of key `key` of h
+  void set_vid(int c, size_t i, const HostBlock &h, int key, uint32_t vid) {
+    RawVec<uint64_t> &off = c ? name_off : svc_off;
+    RawVec<uint32_t> &len = c ? name_len : svc_len;
+    if (key < 0 || vid == kNone) {
+      len[i] = 0;
+      off[i] = 0;
+      return;
+    }
+    VcSlot *slot = vid < vc[c].size() ? &vc[c][vid] : nullptr;
+    if (slot && slot->gen == vc_gen) {
+      len[i] = slot->len;
+      off[i] = slot->off;
+      return;
+    }
+    const std::string_view v = h.dict_value(key, vid);
+    len[i] = uint32_t(v.size());
+    off[i] = v.empty() ? 0 : intern_lookup(v.data(), v.size());
+    if (slot) *slot = VcSlot{vc_gen, uint32_t(v.size()), off[i]};
+  }
   size_t size() const { return start.size(); }
   void resize(size_t n) {
     ids.resize(16 * n);
@@ -401,8 +439,7 @@ struct ResultHolder {
     for (auto *v : {&dur, &block, &svc_len, &name_len}) v->resize(n);
     id_len.resize(n);
   }
-  void set(size_t i, const uint8_t *id, uint8_t il, uint64_t s, uint64_t e, uint32_t b, uint64_t en, const char *sv,
-           size_t svl, const char *nm, size_t nml) {
+  void set_rec(size_t i, const uint8_t *id, uint8_t il, uint64_t s, uint64_t e, uint32_t b, uint64_t en) {
     std::memcpy(&ids[16 * i], id, 16);
     id_len[i] = il;
     start[i] = s;
@@ -410,6 +447,10 @@ struct ResultHolder {
     dur[i] = uint32_t((e - s) / 1000000ULL);  // util.go:33
     block[i] = b;
     entry[i] = en;
+  }
+  void set(size_t i, const uint8_t *id, uint8_t il, uint64_t s, uint64_t e, uint32_t b, uint64_t en, const char *sv,
+           size_t svl, const char *nm, size_t nml) {
+    set_rec(i, id, il, s, e, b, en);
     set_str(svc_off, svc_len, i, sv, svl);
     set_str(name_off, name_len, i, nm, nml);
   }
@@ -1058,8 +1099,8 @@ struct IdSet {
   std::vector<uint8_t> used;
   size_t n = 0;
   void clear() {
+    if (n) std::fill(used.begin(), used.end(), uint8_t(0));
     n = 0;
-    std::fill(used.begin(), used.end(), uint8_t(0));
   }
   size_t size() const { return n; }
   bool insert(const uint8_t *id) {
@@ -1616,6 +1657,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     const clk::time_point t_dev = trace ? clk::now() : clk::time_point();
     res->reserve(nrec);
     res->resize(nrec);
+    const clk::time_point t_res = trace ? clk::now() : clk::time_point();
     size_t nout = 0;
     // A large full scan (no limit, no live block: every record of every inspected block is
     // kept, nothing to consume) is assembled on several threads; otherwise one thread
@@ -1695,13 +1737,14 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       }
       m.blocks_inspected++;
       uint64_t stop_entry = UINT64_MAX;
+      if (per_block[i].second)
+        res->vid_block(h.svc_key >= 0 ? h.keys[size_t(h.svc_key)].nvals() : 0,
+                       h.name_key >= 0 ? h.keys[size_t(h.name_key)].nvals() : 0);
       for (size_t ri = 0; ri < per_block[i].second; ri++) {
         const SearchOut::Rec *r = per_block[i].first + ri;
-        std::string_view sv, nm;
-        if (h.svc_key >= 0 && r->svc != kNone) sv = h.dict_value(h.svc_key, r->svc);
-        if (h.name_key >= 0 && r->name != kNone) nm = h.dict_value(h.name_key, r->name);
-        res->set(nout++, r->id, uint8_t(r->block_il >> 24), r->start, r->end, uint32_t(i), r->entry, sv.data(),
-                 sv.size(), nm.data(), nm.size());
+        res->set_rec(nout, r->id, uint8_t(r->block_il >> 24), r->start, r->end, uint32_t(i), r->entry);
+        res->set_vid(0, nout, h, h.svc_key, r->svc);
+        res->set_vid(1, nout++, h, h.name_key, r->name);
         if (limit) {
           distinct.insert(r->id);
           if (distinct.size() >= limit) {
@@ -1725,11 +1768,15 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
           m.bytes_inspected += h.page_fb_bytes[p];
       }
     }
+    const clk::time_point t_fin = trace ? clk::now() : clk::time_point();
     res->resize(nout);
     res->finalize();
     *out = &guard_res.release()->pub;
     if (prof_on()) {
       const clk::time_point t_end = clk::now();
+      prof_add("tsg_search.results.finalize", std::chrono::duration<double, std::micro>(t_end - t_fin).count());
+      prof_add("tsg_search.results.alloc", std::chrono::duration<double, std::micro>(t_res - t_dev).count());
+      prof_add("tsg_search.results.records", std::chrono::duration<double, std::micro>(t_fin - t_res).count());
       prof_add("tsg_search.device", std::chrono::duration<double, std::micro>(t_dev - t_in).count());
       prof_add("tsg_search.results", std::chrono::duration<double, std::micro>(t_end - t_dev).count());
     } else if (trace) {

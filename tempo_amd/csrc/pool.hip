@@ -947,6 +947,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       const uint64_t at = uint64_t(PA.blk[ps].ubase) * kPoolTile + (r.entry - PA.ebase[ps]);
       keys[nrec++] = (at << 20) | slot;
     }
+  tr.mark("post.keys");
   uint32_t lb = 6;
   while ((1ull << lb) < total && lb < 20) lb++;
   uint32_t sb = 0;
@@ -976,6 +977,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   // limit L: each block's part keeps its first L matches in scan order (the records of a
   // part all lie in its range [e0, e1)); the sorted records of a block are contiguous, so
   // the cut keeps a prefix of each block's run
+  tr.mark("post.sort");
   auto cut = [&](uint64_t i) { return limit ? std::min<uint64_t>(limit, segs[i].cap) : segs[i].cap; };
   out.recs.resize(total);
   uint64_t kept = 0;
