@@ -490,6 +490,11 @@ struct LPage {
   std::vector<uint32_t> vloc;     // phase B: per value reference, its id in its hash shard
   std::vector<uint32_t> kv_sid;   // phase B: the table's value set id within its key
   std::vector<uint32_t> bykey, bykey0;  // tables grouped by provisional key (CSR)
+  struct KStat {  // per provisional key: its tables in this page, their values and value bytes
+    uint64_t tables = 0, refs = 0, bytes = 0;
+    bool multi = false;  // some table holds no value or several
+  };
+  std::vector<KStat> kstat;
 };
 
 // open addressing: table position -> page-local table index (reset per page)
@@ -604,8 +609,14 @@ void parse_lpage(const uint8_t *data, size_t dlen, int enc, const IndexRecord &r
         pp.kv_key.push_back(kid);
         const uint16_t vo = kv.field(kKvValue);
         const uint32_t vn = vo ? kv.vector_len(vo) : 0, vs = vo ? kv.vector_start(vo) : 0;
+        if (kid >= pp.kstat.size()) pp.kstat.resize(size_t(kid) + 1);
+        LPage::KStat &ks = pp.kstat[kid];
+        ks.tables++;
+        ks.refs += vn;
+        ks.multi = ks.multi || vn != 1;
         for (uint32_t q = 0; q < vn; q++) {
           const std::string_view v = kv.byte_vector(vs + 4 * q);
+          ks.bytes += v.size();
           pp.vals.push_back(v);
           pp.vhash.push_back(hash_bytes(v.data(), v.size()));
         }
@@ -885,21 +896,20 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
       uint32_t P = 1;      // value shards
     };
     std::vector<KInfo> kin(nk);
-    for_each_index(nk, nthreads, [&](size_t k) {
+    for (size_t k = 0; k < nk; k++) {  // (the pages counted their keys' tables as they parsed)
       KInfo &I = kin[k];
+      const uint32_t pk = ord[k];
       for (size_t i = 0; i < np; i++) {
         const LPage &pp = pages[i];
-        for (uint32_t b = pp.bykey0[k]; b < pp.bykey0[k + 1]; b++) {
-          const uint32_t t = pp.bykey[b];
-          const uint32_t nv = pp.kv_v0[t + 1] - pp.kv_v0[t];
-          I.tables++;
-          I.refs += nv;
-          I.single = I.single && nv == 1;
-          for (uint32_t v = pp.kv_v0[t]; v < pp.kv_v0[t + 1]; v++) I.bytes += pp.vals[v].size();
-        }
+        if (pk >= pp.kstat.size()) continue;
+        const LPage::KStat &ks = pp.kstat[pk];
+        I.tables += ks.tables;
+        I.refs += ks.refs;
+        I.bytes += ks.bytes;
+        I.single = I.single && !ks.multi;
       }
       while (I.P < 16 && I.refs / I.P > 65536) I.P <<= 1;
-    });
+    }
     auto shard_of = [](uint64_t h, uint32_t P) { return uint32_t(h >> 48) & (P - 1); };
     // each shard's value references (page << 32 | value), in page order: one pass per key
     std::vector<std::vector<std::vector<uint64_t>>> refs(nk);
@@ -1203,7 +1213,10 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
     hb.min_dur = h.u64(kHdrMin);
     hb.max_dur = h.u64(kHdrMax);
   }
+  const auto th0 = std::chrono::steady_clock::now();
   index_header(hb);
+  if (prof_on())
+    prof_add("load.hdr", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - th0).count());
   std::vector<IndexRecord> recs =
       read_index(index, index_len, hb.meta.index_page_size, hb.meta.index_records, &hb.index_truncated);
   if (nthreads <= 0) nthreads = host_threads();

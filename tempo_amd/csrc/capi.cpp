@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <condition_variable>
@@ -16,6 +17,11 @@
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "block.hpp"
 #include "common.hpp"
@@ -591,8 +597,15 @@ static void open_common(tsg_ctx *ctx, Decode &&decode, int device_hint, tsg_bloc
   auto *b = new tsg_block();
   b->ctx = ctx;
   try {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     decode(*b->b.host);
+    const auto t1 = clk::now();
     if (b->b.host->has_meta) block_upload(ctx->c, b->b, device_hint);
+    if (prof_on()) {
+      prof_add("open.decode", std::chrono::duration<double, std::micro>(t1 - t0).count());
+      prof_add("open.upload", std::chrono::duration<double, std::micro>(clk::now() - t1).count());
+    }
   } catch (...) {
     block_free(b->b);
     delete b;
@@ -675,17 +688,53 @@ int tsg_pipeline_matches_header(const tsg_query *q, const uint8_t *header, size_
   return guard([&] { *matches = pipeline_matches_block(*q, header, len) ? 1 : 0; });
 }
 
+// A read-only private mapping of a whole file, pages populated up front (the page data is
+// only read while the block decodes: no copy of it into a heap buffer, no zero fill)
+struct MappedFile {
+  const uint8_t *p = nullptr;
+  size_t n = 0;
+  void *m = MAP_FAILED;
+  std::vector<uint8_t> heap;  // (empty files, or a file the kernel will not map: read instead)
+  bool open(const std::string &path) {
+    const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+      if (errno == ENOENT) return false;
+      fail(TSG_E_IO, "open " + path + ": " + std::strerror(errno));
+    }
+    struct stat st;
+    if (fstat(fd, &st) == 0 && st.st_size > 0)
+      m = mmap(nullptr, size_t(st.st_size), PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    ::close(fd);
+    if (m != MAP_FAILED) {
+      p = static_cast<const uint8_t *>(m);
+      n = size_t(st.st_size);
+      return true;
+    }
+    if (!read_file(path, heap)) return false;
+    p = heap.data();
+    n = heap.size();
+    return true;
+  }
+  ~MappedFile() {
+    if (m != MAP_FAILED) munmap(m, n);
+  }
+};
+
 int tsg_block_open(tsg_ctx *ctx, const char *dir, int device_hint, tsg_block **out) {
   if (!ctx || !dir || !out) return TSG_E_INVALID;
   return guard([&] {
-    std::vector<uint8_t> meta, header, index, data;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    std::vector<uint8_t> meta, header, index;
+    MappedFile data;
     if (!read_file(join(dir, "search.meta.json"), meta)) fail(TSG_E_NOT_FOUND, "search.meta.json not found");
     if (!read_file(join(dir, "search-header"), header)) fail(TSG_E_IO, "search-header missing");
     if (!read_file(join(dir, "search-index"), index)) fail(TSG_E_IO, "search-index missing");
-    if (!read_file(join(dir, "search"), data)) fail(TSG_E_IO, "search missing");
+    if (!data.open(join(dir, "search"))) fail(TSG_E_IO, "search missing");
+    if (prof_on()) prof_add("open.read", std::chrono::duration<double, std::micro>(clk::now() - t0).count());
     open_common(ctx, [&](HostBlock &h) {
-      decode_search_block(meta.data(), meta.size(), true, std::move(header), index.data(), index.size(), data.data(),
-                          data.size(), 0, h);
+      decode_search_block(meta.data(), meta.size(), true, std::move(header), index.data(), index.size(), data.p,
+                          data.n, 0, h);
     }, device_hint, out);
   });
 }
