@@ -489,6 +489,7 @@ struct LPage {
   std::vector<uint64_t> vhash;
   std::vector<uint32_t> vloc;     // phase B: per value reference, its id in its hash shard
   std::vector<uint32_t> kv_sid;   // phase B: the table's value set id within its key
+  std::vector<uint64_t> kv_shash; // phase B: a multi-valued table's set hash
   std::vector<uint32_t> bykey, bykey0;  // tables grouped by provisional key (CSR)
   struct KStat {  // per provisional key: its tables in this page, their values and value bytes
     uint64_t tables = 0, refs = 0, bytes = 0;
@@ -1019,6 +1020,10 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
     };
     std::vector<uint32_t> SP(nk, 1);
     std::vector<std::vector<std::vector<uint64_t>>> srefs(nk);  // per set shard: page << 32 | table
+    bool any_multi = false;
+    for (size_t k = 0; k < nk; k++) any_multi = any_multi || !kin[k].single;
+    if (any_multi)  // each multi-valued table's set hash, computed once (kv_shash)
+      for_each_index(np, nthreads, [&](size_t i) { pages[i].kv_shash.resize(pages[i].kv_key.size()); });
     for_each_index(nk, nthreads, [&](size_t k) {
       if (kin[k].single) return;
       while (SP[k] < 16 && kin[k].tables / SP[k] > 65536) SP[k] <<= 1;
@@ -1029,7 +1034,7 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
         for (uint32_t b = pp.bykey0[k]; b < pp.bykey0[k + 1]; b++) {
           const uint32_t t = pp.bykey[b];
           const uint64_t h = set_hash(pp, uint32_t(k), t);
-          pp.kv_sid[t] = uint32_t(h >> 32);  // (the set hash's top half until the set id is known)
+          pp.kv_shash[t] = h;
           srefs[k][shard_of(h, SP[k])].push_back((uint64_t(i) << 32) | t);
         }
       }
@@ -1060,7 +1065,7 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
         const uint32_t t = uint32_t(r);
         tmp.clear();
         for (uint32_t v = pp.kv_v0[t]; v < pp.kv_v0[t + 1]; v++) tmp.push_back(vid_of(pp, k, v));
-        const uint64_t h = set_hash(pp, k, t);
+        const uint64_t h = pp.kv_shash[t];
         uint32_t sid = kNone;
         for (size_t i = ValueShard::probe0(h, mask);; i = (i + 1) & mask) {
           const uint64_t xs = S.slot[i];
@@ -1111,7 +1116,7 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
         LPage &pp = pages[i];
         for (uint32_t b = pp.bykey0[k]; b < pp.bykey0[k + 1]; b++) {
           const uint32_t t = pp.bykey[b];
-          pp.kv_sid[t] += sbase[k][shard_of(set_hash(pp, uint32_t(k), t), SP[k])];
+          pp.kv_sid[t] += sbase[k][shard_of(pp.kv_shash[t], SP[k])];
         }
       }
     });
