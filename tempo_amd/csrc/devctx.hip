@@ -123,10 +123,9 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
   const HostBlock &h = *b.host;
   d.device = dc.ordinal;
   d.n = h.n;
-  std::lock_guard<std::mutex> lk(dc.mu);
-  HIP_OK(hipSetDevice(dc.ordinal));
-  hipStream_t s = dc.stream;
   size_t n = h.n;
+  // Every host-side array is built first, without the device lock (blocks opened together
+  // prepare theirs concurrently); the lock is held for the allocations and copies only.
   // [dur32 | start_s | end_s | ds], npad entries each (whole tiles: kColPad), one allocation.
   // ds, the pool kernels' compact form of the other three (4 B where they read 12):
   //   bits 0..15  D16 = 2 * floor(dur / 1 ms) + (dur % 1 ms != 0), saturated at 0xffff: for whole-
@@ -149,25 +148,17 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     const uint32_t span = es - ss;  // (uint32: an end before the start wraps to a large value)
     scan[3 * npad + i] = uint32_t(d16) | (span < 0xffffu ? span : 0xffffu) << 16;
   }
-  d.dur32 = dev_upload(d, scan.data(), scan.size(), s);
-  d.start_s = d.dur32 + npad;
-  d.end_s = d.dur32 + 2 * npad;
-  d.dur64 = dev_upload(d, dur64.data(), n, s);
   // one-byte key columns: one allocation, npad bytes per narrow key
-  {
-    d.narrow_slot.assign(h.keys.size(), -1);
-    int nn = 0;
-    for (size_t k = 0; k < h.keys.size(); k++)
-      if (h.keys[k].width() == 1) d.narrow_slot[k] = nn++;
-    std::vector<uint8_t> ncol(std::max<size_t>(size_t(nn), 1) * npad, 0xff);
-    for (size_t k = 0; k < h.keys.size(); k++) {
-      if (d.narrow_slot[k] < 0) continue;
-      uint8_t *dst = ncol.data() + size_t(d.narrow_slot[k]) * npad;
-      const auto &col = h.keys[k].col;
-      for (size_t i = 0; i < n; i++) dst[i] = col[i] == kNone ? 0xff : uint8_t(col[i]);
-    }
-    d.narrow_base = dev_upload(d, ncol.data(), ncol.size(), s);
-    HIP_OK(hipStreamSynchronize(s));  // (ncol is a temporary)
+  d.narrow_slot.assign(h.keys.size(), -1);
+  int nn = 0;
+  for (size_t k = 0; k < h.keys.size(); k++)
+    if (h.keys[k].width() == 1) d.narrow_slot[k] = nn++;
+  std::vector<uint8_t> ncol(std::max<size_t>(size_t(nn), 1) * npad, 0xff);
+  for (size_t k = 0; k < h.keys.size(); k++) {
+    if (d.narrow_slot[k] < 0) continue;
+    uint8_t *dst = ncol.data() + size_t(d.narrow_slot[k]) * npad;
+    const auto &col = h.keys[k].col;
+    for (size_t i = 0; i < n; i++) dst[i] = col[i] == kNone ? 0xff : uint8_t(col[i]);
   }
   b.narrow.assign(h.keys.size(), nullptr);
   for (size_t k = 0; k < h.keys.size(); k++) {
@@ -181,41 +172,27 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     nd.identity = kc.identity;
     b.narrow[k] = intern_narrow(c, std::move(nd));
   }
-  d.ids = dev_upload(d, h.ids.data(), n * 16, s);
-  d.start_ns = dev_upload(d, h.start.data(), n, s);
-  d.end_ns = dev_upload(d, h.end.data(), n, s);
   std::vector<uint32_t> names(2 * n);
   for (size_t i = 0; i < n; i++) {
     names[2 * i] = h.svc_vid.empty() ? kNone : h.svc_vid[i];
     names[2 * i + 1] = h.name_vid.empty() ? kNone : h.name_vid[i];
   }
-  d.names = dev_upload(d, names.data(), 2 * n, s);
-  d.id_len = dev_upload(d, h.id_len.data(), n, s);
-  // the staging vectors must outlive the async copies
-  HIP_OK(hipStreamSynchronize(s));
-  for (const KeyColumn &kc : h.keys) {
-    DevKey k;
-    k.name = kc.name;
-    k.width = kc.width();
-    k.nvals = kc.nvals();
-    k.nsets = kc.nsets();
-    k.identity = kc.identity;
-    if (k.width == 1) {
-      k.col = const_cast<uint8_t *>(d.narrow_base) + size_t(d.narrow_slot[size_t(&kc - h.keys.data())]) * npad;
-    } else if (k.width == 2) {
-      std::vector<uint16_t> col(n);
-      for (size_t i = 0; i < n; i++) col[i] = kc.col[i] == kNone ? 0xffff : uint16_t(kc.col[i]);
-      k.col = dev_upload(d, col.data(), n, s, kColPad);
-      HIP_OK(hipStreamSynchronize(s));
-    } else {
-      k.col = dev_upload(d, kc.col.data(), n, s, kColPad);
+  // per key: its 16-bit column (width 2) and one contiguous blob in the order a workgroup
+  // stages it into LDS: [value offsets nvals+1 | value bytes (whole words) | set offsets
+  // nsets+1 | set values] (set arrays only for non-identity keys)
+  const size_t nk = h.keys.size();
+  std::vector<std::vector<uint16_t>> col16(nk);
+  std::vector<std::vector<uint32_t>> blobs(nk);
+  for (size_t k = 0; k < nk; k++) {
+    const KeyColumn &kc = h.keys[k];
+    if (kc.width() == 2) {
+      col16[k].resize(n);
+      for (size_t i = 0; i < n; i++) col16[k][i] = kc.col[i] == kNone ? 0xffff : uint16_t(kc.col[i]);
     }
-    // one contiguous blob per key, in the order a workgroup stages it into LDS:
-    // [value offsets nvals+1 | value bytes (whole words) | set offsets nsets+1 | set values]
-    // (set arrays only for non-identity keys)
     const size_t bw = (kc.dict_bytes.size() + 3) / 4;
     const size_t nso = kc.identity ? 0 : kc.set_off.size(), nsv = kc.identity ? 0 : kc.set_vals.size();
-    std::vector<uint32_t> blob(kc.dict_off.size() + bw + nso + nsv, 0);
+    std::vector<uint32_t> &blob = blobs[k];
+    blob.assign(kc.dict_off.size() + bw + nso + nsv, 0);
     uint32_t *bp = blob.data();
     std::memcpy(bp, kc.dict_off.data(), kc.dict_off.size() * 4);
     bp += kc.dict_off.size();
@@ -223,8 +200,39 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     bp += bw;
     if (nso) std::memcpy(bp, kc.set_off.data(), nso * 4);
     if (nsv) std::memcpy(bp + nso, kc.set_vals.data(), nsv * 4);
-    uint32_t *dblob = dev_upload(d, blob.data(), blob.size(), s);
-    HIP_OK(hipStreamSynchronize(s));  // (blob is a temporary)
+  }
+
+  std::lock_guard<std::mutex> lk(dc.mu);
+  HIP_OK(hipSetDevice(dc.ordinal));
+  hipStream_t s = dc.stream;
+  d.dur32 = dev_upload(d, scan.data(), scan.size(), s);
+  d.start_s = d.dur32 + npad;
+  d.end_s = d.dur32 + 2 * npad;
+  d.dur64 = dev_upload(d, dur64.data(), n, s);
+  d.narrow_base = dev_upload(d, ncol.data(), ncol.size(), s);
+  d.ids = dev_upload(d, h.ids.data(), n * 16, s);
+  d.start_ns = dev_upload(d, h.start.data(), n, s);
+  d.end_ns = dev_upload(d, h.end.data(), n, s);
+  d.names = dev_upload(d, names.data(), 2 * n, s);
+  d.id_len = dev_upload(d, h.id_len.data(), n, s);
+  for (size_t kk = 0; kk < nk; kk++) {
+    const KeyColumn &kc = h.keys[kk];
+    DevKey k;
+    k.name = kc.name;
+    k.width = kc.width();
+    k.nvals = kc.nvals();
+    k.nsets = kc.nsets();
+    k.identity = kc.identity;
+    if (k.width == 1) {
+      k.col = const_cast<uint8_t *>(d.narrow_base) + size_t(d.narrow_slot[kk]) * npad;
+    } else if (k.width == 2) {
+      k.col = dev_upload(d, col16[kk].data(), n, s, kColPad);
+    } else {
+      k.col = dev_upload(d, kc.col.data(), n, s, kColPad);
+    }
+    const size_t bw = (kc.dict_bytes.size() + 3) / 4;
+    const size_t nso = kc.identity ? 0 : kc.set_off.size(), nsv = kc.identity ? 0 : kc.set_vals.size();
+    uint32_t *dblob = dev_upload(d, blobs[kk].data(), blobs[kk].size(), s);
     k.dict_off = dblob;
     k.dict_bytes = reinterpret_cast<uint8_t *>(dblob + kc.dict_off.size());
     k.dict_nbytes = kc.dict_bytes.size();
@@ -235,6 +243,8 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     }
     d.keys.push_back(k);
   }
+  // the staging vectors must outlive the async copies
+  HIP_OK(hipStreamSynchronize(s));
   upload_desc(d, s);
 }
 

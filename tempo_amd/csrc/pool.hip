@@ -936,6 +936,11 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   thread_local std::vector<uint64_t> per;
   per.assign(nsegs, 0);
   const uint64_t span = uint64_t(U) * kPoolTile;  // positions < span <= 2^31 * 512
+  uint32_t lb = 6;
+  while ((1ull << lb) < total && lb < 20) lb++;
+  uint32_t sb = 0;
+  while (((span - 1) >> sb) >= (1ull << lb)) sb++;  // bucket of the largest position < 2^lb
+  bucket.assign((size_t(1) << lb) + 1, 0);
   uint64_t nrec = 0;
   for (uint32_t w = 0; w < W; w++)
     for (uint32_t i = 0; i < counts[w]; i++) {
@@ -946,14 +951,9 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
       per[ps]++;
       const uint64_t at = uint64_t(PA.blk[ps].ubase) * kPoolTile + (r.entry - PA.ebase[ps]);
       keys[nrec++] = (at << 20) | slot;
+      bucket[size_t(at >> sb) + 1]++;  // (bucket counts in the same pass)
     }
   tr.mark("post.keys");
-  uint32_t lb = 6;
-  while ((1ull << lb) < total && lb < 20) lb++;
-  uint32_t sb = 0;
-  while (((span - 1) >> sb) >= (1ull << lb)) sb++;  // bucket of the largest position < 2^lb
-  bucket.assign((size_t(1) << lb) + 1, 0);
-  for (uint64_t i = 0; i < total; i++) bucket[size_t((keys[i] >> 20) >> sb) + 1]++;
   for (size_t b = 1; b < bucket.size(); b++) bucket[b] += bucket[b - 1];
   for (uint64_t i = 0; i < total; i++) sorted[bucket[size_t((keys[i] >> 20) >> sb)]++] = keys[i];
   // (bucket[b] is now the end of bucket b)
