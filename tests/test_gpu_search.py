@@ -454,3 +454,31 @@ def test_search_raw_tuple_identity_cache(engine, tmp_path):
     finally:
         c.close()
         b.close()
+
+
+def test_concurrent_opens_match_oracle(engine, tmp_path):
+    """Blocks opened from several threads at once (the loader then splits the CPUs between
+    the decodes, and the uploads prepare their arrays outside the device lock): every block's
+    columns, dictionaries and names come out as the oracle reads them."""
+    from concurrent.futures import ThreadPoolExecutor
+    specs = [(40_000, 21, 0, T.ENC_SNAPPY), (20_000, 22, 1, T.ENC_SNAPPY), (30_000, 23, 0, T.ENC_NONE),
+             (40_000, 24, 0, T.ENC_SNAPPY)]
+    paths = []
+    for i, (n, seed, prof, enc) in enumerate(specs):
+        p = os.path.join(str(tmp_path), f"c{i}")
+        T.synth_search_block(p, n, seed=seed, profile=prof, encoding=enc, page_size=64 * 1024)
+        paths.append(p)
+    with ThreadPoolExecutor(len(paths)) as ex:
+        blocks = list(ex.map(engine.open_block, paths))
+    try:
+        oblocks = [O.Block(p) for p in paths]
+        for tags, mn, mx in [({"service.name": "svc-07"}, 10, 1000), ({"http.method": "get", "status.code": "1"}, 0, 0),
+                             ({"name": "span-0042"}, 0, 0)]:
+            req = T.SearchRequest(tags=tags, min_duration_ms=mn, max_duration_ms=mx)
+            got, met = engine.search(blocks, T.Pipeline(req))
+            exp, omet, st = O.search(oblocks, tags=tags, min_ms=mn, max_ms=mx)
+            assert st == 0 and len(exp) > 0
+            assert_parity(got, met, exp, omet)
+    finally:
+        for b in blocks:
+            b.close()
