@@ -34,6 +34,9 @@ struct Aql {
   hsa_signal_t last{0};
   double ns_per_tick = 1.0;
   std::unordered_map<std::string, AqlKernel> kernels;
+  // the HDP flush register (hsa_amd_hdp_flush_t): host writes through the BAR pass the GPU's
+  // host data path, which buffers them; a write to this register pushes them to memory
+  volatile uint32_t *hdp_flush = nullptr;
 };
 
 static constexpr uint32_t kSlots = 64, kSlotBytes = 8192;
@@ -102,6 +105,14 @@ Aql *aql_open(int hip_ordinal) {
   }, &f);
   if (!f.found) return fail("no HSA agent at the device's PCI location");
   a->agent = f.agent;
+  // the argument slots are written by the host through the BAR: only a large-BAR device maps
+  // all of VRAM for the host; otherwise HIP launches
+  int large_bar = 0;
+  if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, hip_ordinal) != hipSuccess || !large_bar)
+    return fail("not a large-BAR device (argument slots not host-writable)");
+  hsa_amd_hdp_flush_t hdp{};
+  if (hsa_agent_get_info(a->agent, hsa_agent_info_t(HSA_AMD_AGENT_INFO_HDP_FLUSH), &hdp) == HSA_STATUS_SUCCESS)
+    a->hdp_flush = hdp.HDP_MEM_FLUSH_CNTL;
   if (hsa_code_object_reader_create_from_memory(a->code.data(), a->code.size(), &a->reader) != HSA_STATUS_SUCCESS)
     return fail("code object reader");
   if (hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &a->exe) !=
@@ -149,7 +160,7 @@ void aql_close(Aql *a) {
   delete a;
 }
 
-AqlKernel aql_kernel(Aql *a, const char *name) {
+AqlKernel aql_kernel(Aql *a, const char *name, uint32_t max_kernarg) {
   if (!a) return {};
   auto it = a->kernels.find(name);
   if (it != a->kernels.end()) return it->second;
@@ -161,7 +172,13 @@ AqlKernel aql_kernel(Aql *a, const char *name) {
     hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.group);
     hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.priv);
     hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kernarg);
-    if (k.kernarg > kSlotBytes) k.kobj = 0;
+    // the slot holds the kernel's own argument struct and nothing else: a kernel that reads
+    // implicit arguments (blockDim / gridDim, printf: hidden arguments past the struct under
+    // code object v5) would read unwritten bytes, so it launches through HIP
+    if (k.kernarg > kSlotBytes || k.kernarg > max_kernarg) {
+      k.kobj = 0;
+      note("kernel reads implicit arguments (kernarg segment larger than its argument struct)");
+    }
   } else {
     note("kernel symbol missing from the code object");
   }
@@ -193,15 +210,28 @@ int aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uint
     std::memcpy(slot + pt.first, src + pt.first, pt.second);
     last = pt.first + pt.second;
   }
-  // the argument words reach device memory before the packet can be read: the write-combined
-  // BAR stores are flushed (sfence) ahead of the doorbell store, and posted writes to the
-  // device stay in order; TSG_AQL_READBACK=1 reads the last word back instead (as HIP does)
-  static const bool readback = [] {
-    const char *e = std::getenv("TSG_AQL_READBACK");
-    return e && std::atoi(e) != 0;
+  // The argument words must be in device memory before the kernel's waves load them. The
+  // BAR stores are write-combined (sfence drains them onto the bus); on the device they pass
+  // the host data path (HDP), which buffers host writes, and the doorbell reaches the command
+  // processor on another path. Default (TSG_AQL_FENCE=hdp): write the HDP flush register and
+  // read it back — the read returns after the flush, so every argument word is in memory
+  // before the doorbell is rung (HIP flushes the same way before a launch whose
+  // arguments live in device memory). `readback`: read the last argument word back instead;
+  // `sfence`: posted-write order only (opt-in, measured faster, not guaranteed).
+  static const int mode = [] {
+    const char *e = std::getenv("TSG_AQL_FENCE");
+    if (e && !std::strcmp(e, "sfence")) return 0;
+    if (e && !std::strcmp(e, "readback")) return 1;
+    if (const char *r = std::getenv("TSG_AQL_READBACK"); r && std::atoi(r) != 0) return 1;
+    return 2;
   }();
-  if (readback) (void)*reinterpret_cast<volatile uint32_t *>(slot + ((last - 1) & ~3u));
-  else __builtin_ia32_sfence();
+  __builtin_ia32_sfence();
+  if (mode == 2 && a->hdp_flush) {
+    *a->hdp_flush = 1u;
+    (void)*a->hdp_flush;
+  } else if (mode >= 1) {
+    (void)*reinterpret_cast<volatile uint32_t *>(slot + ((last - 1) & ~3u));
+  }
   hsa_queue_t *q = a->queue;
   const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
   while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {

@@ -22,8 +22,9 @@ struct AqlKernel {
 // TSG_AQL=0, no code object, or any HSA call failing (then the caller launches through HIP).
 Aql *aql_open(int hip_ordinal);
 void aql_close(Aql *a);
-// a kernel of the code object by its symbol name (without ".kd")
-AqlKernel aql_kernel(Aql *a, const char *name);
+// a kernel of the code object by its symbol name (without ".kd"); kobj = 0 (launch through
+// HIP) when its kernarg segment is larger than max_kernarg, the size of its argument struct
+AqlKernel aql_kernel(Aql *a, const char *name, uint32_t max_kernarg);
 // One dispatch of grid x block threads with dyn_lds bytes of dynamic LDS. The kernel's
 // argument block is assembled in a device-memory slot from `parts` (offset, bytes) of `args`
 // (only the parts the kernel reads for this launch: the rest of the slot is stale).

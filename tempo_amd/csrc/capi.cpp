@@ -26,26 +26,18 @@
 #include "block.hpp"
 #include "common.hpp"
 #include "engine.hpp"
+#include "park.hpp"
 #include "proto.hpp"
 #include "writer.hpp"
 
 // One persistent host thread per device for multi-device calls: a search or lookup whose
 // blocks span devices hands each further device's part to that device's worker (the caller
 // runs the first device's part itself) instead of starting a thread per device per call.
-// A lock for the short critical sections concurrent searches share (the coalescer's
-// queue, the result-holder pool): a contended std::mutex parks a caller in the kernel and
-// its wake-up costs tens of microseconds, more than the work it guards.
-struct SpinLock {
-  std::atomic<bool> f{false};
-  void lock() {
-    for (uint32_t n = 0;; n++) {
-      if (!f.load(std::memory_order_relaxed) && !f.exchange(true, std::memory_order_acquire)) return;
-      if (n < 4096) __builtin_ia32_pause();
-      else std::this_thread::yield();
-    }
-  }
-  void unlock() { f.store(false, std::memory_order_release); }
-};
+// Short critical sections concurrent searches share (the coalescer's queue, the result-holder
+// pool) take a ParkLock (park.hpp): a bounded spin, then the futex — a contended std::mutex
+// parks at once and its wake-up costs tens of microseconds, an unbounded spin keeps a
+// preempted holder off its CPU.
+using SpinLock = tsg::ParkLock;
 
 struct DevWorker {
   std::mutex m;
@@ -224,19 +216,15 @@ struct tsg_ctx {
     SpinLock m;
     std::vector<CoalReq *> pending;
     std::atomic<bool> busy{false};
-    // waiters spin for about one launch, then park here until the leader hands off (an
-    // oversubscribed host must not run a spinning waiter instead of the leader)
-    std::mutex wm;
-    std::condition_variable cv;
-    std::atomic<int> sleepers{0};
+    // waiters spin (bounded, and only while the host has CPUs to spare), then park on `park`
+    // until the leader hands off (park.hpp: an oversubscribed host must not run a spinning
+    // waiter instead of the leader)
+    tsg::EpochPark park;
+    std::atomic<int> spinning{0};
     // searches with a block on this device that have not reached their device stage yet:
     // the leader waits (bounded) for them to queue
     std::atomic<int> approaching{0};
-    void wake() {
-      if (sleepers.load(std::memory_order_acquire) == 0) return;
-      std::lock_guard<std::mutex> lk(wm);
-      cv.notify_all();
-    }
+    void wake() { park.notify(); }
   };
   // one per device, created at tsg_init (read without a lock afterwards)
   std::vector<std::pair<const void *, std::unique_ptr<Coalescer>>> coal;
@@ -967,6 +955,16 @@ static bool same_query(const tsg_query &a, const tsg_query &b) {
   return true;
 }
 
+// How long a coalesced caller spins before it parks (TSG_WAIT_SPIN_US, default 40 µs: about
+// a limit query's launch, so that on a host with CPUs to spare the hand-off costs no wake-up).
+static uint64_t wait_spin_ns() {
+  static const uint64_t ns = [] {
+    const char *e = std::getenv("TSG_WAIT_SPIN_US");
+    return uint64_t(e ? std::max(0, std::atoi(e)) : 40) * 1000ull;
+  }();
+  return ns;
+}
+
 // device_search through the device's coalescer (tsg_ctx::Coalescer). TSG_COALESCE=0 turns
 // it off; TSG_COALESCE_US (default 30) bounds the leader's wait for approaching callers.
 static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std::pair<uint32_t, Block *>> &list,
@@ -998,23 +996,29 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
   }
   ap.leave();
   const auto t_wait = std::chrono::steady_clock::now();
-  for (uint32_t spins = 0; !r.done.load(std::memory_order_acquire); spins++) {
+  bool spun = false;
+  for (;;) {
+    if (r.done.load(std::memory_order_acquire)) break;
     bool expect = false;
     if (c.busy.load(std::memory_order_relaxed) ||
         !c.busy.compare_exchange_strong(expect, true, std::memory_order_acq_rel)) {
-      // spin about one query (a launch + its host work, ~60-120 us; a parked waiter pays a
-      // futex wake-up of tens of us), then park until the leader hands off
-      if ((spins & 63u) != 63u ||
-          std::chrono::steady_clock::now() - t_wait < std::chrono::microseconds(250)) {
-        __builtin_ia32_pause();
-        continue;
+      // A waiter: the leader hands off by setting `done` (or clearing `busy`) and bumping the
+      // park epoch. Spin once, for at most spin_ns and only while fewer waiters spin than the
+      // caller's CPUs leave room for beside the leader; then park (bounded re-checks).
+      const uint32_t e = c.park.read();
+      auto ready = [&] { return r.done.load(std::memory_order_acquire) || !c.busy.load(std::memory_order_acquire); };
+      if (ready()) continue;
+      if (!spun) {
+        spun = true;
+        const int cpus = tsg::host_threads_now();
+        if (c.spinning.fetch_add(1, std::memory_order_acq_rel) + 2 < cpus && tsg::spin_for(wait_spin_ns(), ready)) {
+          c.spinning.fetch_sub(1, std::memory_order_acq_rel);
+          continue;
+        }
+        c.spinning.fetch_sub(1, std::memory_order_acq_rel);
       }
-      std::unique_lock<std::mutex> lk(c.wm);
-      c.sleepers.fetch_add(1, std::memory_order_acq_rel);
-      c.cv.wait_for(lk, std::chrono::microseconds(500), [&] {
-        return r.done.load(std::memory_order_acquire) || !c.busy.load(std::memory_order_acquire);
-      });
-      c.sleepers.fetch_sub(1, std::memory_order_acq_rel);
+      if (prof_on()) prof_add("coal.park", 1.0);
+      c.park.wait(e, 2'000'000);
       continue;
     }
     if (r.done.load(std::memory_order_acquire)) {  // served while we took the lead
@@ -1026,13 +1030,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
     const bool prof = prof_on();
     const auto t_lead = std::chrono::steady_clock::now();
     if (prof) prof_add("coal.lead_after_us", std::chrono::duration<double, std::micro>(t_lead - t_wait).count());
-    if (window_ns) {
-      const auto t0 = std::chrono::steady_clock::now();
-      while (c.approaching.load(std::memory_order_acquire) > 0 &&
-             uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
-                          .count()) < window_ns)
-        __builtin_ia32_pause();
-    }
+    if (window_ns) tsg::spin_for(window_ns, [&] { return c.approaching.load(std::memory_order_acquire) <= 0; });
     // the batch: this caller's part first, then every queued part with the same query,
     // per-block limit and flags, up to one launch's blocks
     thread_local std::vector<tsg_ctx::CoalReq *> batch;

@@ -239,8 +239,10 @@ static size_t snappy_framed_size(const uint8_t *src, size_t n) {
 
 void snappy_framed_decode(const uint8_t *src, size_t n, std::vector<uint8_t> &out) {
   out.clear();
-  // one allocation (and one zero fill) for the whole stream instead of a growing vector
-  out.reserve(snappy_framed_size(src, n));
+  // one allocation (and one zero fill) for the whole stream instead of a growing vector; the
+  // chunk headers are not checked yet, so the reserve is capped (a corrupt header can claim
+  // 64 KiB for an 11-byte chunk) and the vector grows past it if it must
+  out.reserve(std::min<size_t>(snappy_framed_size(src, n), 16 * n + (size_t(1) << 20)));
   size_t s = 0;
   bool hdr = false;
   while (s < n) {

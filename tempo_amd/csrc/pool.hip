@@ -791,7 +791,8 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
     // dispatch timestamps, as the untimed ones run); explicit per-call timing stays on HIP events
     const bool aql_timed = first && defer && !time_scan;
     if ((!timed || aql_timed) && !want_stamps && dc.aql)
-      ak = aql_kernel(dc.aql, kernel_symbol(use_static, q.nterms, has_dur, q.has_range, dc.pool_nt).c_str());
+      ak = aql_kernel(dc.aql, kernel_symbol(use_static, q.nterms, has_dur, q.has_range, dc.pool_nt).c_str(),
+                      uint32_t(sizeof(PoolArgs)));
     if (ak.kobj) {
       // our own AQL packet (aql.hpp): only the argument words this launch's kernel reads
       thread_local std::vector<std::pair<uint32_t, uint32_t>> parts;

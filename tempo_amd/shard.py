@@ -392,7 +392,8 @@ def distributed_search_limit(search, cancel, limit: int, group=None, dst: int = 
        before it as `seen` (unless none), stopping exactly where the single consumer stops;
        ranks after it are told to drop, cancelling a search still running (tsg_cancel).
     3. The kept responses are gathered to `dst` and concatenated in rank order.
-    Messages are point-to-point over `group` (gloo: host tensors)."""
+    Messages are point-to-point over `group` (gloo: host tensors). limit <= 0 means every
+    match, as in tsg_search: no rank is a stop point, every response is kept."""
     import threading
 
     import torch
@@ -488,7 +489,7 @@ def distributed_search_limit(search, cancel, limit: int, group=None, dst: int = 
             if k not in seen_set:
                 seen_set.add(k)
                 seen_ids.append(x)
-                if len(seen_set) >= limit:
+                if limit > 0 and len(seen_set) >= limit:  # (limit <= 0: every match, no stop)
                     reached = True
                     break
         if reached:

@@ -239,7 +239,8 @@ def shim_pattern_lib():
         S = C.CDLL(path)
         vp = C.c_void_p
         S.tsgx_shim_pattern.argtypes = [vp, C.POINTER(vp), C.c_size_t, C.c_size_t, C.POINTER(_Query), C.c_uint32,
-                                        C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+                                        C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64)]
         _shim = S
     return _shim
 
@@ -582,18 +583,23 @@ class Engine:
         _check(lib().tsg_cancel(self.h, query_id))
 
     def shim_pattern(self, sets: Sequence[Sequence["BackendSearchBlock"]], pipeline: Pipeline, rounds: int,
-                     limit: int = 0):
+                     limit: int = 0, digest: bool = False):
         """The Go shim's ingester call pattern (instance_search.go:164-185) driven from C
         threads (libtsg_shim_pattern.so): per query, one thread per block, each a tsg_search
         over its one block with `limit`; query r searches sets[r % len(sets)] (equal-sized
-        sets). Returns (per-query wall ns, per-query record counts)."""
+        sets). Returns (per-query wall ns, per-query record counts), and with digest=True
+        also the per-query record digests (shim_digest: the sum over the set's blocks of
+        FNV-1a 64 over each block's ordered (entry, id, start) records)."""
         sp = shim_pattern_lib()
         nb = len(sets[0])
         assert nb and all(len(s) == nb for s in sets)
         arr = (C.c_void_p * (nb * len(sets)))(*[b.h for s in sets for b in s])
         ns = (C.c_uint64 * rounds)()
         nm = (C.c_uint64 * rounds)()
-        _check(sp.tsgx_shim_pattern(self.h, arr, nb, len(sets), pipeline.query, limit, rounds, ns, nm))
+        dg = (C.c_uint64 * rounds)() if digest else None
+        _check(sp.tsgx_shim_pattern(self.h, arr, nb, len(sets), pipeline.query, limit, rounds, ns, nm, dg))
+        if digest:
+            return list(ns), list(nm), list(dg)
         return list(ns), list(nm)
 
     def kernel_times(self, cap: int = 65536) -> List[int]:

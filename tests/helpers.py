@@ -146,3 +146,21 @@ def damage_data_page(path, k, how="payload"):
     elif how == "truncate":
         b = b[:start + length // 2]
     open(p, "wb").write(bytes(b))
+
+
+def shim_digest(per_block):
+    """tsgx_shim_pattern's per-round digest (shim_pattern.cpp result_digest) from the oracle's
+    ordered matches of each block of the set: the sum mod 2^64 over blocks i of FNV-1a 64 over
+    (i as u32, then per match its scan position u64, its id right-aligned in 16 bytes, its start u64)."""
+    import struct
+    M = (1 << 64) - 1
+    total = 0
+    for i, matches in enumerate(per_block):
+        h = 0xcbf29ce484222325
+        buf = bytearray(struct.pack("<I", i))
+        for m in matches:
+            buf += struct.pack("<Q", m["entry_idx"]) + bytes(16 - len(m["id"])) + m["id"] + struct.pack("<Q", m["start_ns"])
+        for b in buf:
+            h = ((h ^ b) * 0x100000001b3) & M
+        total = (total + h) & M
+    return total

@@ -114,9 +114,10 @@ def expected(paths, limit):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("limit", [5, 40, 10_000])
+@pytest.mark.parametrize("limit", [0, 5, 40, 10_000])
 def test_limit_over_ranks_equals_one_consumer(tmp_path, world, limit):
-    """Sparse blocks: the stop lands in rank 0, in a later rank, or nowhere (every match)."""
+    """Sparse blocks: the stop lands in rank 0, in a later rank, or nowhere (every match).
+    limit 0 is "every match" (as in tsg_search): no rank is a stop point."""
     paths = _make_blocks(str(tmp_path))
     got, _ = run(paths, world, limit)
     exp = expected(paths, limit)
