@@ -50,6 +50,10 @@ T0 = 1_700_000_000
 QUERY = dict(tags={"service.name": "svc-07", "http.method": "get", "status.code": "error"},
              min_duration_ms=10, max_duration_ms=1000, start=T0 + 900, end=T0 + 2700)
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# device of the small timing / count tensors reduced over the ranks: cuda over RCCL, or the
+# host under --ranks-share-gpu (several ranks on one GPU: the process group is gloo)
+RED_DEVICE = "cuda"
+SHARED_GPU = False
 # The config-2 query (3 u8 term columns, duration + range filters, 10 blocks) runs
 # the one-launch path; TSG_NO_FAST=1 forces the general path (prep + search kernels).
 # The last template argument of the one-launch kernel is segment mode (per-workgroup
@@ -165,7 +169,8 @@ def parse():
                     help="extra timed steps on one set (the MALL-resident regime), reported beside; 0 = skip")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="threads of the columnar CPU baseline (0 = this process's CPU share, at most 16)")
+                    help="threads of the CPU baselines (0 = this job's CPU share: the process's CPUs, at most 16, "
+                         "the GPU box's per-GPU share)")
     ap.add_argument("--events", type=int, default=4,
                     help="HIP events around the search kernel of every N-th timed step (roofline.achieved: "
                          "the average over those launches); 0 = off")
@@ -193,12 +198,19 @@ def parse():
     ap.add_argument("--cfg3-blocks", type=int, default=25)
     ap.add_argument("--cfg3-entries", type=int, default=5_000_000)
     ap.add_argument("--cfg3-steps", type=int, default=64)
+    ap.add_argument("--cfg1", type=int, default=1,
+                    help="config-1 leg (rank 0): one 1 M-entry block, one tag=value; GPU steps + the CPU pipeline "
+                         "restated (single thread and the reference harness's 10-thread shape) after the GPU legs")
+    ap.add_argument("--cfg1-steps", type=int, default=100)
     ap.add_argument("--cfg5", type=int, default=1, help="config-5 leg: batched trace-ID lookup (0 = skip)")
     ap.add_argument("--cfg5-blocks", type=int, default=200)
     ap.add_argument("--cfg5-objects", type=int, default=100_000)
     ap.add_argument("--cfg5-probes", type=int, default=10_000_000, help="probes over all ranks (sharded by id)")
     ap.add_argument("--cfg5-steps", type=int, default=5)
     ap.add_argument("--parity", type=int, default=1, help="oracle parity of the cfg3/cfg4/cfg5 legs (untimed)")
+    ap.add_argument("--ranks-share-gpu", action="store_true",
+                    help="N > 1 on fewer GPUs: every rank on device 0 with a gloo process group (a rehearsal "
+                         "of the multi-rank legs on a 1-GPU lease; RCCL legs are reported as skipped)")
     ap.add_argument("--pin", default="auto", choices=["auto", "none"],
                     help="auto: keep this process on the CPUs of its GPU's NUMA node (tsg_device_numa_node)")
     ap.add_argument("--workdir", default=None)
@@ -246,7 +258,7 @@ def launch_ranks(args, argv, device_count=None):
     if device_count is None:
         import torch
         device_count = torch.cuda.device_count()
-    if device_count < args.gpus:
+    if device_count < args.gpus and not (args.ranks_share_gpu and device_count >= 1):
         print(f"bench: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {device_count}",
               file=sys.stderr, flush=True)
         return 2
@@ -364,38 +376,48 @@ def parallel(fn, items):
     return out
 
 
-def cpu_baselines(paths, got, threads):
+def cpu_baselines(paths, got, threads, oracle_threads=None):
     """The reference's scan restated (oracle: snappy decode + flatbuffer walk + ContainsTag,
     one thread per block like instance.searchLocalBlocks) and the CPU columnar variant
-    (the same predicates over host-decoded columns, `threads` threads), both on every
-    block of this rank's set. Returns the cpu_baseline object."""
+    (the same predicates over host-decoded columns, `threads` threads), both on this rank's
+    set. The oracle leg runs one thread per block over `oracle_threads` block searches (the
+    set's blocks cycled: every thread a whole-block search, BASELINE.md row 2's model on as
+    many cores as the job may use); parity is checked on one pass over the set. Returns the
+    cpu_baseline object."""
     from oracle import oracle as O
     q = dict(tags=QUERY["tags"], min_ms=QUERY["min_duration_ms"], max_ms=QUERY["max_duration_ms"],
              start=QUERY["start"], end=QUERY["end"])
     oblocks = [O.Block(p) for p in paths]
     nb = len(oblocks)
+    exp, omet, st = O.search(oblocks, nthreads=nb, **q)
+    per_block = omet["traces_inspected"] / nb
+    nthr = max(nb, int(oracle_threads or nb))
+    work = [oblocks[i % nb] for i in range(nthr)]  # one block search per thread
     t0 = time.perf_counter()
     reps = 0
     while True:
-        exp, omet, st = O.search(oblocks, nthreads=nb, **q)
+        _, wmet, wst = O.search(work, nthreads=nthr, **q)
         reps += 1
         if time.perf_counter() - t0 > 10 or reps >= 5:
             break
     cpu_s = (time.perf_counter() - t0) / reps
-    entries = omet["traces_inspected"]
+    entries = wmet["traces_inspected"]
     # parity of the GPU's full result against it: every field of every match, in order
     gk = [(m.block_idx, m.entry_idx, m.trace_id, m.start_time_unix_nano, m.end_time_unix_nano, m.duration_ms,
            m.root_service_name.encode(), m.root_trace_name.encode()) for m in got]
     ek = [(m["block_idx"], m["entry_idx"], m["id"], m["start_ns"], m["end_ns"], m["duration_ms"], m["root_service"],
            m["root_name"]) for m in exp]
     out = {
-        "value": entries / cpu_s, "unit": "entries/s", "cores": nb, "kind": "port",
+        "value": entries / cpu_s, "unit": "entries/s", "cores": nthr, "kind": "port",
         "sample": f"oracle BackendSearchBlock.Search restatement (snappy decode + flatbuffer walk + ContainsTag "
-                  f"included), all {nb} blocks ({entries} entries) of the GPU's set, one thread per block "
-                  f"(instance.searchLocalBlocks), {reps} rep(s)",
+                  f"included), one thread per block search: {nthr} whole-block searches of 1 M entries at once "
+                  f"({nb} distinct blocks of the GPU's set, cycled; {entries} entries), {reps} rep(s); "
+                  f"{nthr} threads = this job's CPU share of the box (nproc {os.cpu_count()})",
+        "per_thread_entries_per_s": entries / cpu_s / nthr,
         "decompression_included": True,
         "nproc": os.cpu_count(), "cpu_share": len(os.sched_getaffinity(0)), "cpu_model": cpu_model(),
-        "parity": gk == ek and omet["blocks_inspected"] == nb,
+        "parity": st == 0 and wst == 0 and gk == ek and omet["blocks_inspected"] == nb,
+        "entries_per_block": per_block,
     }
     # columnar: decode once (not timed, like the GPU's resident columns), then time the scan
     t0 = time.perf_counter()
@@ -410,14 +432,69 @@ def cpu_baselines(paths, got, threads):
             break
     col_s = (time.perf_counter() - t0) / reps
     out["columnar"] = {
-        "value": entries / col_s, "unit": "entries/s", "cores": threads,
-        "sample": f"the same {entries} entries decoded once into host columns ({build_s:.1f}s, untimed), "
-                  f"Pipeline predicates over the columns on {threads} threads, {reps} rep(s); threads capped "
-                  f"at 16 = one GPU job's CPU share of the shared GPU box (of {os.cpu_count()} CPUs there), "
-                  f"not every host core; --cpu-threads overrides",
+        "value": omet["traces_inspected"] / col_s, "unit": "entries/s", "cores": threads,
+        "sample": f"the same {omet['traces_inspected']} entries decoded once into host columns ({build_s:.1f}s, "
+                  f"untimed), Pipeline predicates over the columns on {threads} threads, {reps} rep(s); threads = "
+                  f"this job's CPU share of the shared GPU box (of {os.cpu_count()} CPUs there); --cpu-threads overrides",
         "parity": cm == len(got) and ch == O.match_hash([(m.block_idx, m.entry_idx) for m in got]),
     }
     return out
+
+
+CFG1_QUERY = dict(tags={"service.name": "svc-07"})
+
+
+def cfg1_leg(args, eng, block, path, steps):
+    """BASELINE config 1: one synthetic local-disk search block (1 M traces, ~20 tags each),
+    one tag=value matcher. The GPU leg here (tsg_search over that one resident block, timed
+    steps); the CPU legs (the reference pipeline restated, the reference harness's shape) run
+    after the GPU legs, in the returned closure, with parity of the GPU's matches."""
+    import tempo_amd as T
+    pipe = T.Pipeline(T.SearchRequest(**CFG1_QUERY))
+    blk = (block,)
+    cols, gmet = eng.search_columns(list(blk), pipe)
+    for _ in range(5):
+        eng.search_raw(blk, pipe)
+    eng.kernel_times()
+    ts = []
+    for i in range(steps):
+        t0 = time.perf_counter()
+        eng.search_raw(blk, pipe, flags=T.SEARCH_TIME_DEFER if i % 4 == 2 else 0, metrics=False)
+        ts.append(time.perf_counter() - t0)
+    kns = eng.kernel_times()
+    entries = gmet.inspected_traces
+    res = {"workload": "config 1: one 1 M-entry block (~20 tags per entry, snappy 1 MiB pages), tag=value "
+                       "{service.name: svc-07}, full scan", "entries": entries, "matches": len(cols["start_ns"]),
+           "gpu": {"steps": steps, "step_us": pct([x * 1e6 for x in ts]), "kernel_us": pct([x / 1e3 for x in kns]),
+                   "entries_per_s": entries * steps / sum(ts),
+                   "scan_bytes": gmet.scan_bytes}}
+
+    def cpu():
+        from oracle import oracle as O
+        ob = O.Block(path)
+        q = oracle_query(CFG1_QUERY)
+        t0 = time.perf_counter()
+        exp, omet, st = O.search([ob], **q)
+        one_s = time.perf_counter() - t0
+        ok = st == 0 and columns_vs_oracle(cols, gmet, exp, omet, 1)
+        # the reference harness's shape (backend_search_block_test.go:128-172): 10 goroutines,
+        # each searching the block 10 times; here 10 threads x 2 searches (bounded sample)
+        loops = 2
+        t0 = time.perf_counter()
+        for _ in range(loops):
+            _, hm, _ = O.search([ob] * 10, nthreads=10, **q)
+        h_s = time.perf_counter() - t0
+        return {"ok": bool(ok), "checked": "every match (every field, in order) + metrics vs the oracle",
+                "cpu_single_thread": {"value": omet["traces_inspected"] / one_s, "unit": "entries/s", "cores": 1,
+                                      "kind": "port", "mib_per_s": omet["bytes_inspected"] / one_s / 2**20,
+                                      "sample": "one BackendSearchBlock.Search of the block (oracle restatement, "
+                                                "snappy decode + flatbuffer walk included)"},
+                "cpu_harness_shape": {"value": 10 * loops * omet["traces_inspected"] / h_s, "unit": "entries/s",
+                                      "cores": 10, "kind": "port",
+                                      "mib_per_s": 10 * loops * omet["bytes_inspected"] / h_s / 2**20,
+                                      "sample": f"10 threads x {loops} searches of the block at once (the reference "
+                                                f"benchmark runs 10 goroutines x 10)"}}
+    return res, cpu
 
 
 def concurrent_leg(args, base, pipe, streams, entries, dist, world, local):
@@ -463,7 +540,7 @@ def concurrent_leg(args, base, pipe, streams, entries, dist, world, local):
         raise errs[0]
     if dist:
         dist.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=RED_DEVICE)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     for cs in csets:
@@ -571,7 +648,7 @@ def cfg3_leg(args, eng, pipe, workdir, rank, world, dist, sflags, gen_thread=Non
     kns = eng.kernel_times() if sflags else []
     if dist:
         dist.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=RED_DEVICE)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     scan_bytes = met.scan_bytes
@@ -807,7 +884,7 @@ def cfg5_leg(args, eng, shared, rank, world, dist, gen_thread=None):
     elapsed = time.perf_counter() - t0
     kmed = sorted(kns)[len(kns) // 2]
     if dist:
-        t = torch.tensor([elapsed, float(kmed)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, float(kmed)], dtype=torch.float64, device=RED_DEVICE)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kmed = float(t[0].item()), float(t[1].item())
     res = {"workload": f"config 5: {args.cfg5_probes} probe ids (50 % present) x {args.cfg5_blocks} v2 blocks "
@@ -821,12 +898,14 @@ def cfg5_leg(args, eng, shared, rank, world, dist, gen_thread=None):
            "requests_per_probe": "6.3 random 64-B slab reads (PMC FETCH_SIZE, profiles/r03_lookup)"}
     if dist:
         t0 = time.perf_counter()
-        allhits = shard.distributed_lookup(lambda x: eng.lookup(blocks, x)[0], probes, device="cuda")
+        allhits = shard.distributed_lookup(lambda x: eng.lookup(blocks, x)[0], probes, device=RED_DEVICE)
         torch.cuda.synchronize()
-        res["rccl_gather"] = {"s": time.perf_counter() - t0,
-                              "hits": int(len(allhits)) if allhits is not None else None,
-                              "note": "lookup of every rank's slice + dist.gather of the hit tables "
-                                      "to rank 0 over RCCL (nccl backend, cuda tensors)"}
+        res["rccl_gather" if not SHARED_GPU else "gloo_gather"] = {
+            "s": time.perf_counter() - t0, "hits": int(len(allhits)) if allhits is not None else None,
+            "note": "lookup of every rank's slice + dist.gather of the hit tables to rank 0 over RCCL "
+                    "(nccl backend, cuda tensors)" if not SHARED_GPU else
+                    "ranks share one GPU (--ranks-share-gpu): the hit tables gathered over gloo; the RCCL "
+                    "gather is skipped (RCCL needs one GPU per rank)"}
     for b in blocks:
         b.close()
     check = probes[:20_000] if rank == 0 else None
@@ -884,6 +963,9 @@ def merge_leg(args, eng, base, pipe, rank, world, dist):
             res["merged_traces"] = len(merged)
             res["inspected_traces"] = merged.metrics.inspected_traces
             res["block_errors"] = sum(1 for x in merged.block_status if x)
+        if SHARED_GPU:
+            res["rccl"] = "skipped: shared device (--ranks-share-gpu: RCCL needs one GPU per rank)"
+            return res
         # the same gather as cuda byte tensors over the default (nccl = RCCL over xGMI) group
         m2 = shard.distributed_search_packed(local, everything, nb, device="cuda", columns=True)
         dist.barrier()
@@ -908,6 +990,11 @@ def main():
     if re is None:  # --gpus N, no torchrun around us: start the ranks (nothing has touched a GPU)
         sys.exit(launch_ranks(args, sys.argv[1:]))
     rank, world, local = re
+    global RED_DEVICE, SHARED_GPU
+    if args.ranks_share_gpu and world > 1:
+        # a rehearsal of the N-rank path on a 1-GPU lease: every rank on device 0, collectives
+        # over gloo (the RCCL legs report "skipped: shared device")
+        SHARED_GPU, RED_DEVICE, local = True, "cpu", 0
     if args.cfg3 is None:
         args.cfg3 = 1  # (config 3 is an 8-GPU config: every rank runs its share)
     if args.cfg4 is None:
@@ -917,7 +1004,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if SHARED_GPU else "nccl")
     torch.cuda.set_device(local)
 
     import tempo_amd as T
@@ -1026,10 +1113,10 @@ def main():
     scan_ns = eng.kernel_times() if args.events else []
     if dist:
         dist.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=RED_DEVICE)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        te = torch.tensor([entries], dtype=torch.float64, device="cuda")
+        te = torch.tensor([entries], dtype=torch.float64, device=RED_DEVICE)
         dist.all_reduce(te, op=dist.ReduceOp.SUM)
         total_entries = int(te.item())
     else:
@@ -1047,7 +1134,7 @@ def main():
         "metric": METRIC,
         "value": value,
         "unit": "entries/s",
-        "n_gpus": world,
+        "n_gpus": 1 if SHARED_GPU else world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -1061,7 +1148,8 @@ def main():
                         "full scan (limit 0), ordered match list",
             "blocks_per_gpu": args.blocks, "entries_per_block": args.entries, "entries_per_gpu": entries,
             "resident_sets": len(sets), "query": QUERY, "limit": 0, "matches_per_gpu": len(got),
-            "parallelism": f"block-sharded x{world}",
+            "parallelism": f"block-sharded x{world}" + (" ranks on ONE GPU (--ranks-share-gpu rehearsal)"
+                                                         if SHARED_GPU else ""),
         },
         "achieved_hbm_gbps": achieved,
         "roofline": {
@@ -1139,6 +1227,10 @@ def main():
     if world > 1 and args.merge_steps:
         out["merge"] = merge_leg(args, eng, base, pipe, rank, world, dist)
 
+    cfg1_cpu = None
+    if args.cfg1 and rank == 0:
+        out["cfg1"], cfg1_cpu = cfg1_leg(args, eng, base[0], paths[0], args.cfg1_steps)
+
     for s in sets:
         for b in s:
             b.close()
@@ -1162,7 +1254,12 @@ def main():
             dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=g)
             out["parity_all_ranks"] = bool(ok.item())
     if rank == 0 and world == 1 and args.cpu_baseline:
-        out["cpu_baseline"] = cpu_baselines(paths, got, cpu_threads)
+        out["cpu_baseline"] = cpu_baselines(paths, got, cpu_threads, oracle_threads=cpu_threads)
+    if cfg1_cpu is not None:
+        try:
+            out["cfg1"]["parity"] = cfg1_cpu()
+        except Exception as e:  # noqa: BLE001  (reported; the timed figures stand)
+            out["cfg1"]["parity"] = {"ok": False, "error": repr(e)}
 
     if rank == 0:
         print(json.dumps(out), flush=True)

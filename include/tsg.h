@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define TSG_ABI_VERSION 5
+#define TSG_ABI_VERSION 6
 
 /* Status codes. */
 #define TSG_OK 0
@@ -208,6 +208,16 @@ int tsg_pipeline_matches_header(const tsg_query *q, const uint8_t *header, size_
  * checksums and framing, decodes every page once into the device-resident
  * columnar layout on device (device_hint % devices). */
 int tsg_block_open(tsg_ctx *ctx, const char *block_dir, int device_hint, tsg_block **out);
+/* ABI 6: one page range of a block — index records [first_page, first_page + npages), npages
+ * past the end = to the end — as its own resident block. The frontend splits a large block
+ * into jobs of whole pages sized by bytes (StartPage / PagesToSearch of a SearchBlockRequest,
+ * modules/frontend/searchsharding.go:325-367); tempo_amd.shard.plan_shards does the same to
+ * balance blocks over ranks. A range's search applies the block's header filter; a range that
+ * does not start at page 0 counts neither the header's bytes nor the block as inspected or
+ * skipped, so the ranges of a block sum to the block's metrics. Scan positions (entry_idx)
+ * are inside the range. */
+int tsg_block_open_pages(tsg_ctx *ctx, const char *block_dir, uint32_t first_page, uint32_t npages,
+                         int device_hint, tsg_block **out);
 /* Same from caller buffers (copied). meta_json may be NULL -> TSG_E_NOT_FOUND. */
 int tsg_block_open_mem(tsg_ctx *ctx, const uint8_t *meta_json, size_t meta_len,
                        const uint8_t *header, size_t header_len, const uint8_t *index,

@@ -59,6 +59,8 @@ def lib():
         L = C.CDLL(LIB_PATH)
         vp = C.c_void_p
         L.orc_block_load.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.orc_block_set_pages.argtypes = [vp, C.c_uint32, C.c_uint32]
+        L.orc_block_set_pages.restype = None
         L.orc_wal_block_load.argtypes = [C.c_char_p, C.POINTER(vp)]
         L.orc_entry_to_bytes.argtypes = [C.c_char_p, C.c_size_t, C.c_uint64, C.c_uint64, C.c_uint32,
                                          C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.POINTER(C.c_char_p),
@@ -137,12 +139,16 @@ def make_request(tags=None, min_ms=0, max_ms=0, start=0, end=0, limit=0):
 
 
 class Block:
-    def __init__(self, path, wal=False):
+    def __init__(self, path, wal=False, pages=None):
+        """pages = (first_page, npages): only those index records are searched (npages 0 = to
+        the end); a range after page 0 counts neither the header nor the block itself."""
         self.h = C.c_void_p()
         load = lib().orc_wal_block_load if wal else lib().orc_block_load
         rc = load(path.encode(), C.byref(self.h))
         if rc != 0:
             raise OSError(f"orc_{'wal_' if wal else ''}block_load({path}) -> {rc}")
+        if pages is not None:
+            lib().orc_block_set_pages(self.h, int(pages[0]), int(pages[1]))
 
     def nbytes(self):
         return lib().orc_block_bytes(self.h)

@@ -855,7 +855,17 @@ struct orc_block {
   size_t index_len;
   uint8_t *data;
   size_t data_len;
+  /* a page range of the block (tempo_amd.shard's split of a large block over ranks):
+   * index records [first_page, first_page + npages), npages 0 = to the end. A range that does
+   * not start at page 0 counts neither the header's bytes nor the block as inspected/skipped
+   * (the range at page 0 does), so the ranges' metrics sum to the whole block's. */
+  uint32_t first_page, npages;
 };
+
+void orc_block_set_pages(orc_block *b, uint32_t first_page, uint32_t npages) {
+  b->first_page = first_page;
+  b->npages = npages;
+}
 
 int orc_block_load(const char *dir, orc_block **out) {
   orc_block *b = (orc_block *)calloc(1, sizeof(*b));
@@ -1003,19 +1013,21 @@ static int block_search(const orc_block *b, uint32_t bidx, const orc_pipeline *p
   if (b->wal) return wal_search(b, bidx, p, out, consume, cctx, quit);
   if (!b->has_meta) return ORC_OK; /* ErrDoesNotExist -> nil (:191-203) */
   if (strcmp(b->version, "v2") != 0) return ORC_UNSUPPORTED_ENCODING; /* encoding.FromVersion */
-  out->met.bytes_inspected += b->header_len; /* :217 */
+  const int tail = b->first_page > 0; /* a page range after the block's first page */
+  if (!tail) out->met.bytes_inspected += b->header_len; /* :217 */
   fbt h = fb_root(b->header, b->header_len);
   if (!pipeline_matches_block(p, &h)) {
-    out->met.blocks_skipped++;
+    if (!tail) out->met.blocks_skipped++;
     return ORC_OK;
   }
-  out->met.blocks_inspected++;
+  if (!tail) out->met.blocks_inspected++;
   if (b->enc < 0) return ORC_UNSUPPORTED_ENCODING; /* NewDataReader -> getReaderPool */
   orc_index ix;
   index_init(&ix, b->index, b->index_len, b->index_page_size, b->index_records);
   int rc = ORC_OK;
-  uint64_t scan_pos = 0;
-  for (int64_t i = 0;; i++) { /* for !sr.Quit() (:247) */
+  uint64_t scan_pos = 0; /* (a page range: positions inside the range) */
+  const int64_t i_end = b->npages ? (int64_t)b->first_page + b->npages : INT64_MAX;
+  for (int64_t i = b->first_page; i < i_end; i++) { /* for !sr.Quit() (:247) */
     if (*quit) break;
     const uint8_t *rec;
     int r = index_at(&ix, i, &rec);

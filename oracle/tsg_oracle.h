@@ -73,6 +73,8 @@ typedef struct orc_block orc_block; /* search block files held in memory */
 #define ORC_IO 9
 
 int orc_block_load(const char *dir, orc_block **out);
+/* search only index records [first_page, first_page + npages) (npages 0 = to the end) */
+void orc_block_set_pages(orc_block *b, uint32_t first_page, uint32_t npages);
 /* A search WAL file "<blockID>:<tenant>:v2:<encoding>[:...]" (StreamingSearchBlock):
  * orc_search replays it (header, sort, dedupe/combine) and searches it. */
 int orc_wal_block_load(const char *path, orc_block **out);

@@ -11,6 +11,7 @@
 #include <atomic>
 #include <chrono>
 #include <exception>
+#include <memory>
 #include <mutex>
 #include <thread>
 
@@ -1191,7 +1192,7 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
 
 void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
                          const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
-                         HostBlock &hb) {
+                         HostBlock &hb, uint32_t first_page, uint32_t npages) {
   struct Share {  // (this decode counts in g_decoding; its phases take their share when auto-sized)
     bool prev;
     explicit Share(bool on) : prev(t_share) {
@@ -1224,6 +1225,13 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
     prof_add("load.hdr", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - th0).count());
   std::vector<IndexRecord> recs =
       read_index(index, index_len, hb.meta.index_page_size, hb.meta.index_records, &hb.index_truncated);
+  if (first_page > 0 || npages < recs.size()) {  // a page range (records past a damaged one are gone already)
+    const size_t a = std::min<size_t>(first_page, recs.size());
+    const size_t b = a + std::min<size_t>(npages, recs.size() - a);
+    recs = std::vector<IndexRecord>(recs.begin() + ptrdiff_t(a), recs.begin() + ptrdiff_t(b));
+    hb.part_first_page = first_page;
+    hb.part_tail = first_page > 0;
+  }
   if (nthreads <= 0) nthreads = host_threads();
   nthreads = std::min<int>(nthreads, 64);
 
@@ -1254,67 +1262,71 @@ void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present
 }
 
 // ---- header values == dictionary (hdr_defer) -------------------------------------------
-namespace {
-inline uint64_t fmix64(uint64_t x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdULL;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ULL;
-  x ^= x >> 33;
-  return x;
-}
-inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-// A multiset of values as two sums of avalanched forms of each value's xxhash64 (the hash
-// the loader interned the value with: the dictionary side costs no second pass over its bytes)
-struct H128 {
-  uint64_t a = 0, b = 0;
-  void add_hash(uint64_t h) {
-    a += fmix64(h);  // multiset: a sum, so the order of the values does not matter
-    b += fmix64(rotl64(h, 29) ^ 0x9E3779B97F4A7C15ULL);
-  }
-};
-// sum of H128 over items [0, n) (hash(i) -> the value's xxhash64), on up to nthreads threads
-template <class Hash>
-H128 multiset_hash(size_t n, int nthreads, Hash &&hash) {
-  const size_t nt = std::max<size_t>(1, std::min<size_t>(size_t(std::max(1, phase_threads(nthreads))), n / 16384));
-  std::vector<H128> part(nt);
-  auto run = [&](size_t t) {
-    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
-    for (size_t i = lo; i < hi; i++) part[t].add_hash(hash(i));
-  };
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < nt; t++) th.emplace_back(run, t);
-  run(0);
-  for (auto &x : th) x.join();
-  H128 s;
-  for (auto &p : part) {
-    s.a += p.a;
-    s.b += p.b;
-  }
-  return s;
-}
-}  // namespace
-
+// A large key's header values are deferred to the device pass only when they are exactly the
+// block's dictionary values: equal counts, and every header value found byte for byte in the
+// dictionary, no dictionary value found twice (the dictionary's values are distinct, so this
+// is a bijection). The dictionary side is keyed by the xxhash64 each value was interned with
+// (KeyColumn::dict_vh: no second pass over its bytes); a header value's hash only picks the
+// candidates, the bytes decide (the earlier count + multiset-hash test rested on
+// the hash alone). TSG_VERIFY_HASH_BITS (tests only) keeps that many low bits of the hash, so
+// that unequal values collide and the byte comparison is what separates them.
 void verify_header_dicts(HostBlock &hb, int nthreads) {
   hb.hdr_defer.assign(hb.hdr_keys.size(), 0);
   if (!hb.hdr_index) return;
   if (nthreads <= 0) nthreads = host_threads();
-  nthreads = std::min(nthreads, 32);
+  nthreads = std::max(1, std::min(phase_threads(nthreads), 32));
+  uint64_t mask = ~0ull;
+  if (const char *e = std::getenv("TSG_VERIFY_HASH_BITS")) {
+    const int bits = std::atoi(e);
+    if (bits >= 0 && bits < 64) mask = (1ull << bits) - 1;
+  }
+  auto mix = [](uint64_t h) {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdULL;
+    h ^= h >> 33;
+    return h;
+  };
   for (size_t hk = 0; hk < hb.hdr_keys.size(); hk++) {
     auto it = hb.key_index.find(std::string(hb.hdr_keys[hk]));
     if (it == hb.key_index.end()) continue;
-    const KeyColumn &kc = hb.keys[size_t(it->second)];
+    const int key = it->second;
+    const KeyColumn &kc = hb.keys[size_t(key)];
     if (kc.dict_bytes.size() <= kDeferMinBytes) continue;
     const uint32_t v0 = hb.hdr_val0[hk], v1 = hb.hdr_val0[hk + 1];
-    if (v1 - v0 != kc.nvals() || kc.dict_vh.size() != kc.nvals()) continue;
-    // (the dictionary's values are distinct (interned): equal counts and equal multiset hashes
-    // mean the header lists exactly those values, each once)
-    const H128 h = multiset_hash(v1 - v0, nthreads, [&](size_t i) {
-      const std::string_view v = hb.hdr_vals[v0 + i];
-      return xxhash64(reinterpret_cast<const uint8_t *>(v.data()), v.size());
-    });
-    const H128 d = multiset_hash(kc.nvals(), nthreads, [&](size_t i) { return kc.dict_vh[i]; });
-    hb.hdr_defer[hk] = h.a == d.a && h.b == d.b;
+    const uint32_t n = kc.nvals();
+    if (v1 - v0 != n || kc.dict_vh.size() != n) continue;
+    // open addressing over the dictionary's value ids by (masked) hash
+    size_t cap = 16;
+    while (cap < 2 * size_t(n)) cap <<= 1;
+    std::vector<uint32_t> slot(cap, kNone);
+    for (uint32_t d = 0; d < n; d++) {
+      size_t i = mix(kc.dict_vh[d] & mask) & (cap - 1);
+      while (slot[i] != kNone) i = (i + 1) & (cap - 1);
+      slot[i] = d;
+    }
+    std::unique_ptr<std::atomic<uint8_t>[]> used(new std::atomic<uint8_t>[n]());
+    std::atomic<bool> ok{true};
+    const size_t nt = std::max<size_t>(1, std::min<size_t>(size_t(nthreads), n / 4096));
+    auto run = [&](size_t t) {
+      const size_t lo = size_t(n) * t / nt, hi = size_t(n) * (t + 1) / nt;
+      for (size_t j = lo; j < hi && ok.load(std::memory_order_relaxed); j++) {
+        const std::string_view v = hb.hdr_vals[v0 + j];
+        const uint64_t h = xxhash64(reinterpret_cast<const uint8_t *>(v.data()), v.size()) & mask;
+        bool found = false;
+        for (size_t i = mix(h) & (cap - 1); slot[i] != kNone; i = (i + 1) & (cap - 1)) {
+          const uint32_t d = slot[i];
+          if ((kc.dict_vh[d] & mask) != h || hb.dict_value(key, d) != v) continue;
+          found = !used[d].exchange(1, std::memory_order_relaxed);  // (a second copy: not the dictionary)
+          break;
+        }
+        if (!found) ok.store(false, std::memory_order_relaxed);
+      }
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; t++) th.emplace_back(run, t);
+    run(0);
+    for (auto &x : th) x.join();
+    hb.hdr_defer[hk] = ok.load() ? 1 : 0;
   }
   for (auto &kc : hb.keys) std::vector<uint64_t>().swap(kc.dict_vh);
 }

@@ -142,6 +142,13 @@ struct HostBlock {
   // resident and stop_status / stop_msg is the error the reference's Search returns
   // after their matches (backend_search_block.go:258-266); 0 = none.
   bool index_truncated = false;
+  // a page range of the block (tsg_block_open_pages: one rank's share of a large block): index
+  // records [part_first_page, +n). part_tail: the range does not start at page 0, so its
+  // searches count neither the header's bytes nor the block as inspected / skipped (the range
+  // at page 0 does: the ranges' metrics sum to the whole block's); scan positions are inside
+  // the range
+  uint32_t part_first_page = 0;
+  bool part_tail = false;
   int stop_status = 0;
   std::string stop_msg;
   // WAL blocks: the mutable header's (key -> values) map (Tags / TagValues / block filter).
@@ -166,7 +173,7 @@ struct HostBlock {
   std::vector<uint32_t> hdr_val0;
   bool hdr_index = false;
   // per header key (hdr_keys order): 1 = the key's value list is the block's dictionary for
-  // that key (same count, same 128-bit multiset hash; checked at open, verify_header_dicts)
+  // that key (same values, compared byte for byte at open: verify_header_dicts)
   // and the dictionary is large (> kDeferMinBytes). MatchesBlock's "any header value of the
   // key contains the needle" is then the device dictionary pass's "any dictionary value
   // matched", and the host does not scan the values (24 ms per query on config 4)
@@ -193,14 +200,16 @@ struct HostBlock {
 
 // Dictionaries above this size take MatchesBlock's tag test from the device (hdr_defer).
 constexpr uint64_t kDeferMinBytes = 1u << 20;
-// Fills hdr_defer (block.cpp): count + order-independent 128-bit hash of the header's values
-// of each large key against the key's dictionary values, hashed on up to nthreads threads.
+// Fills hdr_defer (block.cpp): a large key's header values are exactly its dictionary values
+// (equal counts; each header value found byte for byte, no dictionary value twice), checked on
+// up to nthreads threads.
 void verify_header_dicts(HostBlock &hb, int nthreads);
 
 // Reads + decodes a block (meta missing -> has_meta=false, TSG_OK). nthreads <= 0: all cores.
+// first_page / npages: only those index records (npages UINT32_MAX = to the end).
 void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
                          const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
-                         HostBlock &out);
+                         HostBlock &out, uint32_t first_page = 0, uint32_t npages = 0xFFFFFFFFu);
 
 // newStreamingSearchBlockFromWALReplay + the deduping iterator of its Search
 // (tempodb/search/rescan_blocks.go:74-107, tempodb/wal/replay.go:15-71,

@@ -726,6 +726,22 @@ int tsg_block_open(tsg_ctx *ctx, const char *dir, int device_hint, tsg_block **o
     }, device_hint, out);
   });
 }
+int tsg_block_open_pages(tsg_ctx *ctx, const char *dir, uint32_t first_page, uint32_t npages, int device_hint,
+                         tsg_block **out) {
+  if (!ctx || !dir || !out || !npages) return TSG_E_INVALID;
+  return guard([&] {
+    std::vector<uint8_t> meta, header, index;
+    MappedFile data;
+    if (!read_file(join(dir, "search.meta.json"), meta)) fail(TSG_E_NOT_FOUND, "search.meta.json not found");
+    if (!read_file(join(dir, "search-header"), header)) fail(TSG_E_IO, "search-header missing");
+    if (!read_file(join(dir, "search-index"), index)) fail(TSG_E_IO, "search-index missing");
+    if (!data.open(join(dir, "search"))) fail(TSG_E_IO, "search missing");
+    open_common(ctx, [&](HostBlock &h) {
+      decode_search_block(meta.data(), meta.size(), true, std::move(header), index.data(), index.size(), data.p,
+                          data.n, 0, h, first_page, npages);
+    }, device_hint, out);
+  });
+}
 int tsg_block_open_mem(tsg_ctx *ctx, const uint8_t *meta, size_t ml, const uint8_t *header, size_t hl,
                        const uint8_t *index, size_t il, const uint8_t *data, size_t dl, int device_hint,
                        tsg_block **out) {
@@ -1017,8 +1033,12 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
         }
         c.spinning.fetch_sub(1, std::memory_order_acq_rel);
       }
-      if (prof_on()) prof_add("coal.park", 1.0);
-      c.park.wait(e, 2'000'000);
+      const auto tp = std::chrono::steady_clock::now();
+      const bool woke = c.park.wait(e, 5'000'000);
+      if (prof_on()) {
+        prof_add("coal.park_us", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
+        if (!woke) prof_add("coal.park_timeout", 1.0);
+      }
       continue;
     }
     if (r.done.load(std::memory_order_acquire)) {  // served while we took the lead
@@ -1717,14 +1737,14 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         const HostBlock &h = *blocks[i]->b.host;
         size_t k = 0;
         if (state[i] != 0) {
-          m.bytes_inspected += h.header.size();
+          if (!h.part_tail) m.bytes_inspected += h.header.size();
           if (state[i] == 2 && defer[i])  // (as below)
             state[i] = anym[i] >= 0 ? ((defer[i] & ~uint32_t(anym[i])) ? 1 : 2)
                                     : (pipeline_matches_block_indexed(*q, h) ? 2 : 1);
           if (state[i] == 1) {
-            m.blocks_skipped++;
+            if (!h.part_tail) m.blocks_skipped++;
           } else {
-            m.blocks_inspected++;
+            if (!h.part_tail) m.blocks_inspected++;
             k = per_block[i].second;
             m.traces_inspected += uint32_t(h.n);
             m.bytes_inspected += h.fb_bytes;
@@ -1770,7 +1790,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         m.bytes_inspected += h.trace_bytes0[nt];
         continue;
       }
-      m.bytes_inspected += h.header.size();
+      if (!h.part_tail) m.bytes_inspected += h.header.size();  // (a page range after page 0: not again)
       if (state[i] == 2 && defer[i]) {
         // MatchesBlock's deferred terms: a key whose values all miss the needle skips the
         // block (its scan found nothing: the term's bitmap is empty). Not reported (the block
@@ -1779,10 +1799,10 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         else state[i] = pipeline_matches_block_indexed(*q, h) ? 2 : 1;
       }
       if (state[i] == 1) {
-        m.blocks_skipped++;
+        if (!h.part_tail) m.blocks_skipped++;
         continue;
       }
-      m.blocks_inspected++;
+      if (!h.part_tail) m.blocks_inspected++;
       uint64_t stop_entry = UINT64_MAX;
       if (per_block[i].second)
         res->vid_block(h.svc_key >= 0 ? h.keys[size_t(h.svc_key)].nvals() : 0,

@@ -15,6 +15,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <atomic>
 #include <chrono>
 #include <climits>
@@ -22,7 +23,8 @@
 
 namespace tsg {
 
-inline void futex_wait_u32(std::atomic<uint32_t> *a, uint32_t expected, int64_t timeout_ns = -1) {
+// returns false when the wait ended by its timeout
+inline bool futex_wait_u32(std::atomic<uint32_t> *a, uint32_t expected, int64_t timeout_ns = -1) {
   static_assert(sizeof(std::atomic<uint32_t>) == 4, "futex word");
   struct timespec ts, *tp = nullptr;
   if (timeout_ns >= 0) {
@@ -30,7 +32,8 @@ inline void futex_wait_u32(std::atomic<uint32_t> *a, uint32_t expected, int64_t 
     ts.tv_nsec = long(timeout_ns % 1000000000);
     tp = &ts;
   }
-  syscall(SYS_futex, reinterpret_cast<uint32_t *>(a), FUTEX_WAIT_PRIVATE, expected, tp, nullptr, 0);
+  return !(syscall(SYS_futex, reinterpret_cast<uint32_t *>(a), FUTEX_WAIT_PRIVATE, expected, tp, nullptr, 0) == -1 &&
+           errno == ETIMEDOUT);
 }
 inline void futex_wake_u32(std::atomic<uint32_t> *a, int n = INT_MAX) {
   syscall(SYS_futex, reinterpret_cast<uint32_t *>(a), FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
@@ -85,11 +88,13 @@ struct EpochPark {
   std::atomic<int> sleepers{0};
   uint32_t read() const { return epoch.load(std::memory_order_acquire); }
   // parks until the epoch moves past `seen` (or timeout_ns passes: a safety net, never the
-  // hand-off itself)
-  void wait(uint32_t seen, int64_t timeout_ns) {
+  // hand-off itself); false when it ended by the timeout
+  bool wait(uint32_t seen, int64_t timeout_ns) {
     sleepers.fetch_add(1, std::memory_order_seq_cst);
-    if (epoch.load(std::memory_order_seq_cst) == seen) futex_wait_u32(&epoch, seen, timeout_ns);
+    bool woke = true;
+    if (epoch.load(std::memory_order_seq_cst) == seen) woke = futex_wait_u32(&epoch, seen, timeout_ns);
     sleepers.fetch_sub(1, std::memory_order_relaxed);
+    return woke;
   }
   void notify() {
     epoch.fetch_add(1, std::memory_order_seq_cst);

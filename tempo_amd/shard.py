@@ -58,6 +58,96 @@ def shard_range(n_blocks: int, world: int, rank: int) -> range:
     return range(n_blocks * rank // world, n_blocks * (rank + 1) // world)
 
 
+@dataclass(frozen=True)
+class Part:
+    """One rank's piece of a query's block list: block `block` (its index in the list) whole
+    (npages == 0), or its index records [first_page, first_page + npages)."""
+    block: int
+    first_page: int = 0
+    npages: int = 0
+
+    @property
+    def whole(self) -> bool:
+        return self.npages == 0
+
+    def pages(self):
+        """(first_page, npages) for Engine.open_block(pages=...) / oracle.Block(pages=...), or None."""
+        return None if self.whole else (self.first_page, self.npages)
+
+
+def block_sizes(paths: Sequence[str]) -> Tuple[List[int], List[int]]:
+    """(bytes, pages) of each search block directory: the size of its `search` file and the
+    index records its search.meta.json declares (0, 0 when the block has no search data: a
+    no-op for Search). The frontend sizes jobs the same way: bytes per page = size / records
+    (modules/frontend/searchsharding.go:331-339)."""
+    import json
+    import os
+    sizes, pages = [], []
+    for p in paths:
+        try:
+            with open(os.path.join(p, "search.meta.json")) as f:
+                n = int(json.load(f).get("indexRecords", 0))
+            sz = os.path.getsize(os.path.join(p, "search"))
+        except (OSError, ValueError):
+            n, sz = 0, 0
+        sizes.append(sz if n else 0)
+        pages.append(n)
+    return sizes, pages
+
+
+def plan_shards(sizes: Sequence[int], pages: Sequence[int], world: int, split: bool = True) -> List[List[Part]]:
+    """Size-balanced shards of a query's blocks over `world` ranks: rank r
+    takes a contiguous stretch of the blocks in query order — rank order stays block order,
+    which the frontend merge's tie order and the limit protocol (distributed_search_limit)
+    rely on — ending where the cumulative bytes reach (r + 1) / world of the total. A cut that
+    falls inside a block splits it at the page boundary nearest the cut (split=True: pages of
+    size / records bytes, the frontend's estimate, searchsharding.go:331-339, so one giant
+    block is spread over several ranks); with split=False the cut moves to the nearer block
+    boundary (whole blocks only). Every page of every block lands in exactly one part."""
+    if world <= 0:
+        raise ValueError(f"bad world {world}")
+    nb = len(sizes)
+    if len(pages) != nb:
+        raise ValueError("sizes and pages differ in length")
+    cum = [0]
+    for sz in sizes:
+        cum.append(cum[-1] + max(0, int(sz)))
+    total = cum[-1]
+    # cut r (1 <= r < world) as a position (block, page): everything before it goes to ranks < r
+    cuts = [(0, 0)]
+    for r in range(1, world):
+        c = total * r / world
+        b = 0
+        while b < nb and cum[b + 1] <= c:
+            b += 1
+        if b >= nb:
+            pos = (nb, 0)
+        else:
+            if split and pages[b] > 1 and sizes[b] > 0:
+                k = int(round((c - cum[b]) / (sizes[b] / pages[b])))
+                k = min(max(k, 0), pages[b])
+            else:
+                k = 0 if c - cum[b] <= cum[b + 1] - c else pages[b]
+            pos = (b, k) if k < pages[b] else (b + 1, 0)
+        cuts.append(max(pos, cuts[-1]))
+    cuts.append((nb, 0))
+    out = []
+    for r in range(world):
+        (b0, p0), (b1, p1) = cuts[r], cuts[r + 1]
+        parts = []
+        for b in range(b0, min(b1 + 1, nb)):
+            lo = p0 if b == b0 else 0
+            hi = p1 if b == b1 else pages[b]
+            if b == b1 and p1 == 0:
+                break
+            if lo == 0 and hi >= pages[b]:
+                parts.append(Part(b))
+            elif hi > lo:
+                parts.append(Part(b, lo, hi - lo))
+        out.append(parts)
+    return out
+
+
 def _pad8(x):
     return (x + 7) & ~7
 

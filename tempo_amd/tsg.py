@@ -143,7 +143,7 @@ class _LookupResult(C.Structure):
 EXPORTED = [
     "tsg_init", "tsg_shutdown", "tsg_device_count", "tsg_device_numa_node", "tsg_last_error", "tsg_abi_version", "tsg_cancel",
     "tsg_pipeline_new", "tsg_pipeline_query", "tsg_pipeline_free", "tsg_pipeline_matches_header",
-    "tsg_block_open", "tsg_block_open_mem", "tsg_block_clone", "tsg_wal_block_open", "tsg_wal_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
+    "tsg_block_open", "tsg_block_open_pages", "tsg_block_open_mem", "tsg_block_clone", "tsg_wal_block_open", "tsg_wal_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
     "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_kernel_times", "tsg_results_combine",
     "tsg_v2block_open", "tsg_v2block_close", "tsg_lookup_ids", "tsg_lookup_result_free", "tsg_find_ids",
     "tsg_find_result_free", "tsg_proto_block_open", "tsg_proto_block_close", "tsg_proto_block_info",
@@ -176,6 +176,7 @@ def lib():
         L.tsg_pipeline_free.argtypes = [vp]
         L.tsg_pipeline_matches_header.argtypes = [C.POINTER(_Query), C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
         L.tsg_block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
+        L.tsg_block_open_pages.argtypes = [vp, C.c_char_p, C.c_uint32, C.c_uint32, C.c_int, C.POINTER(vp)]
         L.tsg_block_close.argtypes = [vp]
         L.tsg_block_clone.argtypes = [vp, vp, C.c_int, C.POINTER(vp)]
         L.tsg_wal_block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
@@ -408,8 +409,10 @@ class Engine:
         """Replay a search WAL file (<blockID>:<tenant>:v2:<encoding>[:...]) onto a device."""
         return StreamingSearchBlock(self, path, device)
 
-    def open_block(self, path: str, device: int = 0) -> "BackendSearchBlock":
-        return BackendSearchBlock(self, path, device)
+    def open_block(self, path: str, device: int = 0, pages=None) -> "BackendSearchBlock":
+        """A backend search block resident on `device`; pages = (first_page, npages): only that
+        page range (tsg_block_open_pages, one shard of a large block)."""
+        return BackendSearchBlock(self, path, device, pages=pages)
 
     def open_live_traces(self, traces: Sequence[Sequence[bytes]], device: int = 0) -> "LiveTraces":
         """A snapshot of the ingester's live traces (each a list of searchData segments, in
@@ -762,11 +765,16 @@ def _packed(fn, *args):
 class BackendSearchBlock:
     """A backend search block resident on one device (tsg_block)."""
 
-    def __init__(self, eng: Engine, path: str, device: int = 0, _wal: bool = False, _clone_of=None):
+    def __init__(self, eng: Engine, path: str, device: int = 0, _wal: bool = False, _clone_of=None, pages=None):
         self.path = path
+        self.pages = pages
         self.h = C.c_void_p()
         if _clone_of is not None:
             _check(lib().tsg_block_clone(eng.h, _clone_of.h, device, C.byref(self.h)))
+        elif pages is not None:
+            first, n = int(pages[0]), int(pages[1])
+            _check(lib().tsg_block_open_pages(eng.h, path.encode(), first, min(n, 2**32 - 1), device,
+                                              C.byref(self.h)))
         else:
             opener = lib().tsg_wal_block_open if _wal else lib().tsg_block_open
             _check(opener(eng.h, path.encode(), device, C.byref(self.h)))

@@ -47,7 +47,7 @@ def test_no_device_fails_loudly():
 
 
 def test_abi_version():
-    assert T.lib().tsg_abi_version() == 5
+    assert T.lib().tsg_abi_version() == 6
 
 
 @pytest.mark.parametrize("req,terms", [

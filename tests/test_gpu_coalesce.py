@@ -209,7 +209,7 @@ def test_shim_pattern_driver(engine, blockset):
 
 def test_shim_limit20_oversubscribed(engine, blockset):
     """VERDICT r4 "What's weak" 1: the shim's limit-20 call pattern on a host with fewer CPUs
-    than caller threads. 10 C threads (one per block) on 3 CPUs, 200 queries at the ingester's
+    than caller threads. 10 C threads (one per block) on 4 CPUs, 200 queries at the ingester's
     default limit 20: idle callers park instead of spinning, so no query waits for a
     scheduler tick (the driver's run read 10 ms steps). Every query's records are the
     per-block oracle's (a digest of each block's ordered (entry, id, start) records)."""
@@ -223,12 +223,16 @@ def test_shim_limit20_oversubscribed(engine, blockset):
         exp = [O.search([O.Block(p)], limit=20, nthreads=1, **QA)[0] for p in blockset[:10]]
         want = shim_digest(exp)
         engine.shim_pattern([a, b], pipe, 8, limit=20)  # warm, on every CPU
-        os.sched_setaffinity(0, set(sorted(mask)[:3]))  # (the C threads inherit the mask)
+        # the 4 idlest cores of the process's CPUs (a GPU box's host is shared with other jobs:
+        # a CPU another job keeps busy would time-slice our threads against it)
+        import bench
+        os.sched_setaffinity(0, set(bench.idlest(sorted(mask), 4)))  # (the C threads inherit the mask)
         ns, nm, dg = engine.shim_pattern([a, b], pipe, 200, limit=20, digest=True)
         assert nm == [sum(len(e) for e in exp)] * 200
         assert dg == [want] * 200
-        worst = sorted(ns)[-3:]
-        assert max(ns) < 2_000_000, f"slowest queries {[x / 1e3 for x in worst]} us (10 threads on 3 CPUs)"
+        v = sorted(ns)
+        assert max(ns) < 2_000_000, (f"slowest queries {[x / 1e3 for x in v[-3:]]} us, p50 {v[100] / 1e3} us "
+                                     f"(10 threads on 4 CPUs)")
     finally:
         os.sched_setaffinity(0, mask)
         for x in a + b:

@@ -1,0 +1,81 @@
+#!/bin/bash
+# Round-5 GPU session script. Stages by $1 (comma list); each GPU step under its own timeout,
+# the script stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STAGES="${1:-tests,driver}"
+has() { [[ ",$STAGES," == *",$1,"* ]]; }
+T="python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider"
+B="--cfg3 0 --cfg4 0 --cfg5 0 --shim-steps 0 --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --parity 0"
+summ() {  # one-line summary of a bench JSON line
+  python3 - "$1" "$2" <<'EOF'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+l = d.get("latency_us", {})
+out = [sys.argv[2], "value %.1fG" % (d["value"] / 1e9), "frac %s" % (round(d["roofline"]["frac"], 3) if d["roofline"]["frac"] else None),
+       "step mean %.1f p50 %.1f" % (l["step"]["mean"], l["step"]["p50"]) if l.get("step") else "",
+       "kernel mean %.2f" % l["kernel"]["mean"] if l.get("kernel") else ""]
+if "limit20" in d:
+    out.append("lim20 step mean %.1f" % d["limit20"]["step_us"]["mean"])
+if "shim" in d:
+    s = d["shim"]
+    out.append("shim p50 %.1f p99 %.1f | lim20 p50 %.1f p99 %.1f max %.1f" % (
+        s["query_us"]["p50"], s["query_us"]["p99"], s["limit20"]["query_us"]["p50"], s["limit20"]["query_us"]["p99"],
+        s["limit20"]["query_us"]["max"]))
+print(" ".join(out))
+EOF
+}
+if has over; then  # the oversubscribed shim test, host phases on (non-fatal: the stages after it still run)
+  TSG_PROF=1 timeout -k 10 300 $T -m gpu tests/test_gpu_coalesce.py -k oversubscribed > gpurun_out/over.log 2>&1
+  echo "over rc=$?"; grep -E "slowest|passed|failed" gpurun_out/over.log | tail -3; grep -o "coal.park[a-z_]*=[^ ]*" gpurun_out/over.log | head -8
+fi
+if has tests; then
+  timeout -k 10 600 $T -m gpu ${TESTS:-tests/test_gpu_coalesce.py tests/test_gpu_pool.py --deselect tests/test_gpu_coalesce.py::test_shim_limit20_oversubscribed} > gpurun_out/pt.log 2>&1
+  rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has alltests; then
+  timeout -k 10 900 $T -m gpu tests > gpurun_out/pt_all.log 2>&1
+  rc=$?; echo "alltests rc=$rc"; tail -4 gpurun_out/pt_all.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has driver; then  # the driver's own command
+  timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/driver.json 2> gpurun_out/driver.err
+  rc=$?; echo "driver rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/driver.err; exit $rc; }
+  summ gpurun_out/driver.json driver
+fi
+if has share2; then  # the N=2 legs on one GPU (ranks share device 0, gloo)
+  timeout -k 10 900 python3 bench.py --gpus 2 --ranks-share-gpu --steps 20 --warmup 5 > gpurun_out/share2.json 2> gpurun_out/share2.err
+  rc=$?; echo "share2 rc=$rc"; [ $rc -eq 0 ] || { tail -8 gpurun_out/share2.err; exit $rc; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/share2.json').read().strip().splitlines()[-1]); print({k: (d[k] if not isinstance(d[k], dict) else sorted(d[k].keys())) for k in ('n_gpus','value','merge','cfg3','cfg5','parity_all_ranks') if k in d})"
+fi
+if has shim; then  # the shim leg alone, a few times
+  for k in 1 2 3; do
+    timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --cfg3 0 --cfg4 0 --cfg5 0 --concurrent-steps 0 \
+      --mall-steps 0 --cpu-baseline 0 --parity 0 --limit-steps 0 --shim-steps 400 > gpurun_out/shim_$k.json 2> gpurun_out/shim_$k.err
+    rc=$?; [ $rc -eq 0 ] || { echo "shim rc=$rc"; tail -3 gpurun_out/shim_$k.err; exit $rc; }
+    summ gpurun_out/shim_$k.json shim$k
+  done
+fi
+if has fence; then  # AQL argument-visibility modes, interleaved
+  mkdir -p /tmp/abw
+  for k in 1 2; do
+    for m in hdp sfence readback; do
+      TSG_AQL_FENCE=$m timeout -k 10 300 python -u bench.py --workdir /tmp/abw --steps 400 --warmup 20 $B ${BENCH_ARGS:-} \
+        > gpurun_out/fence_${m}_$k.json 2> gpurun_out/fence_${m}_$k.err
+      rc=$?; [ $rc -eq 0 ] || { echo "fence $m rc=$rc"; tail -3 gpurun_out/fence_${m}_$k.err; exit $rc; }
+      summ gpurun_out/fence_${m}_$k.json "fence-$m"
+    done
+  done
+fi
+if has hostprof; then
+  TSG_PROF=1 timeout -k 10 500 python -u bench.py --steps 200 --warmup 20 $B ${BENCH_ARGS:-} > gpurun_out/hp.json 2> gpurun_out/hp.err
+  rc=$?; echo "hostprof rc=$rc"; grep -v "^\[bench\]" gpurun_out/hp.err | tail -4; [ $rc -eq 0 ] || exit $rc
+fi
+if has rocprof; then  # kernel trace + stats of the main line (profiles/)
+  cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/rp -o rp -- python3 bench.py --steps 200 --warmup 10 $B \
+    > gpurun_out/rp.json 2> gpurun_out/rp.err
+  rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/rp.err; exit $rc; }
+  find gpurun_out/rp -name "*kernel_stats.csv" | head -3
+fi
+echo "done: $STAGES"
