@@ -279,7 +279,9 @@ typedef struct tsg_block_info {
   int32_t index_truncated; /* 1: an index record failed (checksum, framing, zero record): the block
                               ends silently before it, as the reference's Search does */
   int32_t live;            /* 1: live traces (tsg_live_block_open_mem) */
-  int32_t pad0;
+  int32_t hdr_deferred;    /* ABI 6: header keys whose MatchesBlock value test comes from the device
+                              dictionary pass (the header's values are the dictionary, compared
+                              byte for byte at open) */
   uint64_t traces;         /* live: traces (entries = their segments); otherwise = entries */
 } tsg_block_info;
 int tsg_block_info_get(const tsg_block *b, tsg_block_info *out);

@@ -820,7 +820,8 @@ int tsg_block_info_get(const tsg_block *b, tsg_block_info *o) {
   o->stop_status = h.stop_status;
   o->index_truncated = h.index_truncated ? 1 : 0;
   o->live = h.live ? 1 : 0;
-  o->pad0 = 0;
+  o->hdr_deferred = 0;
+  for (uint8_t d : h.hdr_defer) o->hdr_deferred += d ? 1 : 0;
   o->traces = h.live ? h.ntraces() : h.n;
   return TSG_OK;
 }

@@ -101,7 +101,7 @@ class _BlockInfo(C.Structure):
                 ("min_dur_ns", C.c_uint64), ("max_dur_ns", C.c_uint64), ("device", C.c_int32),
                 ("encoding", C.c_int32), ("streaming", C.c_int32), ("partial", C.c_int32),
                 ("stop_status", C.c_int32), ("index_truncated", C.c_int32), ("live", C.c_int32),
-                ("pad0", C.c_int32), ("traces", C.c_uint64)]
+                ("hdr_deferred", C.c_int32), ("traces", C.c_uint64)]
 
 
 class _LookupOpts(C.Structure):

@@ -111,3 +111,31 @@ def test_cfg4_absent_needle_skipped(engine, tmp_path):
     got, met = check(engine, [p], {"db.statement": "where id = 77", "http.url": "/carts/"})
     assert met.inspected_blocks == 1
     check(engine, [p, p], {"db.statement": "from orders", "http.url": "qqzz"}, limit=20)
+
+
+@pytest.mark.parametrize("bits", ["0", "6"])
+def test_forced_hash_collisions(engine, tmp_path, wide_blocks, monkeypatch, bits):
+    """the header-equals-dictionary decision must not rest on a hash. With the
+    test hook TSG_VERIFY_HASH_BITS the open keeps only `bits` bits of each value's hash, so
+    unequal values collide everywhere: a header that differs from the entries by one value
+    must still keep the host filter, and a header equal to the dictionary must still defer —
+    both with the oracle's results and metrics."""
+    monkeypatch.setenv("TSG_VERIFY_HASH_BITS", bits)
+    ents = entries(91, 9000, {100: "/api/v1/in-entries-only/2"})
+    p = write_block(str(tmp_path), "hdr", ents, page_size=256 << 10)
+    hdr_ents = entries(91, 9000, {100: "/api/v1/in-header-only/2"})
+    with open(os.path.join(p, "search-header"), "wb") as f:
+        f.write(T.fb_search_header(hdr_ents))
+    b = engine.open_block(p)
+    assert b.info()["hdr_deferred"] == 0  # one value differs: the host keeps the header test
+    b.close()
+    got, met = check(engine, [p], {"http.url": "in-header-only"})
+    assert not got and met.inspected_blocks == 1
+    got, met = check(engine, [p], {"http.url": "in-entries-only"})
+    assert not got and met.skipped_blocks == 1
+    for w in wide_blocks:  # header == dictionary: deferred to the device pass, collisions or not
+        b = engine.open_block(w)
+        assert b.info()["hdr_deferred"] == 1
+        b.close()
+    got, met = check(engine, wide_blocks, {"http.url": "needle-one"})
+    assert len(got) == 1 and met.skipped_blocks == 2
