@@ -265,6 +265,10 @@ def launch_ranks(args, argv, device_count=None):
     cmd = launch_cmd(argv, args.gpus, free_port())
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if args.ranks_share_gpu:
+        # ranks sharing one GPU: no resident search kernels (each would hold every CU's LDS and
+        # the other rank's queries would wait for it to leave on its idle timeout)
+        env.setdefault("TSG_RESIDENT", "0")
     log("starting %d ranks: %s" % (args.gpus, " ".join(cmd)))
     return subprocess.call(cmd, env=env)
 

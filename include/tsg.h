@@ -191,6 +191,11 @@ int tsg_device_count(tsg_ctx *ctx);
  * polls a completion word and reads its records in pinned host memory: a caller that
  * keeps its search threads on this node's CPUs sees both sooner. */
 int tsg_device_numa_node(tsg_ctx *ctx, int dev);
+/* ABI 6: the device context's resident-search counters, out[0..n): [0] resident launches,
+ * [1] queries they served, [2] relaunches after a launch left on its idle timeout as a query
+ * was posted, [3] quits (another kernel needed the device, a second context opened on it, or
+ * the query shape changed). Zeros when TSG_RESIDENT=0. DESIGN.md §4. */
+int tsg_device_counters(tsg_ctx *ctx, int dev, uint64_t *out, size_t n);
 const char *tsg_last_error(void);
 int tsg_abi_version(void);
 int tsg_cancel(tsg_ctx *ctx, uint64_t query_id);

@@ -270,6 +270,10 @@ int aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uint
   return pslot;
 }
 
+void aql_hdp_flush(Aql *a) {
+  if (a && a->hdp_flush) *a->hdp_flush = 1u;
+}
+
 bool aql_done(Aql *a) { return !a->last.handle || hsa_signal_load_scacquire(a->last) <= 0; }
 
 uint64_t aql_time_ns(Aql *a, int slot) {

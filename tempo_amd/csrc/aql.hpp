@@ -33,6 +33,10 @@ AqlKernel aql_kernel(Aql *a, const char *name, uint32_t max_kernarg);
 // (-1 when no profiling slot is free); otherwise -1.
 int aql_dispatch(Aql *a, const AqlKernel &k, uint32_t grid, uint32_t block, uint32_t dyn_lds, const void *args,
                  const std::vector<std::pair<uint32_t, uint32_t>> &parts, bool profiled = false);
+// Host writes to device memory through the BAR pass the host data path (HDP), which buffers
+// them: a posted write of the HDP flush register pushes them on (no read-back: the reader on
+// the device verifies what it reads). No-op without the register.
+void aql_hdp_flush(Aql *a);
 // true once the last dispatch has completed (its own completion signal: dispatches on the
 // queue complete in order; for a caller's liveness check while it polls the kernel's words)
 bool aql_done(Aql *a);

@@ -658,6 +658,14 @@ int tsg_device_numa_node(tsg_ctx *ctx, int dev) {
   if (!ctx || dev < 0 || size_t(dev) >= ctx->c.devs.size()) return -1;
   return device_numa_node(*ctx->c.devs[size_t(dev)]);
 }
+int tsg_device_counters(tsg_ctx *ctx, int dev, uint64_t *out, size_t n) {
+  if (!ctx || !out || dev < 0 || size_t(dev) >= ctx->c.devs.size()) return TSG_E_INVALID;
+  return guard([&] {
+    uint64_t c[4];
+    device_counters(*ctx->c.devs[size_t(dev)], c);
+    for (size_t i = 0; i < n; i++) out[i] = i < 4 ? c[i] : 0;
+  });
+}
 int tsg_cancel(tsg_ctx *ctx, uint64_t qid) {
   if (!ctx || !qid) return TSG_E_INVALID;
   ctx->cancel(qid);

@@ -14,6 +14,13 @@
 namespace tsg {
 
 int device_ordinal(const DeviceCtx &dc) { return dc.ordinal; }
+void device_counters(DeviceCtx &dc, uint64_t out[4]) {
+  std::lock_guard<std::mutex> lk(dc.mu);
+  out[0] = dc.res_launches;
+  out[1] = dc.res_queries;
+  out[2] = dc.res_relaunches;
+  out[3] = dc.res_quits;
+}
 
 void ctx_init(Ctx &c, const tsg_options *opts) {
   int n = 0;
@@ -45,6 +52,7 @@ void ctx_init(Ctx &c, const tsg_options *opts) {
     HIP_OK(hipMemset(dc->ticket.p, 0, 64));
     dc->err.ensure(64);
     HIP_OK(hipMemset(dc->err.p, 0, 64));
+    context_opened(*dc);
     c.devs.push_back(dc.release());
   }
 }
@@ -53,6 +61,12 @@ void ctx_shutdown(Ctx &c) {
   for (auto &dc : c.devs) {
     (void)hipSetDevice(dc->ordinal);
     (void)hipStreamSynchronize(dc->stream);
+    context_closed(*dc);
+    try {
+      std::lock_guard<std::mutex> lk(dc->mu);
+      resident_release(*dc);  // (its launch leaves before the queue is closed)
+    } catch (...) {
+    }
     aql_close(dc->aql);  // (waits for its queue to drain)
     dc->aql = nullptr;
     for (DevBuf *b : {&dc->desc, &dc->vmatch, &dc->bitmaps, &dc->gran, &dc->ticket, &dc->out, &dc->regions,
@@ -203,6 +217,7 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
   }
 
   std::lock_guard<std::mutex> lk(dc.mu);
+  dc.mem_epoch++;  // (a resident search launch relaunches before it reads new columns)
   HIP_OK(hipSetDevice(dc.ordinal));
   hipStream_t s = dc.stream;
   d.dur32 = dev_upload(d, scan.data(), scan.size(), s);
@@ -295,6 +310,7 @@ void block_clone(Ctx &c, const Block &src, Block &dst, int device_hint) {
   d.device = dc.ordinal;
   d.n = o.n;
   std::lock_guard<std::mutex> lk(dc.mu);
+  dc.mem_epoch++;
   HIP_OK(hipSetDevice(dc.ordinal));
   // the descriptor allocation (last) is rebuilt, every other one copied
   const size_t ncopy = o.allocs.empty() ? 0 : o.allocs.size() - 1;
@@ -344,6 +360,7 @@ void block_clone(Ctx &c, const Block &src, Block &dst, int device_hint) {
 void block_free(Block &b) {
   if (!b.dc) return;
   std::lock_guard<std::mutex> lk(b.dc->mu);
+  b.dc->mem_epoch++;
   (void)hipSetDevice(b.dc->ordinal);
   (void)hipStreamSynchronize(b.dc->stream);
   for (void *p : b.dev.allocs) (void)hipFree(p);

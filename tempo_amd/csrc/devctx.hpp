@@ -7,6 +7,7 @@
 #include <map>
 #include <mutex>
 #include <set>
+#include <string>
 #include <utility>
 
 #include "engine.hpp"
@@ -165,6 +166,19 @@ struct DeviceCtx {
   Aql *aql = nullptr;
   bool aql_tried = false;
   uint32_t pool_parity = 0;
+  // resident search kernel (pool.hip search_resident_kernel; TSG_RESIDENT=0 turns it off): the
+  // mailbox (uncached device memory: doorbell page + slots), the live launch, and the memory
+  // epoch its launch saw (block uploads / frees bump mem_epoch: the next query relaunches, so
+  // the launch's acquire fence sees the new columns and descriptors as any launch does)
+  bool res_on = env_u32("TSG_RESIDENT", 1, 0, 1) != 0;
+  // (TSG_RESIDENT_IDLE_US, read at each launch: the idle timeout in us, default 10000)
+  uint64_t res_launches = 0, res_queries = 0, res_relaunches = 0, res_quits = 0;  // tsg_device_counters
+  uint8_t *res_mem = nullptr;
+  uint32_t res_seq = 0;  // last posted sequence number
+  bool res_alive = false;
+  std::string res_kernel;
+  uint64_t res_epoch = 0, mem_epoch = 0;
+  HostBuf res_host{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};  // [0..63] error word, then query stamps
   std::set<const void *> pool_attr;  // pool kernels whose dynamic LDS limit has been raised
   // TSG_PER_CU=k (1..16): scan workgroups per CU in the grid plan instead of the
   // occupancy (k above it oversubscribes: later workgroups start as earlier ones retire)
@@ -175,7 +189,8 @@ struct DeviceCtx {
   }();
   // TSG_SEARCH_TIME_DEFER: event pairs recorded around search kernels, read by tsg_kernel_times
   std::vector<hipEvent_t> tring;
-  std::vector<int> tring_aql;  // per deferred slot: its AQL profiling slot, or -1 (the event pair)
+  std::vector<int> tring_aql;  // per deferred slot: its AQL profiling slot, -1 (the event pair), -3 (tring_res)
+  std::vector<uint64_t> tring_res;  // per deferred slot served by the resident kernel: its span (ns)
   size_t tring_used = 0;
   bool defer_slot(hipEvent_t &a, hipEvent_t &b) {
     constexpr size_t kMaxDeferred = 4096;
@@ -199,4 +214,13 @@ struct DeviceCtx {
 
 
 int device_numa_node(const DeviceCtx &dc);
+// pool.hip: end the device's resident search launch, if any (before other kernels use the
+// device, at shutdown, or when another context opens on the same device)
+void resident_quit(DeviceCtx &dc);
+void resident_release(DeviceCtx &dc);  // (shutdown: quit, then free the mailbox)
+// contexts open on a device ordinal (a resident launch only when this context is the only one);
+// context_opened ends the resident launches of the other contexts on the device
+int contexts_on(int ordinal);
+void context_opened(DeviceCtx &dc);
+void context_closed(DeviceCtx &dc);
 }  // namespace tsg

@@ -204,6 +204,8 @@ void device_find(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>
                  size_t nids, const tsg_lookup_opts *opts, FindOut &out);
 
 int device_ordinal(const DeviceCtx &dc);
+// resident search counters: launches, queries served, relaunches after an idle-exit race, quits
+void device_counters(DeviceCtx &dc, uint64_t out[4]);
 // Durations of the TSG_SEARCH_TIME_DEFER launches since the last call (waits for the stream).
 void device_kernel_times(DeviceCtx &dc, std::vector<uint64_t> &ns);
 

@@ -470,6 +470,7 @@ void device_find(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>
   }
   const uint32_t np = uint32_t(pages.size());
   std::lock_guard<std::mutex> lkd(dc.mu);
+  resident_quit(dc);  // (the resident search launch holds every CU's LDS)
   HIP_OK(hipSetDevice(dc.ordinal));
   hipStream_t s = dc.stream;
   HIP_OK(hipEventRecord(dc.ev0, s));

@@ -667,6 +667,7 @@ void v2block_free(V2Block &b) {
 void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>> &blocks, const uint8_t (*ids)[16],
                    size_t nids, const tsg_lookup_opts *opts, LookupOut &out) {
   std::lock_guard<std::mutex> lk(dc.mu);
+  resident_quit(dc);  // (the resident search launch holds every CU's LDS)
   HIP_OK(hipSetDevice(dc.ordinal));
   hipStream_t s = dc.stream;
   // per-block prefilter that does not depend on the id (tempodb.go:497-509)

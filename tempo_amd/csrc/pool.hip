@@ -73,6 +73,8 @@ struct PoolArgs {
   // static kernel: the launch's NW waves split the units as wave g -> [g*sq + min(g, sr), ...),
   // the first sr waves one unit more (sq, sr = units / NW, units % NW: no division on the device)
   uint32_t sq, sr;
+  uint32_t nbms, pad0;               // bitmaps in `bms` (the resident kernel's slot checksum)
+  unsigned long long *qstamps;       // resident kernel, timed queries: per workgroup {seen, end} (100 MHz)
 };
 static_assert(sizeof(PoolArgs) <= 4096, "kernel arguments");
 
@@ -608,6 +610,283 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
 }
 
 // ------------------------------------------------------------------------------------
+// resident search (TSG_RESIDENT): the static kernel's scan as a kernel that stays on the
+// device and takes its queries from a mailbox.
+//
+// A narrow search's kernel launch costs more than its own duration suggests: the command
+// processor fetches the AQL packet over PCIe after the doorbell, runs the acquire fence, then
+// launches 4096 waves, whose first loads go out together and whose kernel-argument loads
+// queue behind them (the round-4 staging barrier passed 7 us into a 24 us kernel). A
+// resident launch has its waves in place: the host writes a query's arguments into a
+// mailbox slot of uncached device memory through the BAR, then the slot's header, then the
+// doorbell word; each workgroup's first lane polls the doorbell, the workgroup loads the
+// slot into LDS (one word per thread), checks the header's sequence number and the checksum
+// of the words the query uses (a slot read before the host's writes landed is read again),
+// and scans.
+//
+// Records come out in scan order: wave g of the launch owns a contiguous unit run (the
+// static split), keeps its matches in its own LDS region in scan order (ranks from per-step
+// ballots), and the workgroup writes its waves' regions one after another to its host
+// segment; workgroup w's runs precede workgroup w+1's, so the segments in workgroup order
+// are the reference order and the host only concatenates them (no sort). A wave whose
+// region overflows reports the workgroup as overflowing (the host reruns the query on the
+// other paths).
+//
+// Lifetime: a workgroup leaves when the host posts a quit, or when no query has been posted
+// for idle_ticks of the 100 MHz clock (every wave reaches one of the two); the host relaunches
+// at its next query. A post that races the idle exit is seen by the host as the launch
+// completing with counts missing: it relaunches and posts again (pool.hip resident_*).
+constexpr uint32_t kResSlots = 64, kResSlotBytes = 8192, kResHdrBytes = 64;
+constexpr uint32_t kResSearch = 1, kResQuit = 2;
+struct ResHeader {  // the first 16 B of a mailbox slot; PoolArgs at +kResHdrBytes
+  uint32_t seq, cmd, csum, nwords;
+};
+struct ResidentArgs {
+  const uint32_t *door;  // uncached device memory: [0] = the last posted sequence number
+  const uint8_t *slots;  // uncached device memory: kResSlots x kResSlotBytes (slot = seq % kResSlots)
+  uint32_t *err;         // pinned host: [0] set when a slot never verified (the host fails the query)
+  uint32_t first_seq;    // the first query of this launch
+  uint32_t idle_ticks;   // s_memrealtime ticks without a post before a workgroup leaves
+  uint32_t nthreads, ngroups;
+};
+static_assert(sizeof(PoolArgs) <= kResSlotBytes - kResHdrBytes && sizeof(PoolArgs) % 4 == 0, "mailbox slot");
+
+// The argument words a query with nsegs blocks and nbms bitmaps uses (the host writes only
+// those; the checksum covers exactly them): the block table, descriptors, bitmaps, unit and
+// entry bases, and the scalars from `nsegs` on.
+__host__ __device__ inline bool res_word_used(uint32_t off, uint32_t nsegs, uint32_t nbms) {
+  auto in = [&](uint32_t a, uint32_t n) { return off >= a && off < a + n; };
+  return in(uint32_t(offsetof(PoolArgs, blk)), nsegs * uint32_t(sizeof(PoolBlk))) ||
+         in(uint32_t(offsetof(PoolArgs, desc)), nsegs * 8u) || in(uint32_t(offsetof(PoolArgs, bms)), nbms * 32u) ||
+         in(uint32_t(offsetof(PoolArgs, ubase)), (nsegs + 1) * 4u) || in(uint32_t(offsetof(PoolArgs, ebase)), nsegs * 4u) ||
+         (off >= uint32_t(offsetof(PoolArgs, nsegs)) && off < uint32_t(sizeof(PoolArgs)));
+}
+
+template <int NT, bool DUR, bool RANGE, bool NTL>
+__global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(ResidentArgs R) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_args[sizeof(PoolArgs) / 4];
+  __shared__ uint32_t s_ctl[4];   // [0] command for this round, [1] checksum, [2] header seq, [3] header csum
+  __shared__ uint32_t s_wn[kPoolWaves + 1];
+  extern __shared__ __attribute__((aligned(16))) unsigned long long s_rec[];  // rec_cap x 6 words
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = blockIdx.x, nthreads = R.nthreads, nwv = nthreads >> 6;
+  const uint32_t wave = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(tid) >> 6));
+  const PoolArgs &A = *reinterpret_cast<const PoolArgs *>(s_args);
+  constexpr uint32_t kWords = uint32_t(sizeof(PoolArgs) / 4);
+  for (uint32_t seq = R.first_seq;; seq++) {
+    // ---- wait for query `seq` (one lane polls the doorbell; the others wait at the barrier)
+    if (tid == 0) {
+      uint32_t cmd = kResQuit;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (uint32_t n = 0;; n++) {
+        const uint32_t d = __hip_atomic_load(R.door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (int32_t(d - seq) >= 0) {
+          cmd = kResSearch;
+          break;
+        }
+        if ((n & 15u) == 15u && __builtin_amdgcn_s_memrealtime() - t0 > R.idle_ticks) break;  // idle: leave
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_ctl[0] = cmd;
+    }
+    __syncthreads();
+    if (s_ctl[0] != kResSearch) return;
+    const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
+    // ---- the slot into LDS, verified (header sequence number + checksum of the used words)
+    const uint8_t *slot = R.slots + uint64_t(seq % kResSlots) * kResSlotBytes;
+    const uint32_t *words = reinterpret_cast<const uint32_t *>(slot + kResHdrBytes);
+    bool ok = false;
+    for (uint32_t attempt = 0; attempt < 4096 && !ok; attempt++) {
+      if (attempt) __builtin_amdgcn_s_sleep(8);
+      for (uint32_t i = uint32_t(tid); i < kWords; i += nthreads)
+        s_args[i] = __hip_atomic_load(words + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (tid == 0) {
+        const uint32_t *h = reinterpret_cast<const uint32_t *>(slot);
+        s_ctl[2] = __hip_atomic_load(h + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_ctl[0] = __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_ctl[3] = __hip_atomic_load(h + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_ctl[1] = 0;
+      }
+      __syncthreads();
+      const uint32_t nsegs = s_args[offsetof(PoolArgs, nsegs) / 4], nbms = s_args[offsetof(PoolArgs, nbms) / 4];
+      uint32_t part = 0;
+      if (nsegs <= uint32_t(kArgSegs) && nbms <= uint32_t(kArgBms))
+        for (uint32_t i = uint32_t(tid); i < kWords; i += nthreads)
+          if (res_word_used(4 * i, nsegs, nbms)) part += s_args[i];
+      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+      if (lane == 0) atomicAdd(&s_ctl[1], part);
+      __syncthreads();
+      ok = s_ctl[2] == seq && (s_ctl[0] == kResQuit || (s_ctl[1] == s_ctl[3] && nsegs <= uint32_t(kArgSegs) &&
+                                                          nbms <= uint32_t(kArgBms)));
+      __syncthreads();  // (s_ctl is rewritten by the next attempt)
+    }
+    if (!ok) {  // the slot never verified: the host fails the query (err) and posts again
+      if (tid == 0) host_store(R.err, 1u);
+      return;
+    }
+    if (s_ctl[0] == kResQuit) return;
+    // ---- the query: the static kernel's scan, arguments from LDS
+    const uint32_t nsegs = uint32_t(__builtin_amdgcn_readfirstlane(A.nsegs)), units = uint32_t(__builtin_amdgcn_readfirstlane(A.units));
+    const uint32_t sq = uint32_t(__builtin_amdgcn_readfirstlane(A.sq)), sr = uint32_t(__builtin_amdgcn_readfirstlane(A.sr));
+    const uint32_t gw = w * nwv + wave;
+    const uint32_t u_begin = gw * sq + min(gw, sr), u_end = u_begin + sq + (gw < sr ? 1u : 0u);
+    const uint32_t rec_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.rec_cap)), wcap = rec_cap / nwv;  // per wave region
+    const uint32_t dlo = A.has_min ? A.min32 : 0u, dhi = A.has_max ? A.max32 : 0xffffffffu;
+    const uint32_t start_s = A.start_s, end_s = A.end_s, ucap = A.unit_cap;
+    const uint32_t *s_bm = reinterpret_cast<const uint32_t *>(A.bms);
+    unsigned long long *const wrec = s_rec + uint64_t(wave) * wcap * 6;
+    uint32_t wn = 0;  // this wave's matches so far (records kept: the first wcap)
+    struct Blk {
+      const uint32_t *scan;
+      const uint8_t *col[NT > 0 ? NT : 1];
+      uint32_t npad, nent, ub, ue, eb;
+    } B;
+    uint32_t b = 0;
+    auto set_block = [&](uint32_t bb) {
+      const PoolBlk &P = A.blk[bb];
+      B.scan = uniform_ptr(P.scan);
+#pragma unroll
+      for (int q = 0; q < (NT > 0 ? NT : 1); q++)
+        if (NT > 0) B.col[q] = uniform_ptr(P.col[q]);
+      B.npad = uint32_t(__builtin_amdgcn_readfirstlane(P.npad));
+      B.nent = uint32_t(__builtin_amdgcn_readfirstlane(P.nent));
+      B.ub = uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[bb]));
+      B.ue = uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[bb + 1]));
+      B.eb = uint32_t(__builtin_amdgcn_readfirstlane(A.ebase[bb]));
+    };
+    while (b + 1 < nsegs && u_begin >= uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[b + 1]))) b++;
+    set_block(b);
+    struct Regs {
+      u32x4 d[kSteps], s[kSteps];
+      uint32_t tv[NT > 0 ? NT : 1][kSteps];
+      uint32_t e0;
+    };
+    auto load = [&](Regs &Rg, uint32_t u) {
+      if (u >= B.ue) {
+        while (b + 1 < nsegs && u >= uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[b + 1]))) b++;
+        set_block(b);
+      }
+      Rg.e0 = B.eb + (u - B.ub) * kPoolTile;
+#pragma unroll
+      for (int k = 0; k < kSteps; k++) {
+        const uint64_t e = uint64_t(Rg.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
+        if (DUR || RANGE) Rg.d[k] = stream4<NTL>(B.scan + 3ull * B.npad, e);
+        if (RANGE) Rg.s[k] = stream4<NTL>(B.scan + B.npad, e);
+      }
+#pragma unroll
+      for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
+        if (NT <= 0) break;
+#pragma unroll
+        for (int k = 0; k < kSteps; k++)
+          Rg.tv[q][k] = stream1<NTL>(B.col[q], uint64_t(Rg.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
+      }
+    };
+    // the unit's matches appended to the wave's region in scan order (k, lane, j)
+    auto eval = [&](const Regs &Rg, uint32_t bslot) {
+      const PoolBlk &P = A.blk[bslot];
+      const uint32_t n = uint32_t(__builtin_amdgcn_readfirstlane(P.nent));
+      const uint32_t bmi4 = uint32_t(__builtin_amdgcn_readfirstlane(P.bmi4)), ns4 = uint32_t(__builtin_amdgcn_readfirstlane(P.nsets4));
+      u32x4 ev[kSteps];
+      if (RANGE) unit_ends<NTL>(Rg.d, Rg.s, ev, uniform_ptr(P.scan), uint32_t(__builtin_amdgcn_readfirstlane(P.npad)), Rg.e0, lane);
+      uint32_t mask = unit_mask<NT, DUR, RANGE>(Rg.d, Rg.s, ev, Rg.tv, Rg.e0, n, dlo, dhi, start_s, end_s, bmi4, ns4,
+                                                 s_bm, lane);
+      if (__ballot(mask != 0) == 0) return;
+      if (ucap) mask = cap_unit_mask(mask, ucap, lane);
+      const DevBlockDesc *D = uniform_ptr(A.desc[bslot]);
+      const auto *Dc = K4(D);
+      const uint8_t *ids = Dc->ids;
+      const uint64_t *st_ns = Dc->start_ns, *en_ns = Dc->end_ns;
+      const uint32_t *names = Dc->names;
+      const uint8_t *id_len = Dc->id_len;
+      const uint32_t bidx = uint32_t(__builtin_amdgcn_readfirstlane(P.block_idx));
+      const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+      for (int k = 0; k < kSteps; k++) {
+        const uint32_t nib = (mask >> (4 * k)) & 0xfu;
+        uint32_t lower = 0, tot = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint64_t bb = __ballot((nib >> j) & 1u);
+          lower += uint32_t(__popcll(bb & below));
+          tot += uint32_t(__popcll(bb));
+        }
+        uint32_t r = wn + lower;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (!((nib >> j) & 1u)) continue;
+          if (r < wcap) {
+            const uint32_t ei = Rg.e0 + uint32_t(k) * 256 + uint32_t(lane) * 4 + uint32_t(j);
+            const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
+            const uint64_t st = G(st_ns)[ei], en = G(en_ns)[ei];
+            const uint64_t nm = G(reinterpret_cast<const uint64_t *>(names))[ei];
+            const uint32_t il = G(id_len)[ei];
+            unsigned long long *d = wrec + uint64_t(r) * 6;
+            d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
+            d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
+            d[2] = st;
+            d[3] = en;
+            d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
+            d[5] = nm;
+          }
+          r++;
+        }
+        wn += tot;
+      }
+    };
+    Regs ra, rb;
+    uint32_t u = u_begin, ba = b, bb = b;
+    if (u < u_end) {
+      load(ra, u);
+      ba = b;
+    }
+    while (u < u_end) {
+      const bool has_b = u + 1 < u_end;
+      if (has_b) {
+        load(rb, u + 1);
+        bb = b;
+      }
+      eval(ra, ba);
+      if (!has_b) break;
+      const bool has_a = u + 2 < u_end;
+      if (has_a) {
+        load(ra, u + 2);
+        ba = b;
+      }
+      eval(rb, bb);
+      u += 2;
+    }
+    (void)units;
+    // ---- the workgroup's records (its waves' regions in wave order) to its host segment, then its count
+    if (lane == 0) s_wn[wave] = wn;
+    __syncthreads();
+    uint32_t total = 0, off = 0, over = 0;
+    for (uint32_t v = 0; v < nwv; v++) {
+      const uint32_t c = s_wn[v];
+      if (v < wave) off += min(c, wcap);
+      total += c;
+      over |= c > wcap ? 1u : 0u;
+    }
+    const uint32_t seg_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.seg_cap));
+    const uint32_t mine = min(wn, wcap);
+    if (!over && total <= seg_cap && mine) {
+      auto *dst = reinterpret_cast<unsigned long long *>(uniform_ptr(A.recs)) + (uint64_t(w) * seg_cap + off) * 6;
+      for (uint32_t i = uint32_t(lane); i < mine * 6; i += 64) host_store(dst + i, wrec[i]);
+    }
+    if (tid == 0 && A.qstamps) {
+      unsigned long long *qs = uniform_ptr(A.qstamps);
+      host_store(qs + 2ull * w, t_seen);
+      host_store(qs + 2ull * w + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // the count last (a wave region that overflowed reports more than the LDS buffer holds:
+    // the host reruns the query on the segment / look-back path)
+    if (tid == 0) host_store(uniform_ptr(A.counts) + w, over ? max(total, rec_cap + 1) : total);
+    __syncthreads();  // (s_wn and the regions are reused by the next query)
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // host
 using PoolFn = void (*)(PoolArgs);
 template <int NT, bool NTL>
@@ -656,6 +935,306 @@ static std::string kernel_symbol(bool is_static, uint32_t nterms, bool dur, bool
   std::snprintf(b, sizeof b, "_ZN3tsg%s_kernelILi%uELb%dELb%dELb%dEEEvNS_8PoolArgsE",
                 is_static ? "20search_static" : "18search_pool", std::min(nterms, 4u), int(dur), int(range), int(ntl));
   return b;
+}
+
+// ---- resident search: host side -------------------------------------------------------
+template <int NT, bool NTL>
+static void *resident_fn_t(bool dur, bool range) {
+  if (dur && range) return reinterpret_cast<void *>(search_resident_kernel<NT, true, true, NTL>);
+  if (dur) return reinterpret_cast<void *>(search_resident_kernel<NT, true, false, NTL>);
+  if (range) return reinterpret_cast<void *>(search_resident_kernel<NT, false, true, NTL>);
+  return reinterpret_cast<void *>(search_resident_kernel<NT, false, false, NTL>);
+}
+// (every instantiation referenced, so that the code object beside libtsg.so holds them all:
+// the resident kernel is launched by symbol through the AQL queue only)
+[[maybe_unused]] static void *resident_fn(uint32_t nterms, bool dur, bool range, bool ntl) {
+  switch (std::min(nterms, 4u)) {
+    case 0: return ntl ? resident_fn_t<0, true>(dur, range) : resident_fn_t<0, false>(dur, range);
+    case 1: return ntl ? resident_fn_t<1, true>(dur, range) : resident_fn_t<1, false>(dur, range);
+    case 2: return ntl ? resident_fn_t<2, true>(dur, range) : resident_fn_t<2, false>(dur, range);
+    case 3: return ntl ? resident_fn_t<3, true>(dur, range) : resident_fn_t<3, false>(dur, range);
+    default: return ntl ? resident_fn_t<4, true>(dur, range) : resident_fn_t<4, false>(dur, range);
+  }
+}
+static std::string resident_symbol(uint32_t nterms, bool dur, bool range, bool ntl) {
+  char b[128];
+  std::snprintf(b, sizeof b, "_ZN3tsg22search_resident_kernelILi%uELb%dELb%dELb%dEEEvNS_12ResidentArgsE",
+                std::min(nterms, 4u), int(dur), int(range), int(ntl));
+  return b;
+}
+constexpr size_t kResDoorBytes = 256;  // the doorbell word's page ahead of the slots
+
+// Device contexts open in this process, by device ordinal. A resident launch fills every CU
+// of its device; a second context on the same device (the bench's concurrent streams, a
+// second engine) would wait behind it, so resident launches run only while a context is
+// alone on its device, and opening a second one ends the first one's launch.
+static std::mutex g_ctx_mu;
+static std::multimap<int, DeviceCtx *> g_ctxs;
+int contexts_on(int ordinal) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  return int(g_ctxs.count(ordinal));
+}
+void context_opened(DeviceCtx &dc) {
+  std::vector<DeviceCtx *> others;
+  {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    auto r = g_ctxs.equal_range(dc.ordinal);
+    for (auto it = r.first; it != r.second; ++it) others.push_back(it->second);
+    g_ctxs.emplace(dc.ordinal, &dc);
+  }
+  for (DeviceCtx *o : others) {
+    std::lock_guard<std::mutex> lk(o->mu);
+    resident_quit(*o);
+  }
+}
+void context_closed(DeviceCtx &dc) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  auto r = g_ctxs.equal_range(dc.ordinal);
+  for (auto it = r.first; it != r.second; ++it)
+    if (it->second == &dc) {
+      g_ctxs.erase(it);
+      break;
+    }
+}
+
+// A query (or a quit) into mailbox slot seq % kResSlots: the argument words the query uses
+// (`parts`: the same words res_word_used names, summed for the checksum), then the header,
+// then the doorbell — each step write-combined stores drained by sfence, pushed past the host
+// data path by a posted HDP flush (the kernel re-reads a slot whose header or checksum does
+// not match yet).
+static void res_post(DeviceCtx &dc, uint32_t seq, uint32_t cmd, const PoolArgs *PA,
+                     const std::vector<std::pair<uint32_t, uint32_t>> *parts) {
+  uint8_t *slot = dc.res_mem + kResDoorBytes + size_t(seq % kResSlots) * kResSlotBytes;
+  uint32_t csum = 0;
+  if (PA) {
+    const auto *src = reinterpret_cast<const uint8_t *>(PA);
+    for (const auto &pt : *parts) {
+      std::memcpy(slot + kResHdrBytes + pt.first, src + pt.first, pt.second);
+      for (uint32_t o = 0; o < pt.second; o += 4) {
+        uint32_t v;
+        std::memcpy(&v, src + pt.first + o, 4);
+        csum += v;
+      }
+    }
+  }
+  __builtin_ia32_sfence();
+  const ResHeader h{seq, cmd, csum, 0};
+  std::memcpy(slot, &h, sizeof h);
+  __builtin_ia32_sfence();
+  aql_hdp_flush(dc.aql);
+  *reinterpret_cast<volatile uint32_t *>(dc.res_mem) = seq;
+  __builtin_ia32_sfence();
+  aql_hdp_flush(dc.aql);
+}
+
+// A resident launch of kernel `sym` serving queries from first_seq on. false: unavailable.
+static bool resident_launch(DeviceCtx &dc, const std::string &sym, uint32_t threads, uint32_t W) {
+  if (!dc.res_mem) {
+    void *p = nullptr;
+    const size_t bytes = kResDoorBytes + size_t(kResSlots) * kResSlotBytes;
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) return false;
+    HIP_OK(hipMemsetAsync(p, 0, bytes, dc.stream));
+    HIP_OK(hipStreamSynchronize(dc.stream));
+    dc.res_mem = static_cast<uint8_t *>(p);
+    *reinterpret_cast<volatile uint32_t *>(dc.res_mem) = dc.res_seq;
+  }
+  const AqlKernel ak = aql_kernel(dc.aql, sym.c_str(), uint32_t(sizeof(ResidentArgs)));
+  if (!ak.kobj) return false;
+  dc.res_host.ensure(64 + size_t(W) * 16);
+  auto *err = static_cast<uint32_t *>(dc.res_host.p);
+  __atomic_store_n(err, 0u, __ATOMIC_RELEASE);
+  ResidentArgs RA{};
+  RA.door = reinterpret_cast<const uint32_t *>(dc.res_mem);
+  RA.slots = dc.res_mem + kResDoorBytes;
+  RA.err = err;
+  RA.first_seq = dc.res_seq + 1;
+  RA.idle_ticks = DeviceCtx::env_u32("TSG_RESIDENT_IDLE_US", 10000, 100, 10000000) * 100u;  // (s_memrealtime: 100 MHz)
+  RA.nthreads = threads;
+  RA.ngroups = W;
+  const std::vector<std::pair<uint32_t, uint32_t>> parts{{0u, uint32_t(sizeof RA)}};
+  constexpr size_t kPoolLds = 96 << 10;
+  aql_dispatch(dc.aql, ak, W, threads, uint32_t(kPoolLds), &RA, parts, false);
+  dc.res_alive = true;
+  dc.res_kernel = sym;
+  dc.res_epoch = dc.mem_epoch;
+  dc.res_launches++;
+  return true;
+}
+
+void resident_quit(DeviceCtx &dc) {
+  if (!dc.res_alive) return;
+  dc.res_alive = false;
+  if (!dc.aql || aql_done(dc.aql)) return;  // (left on its own: idle)
+  const uint32_t seq = ++dc.res_seq;
+  res_post(dc, seq, kResQuit, nullptr, nullptr);
+  dc.res_quits++;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!aql_done(dc.aql)) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
+      fail(TSG_E_DEVICE, "resident search kernel did not leave after a quit (2 s)");
+    __builtin_ia32_pause();
+  }
+}
+
+void resident_release(DeviceCtx &dc) {
+  resident_quit(dc);
+  if (dc.res_mem) (void)hipFree(dc.res_mem);
+  dc.res_mem = nullptr;
+  dc.res_host.release();
+}
+
+// The resident path of pool_search: 1 = served (out filled), 0 = the records overflowed (the
+// caller runs the segment / look-back path), -1 = not available (normal launches).
+static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSeg> &segs,
+                           const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q, uint32_t limit,
+                           uint32_t flags, bool has_dur, uint32_t threads, uint32_t W, uint32_t rec_cap, Tracer &tr,
+                           SearchOut &out) {
+  const std::string sym = resident_symbol(q.nterms, has_dur, q.has_range, dc.pool_nt);
+  if (dc.res_alive && (aql_done(dc.aql) || dc.res_kernel != sym || dc.res_epoch != dc.mem_epoch)) resident_quit(dc);
+  if (!dc.res_alive && !resident_launch(dc, sym, threads, W)) return -1;
+  const uint32_t nsegs = PA.nsegs, nbms = PA.nbms;
+  // the argument words this query uses (res_word_used)
+  thread_local std::vector<std::pair<uint32_t, uint32_t>> parts;
+  parts.clear();
+  parts.push_back({uint32_t(offsetof(PoolArgs, blk)), uint32_t(nsegs * sizeof(PoolBlk))});
+  parts.push_back({uint32_t(offsetof(PoolArgs, desc)), uint32_t(nsegs * sizeof(PA.desc[0]))});
+  if (nbms) parts.push_back({uint32_t(offsetof(PoolArgs, bms)), uint32_t(nbms * sizeof(PA.bms[0]))});
+  parts.push_back({uint32_t(offsetof(PoolArgs, ubase)), uint32_t((nsegs + 1) * sizeof(PA.ubase[0]))});
+  parts.push_back({uint32_t(offsetof(PoolArgs, ebase)), uint32_t(nsegs * sizeof(PA.ebase[0]))});
+  parts.push_back({uint32_t(offsetof(PoolArgs, nsegs)), uint32_t(sizeof(PoolArgs) - offsetof(PoolArgs, nsegs))});
+  hipEvent_t e0, e1;
+  const bool timed = (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
+  const size_t hdr = 256, cntb = align_up(size_t(W) * 4, 256);
+  auto *qst = reinterpret_cast<unsigned long long *>(static_cast<uint8_t *>(dc.res_host.p) + 64);
+  uint32_t *counts = nullptr;
+  const uint8_t *recs = nullptr;
+  auto post = [&] {
+    PA.seg_cap = dc.pool_seg;
+    dc.hres.ensure(hdr + cntb + size_t(W) * PA.seg_cap * sizeof(MatchRec));
+    uint8_t *base = static_cast<uint8_t *>(dc.hres.p);
+    counts = reinterpret_cast<uint32_t *>(base + hdr);
+    recs = base + hdr + cntb;
+    PA.counts = counts;
+    PA.recs = base + hdr + cntb;
+    PA.err = reinterpret_cast<uint32_t *>(base);
+    PA.qstamps = timed ? qst : nullptr;
+    std::fill_n(counts, W, kCountPending);
+    res_post(dc, ++dc.res_seq, kResSearch, &PA, &parts);
+    dc.res_queries++;
+  };
+  // every workgroup's count (stored after its records); a launch that ends first (it left on
+  // an idle timeout just as this query was posted) is launched again: it serves the posted
+  // query from its slot
+  auto wait = [&] {
+    const uint32_t seq = dc.res_seq;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 1, relaunches = 0;; it++) {
+      bool all = true;
+      for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
+      if (all) return;
+      if ((it & 0xfffffu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+        fail(TSG_E_DEVICE, "resident search: no answer in 5 s");
+      if ((it & 255u) == 0 && aql_done(dc.aql)) {
+        all = true;
+        for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
+        if (all) return;
+        if (__atomic_load_n(static_cast<uint32_t *>(dc.res_host.p), __ATOMIC_ACQUIRE))
+          fail(TSG_E_DEVICE, "resident search: a mailbox slot never verified");
+        if (++relaunches > 2) fail(TSG_E_DEVICE, "resident search kernel ended without serving the query");
+        std::fill_n(counts, W, kCountPending);
+        dc.res_seq = seq - 1;  // (the launch's first query is the posted one)
+        if (!resident_launch(dc, dc.res_kernel, threads, W)) fail(TSG_E_DEVICE, "resident search relaunch failed");
+        dc.res_seq = seq;
+        dc.res_relaunches++;
+      }
+      __builtin_ia32_pause();
+    }
+  };
+  tr.mark("plan");
+  post();
+  tr.mark("search");
+  wait();
+  tr.mark("sync");
+  auto scan = [&](uint64_t &total, uint32_t &maxc) {
+    total = 0;
+    maxc = 0;
+    for (uint32_t w = 0; w < W; w++) {
+      total += counts[w];
+      maxc = std::max(maxc, counts[w]);
+    }
+  };
+  uint64_t total = 0;
+  uint32_t maxc = 0;
+  scan(total, maxc);
+  uint32_t reruns = 0;
+  // a workgroup's records exceed its host segment: a larger segment and the query again; more
+  // than its LDS regions hold: the other paths
+  while (maxc > std::min(PA.seg_cap, rec_cap)) {
+    if (maxc > rec_cap) {
+      dc.pool_skip = 16;
+      return 0;
+    }
+    uint32_t want = 2 * PA.seg_cap;
+    while (want < maxc) want <<= 1;
+    dc.pool_seg = std::min(want, rec_cap);
+    post();
+    wait();
+    reruns++;
+    scan(total, maxc);
+  }
+  if (dc.pool_seg > 32 && uint64_t(maxc) * 8 < dc.pool_seg) dc.pool_seg >>= 1;
+  if (timed) {  // the query's span on the device: first workgroup to see it .. last to finish
+    unsigned long long lo = ~0ull, hi = 0;
+    for (uint32_t w = 0; w < W; w++) {
+      lo = std::min(lo, __atomic_load_n(qst + 2 * w, __ATOMIC_ACQUIRE));
+      hi = std::max(hi, __atomic_load_n(qst + 2 * w + 1, __ATOMIC_ACQUIRE));
+    }
+    if (dc.tring_res.size() < dc.tring_used) dc.tring_res.resize(dc.tring_used);
+    dc.tring_aql[dc.tring_used - 1] = -3;
+    dc.tring_res[dc.tring_used - 1] = hi > lo ? (hi - lo) * 10ull : 0ull;  // (100 MHz ticks)
+  }
+  out.kernel_ns = out.scan_ns = 0;
+  out.reruns = reruns;
+  tr.mark("events");
+  // records: the segments in workgroup order are the reference order (static runs, each
+  // wave's matches in scan order); a limit keeps each block part's first L
+  const uint32_t seg = PA.seg_cap;
+  const auto *prec = reinterpret_cast<const SearchOut::Rec *>(recs);
+  thread_local std::vector<uint32_t> pos;
+  uint32_t max_idx = 0;
+  for (const auto &sg : segs) max_idx = std::max(max_idx, sg.block_idx);
+  pos.assign(size_t(max_idx) + 1, 0);
+  for (uint32_t i = 0; i < PA.nsegs; i++) pos[segs[i].block_idx] = i;
+  thread_local std::vector<uint64_t> per;
+  per.assign(PA.nsegs, 0);
+  out.recs.resize(total);
+  uint64_t kept = 0;
+  uint64_t run = 0, ps = ~0ull, cut = 0;
+  for (uint32_t w = 0; w < W; w++) {
+    const SearchOut::Rec *r = prec + uint64_t(w) * seg;
+    for (uint32_t i = 0, c = counts[w]; i < c; i++) {
+      const uint32_t bi = r[i].block_il & 0xffffffu;
+      const uint64_t s_i = bi <= max_idx ? pos[bi] : 0;
+      if (s_i != ps) {
+        ps = s_i;
+        run = 0;
+        cut = limit ? std::min<uint64_t>(limit, segs[s_i].cap) : segs[s_i].cap;
+      }
+      if (run++ < cut) {
+        out.recs[kept++] = r[i];
+        per[s_i]++;
+      }
+    }
+  }
+  out.recs.resize(kept);
+  for (uint32_t i = 0; i < PA.nsegs; i++)
+    for (size_t bi = 0; bi < blocks.size(); bi++)
+      if (blocks[bi].first == segs[i].block_idx) out.block_counts[bi] = per[i];
+  out.scan_bytes += uint64_t(W) * 4 + kept * 32;
+  if (has_dur && q.has_range)
+    for (const auto &sg : segs) out.scan_bytes -= 4ull * (sg.n - sg.e0);
+  tr.mark("post");
+  return 1;
 }
 
 // One search_pool_kernel launch for a narrow search (every block scanned whole; a limit
@@ -762,7 +1341,15 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   PA.ngroups = W;
   PA.sq = U / (W * (threads / 64));
   PA.sr = U % (W * (threads / 64));
+  PA.nbms = uint32_t(nbms.size());
   const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
+  // the resident kernel serves the query when it can (the only context on the device, no
+  // per-call HIP events or stamps asked for); otherwise the queue and the CUs are freed first
+  if (dc.res_on && dc.aql && !want_stamps && !time_scan && contexts_on(dc.ordinal) == 1) {
+    const int r = resident_search(dc, PA, segs, blocks, q, limit, flags, has_dur, threads, W, rec_cap, tr, out);
+    if (r >= 0) return r == 1;
+  }
+  resident_quit(dc);
   hipEvent_t e0 = dc.es0, e1 = dc.es1;
   const bool defer = !time_scan && (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
   uint32_t *counts = nullptr;

@@ -188,6 +188,7 @@ void proto_search(ProtoBlock &b, const tsg_proto_request &req, ProtoOut &out) {
   const uint32_t words = (t1 - t0 + 63) / 64;
   {
     std::lock_guard<std::mutex> lk(dc.mu);
+    resident_quit(dc);  // (the resident search launch holds every CU's LDS)
     HIP_OK(hipSetDevice(dc.ordinal));
     hipStream_t s = dc.stream;
     if (t1 > t0) {

@@ -2045,6 +2045,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       return;
     }
   }
+  resident_quit(dc);  // (the other paths' kernels need the CUs the resident search launch holds)
   const FastFn fast_seg = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, true) : nullptr;
   const FastFn fast_lb = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, false) : nullptr;
   const void *kfn = fast ? reinterpret_cast<const void *>(seg ? fast_seg : fast_lb)
@@ -2572,6 +2573,10 @@ void device_kernel_times(DeviceCtx &dc, std::vector<uint64_t> &ns) {
   HIP_OK(hipStreamSynchronize(dc.stream));
   for (size_t i = 0; i < dc.tring_used; i++) {
     if (i < dc.tring_aql.size() && dc.tring_aql[i] == -2) continue;  // (an AQL dispatch left untimed)
+    if (i < dc.tring_aql.size() && dc.tring_aql[i] == -3) {  // a resident query: its span on the device
+      ns.push_back(i < dc.tring_res.size() ? dc.tring_res[i] : 0);
+      continue;
+    }
     if (i < dc.tring_aql.size() && dc.tring_aql[i] >= 0 && dc.aql) {  // an AQL dispatch: its queue's timestamps
       ns.push_back(aql_time_ns(dc.aql, dc.tring_aql[i]));
       continue;

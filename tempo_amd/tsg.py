@@ -141,7 +141,7 @@ class _LookupResult(C.Structure):
 
 # Every symbol include/tsg.h declares (checked by tests/test_abi.py).
 EXPORTED = [
-    "tsg_init", "tsg_shutdown", "tsg_device_count", "tsg_device_numa_node", "tsg_last_error", "tsg_abi_version", "tsg_cancel",
+    "tsg_init", "tsg_shutdown", "tsg_device_count", "tsg_device_numa_node", "tsg_device_counters", "tsg_last_error", "tsg_abi_version", "tsg_cancel",
     "tsg_pipeline_new", "tsg_pipeline_query", "tsg_pipeline_free", "tsg_pipeline_matches_header",
     "tsg_block_open", "tsg_block_open_pages", "tsg_block_open_mem", "tsg_block_clone", "tsg_wal_block_open", "tsg_wal_block_open_mem", "tsg_block_close", "tsg_block_info_get", "tsg_block_tags",
     "tsg_block_tag_values", "tsg_free", "tsg_search", "tsg_result_free", "tsg_kernel_times", "tsg_results_combine",
@@ -176,6 +176,7 @@ def lib():
         L.tsg_pipeline_free.argtypes = [vp]
         L.tsg_pipeline_matches_header.argtypes = [C.POINTER(_Query), C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
         L.tsg_block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
+        L.tsg_device_counters.argtypes = [vp, C.c_int, C.POINTER(C.c_uint64), C.c_size_t]
         L.tsg_block_open_pages.argtypes = [vp, C.c_char_p, C.c_uint32, C.c_uint32, C.c_int, C.POINTER(vp)]
         L.tsg_block_close.argtypes = [vp]
         L.tsg_block_clone.argtypes = [vp, vp, C.c_int, C.POINTER(vp)]
@@ -604,6 +605,13 @@ class Engine:
         if digest:
             return list(ns), list(nm), list(dg)
         return list(ns), list(nm)
+
+    def resident_counters(self, dev: int = 0) -> dict:
+        """tsg_device_counters: the resident search kernel's launches, queries served, relaunches
+        (a launch that left on its idle timeout as a query was posted) and quits."""
+        buf = (C.c_uint64 * 4)()
+        _check(lib().tsg_device_counters(self.h, dev, buf, 4))
+        return dict(zip(("launches", "queries", "relaunches", "quits"), list(buf)))
 
     def kernel_times(self, cap: int = 65536) -> List[int]:
         """Durations (ns) of the searches run with SEARCH_TIME_DEFER since the last

@@ -43,6 +43,17 @@ if has driver; then  # the driver's own command
   rc=$?; echo "driver rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/driver.err; exit $rc; }
   summ gpurun_out/driver.json driver
 fi
+if has resab; then  # resident kernel on/off, interleaved (main line + limit 20)
+  mkdir -p /tmp/abw
+  for k in 1 2; do
+    for m in 1 0; do
+      TSG_RESIDENT=$m timeout -k 10 300 python -u bench.py --workdir /tmp/abw --steps 400 --warmup 20 $B ${BENCH_ARGS:-} \
+        > gpurun_out/res_${m}_$k.json 2> gpurun_out/res_${m}_$k.err
+      rc=$?; [ $rc -eq 0 ] || { echo "resab $m rc=$rc"; tail -3 gpurun_out/res_${m}_$k.err; exit $rc; }
+      summ gpurun_out/res_${m}_$k.json "resident=$m"
+    done
+  done
+fi
 if has share2; then  # the N=2 legs on one GPU (ranks share device 0, gloo)
   timeout -k 10 900 python3 bench.py --gpus 2 --ranks-share-gpu --steps 20 --warmup 5 > gpurun_out/share2.json 2> gpurun_out/share2.err
   rc=$?; echo "share2 rc=$rc"; [ $rc -eq 0 ] || { tail -8 gpurun_out/share2.err; exit $rc; }
