@@ -695,31 +695,68 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(Reside
     // ---- the slot into LDS, verified (header sequence number + checksum of the used words)
     const uint8_t *slot = R.slots + uint64_t(seq % kResSlots) * kResSlotBytes;
     const uint32_t *words = reinterpret_cast<const uint32_t *>(slot + kResHdrBytes);
-    bool ok = false;
-    for (uint32_t attempt = 0; attempt < 4096 && !ok; attempt++) {
-      if (attempt) __builtin_amdgcn_s_sleep(8);
-      for (uint32_t i = uint32_t(tid); i < kWords; i += nthreads)
-        s_args[i] = __hip_atomic_load(words + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (tid == 0) {
-        const uint32_t *h = reinterpret_cast<const uint32_t *>(slot);
-        s_ctl[2] = __hip_atomic_load(h + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        s_ctl[0] = __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        s_ctl[3] = __hip_atomic_load(h + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        s_ctl[1] = 0;
+    // wave 0 reads the slot (header + the argument struct) with 16-byte system-coherent loads
+    // and checks it; 256 workgroups x 52 lines, where a word per thread had been 16x the
+    // requests, all to the same few lines of one memory channel
+    if (wave == 0) {
+      constexpr uint32_t kQuads = (kWords + 3) / 4;
+      bool vok = false;
+      for (uint32_t attempt = 0; attempt < 4096 && !vok; attempt++) {
+        if (attempt) __builtin_amdgcn_s_sleep(8);
+        u32x4 hq, v[(kQuads + 63) / 64];
+        {
+          const u32x4 *hp = reinterpret_cast<const u32x4 *>(slot);
+          asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(hq) : "v"(hp) : "memory");
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < (kQuads + 63) / 64; k++) {
+          const uint32_t qi = min(k * 64 + uint32_t(lane), kQuads - 1);
+          const u32x4 *qp = reinterpret_cast<const u32x4 *>(words) + qi;
+          asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(v[k]) : "v"(qp) : "memory");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // nsegs / nbms, from the lanes holding them
+        constexpr uint32_t kNs = uint32_t(offsetof(PoolArgs, nsegs) / 4), kNb = uint32_t(offsetof(PoolArgs, nbms) / 4);
+        uint32_t ns = 0, nb = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < (kQuads + 63) / 64; k++) {
+          const uint32_t w0 = (k * 64 + uint32_t(lane)) * 4;
+          const uint32_t x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++) {
+            if (w0 + j == kNs) ns = x[j];
+            if (w0 + j == kNb) nb = x[j];
+          }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          ns |= __shfl_xor(ns, o);
+          nb |= __shfl_xor(nb, o);
+        }
+        uint32_t part = 0;
+        const bool sane = ns <= uint32_t(kArgSegs) && nb <= uint32_t(kArgBms);
+#pragma unroll
+        for (uint32_t k = 0; k < (kQuads + 63) / 64; k++) {
+          const uint32_t qi = k * 64 + uint32_t(lane);
+          if (qi >= kQuads) continue;
+          const uint32_t x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t wi = qi * 4 + j;
+            if (wi < kWords) {
+              s_args[wi] = x[j];
+              if (sane && res_word_used(4 * wi, ns, nb)) part += x[j];
+            }
+          }
+        }
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+        vok = hq.x == seq && (hq.y == kResQuit || (sane && part == hq.z));
+        vok = __builtin_amdgcn_readfirstlane(uint32_t(vok)) != 0;
+        if (lane == 0) s_ctl[0] = hq.y;
       }
-      __syncthreads();
-      const uint32_t nsegs = s_args[offsetof(PoolArgs, nsegs) / 4], nbms = s_args[offsetof(PoolArgs, nbms) / 4];
-      uint32_t part = 0;
-      if (nsegs <= uint32_t(kArgSegs) && nbms <= uint32_t(kArgBms))
-        for (uint32_t i = uint32_t(tid); i < kWords; i += nthreads)
-          if (res_word_used(4 * i, nsegs, nbms)) part += s_args[i];
-      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-      if (lane == 0) atomicAdd(&s_ctl[1], part);
-      __syncthreads();
-      ok = s_ctl[2] == seq && (s_ctl[0] == kResQuit || (s_ctl[1] == s_ctl[3] && nsegs <= uint32_t(kArgSegs) &&
-                                                          nbms <= uint32_t(kArgBms)));
-      __syncthreads();  // (s_ctl is rewritten by the next attempt)
+      if (lane == 0) s_ctl[1] = vok ? 1u : 0u;
     }
+    __syncthreads();
+    const bool ok = s_ctl[1] != 0;
     if (!ok) {  // the slot never verified: the host fails the query (err) and posts again
       if (tid == 0) host_store(R.err, 1u);
       return;
@@ -1128,9 +1165,16 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
   auto wait = [&] {
     const uint32_t seq = dc.res_seq;
     const auto t0 = std::chrono::steady_clock::now();
+    const bool prof = prof_on();
+    bool first = !prof;
     for (uint32_t it = 1, relaunches = 0;; it++) {
       bool all = true;
       for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
+      if (!first) {  // (TSG_PROF: post -> the first workgroup's count)
+        for (uint32_t w = 0; w < W && !first; w++) first = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
+        if (first)
+          prof_add("res.first_count", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+      }
       if (all) return;
       if ((it & 0xfffffu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
         fail(TSG_E_DEVICE, "resident search: no answer in 5 s");
@@ -1188,6 +1232,18 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
     for (uint32_t w = 0; w < W; w++) {
       lo = std::min(lo, __atomic_load_n(qst + 2 * w, __ATOMIC_ACQUIRE));
       hi = std::max(hi, __atomic_load_n(qst + 2 * w + 1, __ATOMIC_ACQUIRE));
+    }
+    static const bool dump = std::getenv("TSG_RES_DUMP") != nullptr;
+    if (dump) {  // spread of the workgroups' {seen, end} stamps (us after the first seen)
+      std::vector<double> sn(W), en(W);
+      for (uint32_t w = 0; w < W; w++) {
+        sn[w] = double(qst[2 * w] - lo) / 100.0;
+        en[w] = double(qst[2 * w + 1] - lo) / 100.0;
+      }
+      std::sort(sn.begin(), sn.end());
+      std::sort(en.begin(), en.end());
+      std::fprintf(stderr, "[tsg] resident stamps us: seen p50 %.2f p90 %.2f max %.2f | end p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
+                   sn[W / 2], sn[W * 9 / 10], sn[W - 1], en[W / 10], en[W / 2], en[W * 9 / 10], en[W - 1]);
     }
     if (dc.tring_res.size() < dc.tring_used) dc.tring_res.resize(dc.tring_used);
     dc.tring_aql[dc.tring_used - 1] = -3;

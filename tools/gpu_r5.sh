@@ -82,6 +82,16 @@ if has hostprof; then
   TSG_PROF=1 timeout -k 10 500 python -u bench.py --steps 200 --warmup 20 $B ${BENCH_ARGS:-} > gpurun_out/hp.json 2> gpurun_out/hp.err
   rc=$?; echo "hostprof rc=$rc"; grep -v "^\[bench\]" gpurun_out/hp.err | tail -4; [ $rc -eq 0 ] || exit $rc
 fi
+if has resprof; then  # host phases + workgroup stamp spread, resident on and off
+  for m in 1 0; do
+    TSG_PROF=1 TSG_RES_DUMP=1 TSG_RESIDENT=$m timeout -k 10 300 python -u bench.py --steps 200 --warmup 20 $B --limit-steps 0 \
+      > gpurun_out/rp_$m.json 2> gpurun_out/rp_$m.err
+    rc=$?; echo "resprof $m rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/rp_$m.err; exit $rc; }
+    summ gpurun_out/rp_$m.json "prof resident=$m"
+    grep "resident stamps" gpurun_out/rp_$m.err | tail -3
+    grep -o "plan=[0-9.]*\|search=[0-9.]*\|sync=[0-9.]*\|post=[0-9.]*\|post.keys=[0-9.]*\|post.sort=[0-9.]*\|res.first_count=[0-9.]*\|tsg_search.results=[0-9.]*\|tsg_search.device=[0-9.]*" gpurun_out/rp_$m.err | tr '\n' ' '; echo
+  done
+fi
 if has rocprof; then  # kernel trace + stats of the main line (profiles/)
   cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/rp -o rp -- python3 bench.py --steps 200 --warmup 10 $B \
