@@ -73,7 +73,9 @@ struct PoolArgs {
   // static kernel: the launch's NW waves split the units as wave g -> [g*sq + min(g, sr), ...),
   // the first sr waves one unit more (sq, sr = units / NW, units % NW: no division on the device)
   uint32_t sq, sr;
-  uint32_t nbms, pad0;               // bitmaps in `bms` (the resident kernel's slot checksum)
+  uint32_t nbms;                     // bitmaps in `bms` (the resident kernel's slot checksum)
+  uint32_t wq, wr;                   // resident kernel: workgroup w scans units [w*wq + min(w, wr), +wq + (w < wr))
+  uint32_t pad0;
   unsigned long long *qstamps;       // resident kernel, timed queries: per workgroup {seen, end} (100 MHz)
 };
 static_assert(sizeof(PoolArgs) <= 4096, "kernel arguments");
@@ -638,6 +640,7 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
 // completing with counts missing: it relaunches and posts again (pool.hip resident_*).
 constexpr uint32_t kResSlots = 64, kResSlotBytes = 8192, kResHdrBytes = 64;
 constexpr uint32_t kResSearch = 1, kResQuit = 2;
+constexpr uint32_t kResMaxUnits = 2048;  // units per workgroup (the LDS tables); larger queries launch plainly
 struct ResHeader {  // the first 16 B of a mailbox slot; PoolArgs at +kResHdrBytes
   uint32_t seq, cmd, csum, nwords;
 };
@@ -667,6 +670,8 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(Reside
   __shared__ __attribute__((aligned(16))) uint32_t s_args[sizeof(PoolArgs) / 4];
   __shared__ uint32_t s_ctl[4];   // [0] command for this round, [1] checksum, [2] header seq, [3] header csum
   __shared__ uint32_t s_wn[kPoolWaves + 1];
+  __shared__ uint32_t s_ub[kResMaxUnits], s_uc[kResMaxUnits];  // per unit of the run: LDS record base, count
+  __shared__ uint32_t s_next, s_nrec;
   extern __shared__ __attribute__((aligned(16))) unsigned long long s_rec[];  // rec_cap x 6 words
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = blockIdx.x, nthreads = R.nthreads, nwv = nthreads >> 6;
@@ -762,65 +767,64 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(Reside
       return;
     }
     if (s_ctl[0] == kResQuit) return;
-    // ---- the query: the static kernel's scan, arguments from LDS
-    const uint32_t nsegs = uint32_t(__builtin_amdgcn_readfirstlane(A.nsegs)), units = uint32_t(__builtin_amdgcn_readfirstlane(A.units));
-    const uint32_t sq = uint32_t(__builtin_amdgcn_readfirstlane(A.sq)), sr = uint32_t(__builtin_amdgcn_readfirstlane(A.sr));
-    const uint32_t gw = w * nwv + wave;
-    const uint32_t u_begin = gw * sq + min(gw, sr), u_end = u_begin + sq + (gw < sr ? 1u : 0u);
-    const uint32_t rec_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.rec_cap)), wcap = rec_cap / nwv;  // per wave region
+    // ---- the query. Workgroup w owns the contiguous unit run [ua, ua + nk) (runs differ by at
+    // most one unit: every CU the same share); its waves take the run's units one at a time
+    // from an LDS counter (the first two of each wave implied), so they finish together; a
+    // unit's matches go to the LDS record buffer at once, in scan order, and the unit
+    // remembers where (s_ub / s_uc). At the end the units' counts are prefix-summed and each
+    // unit's records written to the workgroup's host segment at its offset: the segment is in
+    // scan order whichever wave took which unit.
+    const uint32_t nsegs = uint32_t(__builtin_amdgcn_readfirstlane(A.nsegs));
+    const uint32_t wq = uint32_t(__builtin_amdgcn_readfirstlane(A.wq)), wr = uint32_t(__builtin_amdgcn_readfirstlane(A.wr));
+    const uint32_t ua = w * wq + min(w, wr), nk = wq + (w < wr ? 1u : 0u);
+    const uint32_t rec_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.rec_cap));
     const uint32_t dlo = A.has_min ? A.min32 : 0u, dhi = A.has_max ? A.max32 : 0xffffffffu;
     const uint32_t start_s = A.start_s, end_s = A.end_s, ucap = A.unit_cap;
     const uint32_t *s_bm = reinterpret_cast<const uint32_t *>(A.bms);
-    unsigned long long *const wrec = s_rec + uint64_t(wave) * wcap * 6;
-    uint32_t wn = 0;  // this wave's matches so far (records kept: the first wcap)
-    struct Blk {
-      const uint32_t *scan;
-      const uint8_t *col[NT > 0 ? NT : 1];
-      uint32_t npad, nent, ub, ue, eb;
-    } B;
-    uint32_t b = 0;
-    auto set_block = [&](uint32_t bb) {
-      const PoolBlk &P = A.blk[bb];
-      B.scan = uniform_ptr(P.scan);
-#pragma unroll
-      for (int q = 0; q < (NT > 0 ? NT : 1); q++)
-        if (NT > 0) B.col[q] = uniform_ptr(P.col[q]);
-      B.npad = uint32_t(__builtin_amdgcn_readfirstlane(P.npad));
-      B.nent = uint32_t(__builtin_amdgcn_readfirstlane(P.nent));
-      B.ub = uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[bb]));
-      B.ue = uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[bb + 1]));
-      B.eb = uint32_t(__builtin_amdgcn_readfirstlane(A.ebase[bb]));
-    };
-    while (b + 1 < nsegs && u_begin >= uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[b + 1]))) b++;
-    set_block(b);
+    for (uint32_t i = uint32_t(tid); i < nk; i += nthreads) s_uc[i] = 0;
+    if (tid == 0) {
+      s_next = 0;
+      s_nrec = 0;
+    }
+    __syncthreads();
+    uint32_t b = 0;  // the block of the wave's last load (its fields are read from LDS per load)
     struct Regs {
       u32x4 d[kSteps], s[kSteps];
       uint32_t tv[NT > 0 ? NT : 1][kSteps];
-      uint32_t e0;
+      uint32_t e0, k;
     };
-    auto load = [&](Regs &Rg, uint32_t u) {
-      if (u >= B.ue) {
-        while (b + 1 < nsegs && u >= uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[b + 1]))) b++;
-        set_block(b);
-      }
-      Rg.e0 = B.eb + (u - B.ub) * kPoolTile;
+    // (a wave's claims only grow: the block walk only moves forward)
+    auto load = [&](Regs &Rg, uint32_t k) {
+      const uint32_t u = ua + k;
+      while (b + 1 < nsegs && u >= uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[b + 1]))) b++;
+      const PoolBlk &P = A.blk[b];
+      const uint32_t *scan = uniform_ptr(P.scan);
+      const uint32_t npad = uint32_t(__builtin_amdgcn_readfirstlane(P.npad));
+      Rg.k = k;
+      Rg.e0 = uint32_t(__builtin_amdgcn_readfirstlane(A.ebase[b])) +
+              (u - uint32_t(__builtin_amdgcn_readfirstlane(A.ubase[b]))) * kPoolTile;
 #pragma unroll
-      for (int k = 0; k < kSteps; k++) {
-        const uint64_t e = uint64_t(Rg.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4;
-        if (DUR || RANGE) Rg.d[k] = stream4<NTL>(B.scan + 3ull * B.npad, e);
-        if (RANGE) Rg.s[k] = stream4<NTL>(B.scan + B.npad, e);
+      for (int kk = 0; kk < kSteps; kk++) {
+        const uint64_t e = uint64_t(Rg.e0) + uint64_t(kk) * 256 + uint64_t(lane) * 4;
+        if (DUR || RANGE) Rg.d[kk] = stream4<NTL>(scan + 3ull * npad, e);
+        if (RANGE) Rg.s[kk] = stream4<NTL>(scan + npad, e);
       }
 #pragma unroll
       for (int q = 0; q < (NT > 0 ? NT : 1); q++) {
         if (NT <= 0) break;
+        const uint8_t *col = uniform_ptr(P.col[q]);
 #pragma unroll
-        for (int k = 0; k < kSteps; k++)
-          Rg.tv[q][k] = stream1<NTL>(B.col[q], uint64_t(Rg.e0) + uint64_t(k) * 256 + uint64_t(lane) * 4);
+        for (int kk = 0; kk < kSteps; kk++)
+          Rg.tv[q][kk] = stream1<NTL>(col, uint64_t(Rg.e0) + uint64_t(kk) * 256 + uint64_t(lane) * 4);
       }
     };
-    // the unit's matches appended to the wave's region in scan order (k, lane, j)
-    auto eval = [&](const Regs &Rg, uint32_t bslot) {
-      const PoolBlk &P = A.blk[bslot];
+    // the unit's matches into the LDS buffer in scan order (k-step, lane, j)
+    auto eval = [&](const Regs &Rg) {
+      // the unit's block: lanes test the block boundaries, the ballot counts those passed
+      const uint32_t u = ua + Rg.k;
+      const uint32_t blk = uint32_t(__popcll(__ballot(uint32_t(lane) + 1 < nsegs + 0u && uint32_t(lane) < nsegs &&
+                                                      u >= A.ubase[lane + 1])));
+      const PoolBlk &P = A.blk[blk];
       const uint32_t n = uint32_t(__builtin_amdgcn_readfirstlane(P.nent));
       const uint32_t bmi4 = uint32_t(__builtin_amdgcn_readfirstlane(P.bmi4)), ns4 = uint32_t(__builtin_amdgcn_readfirstlane(P.nsets4));
       u32x4 ev[kSteps];
@@ -829,7 +833,18 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(Reside
                                                  s_bm, lane);
       if (__ballot(mask != 0) == 0) return;
       if (ucap) mask = cap_unit_mask(mask, ucap, lane);
-      const DevBlockDesc *D = uniform_ptr(A.desc[bslot]);
+      uint32_t cnt = uint32_t(__popc(mask));
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+      cnt = uint32_t(__builtin_amdgcn_readfirstlane(cnt));
+      if (!cnt) return;
+      uint32_t base = 0;
+      if (lane == 0) {
+        base = atomicAdd(&s_nrec, cnt);
+        s_ub[Rg.k] = base;
+        s_uc[Rg.k] = cnt;
+      }
+      base = uint32_t(__builtin_amdgcn_readfirstlane(base));
+      const DevBlockDesc *D = uniform_ptr(A.desc[blk]);
       const auto *Dc = K4(D);
       const uint8_t *ids = Dc->ids;
       const uint64_t *st_ns = Dc->start_ns, *en_ns = Dc->end_ns;
@@ -837,9 +852,14 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(Reside
       const uint8_t *id_len = Dc->id_len;
       const uint32_t bidx = uint32_t(__builtin_amdgcn_readfirstlane(P.block_idx));
       const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+      // each step's first rank for this lane (ballots: every lane takes part), then the
+      // records one at a time (a loop kept rolled: the gathers of 8 records at once had
+      // pushed the kernel past its 128 registers)
+      uint32_t rank0[kSteps];
+      uint32_t before = 0;
 #pragma unroll
-      for (int k = 0; k < kSteps; k++) {
-        const uint32_t nib = (mask >> (4 * k)) & 0xfu;
+      for (int kk = 0; kk < kSteps; kk++) {
+        const uint32_t nib = (mask >> (4 * kk)) & 0xfu;
         uint32_t lower = 0, tot = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -847,67 +867,82 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(Reside
           lower += uint32_t(__popcll(bb & below));
           tot += uint32_t(__popcll(bb));
         }
-        uint32_t r = wn + lower;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          if (!((nib >> j) & 1u)) continue;
-          if (r < wcap) {
-            const uint32_t ei = Rg.e0 + uint32_t(k) * 256 + uint32_t(lane) * 4 + uint32_t(j);
-            const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
-            const uint64_t st = G(st_ns)[ei], en = G(en_ns)[ei];
-            const uint64_t nm = G(reinterpret_cast<const uint64_t *>(names))[ei];
-            const uint32_t il = G(id_len)[ei];
-            unsigned long long *d = wrec + uint64_t(r) * 6;
-            d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
-            d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
-            d[2] = st;
-            d[3] = en;
-            d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
-            d[5] = nm;
-          }
-          r++;
-        }
-        wn += tot;
+        rank0[kk] = base + before + lower;
+        before += tot;
+      }
+#pragma unroll 1
+      for (uint32_t m = mask; m; m &= m - 1) {
+        const uint32_t bit = uint32_t(__builtin_ctz(m)), kk = bit >> 2, j = bit & 3u;
+        const uint32_t r = (kk ? rank0[1] : rank0[0]) + uint32_t(__popc((mask >> (4 * kk)) & ((1u << j) - 1u)));
+        if (r >= rec_cap) continue;
+        const uint32_t ei = Rg.e0 + kk * 256 + uint32_t(lane) * 4 + j;
+        const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
+        const uint64_t st = G(st_ns)[ei], en = G(en_ns)[ei];
+        const uint64_t nm = G(reinterpret_cast<const uint64_t *>(names))[ei];
+        const uint32_t il = G(id_len)[ei];
+        unsigned long long *d = s_rec + uint64_t(r) * 6;
+        d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
+        d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
+        d[2] = st;
+        d[3] = en;
+        d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
+        d[5] = nm;
       }
     };
+    auto claim = [&]() -> uint32_t {
+      uint32_t c = 0;
+      if (lane == 0) c = atomicAdd(&s_next, 1u);
+      return 2 * nwv + uint32_t(__builtin_amdgcn_readfirstlane(c));
+    };
     Regs ra, rb;
-    uint32_t u = u_begin, ba = b, bb = b;
-    if (u < u_end) {
-      load(ra, u);
-      ba = b;
-    }
-    while (u < u_end) {
-      const bool has_b = u + 1 < u_end;
-      if (has_b) {
-        load(rb, u + 1);
-        bb = b;
+    uint32_t ka = wave, kb = wave + nwv;
+    if (ka < nk) load(ra, ka);
+    if (kb < nk) load(rb, kb);
+    while (ka < nk || kb < nk) {
+      if (ka < nk) {
+        eval(ra);
+        ka = claim();
+        if (ka < nk) load(ra, ka);
       }
-      eval(ra, ba);
-      if (!has_b) break;
-      const bool has_a = u + 2 < u_end;
-      if (has_a) {
-        load(ra, u + 2);
-        ba = b;
+      if (kb < nk) {
+        eval(rb);
+        kb = claim();
+        if (kb < nk) load(rb, kb);
       }
-      eval(rb, bb);
-      u += 2;
     }
-    (void)units;
-    // ---- the workgroup's records (its waves' regions in wave order) to its host segment, then its count
-    if (lane == 0) s_wn[wave] = wn;
     __syncthreads();
-    uint32_t total = 0, off = 0, over = 0;
-    for (uint32_t v = 0; v < nwv; v++) {
-      const uint32_t c = s_wn[v];
-      if (v < wave) off += min(c, wcap);
-      total += c;
-      over |= c > wcap ? 1u : 0u;
+    // ---- units' counts -> exclusive offsets (s_uc in place), then each unit's records to the
+    // host segment at its offset, then the count
+    const uint32_t total = s_nrec;
+    {
+      const uint32_t i0 = 2 * uint32_t(tid), i1 = i0 + 1;
+      const uint32_t c0 = i0 < nk ? s_uc[i0] : 0u, c1 = i1 < nk ? s_uc[i1] : 0u;
+      const uint32_t mine = c0 + c1;
+      uint32_t incl = mine;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      if (lane == 63) s_wn[wave] = incl;
+      __syncthreads();
+      uint32_t woff = 0;
+      for (uint32_t v = 0; v < wave; v++) woff += s_wn[v];
+      const uint32_t ex = woff + incl - mine;
+      __syncthreads();  // (every c0 / c1 read before they are overwritten)
+      if (i0 < nk) s_uc[i0] = ex;
+      if (i1 < nk) s_uc[i1] = ex + c0;
+      __syncthreads();
     }
     const uint32_t seg_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.seg_cap));
-    const uint32_t mine = min(wn, wcap);
-    if (!over && total <= seg_cap && mine) {
-      auto *dst = reinterpret_cast<unsigned long long *>(uniform_ptr(A.recs)) + (uint64_t(w) * seg_cap + off) * 6;
-      for (uint32_t i = uint32_t(lane); i < mine * 6; i += 64) host_store(dst + i, wrec[i]);
+    const bool over = total > rec_cap;
+    if (!over && total <= seg_cap && total) {
+      auto *dst0 = reinterpret_cast<unsigned long long *>(uniform_ptr(A.recs)) + uint64_t(w) * seg_cap * 6;
+      for (uint32_t k = uint32_t(tid); k < nk; k += nthreads) {
+        const uint32_t o = s_uc[k], e = k + 1 < nk ? s_uc[k + 1] : total;
+        if (e == o) continue;
+        const unsigned long long *src = s_rec + uint64_t(s_ub[k]) * 6;
+        for (uint32_t i = 0; i < (e - o) * 6; i++) host_store(dst0 + uint64_t(o) * 6 + i, src[i]);
+      }
     }
     if (tid == 0 && A.qstamps) {
       unsigned long long *qs = uniform_ptr(A.qstamps);
@@ -916,10 +951,10 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(Reside
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // the count last (a wave region that overflowed reports more than the LDS buffer holds:
-    // the host reruns the query on the segment / look-back path)
+    // the count last (more matches than the LDS buffer holds: the host reruns the query on the
+    // segment / look-back path)
     if (tid == 0) host_store(uniform_ptr(A.counts) + w, over ? max(total, rec_cap + 1) : total);
-    __syncthreads();  // (s_wn and the regions are reused by the next query)
+    __syncthreads();  // (the LDS tables are reused by the next query)
   }
 }
 
@@ -1166,26 +1201,41 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
     const uint32_t seq = dc.res_seq;
     const auto t0 = std::chrono::steady_clock::now();
     const bool prof = prof_on();
-    bool first = !prof;
+    thread_local std::vector<uint8_t> seen;
+    seen.assign(W, 0);
+    uint32_t lo = 0, nseen = 0;
+    const uint32_t seg = PA.seg_cap;
     for (uint32_t it = 1, relaunches = 0;; it++) {
-      bool all = true;
-      for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
-      if (!first) {  // (TSG_PROF: post -> the first workgroup's count)
-        for (uint32_t w = 0; w < W && !first; w++) first = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
-        if (first)
+      // counts not seen yet; a finished workgroup's records are pulled into this core's
+      // caches while the others still run (the copy after the wait then hits them)
+      for (uint32_t w = lo; w < W; w++) {
+        if (seen[w]) {
+          if (w == lo) lo++;
+          continue;
+        }
+        const uint32_t c = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE);
+        if (c == kCountPending) continue;
+        seen[w] = 1;
+        if (prof && nseen == 0)
           prof_add("res.first_count", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        nseen++;
+        if (w == lo) lo++;
+        const uint8_t *p0 = recs + uint64_t(w) * seg * sizeof(MatchRec);
+        for (uint64_t o = 0; o < uint64_t(std::min(c, seg)) * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
       }
-      if (all) return;
+      if (lo == W) return;
       if ((it & 0xfffffu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
         fail(TSG_E_DEVICE, "resident search: no answer in 5 s");
       if ((it & 255u) == 0 && aql_done(dc.aql)) {
-        all = true;
+        bool all = true;
         for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
         if (all) return;
         if (__atomic_load_n(static_cast<uint32_t *>(dc.res_host.p), __ATOMIC_ACQUIRE))
           fail(TSG_E_DEVICE, "resident search: a mailbox slot never verified");
         if (++relaunches > 2) fail(TSG_E_DEVICE, "resident search kernel ended without serving the query");
         std::fill_n(counts, W, kCountPending);
+        seen.assign(W, 0);
+        lo = 0;
         dc.res_seq = seq - 1;  // (the launch's first query is the posted one)
         if (!resident_launch(dc, dc.res_kernel, threads, W)) fail(TSG_E_DEVICE, "resident search relaunch failed");
         dc.res_seq = seq;
@@ -1398,10 +1448,13 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   PA.sq = U / (W * (threads / 64));
   PA.sr = U % (W * (threads / 64));
   PA.nbms = uint32_t(nbms.size());
+  PA.wq = U / W;
+  PA.wr = U % W;
   const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
   // the resident kernel serves the query when it can (the only context on the device, no
   // per-call HIP events or stamps asked for); otherwise the queue and the CUs are freed first
-  if (dc.res_on && dc.aql && !want_stamps && !time_scan && contexts_on(dc.ordinal) == 1) {
+  if (dc.res_on && dc.aql && !want_stamps && !time_scan && (U + W - 1) / W <= kResMaxUnits &&
+      contexts_on(dc.ordinal) == 1) {
     const int r = resident_search(dc, PA, segs, blocks, q, limit, flags, has_dur, threads, W, rec_cap, tr, out);
     if (r >= 0) return r == 1;
   }
