@@ -665,8 +665,13 @@ __host__ __device__ inline bool res_word_used(uint32_t off, uint32_t nsegs, uint
          (off >= uint32_t(offsetof(PoolArgs, nsegs)) && off < uint32_t(sizeof(PoolArgs)));
 }
 
+// 12 waves per workgroup (one workgroup per CU): 168 registers per lane, where the pool kernels'
+// 16 waves allow 128 and this kernel's state (two units in flight, the mailbox checks, the
+// ordered record output) spilled to scratch; 24 units in flight per CU still cover the HBM
+// latency (config 2: 34 MB in flight)
+constexpr uint32_t kResWaves = 12, kResThreads = kResWaves * 64;
 template <int NT, bool DUR, bool RANGE, bool NTL>
-__global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(ResidentArgs R) {
+__global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(ResidentArgs R) {
   __shared__ __attribute__((aligned(16))) uint32_t s_args[sizeof(PoolArgs) / 4];
   __shared__ uint32_t s_ctl[4];   // [0] command for this round, [1] checksum, [2] header seq, [3] header csum
   __shared__ uint32_t s_wn[kPoolWaves + 1];
@@ -778,8 +783,9 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_resident_kernel(Reside
     const uint32_t wq = uint32_t(__builtin_amdgcn_readfirstlane(A.wq)), wr = uint32_t(__builtin_amdgcn_readfirstlane(A.wr));
     const uint32_t ua = w * wq + min(w, wr), nk = wq + (w < wr ? 1u : 0u);
     const uint32_t rec_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.rec_cap));
-    const uint32_t dlo = A.has_min ? A.min32 : 0u, dhi = A.has_max ? A.max32 : 0xffffffffu;
-    const uint32_t start_s = A.start_s, end_s = A.end_s, ucap = A.unit_cap;
+    auto rfl = [](uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(v)); };
+    const uint32_t dlo = rfl(A.has_min ? A.min32 : 0u), dhi = rfl(A.has_max ? A.max32 : 0xffffffffu);
+    const uint32_t start_s = rfl(A.start_s), end_s = rfl(A.end_s), ucap = rfl(A.unit_cap);
     const uint32_t *s_bm = reinterpret_cast<const uint32_t *>(A.bms);
     for (uint32_t i = uint32_t(tid); i < nk; i += nthreads) s_uc[i] = 0;
     if (tid == 0) {
@@ -1455,7 +1461,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   // per-call HIP events or stamps asked for); otherwise the queue and the CUs are freed first
   if (dc.res_on && dc.aql && !want_stamps && !time_scan && (U + W - 1) / W <= kResMaxUnits &&
       contexts_on(dc.ordinal) == 1) {
-    const int r = resident_search(dc, PA, segs, blocks, q, limit, flags, has_dur, threads, W, rec_cap, tr, out);
+    const int r = resident_search(dc, PA, segs, blocks, q, limit, flags, has_dur, kResThreads, W, rec_cap, tr, out);
     if (r >= 0) return r == 1;
   }
   resident_quit(dc);
