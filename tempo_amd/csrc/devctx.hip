@@ -7,6 +7,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <new>
+#include <unordered_map>
 
 #include "aql.hpp"
 #include "devctx.hpp"
@@ -14,6 +17,48 @@
 namespace tsg {
 
 int device_ordinal(const DeviceCtx &dc) { return dc.ordinal; }
+
+// ---- cached pinned host blocks (PinnedAlloc) ----------------------------------------------
+// A block is reused for a request of at least half its size; sizes round up to 1 MiB. At most
+// kPinnedCache bytes stay cached (pinning and unpinning hundreds of MB costs milliseconds).
+static std::mutex g_pin_mu;
+static std::multimap<size_t, void *> g_pin_free;  // capacity -> block
+static size_t g_pin_cached = 0;
+static std::unordered_map<void *, size_t> g_pin_cap;
+constexpr size_t kPinnedCache = size_t(2) << 30;
+void *pinned_get(size_t bytes) {
+  if (bytes == 0) bytes = 1;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pin_free.lower_bound(bytes);
+    if (it != g_pin_free.end() && it->first / 2 <= bytes) {
+      void *p = it->second;
+      g_pin_cached -= it->first;
+      g_pin_free.erase(it);
+      return p;
+    }
+  }
+  const size_t cap = (bytes + (size_t(1) << 20) - 1) & ~((size_t(1) << 20) - 1);
+  void *p = nullptr;
+  if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess || !p) throw std::bad_alloc();
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pin_cap[p] = cap;
+  return p;
+}
+void pinned_put(void *p, size_t) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  const size_t cap = g_pin_cap[p];
+  g_pin_free.emplace(cap, p);
+  g_pin_cached += cap;
+  while (g_pin_cached > kPinnedCache && !g_pin_free.empty()) {  // (the smallest go first)
+    auto it = g_pin_free.begin();
+    g_pin_cached -= it->first;
+    g_pin_cap.erase(it->second);
+    (void)hipHostFree(it->second);
+    g_pin_free.erase(it);
+  }
+}
 void device_counters(DeviceCtx &dc, uint64_t out[4]) {
   std::lock_guard<std::mutex> lk(dc.mu);
   out[0] = dc.res_launches;
@@ -77,6 +122,9 @@ void ctx_shutdown(Ctx &c) {
     for (hipEvent_t e : dc->tring) (void)hipEventDestroy(e);
     dc->hdesc.release();
     dc->hout.release();
+    dc->lkstage.release();
+    for (auto &e : dc->lk_ev)
+      if (e) (void)hipEventDestroy(e);
     dc->hres.release();
     dc->hany.release();
     (void)hipEventDestroy(dc->ev0);

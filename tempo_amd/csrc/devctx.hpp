@@ -100,6 +100,10 @@ struct DeviceCtx {
   DevBuf pbm, pout;  // proto search: term bitmaps, per-object match/error bits
   DevBuf fpages, fhits, fres, farena, fcrc, fdst, foff;  // device findOne (find.hip)
   HostBuf hdesc, hout;
+  // lookup: pinned staging of the caller's (pageable) probe ids, two chunks in turn: the host
+  // copies one while the other's DMA runs (lookup.hip upload_ids)
+  HostBuf lkstage;
+  hipEvent_t lk_ev[2] = {nullptr, nullptr};
   // search results, written by the emit kernel directly (coherent: the kernel's
   // stores go over the fabric, visible to the host once the stream is synchronised)
   HostBuf hres{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};

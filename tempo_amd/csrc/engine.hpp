@@ -5,6 +5,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "block.hpp"
@@ -182,11 +183,39 @@ struct V2Block {
 };
 void v2block_open(Ctx &c, V2Block &b, const std::string &dir, int device_hint);
 void v2block_free(V2Block &b);
+// Pinned host memory, cached across calls (devctx.hip): a lookup's hit columns are copied
+// from the device straight into it (no staging copy, no zero fill) and handed to the caller in
+// its tsg_lookup_result; freed blocks go back to the cache for the next call.
+void *pinned_get(size_t bytes);
+void pinned_put(void *p, size_t bytes);
+template <class T>
+struct PinnedAlloc {
+  using value_type = T;
+  PinnedAlloc() = default;
+  template <class U>
+  PinnedAlloc(const PinnedAlloc<U> &) {}
+  T *allocate(size_t n) { return static_cast<T *>(pinned_get(n * sizeof(T))); }
+  void deallocate(T *p, size_t n) { pinned_put(p, n * sizeof(T)); }
+  template <class U>
+  void construct(U *p) {
+    ::new (static_cast<void *>(p)) U;  // default-initialised: resize() writes nothing
+  }
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+  }
+  template <class U>
+  bool operator==(const PinnedAlloc<U> &) const { return true; }
+  template <class U>
+  bool operator!=(const PinnedAlloc<U> &) const { return false; }
+};
+template <class T>
+using PinnedVec = std::vector<T, PinnedAlloc<T>>;
 struct LookupOut {
-  std::vector<uint32_t> id_idx, block_idx;
-  std::vector<int32_t> rec;
-  std::vector<uint64_t> start;
-  std::vector<uint32_t> len;
+  PinnedVec<uint32_t> id_idx, block_idx;
+  PinnedVec<int32_t> rec;
+  PinnedVec<uint64_t> start;
+  PinnedVec<uint32_t> len;
   uint64_t kernel_ns = 0;
 };
 void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>> &blocks, const uint8_t (*ids)[16],

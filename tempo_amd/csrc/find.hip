@@ -428,8 +428,8 @@ void device_find(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>
   device_lookup(dc, blocks, ids, nids, opts, lk);
   out = FindOut();
   const size_t nh = lk.id_idx.size();
-  out.id_idx = lk.id_idx;
-  out.block_idx = lk.block_idx;
+  out.id_idx.assign(lk.id_idx.begin(), lk.id_idx.end());
+  out.block_idx.assign(lk.block_idx.begin(), lk.block_idx.end());
   out.status.assign(nh, TSG_E_NOT_FOUND);
   out.obj_off.assign(nh, 0);
   out.obj_len.assign(nh, 0);

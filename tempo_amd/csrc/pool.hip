@@ -651,6 +651,8 @@ struct ResidentArgs {
   uint32_t first_seq;    // the first query of this launch
   uint32_t idle_ticks;   // s_memrealtime ticks without a post before a workgroup leaves
   uint32_t nthreads, ngroups;
+  uint32_t mode, pad;  // TSG_RES_MODE (experiments): bit 0 = units interleaved over the waves (no LDS claims),
+                       // bit 1 = longer sleeps between doorbell polls
 };
 static_assert(sizeof(PoolArgs) <= kResSlotBytes - kResHdrBytes && sizeof(PoolArgs) % 4 == 0, "mailbox slot");
 
@@ -695,7 +697,8 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
           break;
         }
         if ((n & 15u) == 15u && __builtin_amdgcn_s_memrealtime() - t0 > R.idle_ticks) break;  // idle: leave
-        __builtin_amdgcn_s_sleep(2);
+        if (R.mode & 2u) __builtin_amdgcn_s_sleep(32);
+        else __builtin_amdgcn_s_sleep(2);
       }
       s_ctl[0] = cmd;
     }
@@ -895,7 +898,9 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
         d[5] = nm;
       }
     };
-    auto claim = [&]() -> uint32_t {
+    const bool interleave = (R.mode & 1u) != 0;
+    auto claim = [&](uint32_t prev) -> uint32_t {
+      if (interleave) return prev + 2 * nwv;
       uint32_t c = 0;
       if (lane == 0) c = atomicAdd(&s_next, 1u);
       return 2 * nwv + uint32_t(__builtin_amdgcn_readfirstlane(c));
@@ -907,12 +912,12 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     while (ka < nk || kb < nk) {
       if (ka < nk) {
         eval(ra);
-        ka = claim();
+        ka = claim(ka);
         if (ka < nk) load(ra, ka);
       }
       if (kb < nk) {
         eval(rb);
-        kb = claim();
+        kb = claim(kb);
         if (kb < nk) load(rb, kb);
       }
     }
@@ -1129,6 +1134,7 @@ static bool resident_launch(DeviceCtx &dc, const std::string &sym, uint32_t thre
   RA.idle_ticks = DeviceCtx::env_u32("TSG_RESIDENT_IDLE_US", 10000, 100, 10000000) * 100u;  // (s_memrealtime: 100 MHz)
   RA.nthreads = threads;
   RA.ngroups = W;
+  RA.mode = DeviceCtx::env_u32("TSG_RES_MODE", 0, 0, 255);
   const std::vector<std::pair<uint32_t, uint32_t>> parts{{0u, uint32_t(sizeof RA)}};
   constexpr size_t kPoolLds = 96 << 10;
   aql_dispatch(dc.aql, ak, W, threads, uint32_t(kPoolLds), &RA, parts, false);
@@ -1211,6 +1217,7 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
     seen.assign(W, 0);
     uint32_t lo = 0, nseen = 0;
     const uint32_t seg = PA.seg_cap;
+    static const bool prefetch = DeviceCtx::env_u32("TSG_RES_PREFETCH", 1, 0, 1) != 0;
     for (uint32_t it = 1, relaunches = 0;; it++) {
       // counts not seen yet; a finished workgroup's records are pulled into this core's
       // caches while the others still run (the copy after the wait then hits them)
@@ -1226,8 +1233,10 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
           prof_add("res.first_count", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
         nseen++;
         if (w == lo) lo++;
-        const uint8_t *p0 = recs + uint64_t(w) * seg * sizeof(MatchRec);
-        for (uint64_t o = 0; o < uint64_t(std::min(c, seg)) * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
+        if (prefetch) {
+          const uint8_t *p0 = recs + uint64_t(w) * seg * sizeof(MatchRec);
+          for (uint64_t o = 0; o < uint64_t(std::min(c, seg)) * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
+        }
       }
       if (lo == W) return;
       if ((it & 0xfffffu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))

@@ -92,6 +92,15 @@ if has resprof; then  # host phases + workgroup stamp spread, resident on and of
     grep -o "plan=[0-9.]*\|search=[0-9.]*\|sync=[0-9.]*\|post=[0-9.]*\|post.keys=[0-9.]*\|post.sort=[0-9.]*\|res.first_count=[0-9.]*\|tsg_search.results=[0-9.]*\|tsg_search.device=[0-9.]*" gpurun_out/rp_$m.err | tr '\n' ' '; echo
   done
 fi
+if has resvar; then  # resident kernel variants (TSG_RES_MODE bits, TSG_RES_PREFETCH), host phases each
+  for v in "TSG_RES_MODE=0" "TSG_RES_MODE=1" "TSG_RES_MODE=2" "TSG_RES_PREFETCH=0" "TSG_RESIDENT=0"; do
+    env $v TSG_PROF=1 timeout -k 10 300 python -u bench.py --workdir /tmp/abw --steps 200 --warmup 20 $B --limit-steps 0 \
+      > gpurun_out/rv.json 2> gpurun_out/rv.err
+    rc=$?; [ $rc -eq 0 ] || { echo "resvar $v rc=$rc"; tail -3 gpurun_out/rv.err; exit $rc; }
+    summ gpurun_out/rv.json "$v"
+    grep -o "res.first_count=[0-9.]*\|sync=[0-9.]*\|post=[0-9.]*" gpurun_out/rv.err | head -3 | tr '\n' ' '; echo
+  done
+fi
 if has rocprof; then  # kernel trace + stats of the main line (profiles/)
   cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/rp -o rp -- python3 bench.py --steps 200 --warmup 10 $B \
