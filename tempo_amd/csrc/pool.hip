@@ -947,12 +947,20 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     const uint32_t seg_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.seg_cap));
     const bool over = total > rec_cap;
     if (!over && total <= seg_cap && total) {
+      // consecutive lanes store consecutive words of the segment (the fabric merges them into
+      // whole-line PCIe writes; a record per thread, 8-byte stores each, had been 8x the
+      // transactions and made the host wait ~50 us per query for the last count): output word
+      // i belongs to record p = i / 6, whose unit is found by a binary search of the offsets
       auto *dst0 = reinterpret_cast<unsigned long long *>(uniform_ptr(A.recs)) + uint64_t(w) * seg_cap * 6;
-      for (uint32_t k = uint32_t(tid); k < nk; k += nthreads) {
-        const uint32_t o = s_uc[k], e = k + 1 < nk ? s_uc[k + 1] : total;
-        if (e == o) continue;
-        const unsigned long long *src = s_rec + uint64_t(s_ub[k]) * 6;
-        for (uint32_t i = 0; i < (e - o) * 6; i++) host_store(dst0 + uint64_t(o) * 6 + i, src[i]);
+      for (uint32_t i = uint32_t(tid); i < total * 6; i += nthreads) {
+        const uint32_t p = i / 6, j = i - p * 6;
+        uint32_t lo = 0, hi = nk;  // the last unit whose offset <= p
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_uc[mid] <= p) lo = mid;
+          else hi = mid;
+        }
+        host_store(dst0 + i, s_rec[uint64_t(s_ub[lo] + (p - s_uc[lo])) * 6 + j]);
       }
     }
     if (tid == 0 && A.qstamps) {

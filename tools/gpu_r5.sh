@@ -101,6 +101,20 @@ if has resvar; then  # resident kernel variants (TSG_RES_MODE bits, TSG_RES_PREF
     grep -o "res.first_count=[0-9.]*\|sync=[0-9.]*\|post=[0-9.]*" gpurun_out/rv.err | head -3 | tr '\n' ' '; echo
   done
 fi
+if has resdiag; then  # every query timed: the span per query, by resident set
+  for a in "--sets 4 --events 1" "--sets 1 --events 1" "--sets 4 --events 4"; do
+    TSG_RES_DUMP=1 TSG_PROF=1 timeout -k 10 300 python -u bench.py --workdir /tmp/abw --steps 40 --warmup 8 $B --limit-steps 0 $a \
+      > gpurun_out/rd.json 2> gpurun_out/rd.err
+    rc=$?; [ $rc -eq 0 ] || { echo "resdiag rc=$rc"; tail -3 gpurun_out/rd.err; exit $rc; }
+    summ gpurun_out/rd.json "$a"
+    python3 -c "
+import json,sys
+d=json.loads(open('gpurun_out/rd.json').read().strip().splitlines()[-1])
+print('kernel_us', [round(x) for x in d['latency_us']['kernel'].values()])
+"
+    grep "resident stamps" gpurun_out/rd.err | awk '{print \$NF}' | tail -24 | tr '\n' ' '; echo
+  done
+fi
 if has rocprof; then  # kernel trace + stats of the main line (profiles/)
   cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/rp -o rp -- python3 bench.py --steps 200 --warmup 10 $B \
