@@ -882,7 +882,7 @@ def cfg5_leg(args, eng, shared, rank, world, dist, gen_thread=None):
     t0 = time.perf_counter()
     for _ in range(args.cfg5_steps):
         ts = time.perf_counter()
-        hits, kns_i = eng.lookup(blocks, mine)
+        nh, kns_i = eng.lookup_raw(blocks, mine)  # (the ABI call as a Go caller makes it: no conversion)
         walls.append(time.perf_counter() - ts)
         kns.append(kns_i)
     elapsed = time.perf_counter() - t0
@@ -897,7 +897,9 @@ def cfg5_leg(args, eng, shared, rank, world, dist, gen_thread=None):
            "value": args.cfg5_probes / (kmed / 1e9), "unit": "probes/s",
            "device_ms": kmed / 1e6, "probe_block_pairs_per_s": args.cfg5_probes * args.cfg5_blocks / (kmed / 1e9),
            "host_e2e": {"probes_per_s": args.cfg5_probes * args.cfg5_steps / elapsed,
-                        "step_ms": pct([x * 1e3 for x in walls])},
+                        "step_ms": pct([x * 1e3 for x in walls]),
+                        "note": "tsg_lookup_ids + tsg_lookup_result_free on pageable ids (staged through "
+                                "pinned chunks), hit columns left in the result's pinned arrays"},
            "hits_rank0": int(len(hits)),
            "requests_per_probe": "6.3 random 64-B slab reads (PMC FETCH_SIZE, profiles/r03_lookup)"}
     if dist:

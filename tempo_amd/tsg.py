@@ -19,7 +19,7 @@ import os
 import struct
 import weakref
 from dataclasses import dataclass, field
-from typing import Dict, Iterable, List, Optional, Sequence
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSG_LIB_PATH") or os.path.join(HERE, "libtsg.so")  # (override: A/B runs of two builds)
@@ -662,6 +662,21 @@ class Engine:
                     np.ctypeslib.as_array(r.record_start, (n,)).astype(np.int64),
                     np.ctypeslib.as_array(r.record_length, (n,)).astype(np.int64)]
             return np.stack(cols, axis=1), r.kernel_ns
+        finally:
+            lib().tsg_lookup_result_free(rp)
+
+    def lookup_raw(self, blocks: Sequence["V2Block"], ids) -> Tuple[int, int]:
+        """tsg_lookup_ids + tsg_lookup_result_free, nothing converted: (hits, device ns) — what a
+        Go caller pays per call (its hit columns are the result's arrays as they are)."""
+        import numpy as np
+        ids = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1, 16)
+        arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
+        o = _LookupOpts(0, 0, None, None)
+        rp = C.POINTER(_LookupResult)()
+        _check(lib().tsg_lookup_ids(self.h, arr, len(blocks), ids.ctypes.data, ids.shape[0], C.byref(o),
+                                    C.byref(rp)))
+        try:
+            return int(rp.contents.n), int(rp.contents.kernel_ns)
         finally:
             lib().tsg_lookup_result_free(rp)
 
