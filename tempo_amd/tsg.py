@@ -748,9 +748,13 @@ class Engine:
         self._raw_ids = {}
         for b in list(getattr(self, "_open", ())):
             b.close()
-        if getattr(self, "h", None):
-            lib().tsg_shutdown(self.h)
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.tsg_shutdown(self.h)
             self.h = None
+
+    # an engine dropped without close() releases its device contexts when collected (a second
+    # context on a device keeps the first one's searches off the resident kernel, pool.hip)
+    __del__ = close
 
 
 _block_closes = [0]  # BackendSearchBlock closes so far

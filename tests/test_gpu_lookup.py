@@ -202,6 +202,7 @@ def test_lookup_and_find_across_devices(tmp_path):
     finally:
         for b in blocks:
             b.close()
+        eng.close()
     assert [(g[0], g[1]) for g in fgot] == [(int(r[0]), int(r[1])) for r in got]
     exp = oracle_find(paths, ids)
     for i, b, st, obj in fgot:

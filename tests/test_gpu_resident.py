@@ -35,6 +35,14 @@ def request(q):
                            max_duration_ms=q.get("max_ms", 0), start=q.get("start", 0), end=q.get("end", 0))
 
 
+@pytest.fixture(autouse=True)
+def _alone():
+    """Engines other tests left for the garbage collector are finalised first: a resident
+    launch runs only while its context is the only one on the device."""
+    import gc
+    gc.collect()
+
+
 @pytest.fixture(scope="module")
 def paths(tmp_path_factory):
     d = tmp_path_factory.mktemp("res")
