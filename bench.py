@@ -1110,6 +1110,7 @@ def main():
     gc.collect()
     gc.disable()
     eng.kernel_times()  # (drain)
+    res0 = eng.resident_counters()
     for i in range(max(args.warmup, len(sets))):
         eng.search_raw(sets[i % len(sets)], pipe, flags=0)
     if dist:
@@ -1128,6 +1129,13 @@ def main():
     else:
         total_entries = entries
 
+    res1 = eng.resident_counters()
+    # the main line served by the resident search kernel (pool.hip, TSG_RESIDENT): each query's
+    # device time is its span on the device (the first workgroup to read it .. the last to store
+    # its count, s_memrealtime), not a dispatch's duration (there is none per query)
+    resident = res1["queries"] - res0["queries"] >= args.steps
+    kernel_name = "search_resident_kernel<3, true, true, %s>" % KERNEL.rsplit(", ", 1)[1].rstrip(">") \
+        if resident and KERNEL.startswith("search_pool_kernel") else KERNEL
     ms_per_step = elapsed / args.steps * 1e3
     value = total_entries * args.steps / elapsed
     scan_avg_ns = sum(scan_ns) / len(scan_ns) if scan_ns else 0
@@ -1159,7 +1167,10 @@ def main():
         },
         "achieved_hbm_gbps": achieved,
         "roofline": {
-            "bound": "hbm", "kernel": KERNEL, "achieved": achieved, "peak": PEAK_HBM_GBPS,
+            "bound": "hbm", "kernel": kernel_name, "achieved": achieved, "peak": PEAK_HBM_GBPS,
+            "device_time": ("per-query span in the resident kernel (first workgroup to read the query .. "
+                            "last workgroup's count stored; s_memrealtime, 100 MHz)") if resident else
+                           "dispatch timestamps of the launch (AQL profiling / hipExtLaunchKernel events)",
             "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS if achieved else None,
             "regime": regime,
             "regime_note": (f"each step searches the next of {len(sets)} disjoint resident copies of the set "
@@ -1175,6 +1186,7 @@ def main():
         "flatbuffer_gb_per_gpu": fb_bytes / 1e9,
     }
     out["latency_us"] = {"step": pct([x * 1e6 for x in step_s]), "kernel": pct([x / 1e3 for x in scan_ns])}
+    out["resident"] = {"main_line": resident, **{k: res1[k] - res0[k] for k in res1}}
 
     if args.mall_steps and len(sets) > 1:
         # the same set every step: its columns stay in the Infinity Cache (round 1's regime)

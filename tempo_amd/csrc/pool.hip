@@ -686,36 +686,18 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
   const PoolArgs &A = *reinterpret_cast<const PoolArgs *>(s_args);
   constexpr uint32_t kWords = uint32_t(sizeof(PoolArgs) / 4);
   for (uint32_t seq = R.first_seq;; seq++) {
-    // ---- wait for query `seq` (one lane polls the doorbell; the others wait at the barrier)
-    if (tid == 0) {
-      uint32_t cmd = kResQuit;
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      for (uint32_t n = 0;; n++) {
-        const uint32_t d = __hip_atomic_load(R.door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (int32_t(d - seq) >= 0) {
-          cmd = kResSearch;
-          break;
-        }
-        if ((n & 15u) == 15u && __builtin_amdgcn_s_memrealtime() - t0 > R.idle_ticks) break;  // idle: leave
-        if (R.mode & 2u) __builtin_amdgcn_s_sleep(32);
-        else __builtin_amdgcn_s_sleep(2);
-      }
-      s_ctl[0] = cmd;
-    }
-    __syncthreads();
-    if (s_ctl[0] != kResSearch) return;
-    const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
-    // ---- the slot into LDS, verified (header sequence number + checksum of the used words)
+    // ---- wait for query `seq`: wave 0 polls its mailbox slot itself (header + the argument
+    // struct, 16-byte system-coherent loads: 52 lines per poll), so the poll that sees the
+    // header's sequence number already holds the arguments; they count when the checksum of
+    // the words the query uses matches the header's (a slot read while the host's writes were
+    // still landing is read again). No post for idle_ticks: the workgroup leaves.
     const uint8_t *slot = R.slots + uint64_t(seq % kResSlots) * kResSlotBytes;
     const uint32_t *words = reinterpret_cast<const uint32_t *>(slot + kResHdrBytes);
-    // wave 0 reads the slot (header + the argument struct) with 16-byte system-coherent loads
-    // and checks it; 256 workgroups x 52 lines, where a word per thread had been 16x the
-    // requests, all to the same few lines of one memory channel
     if (wave == 0) {
       constexpr uint32_t kQuads = (kWords + 3) / 4;
-      bool vok = false;
-      for (uint32_t attempt = 0; attempt < 4096 && !vok; attempt++) {
-        if (attempt) __builtin_amdgcn_s_sleep(8);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t got = 0, bad = 0;  // got: 1 verified, 2 idle, 3 never verified
+      for (uint32_t n = 0; !got; n++) {
         u32x4 hq, v[(kQuads + 63) / 64];
         {
           const u32x4 *hp = reinterpret_cast<const u32x4 *>(slot);
@@ -728,6 +710,13 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
           asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(v[k]) : "v"(qp) : "memory");
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t hseq = uint32_t(__builtin_amdgcn_readfirstlane(hq.x));
+        if (hseq != seq) {  // not posted yet
+          if ((n & 15u) == 15u && __builtin_amdgcn_s_memrealtime() - t0 > R.idle_ticks) got = 2;
+          else if (R.mode & 2u) __builtin_amdgcn_s_sleep(32);
+          else __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
         // nsegs / nbms, from the lanes holding them
         constexpr uint32_t kNs = uint32_t(offsetof(PoolArgs, nsegs) / 4), kNb = uint32_t(offsetof(PoolArgs, nbms) / 4);
         uint32_t ns = 0, nb = 0;
@@ -762,15 +751,23 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
           }
         }
         for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-        vok = hq.x == seq && (hq.y == kResQuit || (sane && part == hq.z));
-        vok = __builtin_amdgcn_readfirstlane(uint32_t(vok)) != 0;
-        if (lane == 0) s_ctl[0] = hq.y;
+        const bool vok = hq.y == kResQuit || (sane && part == hq.z);
+        if (__builtin_amdgcn_readfirstlane(uint32_t(vok))) {
+          got = 1;
+          if (lane == 0) s_ctl[0] = hq.y;
+        } else if (++bad > 4096) {
+          got = 3;
+        } else {
+          __builtin_amdgcn_s_sleep(2);
+        }
       }
-      if (lane == 0) s_ctl[1] = vok ? 1u : 0u;
+      if (lane == 0) s_ctl[1] = got;
     }
     __syncthreads();
-    const bool ok = s_ctl[1] != 0;
-    if (!ok) {  // the slot never verified: the host fails the query (err) and posts again
+    const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
+    if (s_ctl[1] == 2) return;  // idle
+    const bool ok = s_ctl[1] == 1;
+    if (!ok) {  // the slot never verified: the host fails the query (err)
       if (tid == 0) host_store(R.err, 1u);
       return;
     }
@@ -1089,10 +1086,10 @@ void context_closed(DeviceCtx &dc) {
 }
 
 // A query (or a quit) into mailbox slot seq % kResSlots: the argument words the query uses
-// (`parts`: the same words res_word_used names, summed for the checksum), then the header,
-// then the doorbell — each step write-combined stores drained by sfence, pushed past the host
-// data path by a posted HDP flush (the kernel re-reads a slot whose header or checksum does
-// not match yet).
+// (`parts`: the same words res_word_used names, summed for the checksum), then the header
+// whose sequence number the kernel polls — write-combined stores drained by sfence, pushed past
+// the host data path by a posted HDP flush (the kernel re-reads a slot whose checksum does not
+// match yet).
 static void res_post(DeviceCtx &dc, uint32_t seq, uint32_t cmd, const PoolArgs *PA,
                      const std::vector<std::pair<uint32_t, uint32_t>> *parts) {
   uint8_t *slot = dc.res_mem + kResDoorBytes + size_t(seq % kResSlots) * kResSlotBytes;
@@ -1111,9 +1108,6 @@ static void res_post(DeviceCtx &dc, uint32_t seq, uint32_t cmd, const PoolArgs *
   __builtin_ia32_sfence();
   const ResHeader h{seq, cmd, csum, 0};
   std::memcpy(slot, &h, sizeof h);
-  __builtin_ia32_sfence();
-  aql_hdp_flush(dc.aql);
-  *reinterpret_cast<volatile uint32_t *>(dc.res_mem) = seq;
   __builtin_ia32_sfence();
   aql_hdp_flush(dc.aql);
 }
