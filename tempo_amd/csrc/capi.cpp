@@ -599,7 +599,9 @@ static void open_common(tsg_ctx *ctx, Decode &&decode, int device_hint, tsg_bloc
     delete b;
     throw;
   }
-  // the device holds the columns now; keep only what the host needs (names, header, pages)
+  // the device holds the columns now; keep only what the host needs (names, header, pages,
+  // and the record columns a dense look-back result is expanded from: ids, id_len, start,
+  // end, svc_vid, name_vid — 41 bytes per entry, search.hip "positions -> records")
   for (size_t k = 0; k < b->b.host->keys.size(); k++) {
     auto &kc = b->b.host->keys[k];
     std::vector<uint32_t>().swap(kc.col);
@@ -610,12 +612,6 @@ static void open_common(tsg_ctx *ctx, Decode &&decode, int device_hint, tsg_bloc
       kc.set_off.resize(1);
     }
   }
-  std::vector<uint8_t>().swap(b->b.host->ids);
-  std::vector<uint8_t>().swap(b->b.host->id_len);
-  std::vector<uint64_t>().swap(b->b.host->start);
-  std::vector<uint64_t>().swap(b->b.host->end);
-  std::vector<uint32_t>().swap(b->b.host->svc_vid);
-  std::vector<uint32_t>().swap(b->b.host->name_vid);
   *out = b;
 }
 

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -2575,11 +2576,17 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       std::vector<const HostBlock *> hb(size_t(max_idx) + 1, nullptr);
       for (const auto &bp : blocks) hb[bp.first] = bp.second->host.get();
       const auto *pos = reinterpret_cast<const uint64_t *>(P.out + P.hdr_bytes);
+      std::atomic<bool> bad{false};
       parallel_ranges(size_t(total), size_t(1) << 16, 16, [&](size_t lo, size_t hi) {
         for (size_t r = lo; r < hi; r++) {
           const uint64_t x = pos[r];
           const uint32_t e = uint32_t(x), bi = uint32_t(x >> 32);
-          const HostBlock &h = *hb[bi <= max_idx ? bi : 0];
+          const HostBlock *hp = bi <= max_idx ? hb[bi] : nullptr;
+          if (!hp || e >= hp->start.size() || uint64_t(e) * 16 + 16 > hp->ids.size()) {
+            bad.store(true, std::memory_order_relaxed);
+            return;
+          }
+          const HostBlock &h = *hp;
           SearchOut::Rec &o = out.recs[r];
           std::memcpy(o.id, h.ids.data() + uint64_t(e) * 16, 16);
           o.start = h.start[e];
@@ -2590,6 +2597,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
           o.name = h.name_vid.empty() ? kNone : h.name_vid[e];
         }
       });
+      if (bad.load()) fail(TSG_E_DEVICE, "look-back position outside its block's host columns");
     } else if (total) {
       // (a dense result is tens of MB of pinned memory: copied on several threads)
       parallel_ranges(size_t(total) * sizeof(MatchRec), size_t(8) << 20, 16, [&](size_t lo, size_t hi) {
