@@ -771,6 +771,9 @@ def cfg4_leg(args, eng, workdir, rank, gen_thread=None):
             ts_all.append(met.kernel_ns)
             scan_ns.append(met.scan_kernel_ns)
             dict_ns.append(met.kernel_ns - met.scan_kernel_ns)
+        if os.environ.get("TSG_PROF"):  # (host phases per query)
+            from tempo_amd import tsg as _tsg
+            _tsg.lib().tsgx_prof_flush(name.encode())
         b_dict = met.device_bytes_read - met.scan_bytes
         dmed = sorted(dict_ns)[len(dict_ns) // 2]
         smed = sorted(scan_ns)[len(scan_ns) // 2]

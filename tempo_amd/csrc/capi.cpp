@@ -315,6 +315,7 @@ struct ResultHolder {
     arena_cap = cap;
   }
   RawVec<const char *> svc_p, name_p;
+  bool ptrs_ready = false;  // svc_p / name_p filled with the records (the arena was final before them)
   std::vector<int32_t> bstatus;      // per caller block
   std::vector<std::string> berr_s;
   std::vector<const char *> berr;
@@ -468,6 +469,7 @@ struct ResultHolder {
     intern_used = 0;
     svc_p.clear();
     name_p.clear();
+    ptrs_ready = false;
     bstatus.clear();
     berr_s.clear();
     berr.clear();
@@ -476,14 +478,16 @@ struct ResultHolder {
   const char *name(size_t i) const { return arena + name_off[i]; }
   void finalize() {
     const size_t n = start.size();
-    svc_p.resize(n);
-    name_p.resize(n);
-    parallel_ranges(n, size_t(1) << 18, 16, [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; i++) {
-        svc_p[i] = svc(i);
-        name_p[i] = name(i);
-      }
-    });
+    if (!ptrs_ready || svc_p.size() != n || name_p.size() != n) {
+      svc_p.resize(n);
+      name_p.resize(n);
+      parallel_ranges(n, size_t(1) << 18, 16, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; i++) {
+          svc_p[i] = svc(i);
+          name_p[i] = name(i);
+        }
+      });
+    }
     pub.n = n;
     pub.trace_id = reinterpret_cast<const uint8_t(*)[16]>(ids.data());
     pub.trace_id_len = id_len.data();
@@ -600,8 +604,11 @@ static void open_common(tsg_ctx *ctx, Decode &&decode, int device_hint, tsg_bloc
     throw;
   }
   // the device holds the columns now; keep only what the host needs (names, header, pages,
-  // and the record columns a dense look-back result is expanded from: ids, id_len, start,
-  // end, svc_vid, name_vid — 41 bytes per entry, search.hip "positions -> records")
+  // and the per-entry result columns ids, id_len, start, end, svc_vid, name_vid — 41 bytes
+  // per entry — that a dense result's scan positions are gathered from: search.hip
+  // "positions -> records", fill_records_direct; kept as columns: at the densities where the
+  // gather matters each column is read as a near-sequential stream, which 48-byte rows per
+  // entry were not (twice the gather time in cfg4's statement+url query)
   for (size_t k = 0; k < b->b.host->keys.size(); k++) {
     auto &kc = b->b.host->keys[k];
     std::vector<uint32_t>().swap(kc.col);
@@ -1104,6 +1111,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
       break;
     }
     thread_local SearchOut bout;
+    bout.want_pos = false;  // (the batch's records are split among the callers below)
     std::exception_ptr err;
     try {
       device_search(*dc, blist, q, limit, flags, bout);
@@ -1213,15 +1221,164 @@ struct IdSet {
   }
 };
 
+// Record `x` (entry | block index << 32, a compact device output) of block h from its host
+// columns (the ones the device columns were uploaded from).
+static inline SearchOut::Rec rec_from_pos(const HostBlock &h, uint64_t x) {
+  const uint32_t e = uint32_t(x);
+  if (e >= h.start.size() || uint64_t(e) * 16 + 16 > h.ids.size())
+    fail(TSG_E_DEVICE, "device position outside its block's host columns");
+  SearchOut::Rec r;
+  std::memcpy(r.id, h.ids.data() + uint64_t(e) * 16, 16);
+  r.start = h.start[e];
+  r.end = h.end[e];
+  r.entry = e;
+  r.block_il = uint32_t(x >> 32) | (uint32_t(h.id_len[e]) << 24);
+  r.svc = h.svc_vid.empty() ? kNone : h.svc_vid[e];
+  r.name = h.name_vid.empty() ? kNone : h.name_vid[e];
+  return r;
+}
+
+// Result arrays of a large full scan whose names are few next to its records: every value of
+// the root.service.name / root.name dictionaries of the blocks with records is interned first
+// (one arena, final before any record is written), then the records are written on several
+// threads, names and their pointers by value id from the per-block tables (no hash probe per
+// name, no offset fix-up pass, no pointer pass in finalize). Records of a block with per_pos
+// are gathered from its host columns; the others copied from per_block. (Non-temporal stores
+// were tried: 12 output streams per thread overflow the write-combining buffers, 3x slower.)
+static bool fill_records_direct(ResultHolder &res, tsg_block *const *blocks,
+                              const std::vector<std::pair<const SearchOut::Rec *, size_t>> &per_block,
+                              const std::vector<const uint64_t *> &per_pos, const std::vector<size_t> &obase,
+                              size_t nout, size_t nt) {
+  const size_t nblocks = obase.size() - 1;
+  struct Names {
+    const HostBlock *h;
+    std::vector<uint64_t> off[2];
+    std::vector<uint32_t> len[2];
+  };
+  // (the worker threads below see these through references: a thread_local named inside the
+  // lambda would be each worker's own, empty instance)
+  thread_local std::vector<Names> tabs_tl;
+  thread_local std::vector<int> tab_of_tl;
+  std::vector<Names> &tabs = tabs_tl;
+  std::vector<int> &tab_of = tab_of_tl;
+  tabs.clear();
+  tab_of.assign(nblocks, -1);
+  size_t nvals = 0;
+  for (size_t i = 0; i < nblocks; i++) {
+    if (obase[i + 1] == obase[i]) continue;
+    const HostBlock *h = blocks[i]->b.host.get();
+    int t = -1;
+    for (size_t k = 0; k < tabs.size() && t < 0; k++)
+      if (tabs[k].h == h) t = int(k);
+    if (t < 0) {
+      if (tabs.size() >= 64) return false;  // (many distinct blocks: the per-thread path)
+      t = int(tabs.size());
+      tabs.push_back(Names{h, {}, {}});
+      for (int c = 0; c < 2; c++) {
+        const int key = c ? h->name_key : h->svc_key;
+        nvals += key >= 0 ? h->keys[size_t(key)].nvals() : 0;
+      }
+    }
+    tab_of[i] = t;
+  }
+  if (nvals * 4 > nout + 4096) return false;
+  for (auto &tb : tabs)
+    for (int c = 0; c < 2; c++) {
+      const int key = c ? tb.h->name_key : tb.h->svc_key;
+      const size_t nv = key >= 0 ? tb.h->keys[size_t(key)].nvals() : 0;
+      tb.off[c].resize(nv);
+      tb.len[c].resize(nv);
+      for (size_t v = 0; v < nv; v++) {
+        const std::string_view x = tb.h->dict_value(key, uint32_t(v));
+        tb.len[c][v] = uint32_t(x.size());
+        tb.off[c][v] = x.empty() ? 0 : res.intern_lookup(x.data(), x.size());
+      }
+    }
+  res.svc_p.resize(nout);
+  res.name_p.resize(nout);
+  const char *const arena = res.arena ? res.arena : "";
+  std::atomic<bool> bad{false};
+  parallel_ranges(nt, 1, int(nt), [&](size_t t0, size_t t1) {
+    for (size_t t = t0; t < t1; t++) {
+      const size_t o0 = nout * t / nt, o1 = nout * (t + 1) / nt;
+      if (o0 >= o1) continue;
+      size_t i = size_t(std::upper_bound(obase.begin(), obase.end(), o0) - obase.begin()) - 1;
+      for (size_t o = o0; o < o1; o++) {
+        while (o >= obase[i + 1]) i++;
+        const HostBlock &h = *blocks[i]->b.host;
+        const Names &tb = tabs[size_t(tab_of[i])];
+        uint8_t id[16];
+        uint64_t st, en, entry;
+        uint32_t svc, name;
+        uint8_t il;
+        if (const uint64_t *pp = per_pos[i]) {
+          const uint32_t e = uint32_t(pp[o - obase[i]]);
+          if (e >= h.start.size() || uint64_t(e) * 16 + 16 > h.ids.size()) {
+            bad.store(true, std::memory_order_relaxed);
+            return;
+          }
+          std::memcpy(id, h.ids.data() + uint64_t(e) * 16, 16);
+          st = h.start[e];
+          en = h.end[e];
+          entry = e;
+          svc = h.svc_vid.empty() ? kNone : h.svc_vid[e];
+          name = h.name_vid.empty() ? kNone : h.name_vid[e];
+          il = h.id_len[e];
+        } else {
+          const SearchOut::Rec &r = per_block[i].first[o - obase[i]];
+          std::memcpy(id, r.id, 16);
+          st = r.start;
+          en = r.end;
+          entry = r.entry;
+          svc = r.svc;
+          name = r.name;
+          il = uint8_t(r.block_il >> 24);
+        }
+        std::memcpy(&res.ids[16 * o], id, 16);
+        res.id_len[o] = il;
+        res.start[o] = st;
+        res.end[o] = en;
+        res.dur[o] = uint32_t((en - st) / 1000000ULL);  // util.go:33
+        res.block[o] = uint32_t(i);
+        res.entry[o] = entry;
+        uint64_t so = 0, no = 0;
+        uint32_t sl = 0, nl = 0;
+        if (svc != kNone && svc < tb.off[0].size()) {
+          so = tb.off[0][svc];
+          sl = tb.len[0][svc];
+        }
+        if (name != kNone && name < tb.off[1].size()) {
+          no = tb.off[1][name];
+          nl = tb.len[1][name];
+        }
+        res.svc_off[o] = so;
+        res.svc_len[o] = sl;
+        res.svc_p[o] = arena + so;
+        res.name_off[o] = no;
+        res.name_len[o] = nl;
+        res.name_p[o] = arena + no;
+      }
+    }
+  });
+  if (bad.load()) fail(TSG_E_DEVICE, "device position outside its block's host columns");
+  res.ptrs_ready = true;
+  return true;
+}
+
 // Result arrays of a large full scan on several threads: output record o of block i is
-// per_block[i].first[o - obase[i]]. Each thread interns its names into an arena of its own
-// (a name = a block dictionary value, interned by address); the arenas are then placed one
-// after another and each thread's name offsets shifted by its arena's place.
+// per_block[i].first[o - obase[i]], or position per_pos[i][o - obase[i]] gathered from block
+// i's host columns. Names few next to the records: fill_records_direct. Otherwise each thread
+// interns its names into an arena of its own (a name = a block dictionary value, interned by
+// address); the arenas are then placed one after another and each thread's name offsets
+// shifted by its arena's place.
 static void fill_records_parallel(ResultHolder &res, tsg_block *const *blocks,
                                   const std::vector<std::pair<const SearchOut::Rec *, size_t>> &per_block,
+                                  const std::vector<const uint64_t *> &per_pos,
                                   const std::vector<size_t> &obase, size_t nout) {
   const size_t hw = size_t(host_threads_now());
   const size_t nt = std::max<size_t>(1, std::min<size_t>({16, hw, nout / 32768}));
+  static const bool rows_path = std::getenv("TSG_FILL_INTERN") == nullptr;  // (A/B: the per-thread arenas)
+  if (rows_path && fill_records_direct(res, blocks, per_block, per_pos, obase, nout, nt)) return;
   struct Local {
     std::vector<ResultHolder::InternSlot> tab;
     size_t used = 0;
@@ -1256,6 +1413,7 @@ static void fill_records_parallel(ResultHolder &res, tsg_block *const *blocks,
     }
   };
   std::vector<Local> loc(nt);
+  std::atomic<bool> bad{false};
   // a name's arena offset by its dictionary value id, per thread and block, where the block's
   // names are few next to its records (an array index instead of a hash probe per name)
   auto dense_ok = [&](size_t i, int key) {
@@ -1293,24 +1451,45 @@ static void fill_records_parallel(ResultHolder &res, tsg_block *const *blocks,
           if (dsv) dsvc.assign(h.keys[size_t(h.svc_key)].nvals(), 0);
           if (dnm) dname.assign(h.keys[size_t(h.name_key)].nvals(), 0);
         }
-        const SearchOut::Rec *r = per_block[i].first + (o - obase[i]);
-        std::memcpy(&res.ids[16 * o], r->id, 16);
-        res.id_len[o] = uint8_t(r->block_il >> 24);
-        res.start[o] = r->start;
-        res.end[o] = r->end;
-        res.dur[o] = uint32_t((r->end - r->start) / 1000000ULL);  // util.go:33
+        uint32_t svc, name;
+        if (const uint64_t *pp = per_pos[i]) {
+          const uint32_t e = uint32_t(pp[o - obase[i]]);
+          if (e >= h.start.size() || uint64_t(e) * 16 + 16 > h.ids.size()) {
+            bad.store(true, std::memory_order_relaxed);
+            return;
+          }
+          std::memcpy(&res.ids[16 * o], h.ids.data() + uint64_t(e) * 16, 16);
+          res.id_len[o] = h.id_len[e];
+          const uint64_t st = h.start[e], en = h.end[e];
+          res.start[o] = st;
+          res.end[o] = en;
+          res.dur[o] = uint32_t((en - st) / 1000000ULL);  // util.go:33
+          res.entry[o] = e;
+          svc = h.svc_vid.empty() ? kNone : h.svc_vid[e];
+          name = h.name_vid.empty() ? kNone : h.name_vid[e];
+        } else {
+          const SearchOut::Rec *r = per_block[i].first + (o - obase[i]);
+          std::memcpy(&res.ids[16 * o], r->id, 16);
+          res.id_len[o] = uint8_t(r->block_il >> 24);
+          res.start[o] = r->start;
+          res.end[o] = r->end;
+          res.dur[o] = uint32_t((r->end - r->start) / 1000000ULL);  // util.go:33
+          res.entry[o] = r->entry;
+          svc = r->svc;
+          name = r->name;
+        }
         res.block[o] = uint32_t(i);
-        res.entry[o] = r->entry;
         std::string_view sv, nm;
-        if (h.svc_key >= 0 && r->svc != kNone) sv = h.dict_value(h.svc_key, r->svc);
-        if (h.name_key >= 0 && r->name != kNone) nm = h.dict_value(h.name_key, r->name);
+        if (h.svc_key >= 0 && svc != kNone) sv = h.dict_value(h.svc_key, svc);
+        if (h.name_key >= 0 && name != kNone) nm = h.dict_value(h.name_key, name);
         res.svc_len[o] = uint32_t(sv.size());
-        res.svc_off[o] = sv.empty() ? 0 : name_off(dsvc, dsv, r->svc, sv);
+        res.svc_off[o] = sv.empty() ? 0 : name_off(dsvc, dsv, svc, sv);
         res.name_len[o] = uint32_t(nm.size());
-        res.name_off[o] = nm.empty() ? 0 : name_off(dname, dnm, r->name, nm);
+        res.name_off[o] = nm.empty() ? 0 : name_off(dname, dnm, name, nm);
       }
     }
   });
+  if (bad.load()) fail(TSG_E_DEVICE, "device position outside its block's host columns");
   std::vector<uint64_t> base(nt + 1, 0);
   for (size_t t = 0; t < nt; t++) base[t + 1] = base[t] + loc[t].arena.size();
   if (base[nt] > res.arena_cap) res.arena_grow(base[nt]);
@@ -1400,6 +1579,8 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     size_t outs_used = 0;
     thread_local std::vector<std::pair<const SearchOut::Rec *, size_t>> per_block;
     per_block.assign(nblocks, {nullptr, 0});
+    thread_local std::vector<const uint64_t *> per_pos;  // block i's scan positions (compact device output)
+    per_pos.assign(nblocks, nullptr);
     size_t nrec = 0;
     // Blocks [b0, b1) (live_only: just the live ones) searched whole, each block capped at
     // dlimit records. Live blocks are never capped: a trace's result combines all its
@@ -1429,6 +1610,9 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         // before every chunk
         const size_t nl = list.size(), step = kChunk ? kChunk : nl;
         SearchOut &o = *slots[slot];
+        // a whole-block full scan (no cap, no live block) takes scan positions: the records
+        // are gathered from the host columns straight into the result arrays
+        o.want_pos = !dlimit && !live_only && !any_live && nl <= step;
         if (nl <= step) {  // one chunk: the device's list as it is (coalesced with concurrent callers)
           check_cancel();
           coalesced_search(ctx, dc, list, *q, dlimit, flags, o, approach);
@@ -1466,10 +1650,26 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         wave_k = std::max<uint64_t>(wave_k, o->kernel_ns);
         wave_s = std::max<uint64_t>(wave_s, o->scan_ns);
         m.scan_bytes += o->scan_bytes;
+        const auto &list = per_dev[d].second;
+        if (o->compact) {  // positions in list order, o->block_counts per list entry
+          uint64_t sum = 0;
+          for (uint64_t c : o->block_counts) sum += c;
+          if (o->block_counts.size() != list.size() || sum != o->pos.size())
+            fail(TSG_E_DEVICE, "device positions do not match their per-block counts");
+          size_t r = 0;
+          for (size_t x = 0; x < list.size(); x++) {
+            if (o->block_counts[x]) {
+              per_block[list[x].first] = {nullptr, size_t(o->block_counts[x])};
+              per_pos[list[x].first] = o->pos.data() + r;
+            }
+            r += size_t(o->block_counts[x]);
+          }
+          nrec += o->pos.size();
+          continue;
+        }
         const auto &recs = o->recs;
         // the device's per-block counts (its list order = record order) when they describe
         // these records; otherwise one pass over the records' block indices
-        const auto &list = per_dev[d].second;
         if (o->block_counts.size() == list.size()) {
           uint64_t sum = 0;
           for (uint64_t c : o->block_counts) sum += c;
@@ -1720,6 +1920,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
       }
       for (size_t i = 0; i < nblocks; i++) {
         per_block[i] = {acc[i].data(), acc[i].size()};
+        per_pos[i] = nullptr;
         nrec += acc[i].size();
       }
     } else {
@@ -1762,7 +1963,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         obase[i + 1] = obase[i] + k;
       }
       nout = obase[nblocks];
-      fill_records_parallel(*res, blocks, per_block, obase, nout);
+      fill_records_parallel(*res, blocks, per_block, per_pos, obase, nout);
     }
     // consume in caller block order (deterministic refinement of instance.Search)
     thread_local IdSet distinct;
@@ -1813,7 +2014,10 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         res->vid_block(h.svc_key >= 0 ? h.keys[size_t(h.svc_key)].nvals() : 0,
                        h.name_key >= 0 ? h.keys[size_t(h.name_key)].nvals() : 0);
       for (size_t ri = 0; ri < per_block[i].second; ri++) {
-        const SearchOut::Rec *r = per_block[i].first + ri;
+        SearchOut::Rec rp;
+        const SearchOut::Rec *r = &rp;
+        if (per_pos[i]) rp = rec_from_pos(h, per_pos[i][ri]);
+        else r = per_block[i].first + ri;
         res->set_rec(nout, r->id, uint8_t(r->block_il >> 24), r->start, r->end, uint32_t(i), r->entry);
         res->set_vid(0, nout, h, h.svc_key, r->svc);
         res->set_vid(1, nout++, h, h.name_key, r->name);

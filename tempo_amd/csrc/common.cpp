@@ -508,8 +508,10 @@ namespace {
 struct ProfTable {
   std::mutex mu;
   std::vector<std::pair<std::string, std::vector<double>>> rows;
-  ~ProfTable() {
+  ~ProfTable() { dump(nullptr); }
+  void dump(const char *label) {
     if (rows.empty()) return;
+    if (label) std::fprintf(stderr, "[tsg] prof [%s]\n", label);
     std::fprintf(stderr, "[tsg] prof p50 us:");
     for (auto &r : rows) {
       std::sort(r.second.begin(), r.second.end());
@@ -530,6 +532,15 @@ ProfTable &prof_table() {
   return t;
 }
 }  // namespace
+
+// Diagnostics (TSG_PROF): print the phase table so far under `label` and start a new one
+// (tools/c45_prof.py: one table per query). Not part of include/tsg.h.
+extern "C" __attribute__((visibility("default"))) void tsgx_prof_flush(const char *label) {
+  ProfTable &t = prof_table();
+  std::lock_guard<std::mutex> lk(t.mu);
+  t.dump(label ? label : "");
+  t.rows.clear();
+}
 int host_threads() {
   static const int n = [] {
     int c = int(std::max(1u, std::thread::hardware_concurrency()));

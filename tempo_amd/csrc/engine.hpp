@@ -130,6 +130,11 @@ struct SearchOut {
     uint32_t svc, name; // value ids of root.service.name / root.name (~0u = absent)
   };
   std::vector<Rec> recs;  // ordered (before the limit cut across blocks)
+  // A caller that takes scan positions (want_pos, set before device_search: a full scan whose
+  // records are gathered from the blocks' host columns straight into the result arrays) may
+  // get them instead of recs: compact set, pos[i] = entry | block index << 32, in record order
+  bool want_pos = false, compact = false;
+  RawVec<uint64_t> pos;
   std::vector<uint64_t> block_counts;
   uint64_t device_bytes = 0, kernel_ns = 0;
   uint64_t scan_ns = 0, scan_bytes = 0;

@@ -1742,6 +1742,8 @@ static void drop_before_ranges(const std::vector<std::pair<uint32_t, Block *>> &
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
                    uint32_t limit, uint32_t flags, SearchOut &out, const EntryRanges *ranges) {
   Tracer tr;
+  out.compact = false;
+  out.pos.clear();
   std::lock_guard<std::mutex> lk(dc.mu);
   HIP_OK(hipSetDevice(dc.ordinal));
   hipStream_t s = dc.stream;
@@ -2567,8 +2569,15 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
     }
     if (!climit && fast && total <= 64) dc.seg_cap = 16;  // sparse again: back to segment mode
     nrec = total;
-    out.recs.resize(total);
-    if (total && P.compact) {
+    if (total && P.compact && out.want_pos && !ranges) {
+      // the caller gathers the records from the host columns itself (into its result arrays)
+      out.pos.resize(total);
+      parallel_ranges(size_t(total) * 8, size_t(4) << 20, 16, [&](size_t lo, size_t hi) {
+        std::memcpy(reinterpret_cast<uint8_t *>(out.pos.data()) + lo, P.out + P.hdr_bytes + lo, hi - lo);
+      });
+      out.compact = true;
+    } else if (total && P.compact) {
+      out.recs.resize(total);
       // positions -> records from each block's host columns (the same values the device
       // columns hold), on several threads
       uint32_t max_idx = 0;
@@ -2600,6 +2609,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       if (bad.load()) fail(TSG_E_DEVICE, "look-back position outside its block's host columns");
     } else if (total) {
       // (a dense result is tens of MB of pinned memory: copied on several threads)
+      out.recs.resize(total);
       parallel_ranges(size_t(total) * sizeof(MatchRec), size_t(8) << 20, 16, [&](size_t lo, size_t hi) {
         std::memcpy(reinterpret_cast<uint8_t *>(out.recs.data()) + lo, P.out + P.hdr_bytes + lo, hi - lo);
       });

@@ -115,6 +115,20 @@ print('kernel_us', [round(x) for x in d['latency_us']['kernel'].values()])
     grep "resident stamps" gpurun_out/rd.err | awk '{print \$NF}' | tail -24 | tr '\n' ' '; echo
   done
 fi
+if has c45prof; then  # configs 4 and 5 with host phases; look-back records compact vs full
+  for v in ${C45_VARIANTS:-TSG_PROF=1 TSG_LB_FULL=1}; do
+    env $v TSG_PROF=1 timeout -k 10 400 python -u tools/c45_prof.py --parity 0 ${BENCH_ARGS:-} \
+      > gpurun_out/c45_$v.json 2> gpurun_out/c45_$v.err
+    rc=$?; echo "c45prof $v rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/c45_$v.err; exit $rc; }
+    python3 tools/prof_table.py gpurun_out/c45_$v.err sync post coal.call_us tsg_search.results.records tsg_search.results.finalize tsg_search.device
+    python3 -c "
+import json
+d=json.loads(open('gpurun_out/c45_$v.json').read().strip().splitlines()[-1])
+for n,q in d['cfg4']['queries'].items(): print(n, 'step', round(q['step_us']['p50']), 'dev', round(q['device_us']['p50']), 'scan', round(q['scan_us']['p50']), 'dict', round(q['dict_pass_us']['p50']), 'matches', q['matches'])
+c=d['cfg5']; print('cfg5 dev_ms', c['device_ms'], 'host_e2e p50', round(c['host_e2e']['step_ms']['p50'],2))
+"
+  done
+fi
 if has rocprof; then  # kernel trace + stats of the main line (profiles/)
   cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/rp -o rp -- python3 bench.py --steps 200 --warmup 10 $B \
