@@ -1190,7 +1190,7 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
   }
 }
 
-void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
+void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, Bytes header,
                          const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
                          HostBlock &hb, uint32_t first_page, uint32_t npages) {
   struct Share {  // (this decode counts in g_decoding; its phases take their share when auto-sized)

@@ -163,7 +163,7 @@ struct HostBlock {
   std::vector<uint64_t> trace_row0, trace_bytes0;
   uint32_t ntraces() const { return trace_row0.empty() ? 0u : uint32_t(trace_row0.size() - 1); }
   SearchMeta meta;
-  std::vector<uint8_t> header;  // raw search-header flatbuffer (kept for MatchesBlock/Tags)
+  Bytes header;  // raw search-header flatbuffer (kept for MatchesBlock/Tags)
   uint64_t min_dur = 0, max_dur = 0;
   // the header's tag table walked once at open (MatchesBlock per query without decoding
   // the flatbuffer again): keys in the header's own order, each key's values (CSR), views
@@ -207,7 +207,7 @@ void verify_header_dicts(HostBlock &hb, int nthreads);
 
 // Reads + decodes a block (meta missing -> has_meta=false, TSG_OK). nthreads <= 0: all cores.
 // first_page / npages: only those index records (npages UINT32_MAX = to the end).
-void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, std::vector<uint8_t> header,
+void decode_search_block(const uint8_t *meta, size_t meta_len, bool meta_present, Bytes header,
                          const uint8_t *index, size_t index_len, const uint8_t *data, size_t data_len, int nthreads,
                          HostBlock &out, uint32_t first_page = 0, uint32_t npages = 0xFFFFFFFFu);
 

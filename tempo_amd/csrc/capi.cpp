@@ -724,7 +724,8 @@ int tsg_block_open(tsg_ctx *ctx, const char *dir, int device_hint, tsg_block **o
   return guard([&] {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
-    std::vector<uint8_t> meta, header, index;
+    std::vector<uint8_t> meta, index;
+    Bytes header;
     MappedFile data;
     if (!read_file(join(dir, "search.meta.json"), meta)) fail(TSG_E_NOT_FOUND, "search.meta.json not found");
     if (!read_file(join(dir, "search-header"), header)) fail(TSG_E_IO, "search-header missing");
@@ -741,7 +742,8 @@ int tsg_block_open_pages(tsg_ctx *ctx, const char *dir, uint32_t first_page, uin
                          tsg_block **out) {
   if (!ctx || !dir || !out || !npages) return TSG_E_INVALID;
   return guard([&] {
-    std::vector<uint8_t> meta, header, index;
+    std::vector<uint8_t> meta, index;
+    Bytes header;
     MappedFile data;
     if (!read_file(join(dir, "search.meta.json"), meta)) fail(TSG_E_NOT_FOUND, "search.meta.json not found");
     if (!read_file(join(dir, "search-header"), header)) fail(TSG_E_IO, "search-header missing");
@@ -759,7 +761,7 @@ int tsg_block_open_mem(tsg_ctx *ctx, const uint8_t *meta, size_t ml, const uint8
   if (!ctx || !out) return TSG_E_INVALID;
   return guard([&] {
     if (!meta) fail(TSG_E_NOT_FOUND, "search.meta.json not provided");
-    std::vector<uint8_t> hv(header, header + hl);
+    Bytes hv(header, header + hl);
     open_common(ctx, [&](HostBlock &h) { decode_search_block(meta, ml, true, std::move(hv), index, il, data, dl, 0, h); },
                 device_hint, out);
   });
@@ -1238,34 +1240,27 @@ static inline SearchOut::Rec rec_from_pos(const HostBlock &h, uint64_t x) {
   return r;
 }
 
-// Result arrays of a large full scan whose names are few next to its records: every value of
-// the root.service.name / root.name dictionaries of the blocks with records is interned first
-// (one arena, final before any record is written), then the records are written on several
-// threads, names and their pointers by value id from the per-block tables (no hash probe per
-// name, no offset fix-up pass, no pointer pass in finalize). Records of a block with per_pos
-// are gathered from its host columns; the others copied from per_block. (Non-temporal stores
-// were tried: 12 output streams per thread overflow the write-combining buffers, 3x slower.)
-static bool fill_records_direct(ResultHolder &res, tsg_block *const *blocks,
-                              const std::vector<std::pair<const SearchOut::Rec *, size_t>> &per_block,
-                              const std::vector<const uint64_t *> &per_pos, const std::vector<size_t> &obase,
-                              size_t nout, size_t nt) {
-  const size_t nblocks = obase.size() - 1;
+// Per distinct HostBlock: its root.service.name / root.name values' arena offsets and lengths
+// by value id (every value interned up front: the arena is final before any record is written).
+struct FillNames {
   struct Names {
     const HostBlock *h;
     std::vector<uint64_t> off[2];
     std::vector<uint32_t> len[2];
   };
-  // (the worker threads below see these through references: a thread_local named inside the
-  // lambda would be each worker's own, empty instance)
-  thread_local std::vector<Names> tabs_tl;
-  thread_local std::vector<int> tab_of_tl;
-  std::vector<Names> &tabs = tabs_tl;
-  std::vector<int> &tab_of = tab_of_tl;
+  std::vector<Names> tabs;
+  std::vector<int> tab_of;  // per caller block: its table (-1: none)
+};
+// Tables for the caller blocks i with use[i]; false when the names are many next to `nrec`
+// records (or the blocks many distinct ones): the per-thread arena path is used then.
+static bool fill_names(ResultHolder &res, tsg_block *const *blocks, size_t nblocks, size_t nrec,
+                       const std::vector<uint8_t> &use, FillNames &fn) {
+  auto &tabs = fn.tabs;
   tabs.clear();
-  tab_of.assign(nblocks, -1);
+  fn.tab_of.assign(nblocks, -1);
   size_t nvals = 0;
   for (size_t i = 0; i < nblocks; i++) {
-    if (obase[i + 1] == obase[i]) continue;
+    if (!use[i]) continue;
     const HostBlock *h = blocks[i]->b.host.get();
     int t = -1;
     for (size_t k = 0; k < tabs.size() && t < 0; k++)
@@ -1273,15 +1268,16 @@ static bool fill_records_direct(ResultHolder &res, tsg_block *const *blocks,
     if (t < 0) {
       if (tabs.size() >= 64) return false;  // (many distinct blocks: the per-thread path)
       t = int(tabs.size());
-      tabs.push_back(Names{h, {}, {}});
+      tabs.push_back(FillNames::Names{h, {}, {}});
       for (int c = 0; c < 2; c++) {
         const int key = c ? h->name_key : h->svc_key;
         nvals += key >= 0 ? h->keys[size_t(key)].nvals() : 0;
       }
     }
-    tab_of[i] = t;
+    fn.tab_of[i] = t;
   }
-  if (nvals * 4 > nout + 4096) return false;
+  if (nvals * 4 > nrec + 4096) return false;
+  const auto t_names = std::chrono::steady_clock::now();
   for (auto &tb : tabs)
     for (int c = 0; c < 2; c++) {
       const int key = c ? tb.h->name_key : tb.h->svc_key;
@@ -1294,74 +1290,195 @@ static bool fill_records_direct(ResultHolder &res, tsg_block *const *blocks,
         tb.off[c][v] = x.empty() ? 0 : res.intern_lookup(x.data(), x.size());
       }
     }
-  res.svc_p.resize(nout);
-  res.name_p.resize(nout);
+  if (prof_on())
+    prof_add("fill.names", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_names).count());
+  return true;
+}
+
+// Output records [o_begin, o_end) (record o of block i: obase[i] <= o < obase[i + 1]) on nt
+// threads, names from fn (fill_names done; the arena no longer grows); the result arrays
+// hold o_end records.
+static void fill_direct_range(ResultHolder &res, tsg_block *const *blocks,
+                              const std::vector<std::pair<const SearchOut::Rec *, size_t>> &per_block,
+                              const std::vector<const uint64_t *> &per_pos, const std::vector<size_t> &obase,
+                              size_t o_begin, size_t o_end, size_t nt, const FillNames &fn) {
+  using Names = FillNames::Names;
+  const auto &tabs = fn.tabs;
+  const auto &tab_of = fn.tab_of;
+  const size_t nout = o_end - o_begin;
+  if (!nout) return;
+  res.svc_p.resize(o_end);
+  res.name_p.resize(o_end);
   const char *const arena = res.arena ? res.arena : "";
   std::atomic<bool> bad{false};
+  const bool prof = prof_on();
+  static const bool passes = [] {  // TSG_FILL_PASSES=0: positions gathered record by record (A/B)
+    const char *e = std::getenv("TSG_FILL_PASSES");
+    return !e || std::atoi(e) != 0;
+  }();
+  static const bool nts = [] {  // TSG_FILL_NT=0: the passes with plain stores (A/B)
+    const char *e = std::getenv("TSG_FILL_NT");
+    return !e || std::atoi(e) != 0;
+  }();
+  const auto t_par = std::chrono::steady_clock::now();
+  // a name column's (offset, length, pointer) for value id v of table c
+  auto put_name = [&](const Names &tb, int c, uint32_t v, size_t o) {
+    uint64_t off = 0;
+    uint32_t len = 0;
+    if (v != kNone && v < tb.off[c].size()) {
+      off = tb.off[c][v];
+      len = tb.len[c][v];
+    }
+    (c ? res.name_off : res.svc_off)[o] = off;
+    (c ? res.name_len : res.svc_len)[o] = len;
+    (c ? res.name_p : res.svc_p)[o] = arena + off;
+  };
+  // Each thread takes a contiguous output range and walks it block run by block run. A run of
+  // scan positions is filled in column passes (each pass: the positions, one or two source
+  // columns, its own outputs — a record-at-a-time gather kept 6 input and 12 output streams
+  // open per thread: 4.2 vs 2.9 ms for config 4's 1.85 M records, tools/probe/fill_probe.cpp);
+  // a run of device records is copied record by record (one input stream).
   parallel_ranges(nt, 1, int(nt), [&](size_t t0, size_t t1) {
     for (size_t t = t0; t < t1; t++) {
-      const size_t o0 = nout * t / nt, o1 = nout * (t + 1) / nt;
+      const size_t o0 = o_begin + nout * t / nt, o1 = o_begin + nout * (t + 1) / nt;
       if (o0 >= o1) continue;
       size_t i = size_t(std::upper_bound(obase.begin(), obase.end(), o0) - obase.begin()) - 1;
-      for (size_t o = o0; o < o1; o++) {
-        while (o >= obase[i + 1]) i++;
+      for (size_t r0 = o0; r0 < o1; i++) {
+        if (r0 >= obase[i + 1]) continue;
+        const size_t r1 = std::min(o1, obase[i + 1]);
         const HostBlock &h = *blocks[i]->b.host;
         const Names &tb = tabs[size_t(tab_of[i])];
-        uint8_t id[16];
-        uint64_t st, en, entry;
-        uint32_t svc, name;
-        uint8_t il;
-        if (const uint64_t *pp = per_pos[i]) {
-          const uint32_t e = uint32_t(pp[o - obase[i]]);
-          if (e >= h.start.size() || uint64_t(e) * 16 + 16 > h.ids.size()) {
-            bad.store(true, std::memory_order_relaxed);
-            return;
+        const uint64_t *pp = per_pos[i] ? per_pos[i] - obase[i] : nullptr;
+        if (pp && !passes) {
+          for (size_t o = r0; o < r1; o++) {
+            const uint32_t e = uint32_t(pp[o]);
+            if (e >= h.start.size() || uint64_t(e) * 16 + 16 > h.ids.size()) {
+              bad.store(true, std::memory_order_relaxed);
+              return;
+            }
+            std::memcpy(&res.ids[16 * o], h.ids.data() + uint64_t(e) * 16, 16);
+            const uint64_t st = h.start[e], en = h.end[e];
+            res.start[o] = st;
+            res.end[o] = en;
+            res.dur[o] = uint32_t((en - st) / 1000000ULL);  // util.go:33
+            res.id_len[o] = h.id_len[e];
+            res.entry[o] = e;
+            res.block[o] = uint32_t(i);
+            put_name(tb, 0, h.svc_vid.empty() ? kNone : h.svc_vid[e], o);
+            put_name(tb, 1, h.name_vid.empty() ? kNone : h.name_vid[e], o);
           }
-          std::memcpy(id, h.ids.data() + uint64_t(e) * 16, 16);
-          st = h.start[e];
-          en = h.end[e];
-          entry = e;
-          svc = h.svc_vid.empty() ? kNone : h.svc_vid[e];
-          name = h.name_vid.empty() ? kNone : h.name_vid[e];
-          il = h.id_len[e];
+        } else if (pp && nts) {  // the same passes with non-temporal stores (no read for ownership)
+          typedef long long v2di __attribute__((vector_size(16)));
+          for (size_t o = r0; o < r1; o++) {
+            const uint32_t e = uint32_t(pp[o]);
+            if (e >= h.start.size() || uint64_t(e) * 16 + 16 > h.ids.size()) {
+              bad.store(true, std::memory_order_relaxed);
+              return;
+            }
+            v2di v;
+            std::memcpy(&v, h.ids.data() + uint64_t(e) * 16, 16);
+            __builtin_nontemporal_store(v, reinterpret_cast<v2di *>(&res.ids[16 * o]));
+          }
+          for (size_t o = r0; o < r1; o++) {
+            const uint32_t e = uint32_t(pp[o]);
+            const uint64_t st = h.start[e], en = h.end[e];
+            __builtin_nontemporal_store(st, &res.start[o]);
+            __builtin_nontemporal_store(en, &res.end[o]);
+            __builtin_nontemporal_store(uint32_t((en - st) / 1000000ULL), &res.dur[o]);  // util.go:33
+          }
+          for (size_t o = r0; o < r1; o++) {
+            const uint32_t e = uint32_t(pp[o]);
+            res.id_len[o] = h.id_len[e];
+            __builtin_nontemporal_store(uint64_t(e), &res.entry[o]);
+            __builtin_nontemporal_store(uint32_t(i), &res.block[o]);
+          }
+          for (int c = 0; c < 2; c++) {
+            const std::vector<uint32_t> &vid = c ? h.name_vid : h.svc_vid;
+            uint64_t *offp = c ? res.name_off.data() : res.svc_off.data();
+            uint32_t *lenp = c ? res.name_len.data() : res.svc_len.data();
+            const char **ptrp = c ? res.name_p.data() : res.svc_p.data();
+            for (size_t o = r0; o < r1; o++) {
+              const uint32_t v = vid.empty() ? kNone : vid[uint32_t(pp[o])];
+              uint64_t off = 0;
+              uint32_t len = 0;
+              if (v != kNone && v < tb.off[c].size()) {
+                off = tb.off[c][v];
+                len = tb.len[c][v];
+              }
+              __builtin_nontemporal_store(off, &offp[o]);
+              __builtin_nontemporal_store(len, &lenp[o]);
+              __builtin_nontemporal_store(arena + off, &ptrp[o]);
+            }
+          }
+          __builtin_ia32_sfence();
+        } else if (pp) {
+          for (size_t o = r0; o < r1; o++) {
+            const uint32_t e = uint32_t(pp[o]);
+            if (e >= h.start.size() || uint64_t(e) * 16 + 16 > h.ids.size()) {
+              bad.store(true, std::memory_order_relaxed);
+              return;
+            }
+            std::memcpy(&res.ids[16 * o], h.ids.data() + uint64_t(e) * 16, 16);
+          }
+          for (size_t o = r0; o < r1; o++) {
+            const uint32_t e = uint32_t(pp[o]);
+            const uint64_t st = h.start[e], en = h.end[e];
+            res.start[o] = st;
+            res.end[o] = en;
+            res.dur[o] = uint32_t((en - st) / 1000000ULL);  // util.go:33
+          }
+          for (size_t o = r0; o < r1; o++) {
+            const uint32_t e = uint32_t(pp[o]);
+            res.id_len[o] = h.id_len[e];
+            res.entry[o] = e;
+            res.block[o] = uint32_t(i);
+          }
+          for (size_t o = r0; o < r1; o++) put_name(tb, 0, h.svc_vid.empty() ? kNone : h.svc_vid[uint32_t(pp[o])], o);
+          for (size_t o = r0; o < r1; o++) put_name(tb, 1, h.name_vid.empty() ? kNone : h.name_vid[uint32_t(pp[o])], o);
         } else {
-          const SearchOut::Rec &r = per_block[i].first[o - obase[i]];
-          std::memcpy(id, r.id, 16);
-          st = r.start;
-          en = r.end;
-          entry = r.entry;
-          svc = r.svc;
-          name = r.name;
-          il = uint8_t(r.block_il >> 24);
+          const SearchOut::Rec *rb = per_block[i].first - obase[i];
+          for (size_t o = r0; o < r1; o++) {
+            const SearchOut::Rec &r = rb[o];
+            std::memcpy(&res.ids[16 * o], r.id, 16);
+            res.id_len[o] = uint8_t(r.block_il >> 24);
+            res.start[o] = r.start;
+            res.end[o] = r.end;
+            res.dur[o] = uint32_t((r.end - r.start) / 1000000ULL);  // util.go:33
+            res.block[o] = uint32_t(i);
+            res.entry[o] = r.entry;
+            put_name(tb, 0, r.svc, o);
+            put_name(tb, 1, r.name, o);
+          }
         }
-        std::memcpy(&res.ids[16 * o], id, 16);
-        res.id_len[o] = il;
-        res.start[o] = st;
-        res.end[o] = en;
-        res.dur[o] = uint32_t((en - st) / 1000000ULL);  // util.go:33
-        res.block[o] = uint32_t(i);
-        res.entry[o] = entry;
-        uint64_t so = 0, no = 0;
-        uint32_t sl = 0, nl = 0;
-        if (svc != kNone && svc < tb.off[0].size()) {
-          so = tb.off[0][svc];
-          sl = tb.len[0][svc];
-        }
-        if (name != kNone && name < tb.off[1].size()) {
-          no = tb.off[1][name];
-          nl = tb.len[1][name];
-        }
-        res.svc_off[o] = so;
-        res.svc_len[o] = sl;
-        res.svc_p[o] = arena + so;
-        res.name_off[o] = no;
-        res.name_len[o] = nl;
-        res.name_p[o] = arena + no;
+        r0 = r1;
       }
     }
   });
+  if (prof)
+    prof_add("fill.records", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_par).count());
   if (bad.load()) fail(TSG_E_DEVICE, "device position outside its block's host columns");
   res.ptrs_ready = true;
+}
+
+// Result arrays of a large full scan whose names are few next to its records: every value of
+// the root.service.name / root.name dictionaries of the blocks with records is interned first
+// (one arena, final before any record is written), then the records are written on several
+// threads, names and their pointers by value id from the per-block tables (no hash probe per
+// name, no offset fix-up pass, no pointer pass in finalize). Records of a block with per_pos
+// are gathered from its host columns; the others copied from per_block. (Non-temporal stores
+// were tried: 12 output streams per thread overflow the write-combining buffers, 3x slower.)
+static bool fill_records_direct(ResultHolder &res, tsg_block *const *blocks,
+                                const std::vector<std::pair<const SearchOut::Rec *, size_t>> &per_block,
+                                const std::vector<const uint64_t *> &per_pos, const std::vector<size_t> &obase,
+                                size_t nout, size_t nt) {
+  thread_local FillNames fn_tl;
+  FillNames &fn = fn_tl;
+  const size_t nblocks = obase.size() - 1;
+  thread_local std::vector<uint8_t> use;
+  use.assign(nblocks, 0);
+  for (size_t i = 0; i < nblocks; i++) use[i] = obase[i + 1] > obase[i];
+  if (!fill_names(res, blocks, nblocks, nout, use, fn)) return false;
+  fill_direct_range(res, blocks, per_block, per_pos, obase, 0, nout, nt, fn);
   return true;
 }
 
@@ -1775,6 +1892,207 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     auto seed = [&](IdSet &ids) {
       for (uint64_t i = 0; i < nseen; i++) ids.insert(seen[i]);
     };
+    thread_local std::vector<size_t> obase;
+    // caller blocks [i0, i1): MatchesBlock's deferred terms resolved, metrics, and the output
+    // offsets of their records (obase[i + 1]); returns the records they hold
+    auto account = [&](size_t i0, size_t i1) {
+      for (size_t i = i0; i < i1; i++) {
+        const HostBlock &h = *blocks[i]->b.host;
+        size_t k = 0;
+        if (state[i] != 0) {
+          if (!h.part_tail) m.bytes_inspected += h.header.size();
+          if (state[i] == 2 && defer[i])  // (as in the consumer below)
+            state[i] = anym[i] >= 0 ? ((defer[i] & ~uint32_t(anym[i])) ? 1 : 2)
+                                    : (pipeline_matches_block_indexed(*q, h) ? 2 : 1);
+          if (state[i] == 1) {
+            if (!h.part_tail) m.blocks_skipped++;
+          } else {
+            if (!h.part_tail) m.blocks_inspected++;
+            k = per_block[i].second;
+            m.traces_inspected += uint32_t(h.n);
+            m.bytes_inspected += h.fb_bytes;
+            if (h.stop_status) {
+              res->bstatus[i] = h.stop_status;
+              res->berr_s[i] = h.stop_msg;
+            }
+          }
+        }
+        obase[i + 1] = obase[i] + k;
+      }
+      return obase[i1] - obase[i0];
+    };
+    // ---- pipelined full scan. A full scan whose device work is long (the dictionary pass over
+    // large dictionaries: config 4's statement queries, ~2.5 ms) and whose results are dense
+    // runs as consecutive launches of TSG_PIPE_BLOCKS blocks on a producer thread while this
+    // thread assembles the result arrays of the launches already done: the host's gather of
+    // 1.85 M records (2.4-3.5 ms on 16 CPUs) overlaps the device instead of following it.
+    // Same records in the same order and the same metrics as one launch (caller block order,
+    // each block's records in scan order).
+    bool pipelined = false;
+    std::vector<std::vector<std::pair<uint32_t, Block *>>> pchunks;
+    DeviceCtx *pdev = nullptr;
+    auto pipelined_plan = [&]() -> bool {
+      // (read per query: a test turns it on for small blocks; two getenv calls per full scan)
+      const char *e1 = std::getenv("TSG_PIPE_DICT_MB"), *e2 = std::getenv("TSG_PIPE_BLOCKS");
+      const uint64_t kPipeDict = uint64_t(e1 ? std::atoll(e1) : 2048) << 20;  // wide-term dictionary bytes, all blocks
+      const size_t kPipeBlocks = size_t(std::max(1, e2 ? std::atoi(e2) : 2));
+      if (!kPipeDict || nseen) return false;
+      std::vector<std::pair<uint32_t, Block *>> list;
+      uint64_t dict = 0;
+      for (size_t i = 0; i < nblocks; i++) {
+        if (state[i] != 2 || !blocks[i]->b.dc) continue;
+        Block &b = blocks[i]->b;
+        if (pdev && b.dc != pdev) return false;  // (one device: the plain fan-out otherwise)
+        pdev = b.dc;
+        list.push_back({uint32_t(i), &b});
+        for (uint32_t t = 0; t < q->nterms; t++) {
+          const auto it = b.host->key_index.find(
+              std::string(reinterpret_cast<const char *>(q->keys[t]), q->key_lens[t]));
+          if (it == b.host->key_index.end() || size_t(it->second) >= b.dev.keys.size()) continue;
+          const DevKey &k = b.dev.keys[size_t(it->second)];
+          if (k.width != 1) dict += k.dict_nbytes;
+        }
+      }
+      if (list.size() < 2 || list.size() > kChunk || dict < kPipeDict) return false;
+      for (size_t c0 = 0; c0 < list.size(); c0 += kPipeBlocks)
+        pchunks.emplace_back(list.begin() + c0, list.begin() + std::min(list.size(), c0 + kPipeBlocks));
+      approach.leave();
+      return true;
+    };
+    auto pipelined_run = [&]() -> size_t {
+      const size_t nc = pchunks.size();
+      while (outs.size() < outs_used + nc) outs.emplace_back();
+      std::vector<SearchOut *> po(nc);
+      for (size_t c = 0; c < nc; c++) {
+        po[c] = &outs[outs_used++];
+        po[c]->want_pos = true;
+      }
+      std::atomic<uint32_t> done{0};
+      std::atomic<bool> failed{false}, pstop{false};
+      tsg::EpochPark pk;
+      std::exception_ptr perr;
+      // the producer: one device_search per chunk, back to back
+      std::thread producer([&] {
+        try {
+          for (size_t c = 0; c < nc && !pstop.load(std::memory_order_acquire); c++) {
+            if (ctx->is_cancelled(qid)) fail(TSG_E_CANCELLED, "search cancelled (tsg_cancel)");
+            device_search(*pdev, pchunks[c], *q, 0, flags, *po[c]);
+            done.store(uint32_t(c + 1), std::memory_order_release);
+            pk.notify();
+          }
+        } catch (...) {
+          perr = std::current_exception();
+          failed.store(true, std::memory_order_release);
+          pk.notify();
+        }
+      });
+      struct Join {  // (an early exit here stops the producer after its current launch)
+        std::thread &t;
+        std::atomic<bool> &stop;
+        ~Join() {
+          stop.store(true, std::memory_order_release);
+          if (t.joinable()) t.join();
+        }
+      } join{producer, pstop};
+      // every name of the inspected blocks interned first (the arena is final before any
+      // record is written); the arrays reserved for every entry (virtual: touched as filled)
+      thread_local FillNames fn_tl;
+      FillNames &fn = fn_tl;
+      thread_local std::vector<uint8_t> use;
+      use.assign(nblocks, 0);
+      uint64_t ent = 0;
+      for (const auto &ch : pchunks)
+        for (const auto &bp : ch) {
+          use[bp.first] = 1;
+          ent += bp.second->host->n;
+        }
+      const bool direct = fill_names(*res, blocks, nblocks, size_t(ent / 8), use, fn);
+      res->reserve(size_t(ent));
+      res->svc_p.reserve(size_t(ent));
+      res->name_p.reserve(size_t(ent));
+      obase.assign(nblocks + 1, 0);
+      size_t next_i = 0, filled = 0;
+      const size_t hw = size_t(host_threads_now());
+      for (size_t c = 0; c < nc; c++) {
+        // wait for chunk c (the producer runs on another CPU: a short spin, then park)
+        auto ready = [&] { return done.load(std::memory_order_acquire) > c || failed.load(std::memory_order_acquire); };
+        while (!ready()) {
+          const uint32_t e = pk.read();
+          if (!tsg::spin_for(20'000, ready)) pk.wait(e, 100'000'000);
+        }
+        if (done.load(std::memory_order_acquire) <= c) {  // the producer failed
+          producer.join();
+          std::rethrow_exception(perr);
+        }
+        SearchOut &o = *po[c];
+        note_any(o);
+        m.device_bytes_read += o.device_bytes;
+        m.reruns += o.reruns;
+        m.kernel_ns += o.kernel_ns;
+        m.scan_kernel_ns += o.scan_ns;
+        m.scan_bytes += o.scan_bytes;
+        const auto &list = pchunks[c];
+        // this launch's records per block (its list order = record order)
+        uint64_t sum = 0;
+        for (uint64_t x : o.block_counts) sum += x;
+        const size_t nr = o.compact ? o.pos.size() : o.recs.size();
+        if (o.block_counts.size() == list.size() && sum == nr) {
+          size_t r = 0;
+          for (size_t x = 0; x < list.size(); x++) {
+            const size_t cnt = size_t(o.block_counts[x]);
+            per_block[list[x].first] = {o.compact ? nullptr : o.recs.data() + r, cnt};
+            per_pos[list[x].first] = o.compact && cnt ? o.pos.data() + r : nullptr;
+            r += cnt;
+          }
+        } else if (!o.compact) {  // (records grouped by block already: one pass over their block indices)
+          for (size_t r = 0; r < nr;) {
+            const uint32_t bi = o.recs[r].block_il & 0xffffffu;
+            size_t e = r;
+            while (e < nr && (o.recs[e].block_il & 0xffffffu) == bi) e++;
+            if (bi < nblocks) per_block[bi] = {&o.recs[r], e - r};
+            r = e;
+          }
+        } else {
+          fail(TSG_E_DEVICE, "device positions do not match their per-block counts");
+        }
+        nrec += nr;
+        // the caller blocks up to this launch's last one (the ones between were not searched)
+        const size_t i1 = c + 1 < nc ? size_t(list.back().first) + 1 : nblocks;
+        account(next_i, i1);
+        next_i = i1;
+        const size_t o_end = obase[i1];
+        for (size_t j = i1 + 1; j <= nblocks; j++) obase[j] = o_end;  // (monotone: the fill's binary search)
+        if (o_end > filled) {
+          res->resize(o_end);
+          // (one CPU of the job's share stays with the producer, which polls the device)
+          const size_t nt = std::max<size_t>(1, std::min<size_t>({15, hw > 1 ? hw - 1 : 1, (o_end - filled) / 16384}));
+          if (direct) {
+            fill_direct_range(*res, blocks, per_block, per_pos, obase, filled, o_end, nt, fn);
+          } else {  // (many names: record by record, interned through the result's table)
+            for (size_t i = 0; i < i1; i++) {
+              if (obase[i + 1] <= std::max(obase[i], filled)) continue;
+              const HostBlock &h = *blocks[i]->b.host;
+              res->vid_block(h.svc_key >= 0 ? h.keys[size_t(h.svc_key)].nvals() : 0,
+                             h.name_key >= 0 ? h.keys[size_t(h.name_key)].nvals() : 0);
+              for (size_t oo = std::max(obase[i], filled); oo < obase[i + 1]; oo++) {
+                const size_t ri = oo - obase[i];
+                const SearchOut::Rec rr = per_pos[i] ? rec_from_pos(h, per_pos[i][ri]) : per_block[i].first[ri];
+                res->set_rec(oo, rr.id, uint8_t(rr.block_il >> 24), rr.start, rr.end, uint32_t(i), rr.entry);
+                res->set_vid(0, oo, h, h.svc_key, rr.svc);
+                res->set_vid(1, oo, h, h.name_key, rr.name);
+              }
+            }
+            res->ptrs_ready = false;
+          }
+          filled = o_end;
+        }
+        check_cancel();
+      }
+      if (!direct) res->ptrs_ready = false;
+      if (prof_on()) prof_add("pipe.chunks", double(nc));
+      return filled;
+    };
+
     if (limit && (any_live || inspect_entries > kWave0 || nseen)) {
       thread_local std::vector<std::vector<SearchOut::Rec>> acc;  // per block: its records so far
       if (acc.size() < nblocks) acc.resize(nblocks);
@@ -1923,45 +2241,28 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         per_pos[i] = nullptr;
         nrec += acc[i].size();
       }
+    } else if (!limit && !any_live && pipelined_plan()) {
+      pipelined = true;
     } else {
       search_range(0, nblocks, false, limit);  // (limit > 0 here: no live block)
       check_cancel();
     }
     const clk::time_point t_dev = trace ? clk::now() : clk::time_point();
-    res->reserve(nrec);
-    res->resize(nrec);
+    if (!pipelined) {
+      res->reserve(nrec);
+      res->resize(nrec);
+    }
     const clk::time_point t_res = trace ? clk::now() : clk::time_point();
     size_t nout = 0;
     // A large full scan (no limit, no live block: every record of every inspected block is
     // kept, nothing to consume) is assembled on several threads; otherwise one thread
     // consumes in caller block order (deterministic refinement of instance.Search)
-    const bool par = !limit && !any_live && nrec >= (size_t(1) << 16);
-    if (par) {
-      thread_local std::vector<size_t> obase;
+    const bool par = !pipelined && !limit && !any_live && nrec >= (size_t(1) << 16);
+    if (pipelined) {
+      nout = pipelined_run();
+    } else if (par) {
       obase.assign(nblocks + 1, 0);
-      for (size_t i = 0; i < nblocks; i++) {
-        const HostBlock &h = *blocks[i]->b.host;
-        size_t k = 0;
-        if (state[i] != 0) {
-          if (!h.part_tail) m.bytes_inspected += h.header.size();
-          if (state[i] == 2 && defer[i])  // (as below)
-            state[i] = anym[i] >= 0 ? ((defer[i] & ~uint32_t(anym[i])) ? 1 : 2)
-                                    : (pipeline_matches_block_indexed(*q, h) ? 2 : 1);
-          if (state[i] == 1) {
-            if (!h.part_tail) m.blocks_skipped++;
-          } else {
-            if (!h.part_tail) m.blocks_inspected++;
-            k = per_block[i].second;
-            m.traces_inspected += uint32_t(h.n);
-            m.bytes_inspected += h.fb_bytes;
-            if (h.stop_status) {
-              res->bstatus[i] = h.stop_status;
-              res->berr_s[i] = h.stop_msg;
-            }
-          }
-        }
-        obase[i + 1] = obase[i] + k;
-      }
+      account(0, nblocks);
       nout = obase[nblocks];
       fill_records_parallel(*res, blocks, per_block, per_pos, obase, nout);
     }
@@ -1970,7 +2271,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     distinct.clear();
     seed(distinct);
     bool stopped = limit && distinct.size() >= limit;
-    for (size_t i = 0; i < nblocks && !stopped && !par; i++) {
+    for (size_t i = 0; i < nblocks && !stopped && !par && !pipelined; i++) {
       const HostBlock &h = *blocks[i]->b.host;
       if (state[i] == 0) continue;  // meta missing: no-op (backend_search_block.go:191-203)
       if (h.live) {  // searchLiveTraces (instance_search.go:99-128)

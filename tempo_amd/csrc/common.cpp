@@ -2,13 +2,17 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdio>
 #include <exception>
 #include <mutex>
 #include <thread>
 #include <sched.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
+#include <unistd.h>
+#include <fcntl.h>
 #include <sys/types.h>
 #include <strings.h>
 
@@ -475,6 +479,37 @@ bool read_file(const std::string &path, std::vector<uint8_t> &out) {
   std::fclose(f);
   return true;
 }
+bool read_file(const std::string &path, Bytes &out) {
+  const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    if (errno == ENOENT) return false;
+    fail(TSG_E_IO, "open " + path + ": " + std::strerror(errno));
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    ::close(fd);
+    fail(TSG_E_IO, "stat " + path + ": " + std::strerror(errno));
+  }
+  const size_t n = st.st_size > 0 ? size_t(st.st_size) : 0;
+  out.resize(n);
+  advise_huge(out.data(), n);
+  // chunks of 32 MiB on up to 8 threads (one pread loop each)
+  std::atomic<bool> bad{false};
+  parallel_ranges(n, size_t(32) << 20, 8, [&](size_t lo, size_t hi) {
+    while (lo < hi) {
+      const ssize_t r = ::pread(fd, out.data() + lo, hi - lo, off_t(lo));
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0) {
+        bad.store(true);
+        return;
+      }
+      lo += size_t(r);
+    }
+  });
+  ::close(fd);
+  if (bad.load()) fail(TSG_E_IO, "short read " + path);
+  return true;
+}
 void write_file(const std::string &path, const uint8_t *p, size_t n) {
   FILE *f = std::fopen(path.c_str(), "wb");
   if (!f) fail(TSG_E_IO, "create " + path + ": " + std::strerror(errno));
@@ -557,6 +592,14 @@ int host_threads() {
     return c;
   }();
   return n;
+}
+
+void advise_huge(void *p, size_t bytes) {
+  constexpr uintptr_t kHuge = uintptr_t(2) << 20;
+  if (!p || bytes < 2 * kHuge) return;
+  const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
+  const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
+  if (b > a) madvise(reinterpret_cast<void *>(a), b - a, MADV_HUGEPAGE);
 }
 
 int host_threads_now() {

@@ -7,11 +7,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <new>
 #include <stdexcept>
 #include <type_traits>
 #include <string>
 #include <string_view>
+#include <utility>
 #include <vector>
 
 #include "../../include/tsg.h"
@@ -94,6 +96,28 @@ std::string go_to_lower(std::string_view s);
 
 // ---- files --------------------------------------------------------------------
 bool read_file(const std::string &path, std::vector<uint8_t> &out);  // false if missing
+
+// A byte vector whose resize leaves new bytes uninitialised (a file's bytes are written
+// once by the read: no zero fill of a 1 GB header first).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U> &) noexcept {}
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    if constexpr (sizeof...(A) == 0) ::new (static_cast<void *>(p)) U;
+    else ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+  }
+};
+using Bytes = std::vector<uint8_t, NoInitAlloc<uint8_t>>;
+// Large files are read with parallel preads (several threads copying from the page cache)
+// into huge-page advised memory; false if missing.
+bool read_file(const std::string &path, Bytes &out);
 void write_file(const std::string &path, const uint8_t *p, size_t n);
 void make_dirs(const std::string &path);
 
@@ -109,6 +133,11 @@ void parallel_ranges(size_t n, size_t grain, int max_threads, const std::functio
 
 // A growable array of trivially copyable T without value-initialisation on resize (a result
 // of millions of records is written once; zero-filling it first would be a second pass).
+// Large host arrays written once per query (result columns, record vectors): ask for
+// transparent huge pages on the 2 MiB-aligned interior before its first touch (THP is
+// "madvise" on the GPU hosts; 4 KiB pages cost the dense result fill a TLB miss per few records).
+void advise_huge(void *p, size_t bytes);
+
 template <class T>
 struct RawVec {
   static_assert(std::is_trivially_copyable<T>::value, "RawVec holds plain data");
@@ -124,6 +153,7 @@ struct RawVec {
     if (!q) throw std::bad_alloc();
     p = q;
     cap = c;
+    advise_huge(p, c * sizeof(T));
   }
   void resize(size_t m) {
     if (m > cap) reserve(std::max(m, cap * 2));

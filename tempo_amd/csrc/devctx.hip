@@ -159,6 +159,19 @@ static T *dev_upload(DevBlock &b, const T *src, size_t count, hipStream_t s, siz
   return static_cast<T *>(p);
 }
 
+// count zeroed elements (whole 16-byte words), filled by the caller's copies
+template <typename T>
+static T *dev_zeroed(DevBlock &b, size_t count, hipStream_t s) {
+  void *p = nullptr;
+  const size_t bytes = std::max<size_t>((count * sizeof(T) + 15) / 16 * 16, 16);
+  HIP_OK(hipMalloc(&p, bytes));
+  b.allocs.push_back(p);
+  b.alloc_bytes.push_back(bytes);
+  b.bytes += bytes;
+  HIP_OK(hipMemsetAsync(p, 0, bytes, s));
+  return static_cast<T *>(p);
+}
+
 static void upload_desc(DevBlock &d, hipStream_t s);
 
 // One interned copy per distinct narrow dictionary (content-equal dictionaries of
@@ -241,27 +254,17 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
   }
   // per key: its 16-bit column (width 2) and one contiguous blob in the order a workgroup
   // stages it into LDS: [value offsets nvals+1 | value bytes (whole words) | set offsets
-  // nsets+1 | set values] (set arrays only for non-identity keys)
+  // nsets+1 | set values] (set arrays only for non-identity keys). The blob is assembled on
+  // the device from the key's own arrays (config 4's statement dictionary is ~1 GB: building
+  // it on the host first was a zero fill and a copy of that much)
   const size_t nk = h.keys.size();
   std::vector<std::vector<uint16_t>> col16(nk);
-  std::vector<std::vector<uint32_t>> blobs(nk);
   for (size_t k = 0; k < nk; k++) {
     const KeyColumn &kc = h.keys[k];
     if (kc.width() == 2) {
       col16[k].resize(n);
       for (size_t i = 0; i < n; i++) col16[k][i] = kc.col[i] == kNone ? 0xffff : uint16_t(kc.col[i]);
     }
-    const size_t bw = (kc.dict_bytes.size() + 3) / 4;
-    const size_t nso = kc.identity ? 0 : kc.set_off.size(), nsv = kc.identity ? 0 : kc.set_vals.size();
-    std::vector<uint32_t> &blob = blobs[k];
-    blob.assign(kc.dict_off.size() + bw + nso + nsv, 0);
-    uint32_t *bp = blob.data();
-    std::memcpy(bp, kc.dict_off.data(), kc.dict_off.size() * 4);
-    bp += kc.dict_off.size();
-    if (!kc.dict_bytes.empty()) std::memcpy(bp, kc.dict_bytes.data(), kc.dict_bytes.size());
-    bp += bw;
-    if (nso) std::memcpy(bp, kc.set_off.data(), nso * 4);
-    if (nsv) std::memcpy(bp + nso, kc.set_vals.data(), nsv * 4);
   }
 
   std::lock_guard<std::mutex> lk(dc.mu);
@@ -295,7 +298,14 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     }
     const size_t bw = (kc.dict_bytes.size() + 3) / 4;
     const size_t nso = kc.identity ? 0 : kc.set_off.size(), nsv = kc.identity ? 0 : kc.set_vals.size();
-    uint32_t *dblob = dev_upload(d, blobs[kk].data(), blobs[kk].size(), s);
+    uint32_t *dblob = dev_zeroed<uint32_t>(d, kc.dict_off.size() + bw + nso + nsv, s);
+    auto put = [&](uint32_t *dst, const void *src, size_t bytes) {
+      if (bytes) HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    };
+    put(dblob, kc.dict_off.data(), kc.dict_off.size() * 4);
+    put(dblob + kc.dict_off.size(), kc.dict_bytes.data(), kc.dict_bytes.size());
+    if (nso) put(dblob + kc.dict_off.size() + bw, kc.set_off.data(), nso * 4);
+    if (nsv) put(dblob + kc.dict_off.size() + bw + nso, kc.set_vals.data(), nsv * 4);
     k.dict_off = dblob;
     k.dict_bytes = reinterpret_cast<uint8_t *>(dblob + kc.dict_off.size());
     k.dict_nbytes = kc.dict_bytes.size();

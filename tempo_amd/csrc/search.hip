@@ -1739,6 +1739,14 @@ static void drop_before_ranges(const std::vector<std::pair<uint32_t, Block *>> &
   out.recs.resize(k);
 }
 
+// out.recs sized to n records (not initialised); new storage of a large record array is
+// advised huge pages before the copy touches it
+static void grow_recs(SearchOut &out, size_t n) {
+  const size_t cap0 = out.recs.capacity();
+  out.recs.resize(n);
+  if (out.recs.capacity() != cap0) advise_huge(out.recs.data(), out.recs.capacity() * sizeof(SearchOut::Rec));
+}
+
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
                    uint32_t limit, uint32_t flags, SearchOut &out, const EntryRanges *ranges) {
   Tracer tr;
@@ -2534,7 +2542,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       const uint8_t *p0 = rec + uint64_t(w) * P.seg_cap * sizeof(MatchRec);
       for (uint64_t o = 0; o < c * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
     }
-    out.recs.resize(upper);
+    grow_recs(out, upper);
     for (size_t i = 0; i < segs.size(); i++) {
       uint64_t kept = 0;
       const bool stole = fast && segs[i].tail;  // tail records sit in their claimers' segments
@@ -2577,7 +2585,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       });
       out.compact = true;
     } else if (total && P.compact) {
-      out.recs.resize(total);
+      grow_recs(out, total);
       // positions -> records from each block's host columns (the same values the device
       // columns hold), on several threads
       uint32_t max_idx = 0;
@@ -2609,7 +2617,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       if (bad.load()) fail(TSG_E_DEVICE, "look-back position outside its block's host columns");
     } else if (total) {
       // (a dense result is tens of MB of pinned memory: copied on several threads)
-      out.recs.resize(total);
+      grow_recs(out, total);
       parallel_ranges(size_t(total) * sizeof(MatchRec), size_t(8) << 20, 16, [&](size_t lo, size_t hi) {
         std::memcpy(reinterpret_cast<uint8_t *>(out.recs.data()) + lo, P.out + P.hdr_bytes + lo, hi - lo);
       });

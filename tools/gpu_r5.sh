@@ -116,11 +116,11 @@ print('kernel_us', [round(x) for x in d['latency_us']['kernel'].values()])
   done
 fi
 if has c45prof; then  # configs 4 and 5 with host phases; look-back records compact vs full
-  for v in ${C45_VARIANTS:-TSG_PROF=1 TSG_LB_FULL=1}; do
+  for v in ${C45_VARIANTS:-TSG_PROF=1 TSG_LB_FULL=1}; do  # (variants: env assignments, run in order)
     env $v TSG_PROF=1 timeout -k 10 400 python -u tools/c45_prof.py --parity 0 ${BENCH_ARGS:-} \
       > gpurun_out/c45_$v.json 2> gpurun_out/c45_$v.err
     rc=$?; echo "c45prof $v rc=$rc"; [ $rc -eq 0 ] || { tail -3 gpurun_out/c45_$v.err; exit $rc; }
-    python3 tools/prof_table.py gpurun_out/c45_$v.err sync post coal.call_us tsg_search.results.records tsg_search.results.finalize tsg_search.device
+    python3 tools/prof_table.py gpurun_out/c45_$v.err sync post tsg_search.results.records fill.names fill.records tsg_search.results.finalize tsg_search.device
     python3 -c "
 import json
 d=json.loads(open('gpurun_out/c45_$v.json').read().strip().splitlines()[-1])
