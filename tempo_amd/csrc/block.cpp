@@ -386,7 +386,7 @@ static void canonicalize_narrow_keys(HostBlock &hb) {
     });
     std::vector<uint32_t> vnew(nv);
     for (uint32_t i = 0; i < nv; i++) vnew[vord[i]] = i;
-    std::vector<uint8_t> bytes;
+    Bytes bytes;
     std::vector<uint32_t> off(1, 0);
     for (uint32_t i = 0; i < nv; i++) {
       std::string_view v = hb.dict_value(int(k), vord[i]);
@@ -965,7 +965,8 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
         nb += shards[k][x].bytes.size();
       }
       if (nb > 0xF0000000u) fail(TSG_E_UNSUPPORTED, "dictionary too large");
-      kc.dict_bytes.resize(nb);
+      kc.dict_bytes.resize(nb);  // (not zero-filled: the shards' copies below write every byte)
+      advise_huge(kc.dict_bytes.data(), nb);
       kc.dict_off.resize(nv + 1);
       kc.dict_off[nv] = uint32_t(nb);
       if (nb > kDeferMinBytes) kc.dict_vh.resize(nv);  // (kept for verify_header_dicts)

@@ -113,7 +113,7 @@ static constexpr uint32_t kNone = 0xFFFFFFFFu;
 struct KeyColumn {
   std::string name;
   // value dictionary (distinct values of this key in the block, first-seen order)
-  std::vector<uint8_t> dict_bytes;
+  Bytes dict_bytes;  // (no zero fill on resize: config 4 holds ~1 GB here)
   std::vector<uint32_t> dict_off;  // nvals + 1
   // value sets (the distinct value vectors of this key's KeyValues tables)
   std::vector<uint32_t> set_off;   // nsets + 1

@@ -613,7 +613,7 @@ static void open_common(tsg_ctx *ctx, Decode &&decode, int device_hint, tsg_bloc
     auto &kc = b->b.host->keys[k];
     std::vector<uint32_t>().swap(kc.col);
     if (int(k) != b->b.host->svc_key && int(k) != b->b.host->name_key) {
-      std::vector<uint8_t>().swap(kc.dict_bytes);
+      Bytes().swap(kc.dict_bytes);
       std::vector<uint32_t>().swap(kc.dict_off);
       std::vector<uint32_t>().swap(kc.set_vals);
       kc.set_off.resize(1);

@@ -240,7 +240,7 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
     if (d.narrow_slot[k] < 0) continue;
     const KeyColumn &kc = h.keys[k];
     NarrowDict nd;
-    nd.bytes = kc.dict_bytes;
+    nd.bytes.assign(kc.dict_bytes.begin(), kc.dict_bytes.end());
     nd.off = kc.dict_off;
     nd.set_off = kc.set_off;
     nd.set_vals = kc.set_vals;
