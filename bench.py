@@ -87,6 +87,37 @@ def pmc_traffic(workload_key):
     return None, None
 
 
+def summary(out):
+    """The headline figures of every leg in a few keys, emitted as the line's last key (the
+    driver keeps the tail of long output: these stay visible there)."""
+    def g(*path):
+        d = out
+        for k in path:
+            if not isinstance(d, dict) or k not in d:
+                return None
+            d = d[k]
+        return round(d, 3) if isinstance(d, float) else d
+    s = {"value_G": round(out["value"] / 1e9, 2) if out.get("value") else None,
+         "frac": g("roofline", "frac"), "kernel_avg_us": g("roofline", "avg_launch_us"),
+         "step_us_mean": g("latency_us", "step", "mean"), "step_us_p50": g("latency_us", "step", "p50"),
+         "mall_frac": g("mall", "frac"), "limit20_step_us_mean": g("limit20", "step_us", "mean"),
+         "limit20_kernel_us_p50": g("limit20", "kernel_us", "p50"),
+         "shim_query_us_p50": g("shim", "query_us", "p50"), "shim_limit20_us_p50": g("shim", "limit20", "query_us", "p50"),
+         "shim_limit20_us_p99": g("shim", "limit20", "query_us", "p99"),
+         "cfg3_kernel_us_p50": g("cfg3", "full_scan", "kernel_us", "p50"), "cfg3_frac": g("cfg3", "full_scan", "frac"),
+         "cfg3_first20_us_p50": g("cfg3", "limit20", "time_to_first_20_us", "p50"),
+         "cfg5_device_ms": g("cfg5", "device_ms"), "cfg5_host_e2e_ms_p50": g("cfg5", "host_e2e", "step_ms", "p50"),
+         "load_gb_per_s": g("load_gb_per_s"), "cfg4_load_gb_per_s": g("cfg4", "load_gb_per_s"),
+         "cfg1_kernel_us_p50": g("cfg1", "gpu", "kernel_us", "p50")}
+    for name, q in (g("cfg4", "queries") or {}).items():
+        s["cfg4_" + name] = {"step_over_device": round(q["step_over_device"], 3) if q.get("step_over_device") else None,
+                             "scan_us_p50": round(q["scan_us"]["p50"], 1), "dict_frac": round(q["dict_frac"], 3)
+                             if q.get("dict_frac") else None}
+    s["parity"] = {k: g(k, "parity", "ok") for k in ("cfg1", "cfg3", "cfg4", "cfg5") if k in out}
+    s["cpu_baseline_entries_per_s"] = g("cpu_baseline", "value")
+    return s
+
+
 def pct(xs):
     """p10 / median / p90 of a sample (SURVEY.md §8(d) timing rules)."""
     if not xs:
@@ -1283,6 +1314,7 @@ def main():
             out["cfg1"]["parity"] = {"ok": False, "error": repr(e)}
 
     if rank == 0:
+        out["summary"] = summary(out)  # (last: a reader that keeps only the line's tail still sees it)
         print(json.dumps(out), flush=True)
     if not args.keep and not args.workdir:
         shutil.rmtree(workdir, ignore_errors=True)
