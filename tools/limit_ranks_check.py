@@ -3,7 +3,8 @@
 `--nproc-per-node N` of these under torch.distributed.run). Every rank opens its range of
 the blocks on the device and runs tempo_amd.shard.distributed_search_limit over a gloo group
 with Engine.search_wire / Engine.cancel; rank 0 also runs ONE tsg_search(limit=L) over all
-blocks and writes whether the two agree record for record and in the metrics."""
+blocks and writes whether the two agree record for record and in the metrics, and the
+records and metrics themselves (the test checks them against the oracle's consumer)."""
 import argparse
 import json
 import os
@@ -42,9 +43,12 @@ def main():
             met = lambda r: (r.metrics.inspected_traces, r.metrics.inspected_bytes,  # noqa: E731
                              r.metrics.inspected_blocks, r.metrics.skipped_blocks)
             ok = recs(res) == recs(one) and met(res) == met(one)
+            # the records themselves (the test compares them with the oracle's consumer)
+            out = [[r[0].hex(), r[1], r[2], r[3].decode("utf-8", "replace") if isinstance(r[3], bytes) else r[3],
+                    r[4].decode("utf-8", "replace") if isinstance(r[4], bytes) else r[4]] for r in recs(res)]
             with open(a.out, "w") as f:
                 json.dump({"ok": bool(ok), "n": len(res), "n_one": len(one), "metrics": met(res),
-                           "metrics_one": met(one)}, f)
+                           "metrics_one": met(one), "records": out}, f)
             for b in allb:
                 b.close()
         for b in mine:
