@@ -652,6 +652,7 @@ struct ResidentArgs {
   uint32_t idle_ticks;   // s_memrealtime ticks without a post before a workgroup leaves
   uint32_t nthreads, ngroups;
   uint32_t mode, pad;  // TSG_RES_MODE (experiments): bit 0 = units interleaved over the waves (no LDS claims),
+                       // bit 2 = poll the slot header alone, load the arguments once it shows the query,
                        // bit 1 = longer sleeps between doorbell polls
 };
 static_assert(sizeof(PoolArgs) <= kResSlotBytes - kResHdrBytes && sizeof(PoolArgs) % 4 == 0, "mailbox slot");
@@ -697,11 +698,20 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
       constexpr uint32_t kQuads = (kWords + 3) / 4;
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t got = 0, bad = 0;  // got: 1 verified, 2 idle, 3 never verified
+      const bool hdr_first = (R.mode & 4u) != 0;  // (experiment: poll the header line alone, then load the slot)
       for (uint32_t n = 0; !got; n++) {
         u32x4 hq, v[(kQuads + 63) / 64];
         {
           const u32x4 *hp = reinterpret_cast<const u32x4 *>(slot);
           asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(hq) : "v"(hp) : "memory");
+        }
+        if (hdr_first) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (uint32_t(__builtin_amdgcn_readfirstlane(hq.x)) != seq) {
+            if ((n & 15u) == 15u && __builtin_amdgcn_s_memrealtime() - t0 > R.idle_ticks) got = 2;
+            else __builtin_amdgcn_s_sleep(2);
+            continue;
+          }
         }
 #pragma unroll
         for (uint32_t k = 0; k < (kQuads + 63) / 64; k++) {

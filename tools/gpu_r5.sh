@@ -129,9 +129,33 @@ c=d['cfg5']; print('cfg5 dev_ms', c['device_ms'], 'host_e2e p50', round(c['host_
 "
   done
 fi
+if has varab; then  # env variants of the main line, interleaved twice (VARS: space-separated env assignments; "-" = none)
+  mkdir -p /tmp/abw
+  for k in 1 2; do
+    for v in ${VARS:--}; do
+      e="$v"; [ "$v" = "-" ] && e="TSG_NONE=1"
+      env $e TSG_PROF=1 timeout -k 10 300 python -u bench.py --workdir /tmp/abw --steps 400 --warmup 20 $B --limit-steps 0 --cfg1 0 \
+        > gpurun_out/var.json 2> gpurun_out/var.err
+      rc=$?; [ $rc -eq 0 ] || { echo "varab $v rc=$rc"; tail -3 gpurun_out/var.err; exit $rc; }
+      summ gpurun_out/var.json "$v"
+      grep "prof p50" gpurun_out/var.err | tail -1 | tr ' ' '\n' | grep -E "^(res.first_count|sync|tsg_search.device|tsg_search.results)=" | tr '\n' ' '; echo
+    done
+  done
+fi
+if has pmc; then  # FETCH_SIZE / WRITE_SIZE passes of the main line as plain launches (per-dispatch counters)
+  export TMPDIR=/tmp
+  for c in FETCH_SIZE WRITE_SIZE; do
+    TSG_RESIDENT=0 timeout -k 10 600 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv -- \
+      python3 bench.py --steps 10 --warmup 2 $B --limit-steps 0 --cfg1 0 > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err
+    rc=$?; echo "pmc $c rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+  done
+  python3 tools/pmc_summary.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE --out gpurun_out/pmc_traffic.json \
+    --workload "${PMC_WORKLOAD:-blocks=10,entries=1000000,sets=4,layout=ds}" --source "${PMC_SOURCE:-gpu_r5.sh pmc}" | tee gpurun_out/pmc_summary.txt
+fi
 if has rocprof; then  # kernel trace + stats of the main line (profiles/)
   cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/rp -o rp -- python3 bench.py --steps 200 --warmup 10 $B \
+  TSG_RESIDENT=${ROCPROF_RESIDENT:-0} timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp -o rp -- python3 bench.py --steps 200 --warmup 10 $B --cfg1 0 \
     > gpurun_out/rp.json 2> gpurun_out/rp.err
   rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/rp.err; exit $rc; }
   find gpurun_out/rp -name "*kernel_stats.csv" | head -3
