@@ -153,6 +153,16 @@ if has pmc; then  # FETCH_SIZE / WRITE_SIZE passes of the main line as plain lau
   python3 tools/pmc_summary.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE --out gpurun_out/pmc_traffic.json \
     --workload "${PMC_WORKLOAD:-blocks=10,entries=1000000,sets=4,layout=ds}" --source "${PMC_SOURCE:-gpu_r5.sh pmc}" | tee gpurun_out/pmc_summary.txt
 fi
+if has smoke; then
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+  rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has stamps; then  # resident spans per workgroup on the main line (TSG_RES_DUMP), host phases
+  TSG_RES_DUMP=1 TSG_PROF=1 timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 $B --cfg1 0 --limit-steps 0 \
+    > gpurun_out/stamps.json 2> gpurun_out/stamps.err
+  rc=$?; echo "stamps rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  grep "resident stamps" gpurun_out/stamps.err | tail -3
+fi
 if has rocprof; then  # kernel trace + stats of the main line (profiles/)
   cd /tmp && export TMPDIR=/tmp && cd "$OLDPWD"
   TSG_RESIDENT=${ROCPROF_RESIDENT:-0} timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp -o rp -- python3 bench.py --steps 200 --warmup 10 $B --cfg1 0 \
