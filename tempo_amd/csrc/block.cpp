@@ -944,7 +944,23 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
       ValueShard &S = shards[k][x];
       const auto &R = refs[k][x];
       S.reserve(R.size(), size_t(kin[k].bytes / P + kin[k].bytes / (4 * P)));
-      for (const uint64_t r : R) {
+      // the references' value bytes sit in page buffers long evicted since the parse: they are
+      // prefetched 16 references ahead (and their slots 8 ahead), so the misses of consecutive
+      // references overlap instead of one DRAM round trip each
+      const size_t nr = R.size();
+      const size_t mask = S.slot.size() - 1;
+      for (size_t q = 0; q < nr; q++) {
+        if (q + 16 < nr) {
+          const uint64_t ra = R[q + 16];
+          const LPage &pa = pages[size_t(ra >> 32)];
+          __builtin_prefetch(pa.vals[uint32_t(ra)].data());
+        }
+        if (q + 8 < nr && S.slot.size() - 1 == mask) {
+          const uint64_t rb = R[q + 8];
+          const LPage &pb = pages[size_t(rb >> 32)];
+          __builtin_prefetch(&S.slot[ValueShard::probe0(pb.vhash[uint32_t(rb)], mask)]);
+        }
+        const uint64_t r = R[q];
         LPage &pp = pages[size_t(r >> 32)];
         const uint32_t v = uint32_t(r);
         pp.vloc[v] = S.get(pp.vals[v], pp.vhash[v]);
@@ -1062,7 +1078,14 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
       S.slot.assign(c, 0);
       const size_t mask = c - 1;
       std::vector<uint32_t> tmp;
-      for (const uint64_t r : R) {
+      for (size_t q = 0; q < R.size(); q++) {
+        if (q + 8 < R.size()) {  // (the table's value range and set hash, 8 references ahead)
+          const LPage &pa = pages[size_t(R[q + 8] >> 32)];
+          const uint32_t ta = uint32_t(R[q + 8]);
+          __builtin_prefetch(&pa.kv_v0[ta]);
+          __builtin_prefetch(&pa.kv_shash[ta]);
+        }
+        const uint64_t r = R[q];
         LPage &pp = pages[size_t(r >> 32)];
         const uint32_t t = uint32_t(r);
         tmp.clear();

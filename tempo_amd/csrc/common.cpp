@@ -174,7 +174,13 @@ static void snappy_block_decode(const uint8_t *src, size_t sl, uint8_t *dst, siz
       }
       len = size_t(x) + 1;
       if (len > dl - d || len > sl - s) fail(TSG_E_CORRUPT, "snappy: literal out of range");
-      std::memcpy(dst + d, src + s, len);
+      if (len <= 16 && sl - s >= 16 && dl - d >= 16) {
+        // a short literal (most are): one fixed 16-byte copy, no call; the bytes past `len`
+        // land inside the block and later ops overwrite them
+        std::memcpy(dst + d, src + s, 16);
+      } else {
+        std::memcpy(dst + d, src + s, len);
+      }
       d += len;
       s += len;
       continue;
