@@ -500,36 +500,30 @@ struct LPage {
 };
 
 // open addressing: table position -> page-local table index (reset per page)
+// A page's tables by their position in the page's flatbuffer: tables start on 4-byte words,
+// so position / 4 indexes a direct table (one 8-byte slot per word of the page: {page
+// generation, index + 1}; a new page only bumps the generation). A hash of the position had
+// scattered the lookups of neighbouring tables over the whole table (a cache miss per tag
+// reference); word order keeps an entry's tables, written next to each other, on few lines.
 struct PosMap {
-  std::vector<uint64_t> slot;  // pos << 32 | (index + 1); 0 = empty
-  size_t used = 0;
-  void reset(size_t expect) {
-    size_t cap = 1024;
-    while (cap < 2 * expect) cap <<= 1;
-    if (slot.size() != cap) slot.assign(cap, 0);
-    else std::fill(slot.begin(), slot.end(), 0);
-    used = 0;
+  std::vector<uint64_t> slot;
+  uint32_t gen = 0;
+  void reset(size_t fb_bytes) {
+    const size_t need = fb_bytes / 4 + 1;
+    if (slot.size() < need) slot.assign(need, 0), gen = 0;
+    if (++gen == 0) {  // (wrapped: clear once)
+      std::fill(slot.begin(), slot.end(), 0);
+      gen = 1;
+    }
   }
-  // index of `pos`, or inserts `fresh` and returns kNone
+  // index of the table at `pos`, or records `fresh` for it and returns kNone
   uint32_t find_or_put(uint32_t pos, uint32_t fresh) {
-    if (2 * (used + 1) > slot.size()) {
-      std::vector<uint64_t> old;
-      old.swap(slot);
-      slot.assign(old.size() * 2, 0);
-      used = 0;
-      for (uint64_t x : old)
-        if (x) find_or_put(uint32_t(x >> 32), uint32_t(x) - 1);
-    }
-    const size_t mask = slot.size() - 1;
-    for (size_t h = (uint64_t(pos) * 0x9E3779B97F4A7C15ull) >> 20;; h++) {
-      uint64_t &x = slot[h & mask];
-      if (!x) {
-        x = (uint64_t(pos) << 32) | (uint64_t(fresh) + 1);
-        used++;
-        return kNone;
-      }
-      if (uint32_t(x >> 32) == pos) return uint32_t(x) - 1;
-    }
+    const size_t i = pos >> 2;
+    if (i >= slot.size()) fail(TSG_E_CORRUPT, "flatbuffer table position out of range");
+    uint64_t &x = slot[i];
+    if (uint32_t(x >> 32) == gen) return uint32_t(x) - 1;
+    x = (uint64_t(gen) << 32) | (uint64_t(fresh) + 1);
+    return kNone;
   }
 };
 
@@ -570,7 +564,7 @@ void parse_lpage(const uint8_t *data, size_t dlen, int enc, const IndexRecord &r
     pp.vals.reserve(hint.vals + hint.vals / 4);
     pp.vhash.reserve(hint.vals + hint.vals / 4);
   }
-  pm.reset(hint.tables ? hint.tables + hint.tables / 4 : size_t(pp.n) * 8);
+  pm.reset(fbn);
   std::vector<std::pair<uint32_t, uint32_t>> kpos_ids;  // key string position -> key id
   FbTable e{fb, fbn, 0}, kv{fb, fbn, 0};
   for (uint32_t j = 0; j < pp.n; j++) {
@@ -944,12 +938,23 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
       ValueShard &S = shards[k][x];
       const auto &R = refs[k][x];
       S.reserve(R.size(), size_t(kin[k].bytes / P + kin[k].bytes / (4 * P)));
-      // the references' value bytes sit in page buffers long evicted since the parse: they are
-      // prefetched 16 references ahead (and their slots 8 ahead), so the misses of consecutive
-      // references overlap instead of one DRAM round trip each
+      // A reference's page-level entries (its string view, hash and id slot: arrays shared by
+      // every key of the page, so consecutive references of one key are a line or more apart)
+      // and the value bytes they point to were evicted long ago: the entries are prefetched 32
+      // references ahead, the bytes 16 ahead (their view is in cache by then), the slots 8
+      // ahead, so the misses of consecutive references overlap (one dependent DRAM round trip
+      // per entry each before: ~150-250 ns per reference)
       const size_t nr = R.size();
       const size_t mask = S.slot.size() - 1;
       for (size_t q = 0; q < nr; q++) {
+        if (q + 32 < nr) {
+          const uint64_t rc = R[q + 32];
+          const LPage &pc = pages[size_t(rc >> 32)];
+          const uint32_t vc = uint32_t(rc);
+          __builtin_prefetch(pc.vals.data() + vc);
+          __builtin_prefetch(pc.vhash.data() + vc);
+          __builtin_prefetch(pc.vloc.data() + vc, 1);
+        }
         if (q + 16 < nr) {
           const uint64_t ra = R[q + 16];
           const LPage &pa = pages[size_t(ra >> 32)];
@@ -1079,11 +1084,18 @@ static void load_pages(HostBlock &hb, const std::vector<IndexRecord> &recs, cons
       const size_t mask = c - 1;
       std::vector<uint32_t> tmp;
       for (size_t q = 0; q < R.size(); q++) {
-        if (q + 8 < R.size()) {  // (the table's value range and set hash, 8 references ahead)
-          const LPage &pa = pages[size_t(R[q + 8] >> 32)];
-          const uint32_t ta = uint32_t(R[q + 8]);
+        if (q + 32 < R.size()) {  // (the table's value range and set hash, 32 references ahead)
+          const LPage &pa = pages[size_t(R[q + 32] >> 32)];
+          const uint32_t ta = uint32_t(R[q + 32]);
           __builtin_prefetch(&pa.kv_v0[ta]);
           __builtin_prefetch(&pa.kv_shash[ta]);
+          __builtin_prefetch(&pa.kv_sid[ta], 1);
+        }
+        if (q + 16 < R.size()) {  // (its values' hashes and ids, 16 ahead: the range is in cache)
+          const LPage &pb = pages[size_t(R[q + 16] >> 32)];
+          const uint32_t v0 = pb.kv_v0[uint32_t(R[q + 16])];
+          __builtin_prefetch(pb.vhash.data() + v0);
+          __builtin_prefetch(pb.vloc.data() + v0);
         }
         const uint64_t r = R[q];
         LPage &pp = pages[size_t(r >> 32)];
