@@ -510,7 +510,10 @@ struct PosMap {
   uint32_t gen = 0;
   void reset(size_t fb_bytes) {
     const size_t need = fb_bytes / 4 + 1;
-    if (slot.size() < need) slot.assign(need, 0), gen = 0;
+    if (slot.size() < need) {
+      slot.assign(need, 0);
+      gen = 0;
+    }
     if (++gen == 0) {  // (wrapped: clear once)
       std::fill(slot.begin(), slot.end(), 0);
       gen = 1;
