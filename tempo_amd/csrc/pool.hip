@@ -1250,7 +1250,11 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
           for (uint64_t o = 0; o < uint64_t(std::min(c, seg)) * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
         }
       }
-      if (lo == W) return;
+      if (lo == W) {
+        if (prof)
+          prof_add("res.last_count", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        return;
+      }
       if ((it & 0xfffffu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
         fail(TSG_E_DEVICE, "resident search: no answer in 5 s");
       if ((it & 255u) == 0 && aql_done(dc.aql)) {
@@ -1319,8 +1323,8 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
       }
       std::sort(sn.begin(), sn.end());
       std::sort(en.begin(), en.end());
-      std::fprintf(stderr, "[tsg] resident stamps us: seen p50 %.2f p90 %.2f max %.2f | end p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
-                   sn[W / 2], sn[W * 9 / 10], sn[W - 1], en[W / 10], en[W / 2], en[W * 9 / 10], en[W - 1]);
+      std::fprintf(stderr, "[tsg] resident stamps us: seen p50 %.2f p90 %.2f max %.2f | end min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
+                   sn[W / 2], sn[W * 9 / 10], sn[W - 1], en[0], en[W / 10], en[W / 2], en[W * 9 / 10], en[W - 1]);
     }
     if (dc.tring_res.size() < dc.tring_used) dc.tring_res.resize(dc.tring_used);
     dc.tring_aql[dc.tring_used - 1] = -3;
