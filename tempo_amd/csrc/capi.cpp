@@ -1954,8 +1954,17 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         }
       }
       if (list.size() < 2 || list.size() > kChunk || dict < kPipeDict) return false;
-      for (size_t c0 = 0; c0 < list.size(); c0 += kPipeBlocks)
-        pchunks.emplace_back(list.begin() + c0, list.begin() + std::min(list.size(), c0 + kPipeBlocks));
+      // one block in the last launch (its result fill is the part nothing overlaps) and in the
+      // first (the host starts filling sooner); kPipeBlocks per launch between them
+      const size_t nl = list.size();
+      const size_t edge = kPipeBlocks > 1 && nl >= kPipeBlocks + 2 ? 1 : kPipeBlocks;
+      size_t c0 = 0;
+      while (c0 < nl) {
+        const size_t left = nl - c0;
+        const size_t take = c0 == 0 ? edge : left <= edge ? left : std::min(kPipeBlocks, left - edge);
+        pchunks.emplace_back(list.begin() + c0, list.begin() + c0 + take);
+        c0 += take;
+      }
       approach.leave();
       return true;
     };
