@@ -74,6 +74,7 @@ struct PoolArgs {
   // the first sr waves one unit more (sq, sr = units / NW, units % NW: no division on the device)
   uint32_t sq, sr;
   uint32_t nbms;                     // bitmaps in `bms` (the resident kernel's slot checksum)
+  uint32_t cstride;                  // resident kernel: workgroup w's count at counts[w * cstride] (0 = 1)
   uint32_t wq, wr;                   // resident kernel: workgroup w scans units [w*wq + min(w, wr), +wq + (w < wr))
   uint32_t pad0;
   unsigned long long *qstamps;       // resident kernel, timed queries: per workgroup {seen, end} (100 MHz)
@@ -979,7 +980,9 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     __syncthreads();
     // the count last (more matches than the LDS buffer holds: the host reruns the query on the
     // segment / look-back path)
-    if (tid == 0) host_store(uniform_ptr(A.counts) + w, over ? max(total, rec_cap + 1) : total);
+    if (tid == 0)
+      host_store(uniform_ptr(A.counts) + uint64_t(w) * max(1u, uint32_t(__builtin_amdgcn_readfirstlane(A.cstride))),
+                 over ? max(total, rec_cap + 1) : total);
     __syncthreads();  // (the LDS tables are reused by the next query)
   }
 }
@@ -1200,7 +1203,9 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
   parts.push_back({uint32_t(offsetof(PoolArgs, nsegs)), uint32_t(sizeof(PoolArgs) - offsetof(PoolArgs, nsegs))});
   hipEvent_t e0, e1;
   const bool timed = (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
-  const size_t hdr = 256, cntb = align_up(size_t(W) * 4, 256);
+  // counts a cache line apart (TSG_RES_CSTRIDE, u32 units: 16 = one line per workgroup; 1 = packed)
+  static const uint32_t cs = DeviceCtx::env_u32("TSG_RES_CSTRIDE", 16, 1, 64);
+  const size_t hdr = 256, cntb = align_up(size_t(W) * 4 * cs, 256);
   auto *qst = reinterpret_cast<unsigned long long *>(static_cast<uint8_t *>(dc.res_host.p) + 64);
   uint32_t *counts = nullptr;
   const uint8_t *recs = nullptr;
@@ -1214,7 +1219,8 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
     PA.recs = base + hdr + cntb;
     PA.err = reinterpret_cast<uint32_t *>(base);
     PA.qstamps = timed ? qst : nullptr;
-    std::fill_n(counts, W, kCountPending);
+    PA.cstride = cs;
+    for (uint32_t w = 0; w < W; w++) counts[size_t(w) * cs] = kCountPending;
     res_post(dc, ++dc.res_seq, kResSearch, &PA, &parts);
     dc.res_queries++;
   };
@@ -1238,7 +1244,7 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
           if (w == lo) lo++;
           continue;
         }
-        const uint32_t c = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE);
+        const uint32_t c = __atomic_load_n(counts + size_t(w) * cs, __ATOMIC_ACQUIRE);
         if (c == kCountPending) continue;
         seen[w] = 1;
         if (prof && nseen == 0)
@@ -1259,12 +1265,12 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
         fail(TSG_E_DEVICE, "resident search: no answer in 5 s");
       if ((it & 255u) == 0 && aql_done(dc.aql)) {
         bool all = true;
-        for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + w, __ATOMIC_ACQUIRE) != kCountPending;
+        for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + size_t(w) * cs, __ATOMIC_ACQUIRE) != kCountPending;
         if (all) return;
         if (__atomic_load_n(static_cast<uint32_t *>(dc.res_host.p), __ATOMIC_ACQUIRE))
           fail(TSG_E_DEVICE, "resident search: a mailbox slot never verified");
         if (++relaunches > 2) fail(TSG_E_DEVICE, "resident search kernel ended without serving the query");
-        std::fill_n(counts, W, kCountPending);
+        for (uint32_t w2 = 0; w2 < W; w2++) counts[size_t(w2) * cs] = kCountPending;
         seen.assign(W, 0);
         lo = 0;
         dc.res_seq = seq - 1;  // (the launch's first query is the posted one)
@@ -1284,8 +1290,8 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
     total = 0;
     maxc = 0;
     for (uint32_t w = 0; w < W; w++) {
-      total += counts[w];
-      maxc = std::max(maxc, counts[w]);
+      total += counts[size_t(w) * cs];
+      maxc = std::max(maxc, counts[size_t(w) * cs]);
     }
   };
   uint64_t total = 0;
@@ -1349,7 +1355,7 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
   uint64_t run = 0, ps = ~0ull, cut = 0;
   for (uint32_t w = 0; w < W; w++) {
     const SearchOut::Rec *r = prec + uint64_t(w) * seg;
-    for (uint32_t i = 0, c = counts[w]; i < c; i++) {
+    for (uint32_t i = 0, c = counts[size_t(w) * cs]; i < c; i++) {
       const uint32_t bi = r[i].block_il & 0xffffffu;
       const uint64_t s_i = bi <= max_idx ? pos[bi] : 0;
       if (s_i != ps) {
