@@ -674,12 +674,14 @@ __host__ __device__ inline bool res_word_used(uint32_t off, uint32_t nsegs, uint
 // ordered record output) spilled to scratch; 24 units in flight per CU still cover the HBM
 // latency (config 2: 34 MB in flight)
 constexpr uint32_t kResWaves = 12, kResThreads = kResWaves * 64;
+constexpr uint32_t kResMaxRecs = (96u << 10) / 48;  // the LDS record buffer (kPoolLds / sizeof(MatchRec))
 template <int NT, bool DUR, bool RANGE, bool NTL>
 __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(ResidentArgs R) {
   __shared__ __attribute__((aligned(16))) uint32_t s_args[sizeof(PoolArgs) / 4];
   __shared__ uint32_t s_ctl[4];   // [0] command for this round, [1] checksum, [2] header seq, [3] header csum
   __shared__ uint32_t s_wn[kPoolWaves + 1];
   __shared__ uint32_t s_ub[kResMaxUnits], s_uc[kResMaxUnits];  // per unit of the run: LDS record base, count
+  __shared__ uint32_t s_map[kResMaxRecs];  // output record p (scan order) -> its LDS record
   __shared__ uint32_t s_next, s_nrec;
   extern __shared__ __attribute__((aligned(16))) unsigned long long s_rec[];  // rec_cap x 6 words
   const int tid = threadIdx.x, lane = tid & 63;
@@ -835,8 +837,25 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
           Rg.tv[q][kk] = stream1<NTL>(col, uint64_t(Rg.e0) + uint64_t(kk) * 256 + uint64_t(lane) * 4);
       }
     };
-    // the unit's matches into the LDS buffer in scan order (k-step, lane, j)
-    auto eval = [&](const Regs &Rg) {
+    // the unit's matches into the LDS buffer in scan order (k-step, lane, j), in two halves:
+    // eval_a finds them, ranks them and issues the gathers of each lane's first match; the
+    // caller then issues the wave's next unit loads; eval_b stores the gathered records (its
+    // wait covers the gathers alone: they were issued first) and any further match of a lane
+    // (rare: gathered one at a time). A gather is a full memory latency under the scan's load:
+    // taken before the next unit's loads, it had left the wave one unit in flight meanwhile,
+    // and the workgroups holding matches ended ≈ 0.8 us after those without
+    struct Pend {
+      uint32_t mask, e0, rank0[kSteps], bidx, r, ei, il;
+      bool any, has;
+      u32x4 id;
+      uint64_t st, en, nm;
+      const uint8_t *ids, *id_len;
+      const uint64_t *st_ns, *en_ns;
+      const uint32_t *names;
+    };
+    auto eval_a = [&](const Regs &Rg, Pend &Pd) {
+      Pd.any = false;
+      Pd.has = false;
       // the unit's block: lanes test the block boundaries, the ballot counts those passed
       const uint32_t u = ua + Rg.k;
       const uint32_t blk = uint32_t(__popcll(__ballot(uint32_t(lane) + 1 < nsegs + 0u && uint32_t(lane) < nsegs &&
@@ -863,16 +882,14 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
       base = uint32_t(__builtin_amdgcn_readfirstlane(base));
       const DevBlockDesc *D = uniform_ptr(A.desc[blk]);
       const auto *Dc = K4(D);
-      const uint8_t *ids = Dc->ids;
-      const uint64_t *st_ns = Dc->start_ns, *en_ns = Dc->end_ns;
-      const uint32_t *names = Dc->names;
-      const uint8_t *id_len = Dc->id_len;
-      const uint32_t bidx = uint32_t(__builtin_amdgcn_readfirstlane(P.block_idx));
+      Pd.ids = Dc->ids;
+      Pd.st_ns = Dc->start_ns;
+      Pd.en_ns = Dc->end_ns;
+      Pd.names = Dc->names;
+      Pd.id_len = Dc->id_len;
+      Pd.bidx = uint32_t(__builtin_amdgcn_readfirstlane(P.block_idx));
       const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-      // each step's first rank for this lane (ballots: every lane takes part), then the
-      // records one at a time (a loop kept rolled: the gathers of 8 records at once had
-      // pushed the kernel past its 128 registers)
-      uint32_t rank0[kSteps];
+      // each step's first rank for this lane (ballots: every lane takes part)
       uint32_t before = 0;
 #pragma unroll
       for (int kk = 0; kk < kSteps; kk++) {
@@ -884,26 +901,51 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
           lower += uint32_t(__popcll(bb & below));
           tot += uint32_t(__popcll(bb));
         }
-        rank0[kk] = base + before + lower;
+        Pd.rank0[kk] = base + before + lower;
         before += tot;
       }
+      Pd.any = true;
+      Pd.mask = mask;
+      Pd.e0 = Rg.e0;
+      if (mask) {
+        const uint32_t bit = uint32_t(__builtin_ctz(mask)), kk = bit >> 2, j = bit & 3u;
+        Pd.r = (kk ? Pd.rank0[1] : Pd.rank0[0]) + uint32_t(__popc((mask >> (4 * kk)) & ((1u << j) - 1u)));
+        Pd.ei = Rg.e0 + kk * 256 + uint32_t(lane) * 4 + j;
+        if (Pd.r < rec_cap) {
+          Pd.has = true;
+          Pd.id = *G<u32x4>(Pd.ids + uint64_t(Pd.ei) * 16);
+          Pd.st = G(Pd.st_ns)[Pd.ei];
+          Pd.en = G(Pd.en_ns)[Pd.ei];
+          Pd.nm = G(reinterpret_cast<const uint64_t *>(Pd.names))[Pd.ei];
+          Pd.il = G(Pd.id_len)[Pd.ei];
+        }
+      }
+    };
+    auto put = [&](uint32_t r, const u32x4 &id, uint64_t st, uint64_t en, uint32_t ei, uint32_t bidx, uint32_t il,
+                   uint64_t nm) {
+      unsigned long long *d = s_rec + uint64_t(r) * 6;
+      d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
+      d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
+      d[2] = st;
+      d[3] = en;
+      d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
+      d[5] = nm;
+    };
+    auto eval_b = [&](const Pend &Pd) {
+      if (!Pd.any) return;
+      if (Pd.has) put(Pd.r, Pd.id, Pd.st, Pd.en, Pd.ei, Pd.bidx, Pd.il, Pd.nm);
+      // a lane's further matches, one at a time (a loop kept rolled: the gathers of 8 records
+      // at once had pushed the kernel past its 128 registers)
+      const uint32_t mask = Pd.mask;
 #pragma unroll 1
-      for (uint32_t m = mask; m; m &= m - 1) {
+      for (uint32_t m = mask & (mask - 1u); m; m &= m - 1) {
         const uint32_t bit = uint32_t(__builtin_ctz(m)), kk = bit >> 2, j = bit & 3u;
-        const uint32_t r = (kk ? rank0[1] : rank0[0]) + uint32_t(__popc((mask >> (4 * kk)) & ((1u << j) - 1u)));
+        const uint32_t r = (kk ? Pd.rank0[1] : Pd.rank0[0]) + uint32_t(__popc((mask >> (4 * kk)) & ((1u << j) - 1u)));
         if (r >= rec_cap) continue;
-        const uint32_t ei = Rg.e0 + kk * 256 + uint32_t(lane) * 4 + j;
-        const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
-        const uint64_t st = G(st_ns)[ei], en = G(en_ns)[ei];
-        const uint64_t nm = G(reinterpret_cast<const uint64_t *>(names))[ei];
-        const uint32_t il = G(id_len)[ei];
-        unsigned long long *d = s_rec + uint64_t(r) * 6;
-        d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
-        d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
-        d[2] = st;
-        d[3] = en;
-        d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
-        d[5] = nm;
+        const uint32_t ei = Pd.e0 + kk * 256 + uint32_t(lane) * 4 + j;
+        const u32x4 id = *G<u32x4>(Pd.ids + uint64_t(ei) * 16);
+        put(r, id, G(Pd.st_ns)[ei], G(Pd.en_ns)[ei], ei, Pd.bidx, G(Pd.id_len)[ei],
+            G(reinterpret_cast<const uint64_t *>(Pd.names))[ei]);
       }
     };
     const bool interleave = (R.mode & 1u) != 0;
@@ -917,16 +959,19 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     uint32_t ka = wave, kb = wave + nwv;
     if (ka < nk) load(ra, ka);
     if (kb < nk) load(rb, kb);
+    Pend pd;
     while (ka < nk || kb < nk) {
       if (ka < nk) {
-        eval(ra);
+        eval_a(ra, pd);
         ka = claim(ka);
         if (ka < nk) load(ra, ka);
+        eval_b(pd);
       }
       if (kb < nk) {
-        eval(rb);
+        eval_a(rb, pd);
         kb = claim(kb);
         if (kb < nk) load(rb, kb);
+        eval_b(pd);
       }
     }
     __syncthreads();
@@ -955,20 +1000,20 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     const uint32_t seg_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.seg_cap));
     const bool over = total > rec_cap;
     if (!over && total <= seg_cap && total) {
+      // output record p -> its LDS record: each unit with matches writes its range of the map
+      // (a binary search of the offsets per output word had been ~7 dependent LDS reads)
+      for (uint32_t k = uint32_t(tid); k < nk; k += nthreads) {
+        const uint32_t o = s_uc[k], o1 = k + 1 < nk ? s_uc[k + 1] : total;
+        for (uint32_t p = o; p < o1; p++) s_map[p] = s_ub[k] + (p - o);
+      }
+      __syncthreads();
       // consecutive lanes store consecutive words of the segment (the fabric merges them into
       // whole-line PCIe writes; a record per thread, 8-byte stores each, had been 8x the
-      // transactions and made the host wait ~50 us per query for the last count): output word
-      // i belongs to record p = i / 6, whose unit is found by a binary search of the offsets
+      // transactions and made the host wait ~50 us per query for the last count)
       auto *dst0 = reinterpret_cast<unsigned long long *>(uniform_ptr(A.recs)) + uint64_t(w) * seg_cap * 6;
       for (uint32_t i = uint32_t(tid); i < total * 6; i += nthreads) {
         const uint32_t p = i / 6, j = i - p * 6;
-        uint32_t lo = 0, hi = nk;  // the last unit whose offset <= p
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_uc[mid] <= p) lo = mid;
-          else hi = mid;
-        }
-        host_store(dst0 + i, s_rec[uint64_t(s_ub[lo] + (p - s_uc[lo])) * 6 + j]);
+        host_store(dst0 + i, s_rec[uint64_t(s_map[p]) * 6 + j]);
       }
     }
     if (tid == 0 && A.qstamps) {
@@ -1326,6 +1371,14 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
       for (uint32_t w = 0; w < W; w++) {
         sn[w] = double(qst[2 * w] - lo) / 100.0;
         en[w] = double(qst[2 * w + 1] - lo) / 100.0;
+      }
+      static const bool raw = std::getenv("TSG_RES_DUMP")[0] == '2';
+      if (raw) {  // every workgroup's end (0.01 us after the first seen), workgroup order
+        std::string line = "[tsg] resident ends:";
+        for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(qst[2 * w + 1] - lo);
+        line += "\n[tsg] resident counts:";
+        for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(counts[size_t(w) * cs]);
+        std::fprintf(stderr, "%s\n", line.c_str());
       }
       std::sort(sn.begin(), sn.end());
       std::sort(en.begin(), en.end());
