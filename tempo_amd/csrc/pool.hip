@@ -806,7 +806,10 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
       s_nrec = 0;
     }
     __syncthreads();
-    uint32_t b = 0;  // the block of the wave's last load (its fields are read from LDS per load)
+    // the block of the wave's last load (its fields are read from LDS per load); from the
+    // block holding the run's first unit (a walk from block 0 had put up to nsegs dependent LDS
+    // reads before a late workgroup's first loads)
+    uint32_t b = uint32_t(__popcll(__ballot(uint32_t(lane) + 1 < nsegs && ua >= A.ubase[lane + 1])));
     struct Regs {
       u32x4 d[kSteps], s[kSteps];
       uint32_t tv[NT > 0 ? NT : 1][kSteps];
