@@ -50,6 +50,7 @@ T0 = 1_700_000_000
 QUERY = dict(tags={"service.name": "svc-07", "http.method": "get", "status.code": "error"},
              min_duration_ms=10, max_duration_ms=1000, start=T0 + 900, end=T0 + 2700)
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+T_PATH_RESIDENT = 1  # tsg_metrics.path: served by the resident kernel (tempo_amd.PATH_RESIDENT)
 # device of the small timing / count tensors reduced over the ranks: cuda over RCCL, or the
 # host under --ranks-share-gpu (several ranks on one GPU: the process group is gloo)
 RED_DEVICE = "cuda"
@@ -108,7 +109,9 @@ def summary(out):
          "cfg3_first20_us_p50": g("cfg3", "limit20", "time_to_first_20_us", "p50"),
          "cfg5_device_ms": g("cfg5", "device_ms"), "cfg5_host_e2e_ms_p50": g("cfg5", "host_e2e", "step_ms", "p50"),
          "load_gb_per_s": g("load_gb_per_s"), "cfg4_load_gb_per_s": g("cfg4", "load_gb_per_s"),
-         "cfg1_kernel_us_p50": g("cfg1", "gpu", "kernel_us", "p50")}
+         "cfg1_kernel_us_p50": g("cfg1", "gpu", "kernel_us", "p50"),
+         "batched_device_us_per_query": g("batched", "device_us_per_query"), "batched_frac": g("batched", "frac"),
+         "batched_wall_us_per_query": g("batched", "wall_us_per_query")}
     for name, q in (g("cfg4", "queries") or {}).items():
         s["cfg4_" + name] = {"step_over_device": round(q["step_over_device"], 3) if q.get("step_over_device") else None,
                              "scan_us_p50": round(q["scan_us"]["p50"], 1), "dict_frac": round(q["dict_frac"], 3)
@@ -205,6 +208,10 @@ def parse():
     ap.add_argument("--events", type=int, default=4,
                     help="HIP events around the search kernel of every N-th timed step (roofline.achieved: "
                          "the average over those launches); 0 = off")
+    ap.add_argument("--batch-queries", type=int, default=64,
+                    help="batched leg: config-2 queries per tsg_search_batch call (SURVEY §8(d) batched mode; 0 = skip)")
+    ap.add_argument("--batch-depth", type=int, default=8, help="batched leg: searches in flight at once")
+    ap.add_argument("--batch-reps", type=int, default=6, help="batched leg: timed batches")
     ap.add_argument("--limit-steps", type=int, default=20,
                     help="extra timed searches with limit=20 (early exit, config-3 mode); 0 = skip")
     ap.add_argument("--cfg3", type=int, default=None,
@@ -409,6 +416,37 @@ def parallel(fn, items):
     if errs:
         raise errs[0]
     return out
+
+
+def batch_leg(args, eng, sets, pipe, entries, scan_bytes, nmatch):
+    """SURVEY §8(d)'s batched mode: --batch-queries config-2 queries (the 4 resident copies in
+    turn) in one tsg_search_batch call, --batch-depth in flight: the resident kernel takes the next
+    query from its mailbox while earlier ones finish, the host assembles earlier results meanwhile.
+    device_us_per_query = the batch's resident launch's dispatch duration (AQL dispatch timestamps:
+    the clock rocprofv3's kernel trace reads; launch and quit included) / queries."""
+    k = args.batch_queries
+    items = [(sets[i % len(sets)], pipe) for i in range(k)]
+    eng.search_batch(items[: min(k, 16)], depth=args.batch_depth, unpack=False)  # (warm)
+    walls, devs, ok = [], [], True
+    for _ in range(max(1, args.batch_reps)):
+        t0 = time.perf_counter()
+        res, dns = eng.search_batch(items, depth=args.batch_depth, unpack=False)
+        walls.append(time.perf_counter() - t0)
+        devs.append(dns)
+        ok = ok and all(n == nmatch for n, _ in res) and all(m.path == T_PATH_RESIDENT for _, m in res)
+    wall = sorted(walls)[len(walls) // 2]
+    dv = [d for d in devs if d]
+    dev = sorted(dv)[len(dv) // 2] if dv else 0
+    per_q = dev / k if dev else None
+    ach = scan_bytes / per_q if per_q else None  # bytes / ns = GB/s
+    return {"queries": k, "depth": args.batch_depth, "reps": len(walls),
+            "wall_us_per_query": wall / k * 1e6, "entries_per_s": entries * k / wall,
+            "device_us_per_query": per_q / 1e3 if per_q else None,
+            "device_us_per_query_all": [round(d / k / 1e3, 3) for d in devs],
+            "achieved_gbps": ach, "frac": ach / PEAK_HBM_GBPS if ach else None,
+            "bytes_per_query": scan_bytes, "counts_match_and_resident": ok,
+            "note": "one resident launch per batch serves every query (its dispatch is what a kernel trace shows); "
+                    "device time per query = dispatch duration / queries"}
 
 
 def cpu_baselines(paths, got, threads, oracle_threads=None):
@@ -1094,7 +1132,9 @@ def main():
         log(f"rank {rank}: {len(sets)} resident copies of the set ({len(sets) * dev_bytes / 1e9:.2f} GB)")
 
     all_cpus = os.sched_getaffinity(0)
-    cpu_threads = args.cpu_threads or max(1, min(16, len(all_cpus)))
+    # the CPU baselines' threads: this GPU's share of its node's CPUs (an MI355X node: 8 GPUs;
+    # nproc / 8 = 32 on the 256-CPU boxes), at least 16, at most the CPUs this process may use
+    cpu_threads = args.cpu_threads or max(1, min(len(all_cpus), max((os.cpu_count() or 8) // 8, min(16, len(all_cpus)))))
     if args.pin == "auto":
         # the step polls a completion word and copies its records from pinned host memory:
         # both are served faster from the GPU's own socket (profiles/r01_host).
@@ -1230,6 +1270,9 @@ def main():
         out["mall"] = {"steps": args.mall_steps, "entries_per_s": entries * args.mall_steps / e2,
                        "step_us": pct([x * 1e6 for x in s2]), "kernel_us": pct([x / 1e3 for x in k2]),
                        "achieved_gbps": a2, "frac": a2 / PEAK_HBM_GBPS if a2 else None}
+
+    if args.batch_queries:
+        out["batched"] = batch_leg(args, eng, sets, pipe, entries, scan_bytes, len(got))
 
     if args.limit_steps:
         # SURVEY.md §8(d) config-3 mode on this rank's set: limit=20 (ingester default),

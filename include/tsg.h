@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define TSG_ABI_VERSION 6
+#define TSG_ABI_VERSION 7
 
 /* Status codes. */
 #define TSG_OK 0
@@ -122,7 +122,16 @@ typedef struct tsg_metrics {
   uint64_t kernel_ns;         /* device time of the search kernels (HIP events) */
   uint64_t scan_kernel_ns;    /* device time of the scan_compact kernel alone (HIP events) */
   uint64_t scan_bytes;        /* algorithmic bytes of the scan_compact kernel */
+  /* ABI 7: the kernels that served this search (TSG_PATH_* bits, OR over devices, chunks and
+     limit waves). TSG_PATH_COTENANT: the resident kernel was passed over because another process
+     has a libtsg context on the same GPU (its launch would hold every CU). */
+  uint32_t path;
+  uint32_t reserved;
 } tsg_metrics;
+#define TSG_PATH_RESIDENT 1u /* search_resident_kernel (narrow query, mailbox) */
+#define TSG_PATH_PLAIN 2u    /* search_pool_kernel / search_static_kernel as plain launches */
+#define TSG_PATH_OTHER 4u    /* search_fast_kernel, the dictionary pass, the general path */
+#define TSG_PATH_COTENANT 8u /* the resident kernel declined: another process on the GPU */
 
 /* Ordered match sequence: blocks in caller order, each block's matches in the
  * reference scan order (pages ascending, entry vector index ascending). With
@@ -194,7 +203,11 @@ int tsg_device_numa_node(tsg_ctx *ctx, int dev);
 /* ABI 6: the device context's resident-search counters, out[0..n): [0] resident launches,
  * [1] queries they served, [2] relaunches after a launch left on its idle timeout as a query
  * was posted, [3] quits (another kernel needed the device, a second context opened on it, or
- * the query shape changed). Zeros when TSG_RESIDENT=0. DESIGN.md §4. */
+ * the query shape changed). ABI 7: [4] mailbox slot reads the kernel rejected (check mismatch:
+ * a read that caught the host's writes landing), [5] narrow queries launched plainly because
+ * another process has a libtsg context on the same GPU, [6] narrow queries launched plainly
+ * (any reason), [7] samples taken for the XCD-weighted split. Zeros when TSG_RESIDENT=0.
+ * DESIGN.md §4. */
 int tsg_device_counters(tsg_ctx *ctx, int dev, uint64_t *out, size_t n);
 const char *tsg_last_error(void);
 int tsg_abi_version(void);
@@ -318,6 +331,32 @@ void tsg_free(void *p);
 int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg_query *q,
                const tsg_search_opts *opts, tsg_result **out);
 void tsg_result_free(tsg_result *r);
+
+/* ABI 7: a batch of searches served back to back (SURVEY §8(d) batched mode; the ingester's
+ * concurrent Search calls, modules/ingester/instance_search.go:164-185, in one call). Item i is
+ * one tsg_search (its own blocks, query and options) whose result goes to outs[i] (free each with
+ * tsg_result_free; NULL for a failed item). Up to `depth` items (0 = 16) run at once on internal
+ * threads and skip the coalescer: a narrow query is posted to the resident kernel's mailbox while
+ * earlier ones run, so the device serves them back to back. Returns TSG_OK or the first failing
+ * item's status. device_ns (optional): when each device's resident queries of the batch ran on
+ * one resident launch that this call started and ended, the longest such launch's dispatch
+ * duration (the AQL queue's dispatch timestamps, the clock rocprofv3's kernel trace reads); 0
+ * otherwise. */
+typedef struct tsg_search_item {
+  tsg_block *const *blocks;
+  size_t nblocks;
+  const tsg_query *query;
+  tsg_search_opts opts;
+} tsg_search_item;
+int tsg_search_batch(tsg_ctx *ctx, const tsg_search_item *items, size_t n, uint32_t depth, tsg_result **outs,
+                     uint64_t *device_ns);
+
+/* ABI 7, test hooks (process-wide): "res_torn" = k: the next k resident-kernel posts write the
+ * mailbox slot as a read that caught the host's writes half landed would see it (two argument
+ * words moved by +-d: the plain sum unchanged) and repair it 200 us later; the kernel must
+ * re-read the slot (tsg_device_counters[4] counts the rejected reads). TSG_E_INVALID for an
+ * unknown name. */
+int tsg_debug_set(const char *name, int64_t value);
 
 /* Durations (ns) of the search kernels launched with TSG_SEARCH_TIME_DEFER since
  * the last call, in launch order per device (devices in context order). Waits for

@@ -210,12 +210,16 @@ struct tsg_ctx {
     uint32_t limit, flags;
     tsg::SearchOut *out;
     std::atomic<bool> done{false};
+    std::atomic<bool> taken{false};  // in a leader's batch (set under the coalescer's lock)
     std::exception_ptr err;
   };
   struct Coalescer {
     SpinLock m;
     std::vector<CoalReq *> pending;
-    std::atomic<bool> busy{false};
+    // leaders running device searches at once (TSG_COAL_LEADERS, default 4): queries that
+    // differ run side by side — the resident kernel serves them back to back — while the
+    // requests of one query still join one leader's launch
+    std::atomic<int> leaders{0};
     // waiters spin (bounded, and only while the host has CPUs to spare), then park on `park`
     // until the leader hands off (park.hpp: an oversubscribed host must not run a spinning
     // waiter instead of the leader)
@@ -664,9 +668,9 @@ int tsg_device_numa_node(tsg_ctx *ctx, int dev) {
 int tsg_device_counters(tsg_ctx *ctx, int dev, uint64_t *out, size_t n) {
   if (!ctx || !out || dev < 0 || size_t(dev) >= ctx->c.devs.size()) return TSG_E_INVALID;
   return guard([&] {
-    uint64_t c[4];
+    uint64_t c[8];
     device_counters(*ctx->c.devs[size_t(dev)], c);
-    for (size_t i = 0; i < n; i++) out[i] = i < 4 ? c[i] : 0;
+    for (size_t i = 0; i < n; i++) out[i] = i < 8 ? c[i] : 0;
   });
 }
 int tsg_cancel(tsg_ctx *ctx, uint64_t qid) {
@@ -995,6 +999,10 @@ static uint64_t wait_spin_ns() {
   return ns;
 }
 
+// tsg_search_batch's worker threads: their searches skip the coalescer (each item is its own
+// query; the resident kernel serves the items' queries back to back instead)
+static thread_local bool tl_batch_item = false;
+
 // device_search through the device's coalescer (tsg_ctx::Coalescer). TSG_COALESCE=0 turns
 // it off; TSG_COALESCE_US (default 30) bounds the leader's wait for approaching callers.
 static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std::pair<uint32_t, Block *>> &list,
@@ -1007,8 +1015,12 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
     const char *e = std::getenv("TSG_COALESCE_US");
     return uint64_t(e ? std::max(0, std::atoi(e)) : 30) * 1000ull;
   }();
+  static const int max_leaders = [] {
+    const char *e = std::getenv("TSG_COAL_LEADERS");
+    return e ? std::max(1, std::min(64, std::atoi(e))) : 4;
+  }();
   constexpr size_t kBatchBlocks = 32;  // one launch's kernel-argument capacity
-  if (!on) {
+  if (!on || tl_batch_item) {
     ap.leave();
     device_search(*dc, list, q, limit, flags, out);
     return;
@@ -1029,14 +1041,17 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
   bool spun = false;
   for (;;) {
     if (r.done.load(std::memory_order_acquire)) break;
-    bool expect = false;
-    if (c.busy.load(std::memory_order_relaxed) ||
-        !c.busy.compare_exchange_strong(expect, true, std::memory_order_acq_rel)) {
+    int cur = c.leaders.load(std::memory_order_relaxed);
+    if (r.taken.load(std::memory_order_acquire) || cur >= max_leaders ||
+        !c.leaders.compare_exchange_strong(cur, cur + 1, std::memory_order_acq_rel)) {
       // A waiter: the leader hands off by setting `done` (or clearing `busy`) and bumping the
       // park epoch. Spin once, for at most spin_ns and only while fewer waiters spin than the
       // caller's CPUs leave room for beside the leader; then park (bounded re-checks).
       const uint32_t e = c.park.read();
-      auto ready = [&] { return r.done.load(std::memory_order_acquire) || !c.busy.load(std::memory_order_acquire); };
+      auto ready = [&] {
+        return r.done.load(std::memory_order_acquire) ||
+               (!r.taken.load(std::memory_order_acquire) && c.leaders.load(std::memory_order_acquire) < max_leaders);
+      };
       if (ready()) continue;
       if (!spun) {
         spun = true;
@@ -1056,7 +1071,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
       continue;
     }
     if (r.done.load(std::memory_order_acquire)) {  // served while we took the lead
-      c.busy.store(false, std::memory_order_release);
+      c.leaders.fetch_sub(1, std::memory_order_acq_rel);
       c.wake();
       break;
     }
@@ -1073,11 +1088,15 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
     batch.clear();
     blist.clear();
     owner.clear();
+    bool own_taken = false;
     {
       std::lock_guard<SpinLock> lk(c.m);
+      // (another leader may have taken this request into its batch already: then it serves it)
+      own_taken = std::find(c.pending.begin(), c.pending.end(), &r) == c.pending.end();
       size_t nb = 0;
       auto take = [&](size_t k) {
         tsg_ctx::CoalReq *x = c.pending[k];
+        x->taken.store(true, std::memory_order_release);
         for (const auto &p : *x->list) {
           owner.push_back({uint32_t(batch.size()), p.first});
           blist.push_back({uint32_t(blist.size()), p.second});
@@ -1086,9 +1105,9 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
         batch.push_back(x);
         c.pending[k] = nullptr;
       };
-      for (size_t k = 0; k < c.pending.size(); k++)
+      for (size_t k = 0; k < c.pending.size() && !own_taken; k++)
         if (c.pending[k] == &r) take(k);
-      for (size_t k = 0; k < c.pending.size(); k++) {
+      for (size_t k = 0; k < c.pending.size() && !own_taken; k++) {
         tsg_ctx::CoalReq *x = c.pending[k];
         if (!x || x->limit != limit || x->flags != flags || nb + x->list->size() > kBatchBlocks ||
             !same_query(*x->q, q))
@@ -1096,6 +1115,12 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
         take(k);
       }
       c.pending.erase(std::remove(c.pending.begin(), c.pending.end(), nullptr), c.pending.end());
+    }
+    if (own_taken) {  // a waiter again, for the leader that took it
+      c.leaders.fetch_sub(1, std::memory_order_acq_rel);
+      c.wake();
+      spun = false;
+      continue;
     }
     if (prof) {
       prof_add("coal.window_us", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_lead).count());
@@ -1108,7 +1133,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
         r.err = std::current_exception();
       }
       r.done.store(true, std::memory_order_release);
-      c.busy.store(false, std::memory_order_release);
+      c.leaders.fetch_sub(1, std::memory_order_acq_rel);
       c.wake();
       break;
     }
@@ -1131,7 +1156,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
         }
         x->done.store(true, std::memory_order_release);
       }
-      c.busy.store(false, std::memory_order_release);
+      c.leaders.fetch_sub(1, std::memory_order_acq_rel);
       c.wake();
       break;
     }
@@ -1152,6 +1177,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
       o.scan_ns = bout.scan_ns;
       o.reruns = batch[k] == &r ? bout.reruns : 0;
       o.pool = bout.pool;
+      o.path = bout.path;
       o.term_any.clear();
     }
     for (const auto &rec : bout.recs) {
@@ -1165,7 +1191,7 @@ static void coalesced_search(tsg_ctx *ctx, DeviceCtx *dc, const std::vector<std:
       batch[ow.first]->out->term_any.push_back({ow.second, ta.second});
     }
     for (auto *x : batch) x->done.store(true, std::memory_order_release);
-    c.busy.store(false, std::memory_order_release);
+    c.leaders.fetch_sub(1, std::memory_order_acq_rel);
     c.wake();
     if (prof) prof_add("coal.lead_total_us", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_lead).count());
     break;
@@ -1753,6 +1779,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
           o.scan_ns += more.scan_ns;
           o.scan_bytes += more.scan_bytes;
           o.reruns += more.reruns;
+          o.path |= more.path;
         }
       };
       if (per_dev.empty()) approach.leave();
@@ -1764,6 +1791,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         note_any(*o);
         m.device_bytes_read += o->device_bytes;
         m.reruns += o->reruns;
+        m.path |= o->path;
         wave_k = std::max<uint64_t>(wave_k, o->kernel_ns);
         wave_s = std::max<uint64_t>(wave_s, o->scan_ns);
         m.scan_bytes += o->scan_bytes;
@@ -2037,6 +2065,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         note_any(o);
         m.device_bytes_read += o.device_bytes;
         m.reruns += o.reruns;
+        m.path |= o.path;
         m.kernel_ns += o.kernel_ns;
         m.scan_kernel_ns += o.scan_ns;
         m.scan_bytes += o.scan_bytes;
@@ -2180,6 +2209,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
                        SearchOut &o = wouts[i];
                        o.recs.clear();
                        o.term_any.clear();
+                       o.path = 0;
                        // (a part list longer than one launch's 32 blocks: whole blocks by chunks)
                        const size_t nl = lists[i].size(), step = kChunk ? kChunk : nl;
                        for (size_t c0 = 0; c0 < nl; c0 += step) {
@@ -2198,6 +2228,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
                          o.scan_ns += more.scan_ns;
                          o.scan_bytes += more.scan_bytes;
                          o.reruns += more.reruns;
+                         o.path |= more.path;
                          used_pool[i] = used_pool[i] || more.pool;
                        }
                      });
@@ -2208,6 +2239,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
           m.device_bytes_read += o.device_bytes;
           m.scan_bytes += o.scan_bytes;
           m.reruns += o.reruns;
+          m.path |= o.path;
           wk = std::max<uint64_t>(wk, o.kernel_ns);
           ws = std::max<uint64_t>(ws, o.scan_ns);
           for (const auto &r : o.recs) acc[r.block_il & 0xffffffu].push_back(r);
@@ -2383,6 +2415,59 @@ void tsg_result_free(tsg_result *r) {
   }
   release_holder(reinterpret_cast<ResultHolder *>(r));
 }
+
+int tsg_search_batch(tsg_ctx *ctx, const tsg_search_item *items, size_t n, uint32_t depth, tsg_result **outs,
+                     uint64_t *device_ns) {
+  if (!ctx || (n && (!items || !outs))) return TSG_E_INVALID;
+  if (device_ns) *device_ns = 0;
+  for (size_t i = 0; i < n; i++) outs[i] = nullptr;
+  if (!n) return TSG_OK;
+  // the devices the items' blocks live on: each starts a fresh resident launch with dispatch
+  // timestamps (the batch's device time), ended after the last item
+  std::vector<DeviceCtx *> devs;
+  for (size_t i = 0; i < n; i++)
+    for (size_t b = 0; b < items[i].nblocks; b++) {
+      const tsg_block *blk = items[i].blocks ? items[i].blocks[b] : nullptr;
+      if (blk && blk->b.dc && std::find(devs.begin(), devs.end(), blk->b.dc) == devs.end()) devs.push_back(blk->b.dc);
+    }
+  std::vector<uint64_t> before(devs.size());
+  const int rc0 = guard([&] {
+    for (size_t d = 0; d < devs.size(); d++) before[d] = resident_batch_begin(*devs[d]);
+  });
+  if (rc0) return rc0;
+  const size_t nt = std::min<size_t>(n, depth ? depth : 16);
+  std::atomic<size_t> next{0};
+  std::vector<int> rcs(n, TSG_OK);
+  std::vector<std::string> errs(n);
+  auto run = [&] {
+    tl_batch_item = true;
+    for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) {
+      const tsg_search_item &it = items[i];
+      rcs[i] = tsg_search(ctx, it.blocks, it.nblocks, it.query, &it.opts, &outs[i]);
+      if (rcs[i]) {
+        errs[i] = tsg_last_error();
+        outs[i] = nullptr;
+      }
+    }
+    tl_batch_item = false;
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; t++) th.emplace_back(run);
+  run();
+  for (auto &t : th) t.join();
+  uint64_t dns = 0;
+  const int rc1 = guard([&] {
+    for (size_t d = 0; d < devs.size(); d++) dns = std::max(dns, resident_batch_end(*devs[d], before[d]));
+  });
+  if (device_ns) *device_ns = dns;
+  for (size_t i = 0; i < n; i++)
+    if (rcs[i]) {
+      set_last_error(errs[i]);
+      return rcs[i];
+    }
+  return rc1;
+}
+int tsg_debug_set(const char *name, int64_t value) { return debug_set(name, value); }
 
 int tsg_kernel_times(tsg_ctx *ctx, uint64_t *ns, size_t cap, size_t *n) {
   if (!ctx || !n || (cap && !ns)) return TSG_E_INVALID;

@@ -59,12 +59,16 @@ void pinned_put(void *p, size_t) {
     g_pin_free.erase(it);
   }
 }
-void device_counters(DeviceCtx &dc, uint64_t out[4]) {
+void device_counters(DeviceCtx &dc, uint64_t out[8]) {
   std::lock_guard<std::mutex> lk(dc.mu);
   out[0] = dc.res_launches;
   out[1] = dc.res_queries;
   out[2] = dc.res_relaunches;
   out[3] = dc.res_quits;
+  out[4] = dc.res_rejects;
+  out[5] = dc.res_cotenant_queries;
+  out[6] = dc.res_plain_queries;
+  out[7] = dc.res_xsamples;
 }
 
 void ctx_init(Ctx &c, const tsg_options *opts) {
@@ -269,6 +273,9 @@ void block_upload(Ctx &c, Block &b, int device_hint) {
 
   std::lock_guard<std::mutex> lk(dc.mu);
   dc.mem_epoch++;  // (a resident search launch relaunches before it reads new columns)
+  // the resident launch holds every CU: the stream work below (the zero fill of the dictionary
+  // blobs is a kernel) would wait for its idle exit
+  resident_quit(dc);
   HIP_OK(hipSetDevice(dc.ordinal));
   hipStream_t s = dc.stream;
   d.dur32 = dev_upload(d, scan.data(), scan.size(), s);
@@ -369,6 +376,7 @@ void block_clone(Ctx &c, const Block &src, Block &dst, int device_hint) {
   d.n = o.n;
   std::lock_guard<std::mutex> lk(dc.mu);
   dc.mem_epoch++;
+  resident_quit(dc);  // (as block_upload)
   HIP_OK(hipSetDevice(dc.ordinal));
   // the descriptor allocation (last) is rebuilt, every other one copied
   const size_t ncopy = o.allocs.empty() ? 0 : o.allocs.size() - 1;
@@ -419,6 +427,10 @@ void block_free(Block &b) {
   if (!b.dc) return;
   std::lock_guard<std::mutex> lk(b.dc->mu);
   b.dc->mem_epoch++;
+  try {
+    resident_quit(*b.dc);  // (no launch reads the columns after they are freed)
+  } catch (...) {
+  }
   (void)hipSetDevice(b.dc->ordinal);
   (void)hipStreamSynchronize(b.dc->stream);
   for (void *p : b.dev.allocs) (void)hipFree(p);

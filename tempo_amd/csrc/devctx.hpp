@@ -58,7 +58,8 @@ struct HostBuf {
 
 struct DeviceCtx {
   int ordinal = 0;
-  int num_cu = 0;
+  int num_cu = 0;   // the CUs search launches plan for: dev_cu, or the "groups" test hook
+  int dev_cu = 0;   // the device's
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, es0 = nullptr, es1 = nullptr;
   hipEvent_t mk0 = nullptr, mk1 = nullptr;  // untimed markers around a launch
@@ -183,6 +184,32 @@ struct DeviceCtx {
   std::string res_kernel;
   uint64_t res_epoch = 0, mem_epoch = 0;
   HostBuf res_host{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};  // [0..63] error word, then query stamps
+  // XCD-weighted split (TSG_RES_XSPLIT=0: even runs): each XCD's share of a query's units, from the
+  // workgroups' measured {seen, end} stamps (pool.hip res_calibrate); samples taken so far
+  double res_xf[8] = {0.125, 0.125, 0.125, 0.125, 0.125, 0.125, 0.125, 0.125};
+  uint32_t res_xsamples = 0;
+  uint64_t res_qn = 0;
+  // slot reads the kernel rejected (check mismatch), queries the plain launches served because
+  // another process shares the device, plain-launch narrow queries (tsg_device_counters [4..6])
+  uint64_t res_rejects = 0, res_cotenant_queries = 0, res_plain_queries = 0;
+  int res_cotenant = -1;          // other processes with a libtsg context on this device (-1: not checked)
+  uint32_t res_cotenant_gen = ~0u;  // the shared generation word's value at that check
+  uint32_t *cot_gen = nullptr;      // the GPU's shared generation word (pool.hip cotenant_register)
+  std::string cot_dir, cot_prefix;
+  std::vector<HostBuf> res_quarantine;  // result areas a failed resident query may still write into (kept to shutdown)
+  // queries in flight on the resident launch (concurrent callers release mu while theirs run):
+  // each holds a result area (pool.hip res_area_bytes); seq -> area index
+  struct ResArea {
+    HostBuf buf{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};
+    bool busy = false;
+    uint32_t W = 0;
+    std::string sym;  // the kernel that serves it (a relaunch after an idle exit uses it)
+  };
+  std::vector<ResArea> res_areas;
+  std::map<uint32_t, uint32_t> res_inflight;
+  uint32_t res_threads = 0, res_groups = 0;  // the live launch's shape
+  bool res_profile_next = false;  // tsg_search_batch: the next resident launch gets dispatch timestamps
+  int res_profile_slot = -1;      // ... its AQL profiling slot
   std::set<const void *> pool_attr;  // pool kernels whose dynamic LDS limit has been raised
   // TSG_PER_CU=k (1..16): scan workgroups per CU in the grid plan instead of the
   // occupancy (k above it oversubscribes: later workgroups start as earlier ones retire)

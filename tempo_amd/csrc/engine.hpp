@@ -140,6 +140,8 @@ struct SearchOut {
   uint64_t scan_ns = 0, scan_bytes = 0;
   uint32_t reruns = 0;  // extra launches after a record overflow (timed into scan_ns / kernel_ns when timing)
   bool pool = false;    // served by the pool kernels (they search entry ranges on the device)
+  bool resident = false;  // served by the resident search kernel
+  uint32_t path = 0;      // TSG_PATH_* bits of the kernels that served it (tsg_metrics.path)
   // (block index, term mask) for the blocks whose dictionaries the device pass matched
   // (prep / dict_stream / dict_sets): bit t clear = no value of the block's key for term t
   // contains the needle. MatchesBlock's tag half for keys with HostBlock::hdr_defer.
@@ -239,8 +241,19 @@ void device_find(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>
 
 int device_ordinal(const DeviceCtx &dc);
 // resident search counters: launches, queries served, relaunches after an idle-exit race, quits
-void device_counters(DeviceCtx &dc, uint64_t out[4]);
+void device_counters(DeviceCtx &dc, uint64_t out[8]);
 // Durations of the TSG_SEARCH_TIME_DEFER launches since the last call (waits for the stream).
 void device_kernel_times(DeviceCtx &dc, std::vector<uint64_t> &ns);
+// tsg_search_batch (pool.hip): begin ends the device's resident launch and gives the next one
+// dispatch timestamps (returns the launch count so far); end ends that launch and returns its
+// dispatch duration (ns) when exactly one launch served the batch's resident queries, else 0
+uint64_t resident_batch_begin(DeviceCtx &dc);
+uint64_t resident_batch_end(DeviceCtx &dc, uint64_t launches_before);
+// test hooks (tsg_debug_set): "res_torn", "groups" (search launches plan for this many CUs:
+// e.g. 8 makes a resident query of 6 M entries run > 1536 units per workgroup), "xsplit"
+// (0/1: the resident kernel's XCD-weighted split; default TSG_RES_XSPLIT, 1)
+int debug_set(const char *name, int64_t value);
+uint32_t debug_groups();
+bool debug_xsplit();
 
 }  // namespace tsg

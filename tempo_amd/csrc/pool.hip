@@ -1,10 +1,23 @@
 // pool.hip — MI355X (gfx950) pool search: narrow full scans (limit 0) of Tempo search
 // blocks with one workgroup per CU and a CU-wide work pool. The same predicates,
 // records and result order as search_fast_kernel (search.hip); see DESIGN.md §4.
+#include <dirent.h>
+#include <fcntl.h>
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <sys/file.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
+#include <atomic>
+#include <chrono>
 #include <cstddef>
 #include <cstdio>
 #include <string>
@@ -76,8 +89,11 @@ struct PoolArgs {
   uint32_t nbms;                     // bitmaps in `bms` (the resident kernel's slot checksum)
   uint32_t cstride;                  // resident kernel: workgroup w's count at counts[w * cstride] (0 = 1)
   uint32_t wq, wr;                   // resident kernel: workgroup w scans units [w*wq + min(w, wr), +wq + (w < wr))
-  uint32_t pad0;
+  // resident kernel, XCD-weighted split (xsplit != 0; W a multiple of 8): workgroup w = 8i + x (XCD x)
+  // scans xn[x] + (i < xr[x]) units, the runs in workgroup order (pool.hip res_split)
+  uint32_t xsplit;
   unsigned long long *qstamps;       // resident kernel, timed queries: per workgroup {seen, end} (100 MHz)
+  uint32_t xn[8], xr[8];
 };
 static_assert(sizeof(PoolArgs) <= 4096, "kernel arguments");
 
@@ -642,13 +658,31 @@ __global__ void __launch_bounds__(kPoolThreads, 1) search_static_kernel(PoolArgs
 constexpr uint32_t kResSlots = 64, kResSlotBytes = 8192, kResHdrBytes = 64;
 constexpr uint32_t kResSearch = 1, kResQuit = 2;
 constexpr uint32_t kResMaxUnits = 2048;  // units per workgroup (the LDS tables); larger queries launch plainly
+constexpr uint32_t kResRejectWord = 8;   // ResidentArgs::err word counting rejected slot reads
 struct ResHeader {  // the first 16 B of a mailbox slot; PoolArgs at +kResHdrBytes
-  uint32_t seq, cmd, csum, nwords;
+  uint32_t seq, cmd, h0, h1;  // h0, h1: res_hash of (seq, cmd, the used argument words)
 };
+// The slot check: two independently keyed 32-bit sums of a nonlinear per-word mix of (word, its
+// index, seq). A slot read while the host's writes were still landing holds some words of query
+// seq - kResSlots: an additive checksum accepted any such mix whose plain sum happened to equal
+// the new one; here a stale/new mix passes with probability ~2^-64, and a stale
+// header (another seq, another cmd) never does.
+__host__ __device__ inline uint32_t res_mix(uint32_t x, uint32_t wi, uint32_t seq, uint32_t key) {
+  uint32_t h = x ^ (wi * 0x9E3779B1u) ^ (seq * 0x85EBCA77u) ^ key;
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+constexpr uint32_t kResKey0 = 0x2545F491u, kResKey1 = 0x6C8E9CF5u;
+constexpr uint32_t kResCmdWord = 0xffffffffu;  // (the word index the command is mixed under)
 struct ResidentArgs {
   const uint32_t *door;  // uncached device memory: [0] = the last posted sequence number
   const uint8_t *slots;  // uncached device memory: kResSlots x kResSlotBytes (slot = seq % kResSlots)
-  uint32_t *err;         // pinned host: [0] set when a slot never verified (the host fails the query)
+  uint32_t *err;         // pinned host: [0] set when a slot never verified (the host fails the query),
+                         // [kResRejectWord] the slot reads a workgroup rejected (hash mismatch) for a query
   uint32_t first_seq;    // the first query of this launch
   uint32_t idle_ticks;   // s_memrealtime ticks without a post before a workgroup leaves
   uint32_t nthreads, ngroups;
@@ -747,8 +781,9 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
           ns |= __shfl_xor(ns, o);
           nb |= __shfl_xor(nb, o);
         }
-        uint32_t part = 0;
-        const bool sane = ns <= uint32_t(kArgSegs) && nb <= uint32_t(kArgBms);
+        const uint32_t cmd = uint32_t(__builtin_amdgcn_readfirstlane(hq.y));
+        uint32_t p0 = 0, p1 = 0;
+        const bool sane = ns <= uint32_t(kArgSegs) && nb <= uint32_t(kArgBms) && cmd == kResSearch;
 #pragma unroll
         for (uint32_t k = 0; k < (kQuads + 63) / 64; k++) {
           const uint32_t qi = k * 64 + uint32_t(lane);
@@ -759,15 +794,26 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
             const uint32_t wi = qi * 4 + j;
             if (wi < kWords) {
               s_args[wi] = x[j];
-              if (sane && res_word_used(4 * wi, ns, nb)) part += x[j];
+              if (sane && res_word_used(4 * wi, ns, nb)) {
+                p0 += res_mix(x[j], wi, seq, kResKey0);
+                p1 += res_mix(x[j], wi, seq, kResKey1);
+              }
             }
           }
         }
-        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-        const bool vok = hq.y == kResQuit || (sane && part == hq.z);
+        for (int o = 32; o > 0; o >>= 1) {
+          p0 += __shfl_xor(p0, o);
+          p1 += __shfl_xor(p1, o);
+        }
+        p0 += res_mix(cmd, kResCmdWord, seq, kResKey0);
+        p1 += res_mix(cmd, kResCmdWord, seq, kResKey1);
+        const bool vok = (cmd == kResQuit || sane) && p0 == hq.z && p1 == hq.w;
         if (__builtin_amdgcn_readfirstlane(uint32_t(vok))) {
           got = 1;
-          if (lane == 0) s_ctl[0] = hq.y;
+          if (lane == 0) {
+            s_ctl[0] = cmd;
+            if (bad) host_store(R.err + kResRejectWord, bad);
+          }
         } else if (++bad > 4096) {
           got = 3;
         } else {
@@ -794,7 +840,21 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     // scan order whichever wave took which unit.
     const uint32_t nsegs = uint32_t(__builtin_amdgcn_readfirstlane(A.nsegs));
     const uint32_t wq = uint32_t(__builtin_amdgcn_readfirstlane(A.wq)), wr = uint32_t(__builtin_amdgcn_readfirstlane(A.wr));
-    const uint32_t ua = w * wq + min(w, wr), nk = wq + (w < wr ? 1u : 0u);
+    uint32_t ua = w * wq + min(w, wr), nk = wq + (w < wr ? 1u : 0u);
+    if (__builtin_amdgcn_readfirstlane(A.xsplit)) {
+      // XCD-weighted runs (the host's measured per-XCD rates, res_split): workgroup w = 8i + x;
+      // the runs of every workgroup before it, in workgroup order
+      const uint32_t x = w & 7u, i = w >> 3;
+      uint32_t s = 0;
+#pragma unroll
+      for (uint32_t y = 0; y < 8; y++) {
+        const uint32_t n = uint32_t(__builtin_amdgcn_readfirstlane(A.xn[y]));
+        const uint32_t r = uint32_t(__builtin_amdgcn_readfirstlane(A.xr[y]));
+        s += i * n + min(i, r) + (y < x ? n + (i < r ? 1u : 0u) : 0u);
+      }
+      ua = s;
+      nk = uint32_t(__builtin_amdgcn_readfirstlane(A.xn[x])) + (i < uint32_t(__builtin_amdgcn_readfirstlane(A.xr[x])) ? 1u : 0u);
+    }
     const uint32_t rec_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.rec_cap));
     auto rfl = [](uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(v)); };
     const uint32_t dlo = rfl(A.has_min ? A.min32 : 0u), dhi = rfl(A.has_max ? A.max32 : 0xffffffffu);
@@ -981,8 +1041,10 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     // ---- units' counts -> exclusive offsets (s_uc in place), then each unit's records to the
     // host segment at its offset, then the count
     const uint32_t total = s_nrec;
-    {
-      const uint32_t i0 = 2 * uint32_t(tid), i1 = i0 + 1;
+    // (two units per thread per pass: a run longer than 2 x nthreads units takes more passes,
+    // each carrying the previous passes' total)
+    for (uint32_t base = 0, carry = 0; base < nk; base += 2 * nthreads) {
+      const uint32_t i0 = base + 2 * uint32_t(tid), i1 = i0 + 1;
       const uint32_t c0 = i0 < nk ? s_uc[i0] : 0u, c1 = i1 < nk ? s_uc[i1] : 0u;
       const uint32_t mine = c0 + c1;
       uint32_t incl = mine;
@@ -992,12 +1054,17 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
       }
       if (lane == 63) s_wn[wave] = incl;
       __syncthreads();
-      uint32_t woff = 0;
-      for (uint32_t v = 0; v < wave; v++) woff += s_wn[v];
-      const uint32_t ex = woff + incl - mine;
-      __syncthreads();  // (every c0 / c1 read before they are overwritten)
+      uint32_t woff = 0, pass = 0;
+      for (uint32_t v = 0; v < nwv; v++) {
+        const uint32_t t = s_wn[v];
+        if (v < wave) woff += t;
+        pass += t;
+      }
+      const uint32_t ex = carry + woff + incl - mine;
+      __syncthreads();  // (every c0 / c1 / s_wn read before they are overwritten)
       if (i0 < nk) s_uc[i0] = ex;
       if (i1 < nk) s_uc[i1] = ex + c0;
+      carry += pass;
       __syncthreads();
     }
     const uint32_t seg_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.seg_cap));
@@ -1118,12 +1185,131 @@ constexpr size_t kResDoorBytes = 256;  // the doorbell word's page ahead of the 
 // second engine) would wait behind it, so resident launches run only while a context is
 // alone on its device, and opening a second one ends the first one's launch.
 static std::mutex g_ctx_mu;
+// held by context_opened while it ends other contexts' launches and by context_closed before a
+// context leaves the table: a context being shut down is never touched after it left (ADVICE r5;
+// order: g_life_mu, then a context's mu — nothing holding a context's mu takes g_life_mu)
+static std::mutex g_life_mu;
 static std::multimap<int, DeviceCtx *> g_ctxs;
 int contexts_on(int ordinal) {
   std::lock_guard<std::mutex> lk(g_ctx_mu);
   return int(g_ctxs.count(ordinal));
 }
+
+// ---- other processes on the device. A resident launch holds every CU: a second
+// process's kernels on the same GPU would wait behind it until its idle exit, or starve while it
+// stays busy. Each process with a context on a GPU holds an flock on a file of its own named after
+// the GPU's PCI bus id (TSG_COTENANT_DIR, default /dev/shm, else /tmp) and bumps a generation word
+// in a shared page of that GPU; the resident path runs only while no other live process is
+// registered on the GPU, re-counted (a directory scan; a file whose lock can be taken is a dead
+// process's, removed) whenever the generation word has moved. TSG_COTENANT=0: no check.
+struct CoTenant {
+  int refs = 0, gen_fd = -1, live_fd = -1;
+  uint32_t *gen = nullptr;
+  std::string dir, prefix, live_path;
+};
+static std::mutex g_cot_mu;
+static std::map<std::string, CoTenant> g_cot;
+static std::string bus_id(int ordinal) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, ordinal) != hipSuccess) return std::string();
+  for (char *c = bus; *c; c++) *c = char(std::tolower(uint8_t(*c)));
+  return bus;
+}
+static void cotenant_register(DeviceCtx &dc) {
+  if (DeviceCtx::env_u32("TSG_COTENANT", 1, 0, 1) == 0) return;
+  const std::string bus = bus_id(dc.ordinal);
+  if (bus.empty()) return;
+  std::lock_guard<std::mutex> lk(g_cot_mu);
+  CoTenant &ct = g_cot[bus];
+  struct Publish {  // (every context of the GPU in this process reads the same registration)
+    DeviceCtx &dc;
+    CoTenant &ct;
+    ~Publish() {
+      dc.cot_gen = ct.gen;
+      dc.cot_dir = ct.dir;
+      dc.cot_prefix = ct.prefix;
+    }
+  } publish{dc, ct};
+  if (ct.refs++ > 0) return;
+  const char *e = std::getenv("TSG_COTENANT_DIR");
+  ct.dir = e && *e ? e : access("/dev/shm", W_OK) == 0 ? "/dev/shm" : "/tmp";
+  ct.prefix = "tsg-gpu-" + bus + ".";
+  const std::string gpath = ct.dir + "/" + ct.prefix + "gen";
+  ct.gen_fd = open(gpath.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  if (ct.gen_fd < 0) return;
+  (void)fchmod(ct.gen_fd, 0666);  // (another user's process shares the GPU too)
+  struct stat st;
+  if (fstat(ct.gen_fd, &st) == 0 && st.st_size < 4096 && ftruncate(ct.gen_fd, 4096) != 0) {
+    close(ct.gen_fd);
+    ct.gen_fd = -1;
+    return;
+  }
+  void *m = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, ct.gen_fd, 0);
+  if (m == MAP_FAILED) {
+    close(ct.gen_fd);
+    ct.gen_fd = -1;
+    return;
+  }
+  ct.gen = static_cast<uint32_t *>(m);
+  ct.live_path = ct.dir + "/" + ct.prefix + std::to_string(getpid());
+  ct.live_fd = open(ct.live_path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+  if (ct.live_fd >= 0 && flock(ct.live_fd, LOCK_EX | LOCK_NB) != 0) {
+    close(ct.live_fd);
+    ct.live_fd = -1;
+  }
+  __atomic_fetch_add(ct.gen, 1u, __ATOMIC_SEQ_CST);
+}
+static void cotenant_unregister(DeviceCtx &dc) {
+  if (!dc.cot_gen) return;
+  dc.cot_gen = nullptr;
+  const std::string bus = bus_id(dc.ordinal);
+  std::lock_guard<std::mutex> lk(g_cot_mu);
+  auto it = g_cot.find(bus);
+  if (it == g_cot.end() || --it->second.refs > 0) return;
+  CoTenant &ct = it->second;
+  if (ct.live_fd >= 0) {
+    (void)unlink(ct.live_path.c_str());
+    close(ct.live_fd);  // (the lock goes with it)
+  }
+  if (ct.gen) {
+    __atomic_fetch_add(ct.gen, 1u, __ATOMIC_SEQ_CST);
+    munmap(ct.gen, 4096);
+  }
+  if (ct.gen_fd >= 0) close(ct.gen_fd);
+  g_cot.erase(it);
+}
+// other live processes registered on dc's GPU (0 when the check is off or unavailable)
+static int cotenant_others(DeviceCtx &dc) {
+  uint32_t *gen = dc.cot_gen;  // (mapped while this context is registered)
+  if (!gen) return 0;
+  const uint32_t g = __atomic_load_n(gen, __ATOMIC_ACQUIRE);
+  if (dc.res_cotenant >= 0 && g == dc.res_cotenant_gen) return dc.res_cotenant;
+  const std::string &dir = dc.cot_dir, &prefix = dc.cot_prefix, mine = prefix + std::to_string(getpid());
+  int others = 0;
+  if (DIR *d = opendir(dir.c_str())) {
+    while (dirent *de = readdir(d)) {
+      const std::string name = de->d_name;
+      if (name.compare(0, prefix.size(), prefix) != 0 || name == prefix + "gen" || name == mine) continue;
+      const std::string path = dir + "/" + name;
+      const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+      if (fd < 0) continue;
+      if (flock(fd, LOCK_EX | LOCK_NB) == 0) {  // nobody holds it: a process that died registered
+        (void)unlink(path.c_str());
+      } else {
+        others++;
+      }
+      close(fd);
+    }
+    closedir(d);
+  }
+  dc.res_cotenant = others;
+  dc.res_cotenant_gen = g;
+  return others;
+}
+
 void context_opened(DeviceCtx &dc) {
+  cotenant_register(dc);
+  std::lock_guard<std::mutex> life(g_life_mu);
   std::vector<DeviceCtx *> others;
   {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
@@ -1137,13 +1323,17 @@ void context_opened(DeviceCtx &dc) {
   }
 }
 void context_closed(DeviceCtx &dc) {
-  std::lock_guard<std::mutex> lk(g_ctx_mu);
-  auto r = g_ctxs.equal_range(dc.ordinal);
-  for (auto it = r.first; it != r.second; ++it)
-    if (it->second == &dc) {
-      g_ctxs.erase(it);
-      break;
-    }
+  {
+    std::lock_guard<std::mutex> life(g_life_mu);
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    auto r = g_ctxs.equal_range(dc.ordinal);
+    for (auto it = r.first; it != r.second; ++it)
+      if (it->second == &dc) {
+        g_ctxs.erase(it);
+        break;
+      }
+  }
+  cotenant_unregister(dc);
 }
 
 // A query (or a quit) into mailbox slot seq % kResSlots: the argument words the query uses
@@ -1151,30 +1341,61 @@ void context_closed(DeviceCtx &dc) {
 // whose sequence number the kernel polls — write-combined stores drained by sfence, pushed past
 // the host data path by a posted HDP flush (the kernel re-reads a slot whose checksum does not
 // match yet).
+std::atomic<uint32_t> g_res_torn{0};  // test hook (tsg_debug_set "res_torn"): posts left to tear
 static void res_post(DeviceCtx &dc, uint32_t seq, uint32_t cmd, const PoolArgs *PA,
                      const std::vector<std::pair<uint32_t, uint32_t>> *parts) {
   uint8_t *slot = dc.res_mem + kResDoorBytes + size_t(seq % kResSlots) * kResSlotBytes;
-  uint32_t csum = 0;
+  uint32_t h0 = res_mix(cmd, kResCmdWord, seq, kResKey0), h1 = res_mix(cmd, kResCmdWord, seq, kResKey1);
+  const auto *src = reinterpret_cast<const uint8_t *>(PA);
   if (PA) {
-    const auto *src = reinterpret_cast<const uint8_t *>(PA);
     for (const auto &pt : *parts) {
       std::memcpy(slot + kResHdrBytes + pt.first, src + pt.first, pt.second);
       for (uint32_t o = 0; o < pt.second; o += 4) {
         uint32_t v;
         std::memcpy(&v, src + pt.first + o, 4);
-        csum += v;
+        h0 += res_mix(v, (pt.first + o) / 4, seq, kResKey0);
+        h1 += res_mix(v, (pt.first + o) / 4, seq, kResKey1);
       }
     }
   }
+  // test hook: the slot as a read that caught the host's writes half landed would see it — two
+  // used words moved by +-d (the plain sum of the words unchanged: the additive check of round 5
+  // accepted it) — repaired after 200 us; the kernel must re-read, not run it
+  uint32_t torn = g_res_torn.load(std::memory_order_relaxed);
+  const bool tear = PA && cmd == kResSearch && torn && g_res_torn.compare_exchange_strong(torn, torn - 1);
+  const uint32_t o_s = uint32_t(offsetof(PoolArgs, start_s)), o_e = uint32_t(offsetof(PoolArgs, end_s));
+  if (tear) {
+    uint32_t a, b;
+    std::memcpy(&a, src + o_s, 4);
+    std::memcpy(&b, src + o_e, 4);
+    a += 0x01000000u;
+    b -= 0x01000000u;
+    std::memcpy(slot + kResHdrBytes + o_s, &a, 4);
+    std::memcpy(slot + kResHdrBytes + o_e, &b, 4);
+  }
   __builtin_ia32_sfence();
-  const ResHeader h{seq, cmd, csum, 0};
-  std::memcpy(slot, &h, sizeof h);
+  // the header's check words, then (after an sfence: posted writes arrive in order) its sequence
+  // number, so a read that sees the new seq sees the new check words with it
+  const ResHeader h{seq - 1, cmd, h0, h1};
+  std::memcpy(slot + 4, reinterpret_cast<const uint8_t *>(&h) + 4, sizeof h - 4);
+  __builtin_ia32_sfence();
+  std::memcpy(slot, &seq, 4);
   __builtin_ia32_sfence();
   aql_hdp_flush(dc.aql);
+  if (tear) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200)) __builtin_ia32_pause();
+    std::memcpy(slot + kResHdrBytes + o_s, src + o_s, 4);
+    std::memcpy(slot + kResHdrBytes + o_e, src + o_e, 4);
+    __builtin_ia32_sfence();
+    aql_hdp_flush(dc.aql);
+  }
 }
 
-// A resident launch of kernel `sym` serving queries from first_seq on. false: unavailable.
-static bool resident_launch(DeviceCtx &dc, const std::string &sym, uint32_t threads, uint32_t W) {
+// A resident launch of kernel `sym` serving queries from `first_seq` on. false: unavailable.
+// `profiled`: the dispatch gets a completion signal with dispatch timestamps of its own
+// (tsg_search_batch: the launch's device time, the clock rocprofv3's kernel trace reads).
+static bool resident_launch(DeviceCtx &dc, const std::string &sym, uint32_t threads, uint32_t W, uint32_t first_seq) {
   if (!dc.res_mem) {
     void *p = nullptr;
     const size_t bytes = kResDoorBytes + size_t(kResSlots) * kResSlotBytes;
@@ -1186,23 +1407,28 @@ static bool resident_launch(DeviceCtx &dc, const std::string &sym, uint32_t thre
   }
   const AqlKernel ak = aql_kernel(dc.aql, sym.c_str(), uint32_t(sizeof(ResidentArgs)));
   if (!ak.kobj) return false;
-  dc.res_host.ensure(64 + size_t(W) * 16);
+  dc.res_host.ensure(64);
   auto *err = static_cast<uint32_t *>(dc.res_host.p);
   __atomic_store_n(err, 0u, __ATOMIC_RELEASE);
   ResidentArgs RA{};
   RA.door = reinterpret_cast<const uint32_t *>(dc.res_mem);
   RA.slots = dc.res_mem + kResDoorBytes;
   RA.err = err;
-  RA.first_seq = dc.res_seq + 1;
+  RA.first_seq = first_seq;
   RA.idle_ticks = DeviceCtx::env_u32("TSG_RESIDENT_IDLE_US", 10000, 100, 10000000) * 100u;  // (s_memrealtime: 100 MHz)
   RA.nthreads = threads;
   RA.ngroups = W;
   RA.mode = DeviceCtx::env_u32("TSG_RES_MODE", 0, 0, 255);
   const std::vector<std::pair<uint32_t, uint32_t>> parts{{0u, uint32_t(sizeof RA)}};
   constexpr size_t kPoolLds = 96 << 10;
-  aql_dispatch(dc.aql, ak, W, threads, uint32_t(kPoolLds), &RA, parts, false);
+  const bool prof = dc.res_profile_next;
+  dc.res_profile_next = false;
+  const int ps = aql_dispatch(dc.aql, ak, W, threads, uint32_t(kPoolLds), &RA, parts, prof);
+  if (prof) dc.res_profile_slot = ps;
   dc.res_alive = true;
   dc.res_kernel = sym;
+  dc.res_threads = threads;
+  dc.res_groups = W;
   dc.res_epoch = dc.mem_epoch;
   dc.res_launches++;
   return true;
@@ -1215,10 +1441,11 @@ void resident_quit(DeviceCtx &dc) {
   const uint32_t seq = ++dc.res_seq;
   res_post(dc, seq, kResQuit, nullptr, nullptr);
   dc.res_quits++;
+  // (the launch serves every query posted before the quit first: their callers may be waiting)
   const auto t0 = std::chrono::steady_clock::now();
   while (!aql_done(dc.aql)) {
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
-      fail(TSG_E_DEVICE, "resident search kernel did not leave after a quit (2 s)");
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+      fail(TSG_E_DEVICE, "resident search kernel did not leave after a quit (5 s)");
     __builtin_ia32_pause();
   }
 }
@@ -1228,17 +1455,209 @@ void resident_release(DeviceCtx &dc) {
   if (dc.res_mem) (void)hipFree(dc.res_mem);
   dc.res_mem = nullptr;
   dc.res_host.release();
+  for (auto &a : dc.res_areas) a.buf.release();
+  dc.res_areas.clear();
+  for (auto &b : dc.res_quarantine) b.release();
+  dc.res_quarantine.clear();
+}
+
+uint64_t resident_batch_begin(DeviceCtx &dc) {
+  std::lock_guard<std::mutex> lk(dc.mu);
+  resident_quit(dc);
+  dc.res_profile_next = true;
+  dc.res_profile_slot = -1;
+  return dc.res_launches;
+}
+uint64_t resident_batch_end(DeviceCtx &dc, uint64_t launches_before) {
+  std::lock_guard<std::mutex> lk(dc.mu);
+  const bool one = dc.res_launches == launches_before + 1 && dc.res_profile_slot >= 0;
+  resident_quit(dc);  // (the dispatch completes: its end timestamp is written)
+  dc.res_profile_next = false;
+  const uint64_t ns = one && dc.aql ? aql_time_ns(dc.aql, dc.res_profile_slot) : 0;
+  dc.res_profile_slot = -1;
+  return ns;
+}
+static std::atomic<uint32_t> g_groups{0};
+static std::atomic<bool> g_xsplit{DeviceCtx::env_u32("TSG_RES_XSPLIT", 1, 0, 1) != 0};
+uint32_t debug_groups() { return g_groups.load(std::memory_order_relaxed); }
+bool debug_xsplit() { return g_xsplit.load(std::memory_order_relaxed); }
+int debug_set(const char *name, int64_t value) {
+  if (!name) return TSG_E_INVALID;
+  if (!std::strcmp(name, "res_torn")) {
+    g_res_torn.store(uint32_t(std::max<int64_t>(0, value)));
+    return TSG_OK;
+  }
+  if (!std::strcmp(name, "groups")) {
+    g_groups.store(uint32_t(std::min<int64_t>(4096, std::max<int64_t>(0, value))));
+    return TSG_OK;
+  }
+  if (!std::strcmp(name, "xsplit")) {
+    g_xsplit.store(value != 0);
+    return TSG_OK;
+  }
+  return TSG_E_INVALID;
+}
+
+// A query's result area (pinned, device-written): [256 B header | counts, cstride words per
+// workgroup | stamps, 2 x u64 per workgroup | records, seg_cap per workgroup]. Queries in flight
+// at once (concurrent callers, tsg_search_batch) hold one each; an area is reused only after its
+// query's records were read.
+static constexpr uint32_t kResCountStride = 16;  // one 64-byte line per workgroup's count
+static size_t res_area_bytes(uint32_t W, uint32_t seg) {
+  return 256 + align_up(size_t(W) * 4 * kResCountStride, 256) + align_up(size_t(W) * 16, 256) +
+         size_t(W) * seg * sizeof(MatchRec);
+}
+
+// The oldest posted query whose counts are not all in, when the launch is gone (it left on its
+// idle timeout just as queries were posted): launched again from that query with its kernel; it
+// serves the posted queries from their slots (identical results). Queries that completed are never
+// served again: their areas may have been reused. Caller holds dc.mu.
+static void res_relaunch_inflight(DeviceCtx &dc) {
+  if (!dc.aql || !aql_done(dc.aql)) return;
+  for (const auto &kv : dc.res_inflight) {
+    const DeviceCtx::ResArea &a = dc.res_areas[kv.second];
+    const auto *counts = reinterpret_cast<const uint32_t *>(static_cast<const uint8_t *>(a.buf.p) + 256);
+    bool complete = true;
+    for (uint32_t w = 0; w < a.W && complete; w++)
+      complete = __atomic_load_n(counts + size_t(w) * kResCountStride, __ATOMIC_ACQUIRE) != kCountPending;
+    if (complete) continue;
+    if (!resident_launch(dc, a.sym, dc.res_threads ? dc.res_threads : kResThreads, a.W, kv.first))
+      fail(TSG_E_DEVICE, "resident search relaunch failed");
+    dc.res_relaunches++;
+    return;
+  }
+}
+
+// Wait, with dc.mu released, until pred() holds (pred is evaluated with dc.mu held).
+template <class P>
+static void res_wait_unlocked(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, P &&pred, const char *what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!pred()) {
+    res_relaunch_inflight(dc);
+    lk.unlock();
+    for (int i = 0; i < 64; i++) __builtin_ia32_pause();
+    std::this_thread::yield();
+    lk.lock();
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) fail(TSG_E_DEVICE, what);
+  }
+}
+
+// The XCD-weighted split of U units over W workgroups (W = 8 x G): XCD x's share of the units from
+// the measured rates (res_xf), each XCD's share even over its G workgroups. Off (even runs) for
+// small queries, W not a multiple of 8, or TSG_RES_XSPLIT=0.
+static void res_split(const DeviceCtx &dc, PoolArgs &PA, uint32_t U, uint32_t W) {
+  PA.xsplit = 0;
+  if (!debug_xsplit() || W % 8 || U < 16u * W) return;
+  const uint32_t G = W / 8;
+  uint32_t T[8], sum = 0;
+  for (int x = 0; x < 8; x++) {
+    T[x] = uint32_t(double(U) * dc.res_xf[x]);
+    sum += T[x];
+  }
+  for (int x = 0; sum < U; x = (x + 1) & 7, sum++) T[x]++;  // (rounding: a unit each, in XCD order)
+  for (int x = 0; x < 8 && sum > U; x = (x + 1) & 7)
+    if (T[x]) T[x]--, sum--;
+  for (int x = 0; x < 8; x++) {
+    PA.xn[x] = T[x] / G;
+    PA.xr[x] = T[x] % G;
+  }
+  PA.xsplit = 1;
+}
+static uint32_t res_max_run(const PoolArgs &PA, uint32_t U, uint32_t W) {
+  if (!PA.xsplit) return (U + W - 1) / W;
+  uint32_t m = 0;
+  for (int x = 0; x < 8; x++) m = std::max(m, PA.xn[x] + (PA.xr[x] ? 1u : 0u));
+  return m;
+}
+
+// One query's workgroup stamps {seen, end} -> the XCDs' shares for the next queries. XCD x's
+// workgroups took E_x (mean end after the first seen) for n_x units; its rate n_x / (E_x - c) with
+// c ~ 2 us of fixed cost (first loads, output) moves the shares toward equal ends — the fixed point
+// of the update is E_x equal whatever c is. Shares are smoothed (half old, half new) and kept
+// within +-15 % of even. Queries below 32 units per workgroup are not used (their ends are fixed cost).
+static void res_calibrate(DeviceCtx &dc, const unsigned long long *qst, const PoolArgs &PA, uint32_t U, uint32_t W) {
+  if (W % 8 || U < 32u * W) return;
+  unsigned long long lo = ~0ull;
+  for (uint32_t w = 0; w < W; w++) lo = std::min(lo, qst[2 * w]);
+  double E[8] = {}, n[8] = {};
+  uint32_t cnt[8] = {};
+  for (uint32_t w = 0; w < W; w++) {
+    const uint32_t x = w & 7u, i = w >> 3;
+    const unsigned long long e = qst[2 * w + 1];
+    if (e < lo || e - lo > 100000000ull) return;  // (a stamp not written: skip the sample)
+    E[x] += double(e - lo);
+    n[x] += PA.xsplit ? double(PA.xn[x] + (i < PA.xr[x] ? 1u : 0u)) : double(PA.wq + (w < PA.wr ? 1u : 0u));
+    cnt[x]++;
+  }
+  double r[8], rs = 0;
+  for (int x = 0; x < 8; x++) {
+    if (!cnt[x]) return;
+    const double ex = E[x] / cnt[x], nx = n[x] / cnt[x];
+    r[x] = nx / std::max(ex - 200.0, 0.25 * ex);  // (100 MHz ticks: 200 = 2 us)
+    rs += r[x];
+  }
+  double fs = 0;
+  for (int x = 0; x < 8; x++) {
+    const double f = 0.5 * dc.res_xf[x] + 0.5 * r[x] / rs;
+    dc.res_xf[x] = std::min(0.125 * 1.15, std::max(0.125 * 0.85, f));
+    fs += dc.res_xf[x];
+  }
+  for (int x = 0; x < 8; x++) dc.res_xf[x] /= fs;
+  dc.res_xsamples++;
 }
 
 // The resident path of pool_search: 1 = served (out filled), 0 = the records overflowed (the
-// caller runs the segment / look-back path), -1 = not available (normal launches).
-static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSeg> &segs,
-                           const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q, uint32_t limit,
-                           uint32_t flags, bool has_dur, uint32_t threads, uint32_t W, uint32_t rec_cap, Tracer &tr,
-                           SearchOut &out) {
+// caller runs the segment / look-back path), -1 = not available (normal launches). dc.mu (lk) is
+// released while the query runs: other callers plan and post their queries meanwhile, and the
+// launch serves them back to back.
+static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, PoolArgs &PA,
+                           const std::vector<ScanSeg> &segs, const std::vector<std::pair<uint32_t, Block *>> &blocks,
+                           const tsg_query &q, uint32_t limit, uint32_t flags, bool has_dur, uint32_t threads,
+                           uint32_t W, uint32_t rec_cap, Tracer &tr, SearchOut &out) {
   const std::string sym = resident_symbol(q.nterms, has_dur, q.has_range, dc.pool_nt);
-  if (dc.res_alive && (aql_done(dc.aql) || dc.res_kernel != sym || dc.res_epoch != dc.mem_epoch)) resident_quit(dc);
-  if (!dc.res_alive && !resident_launch(dc, sym, threads, W)) return -1;
+  const uint32_t U = PA.units;
+  res_split(dc, PA, U, W);
+  if (res_max_run(PA, U, W) > kResMaxUnits) return -1;
+  // a free result area (D = TSG_RES_DEPTH queries in flight; a caller beyond that waits for one)
+  static const uint32_t depth = DeviceCtx::env_u32("TSG_RES_DEPTH", 16, 1, kResSlots - 1);
+  if (dc.res_areas.size() < depth) dc.res_areas.resize(depth);
+  auto free_area = [&]() -> int {
+    for (size_t i = 0; i < dc.res_areas.size(); i++)
+      if (!dc.res_areas[i].busy) return int(i);
+    return -1;
+  };
+  if (free_area() < 0)
+    res_wait_unlocked(dc, lk, [&] { return free_area() >= 0; }, "resident search: no result area freed (5 s)");
+  const int ai = free_area();
+  DeviceCtx::ResArea &area = dc.res_areas[size_t(ai)];
+  area.busy = true;
+  area.sym = sym;
+  area.W = W;
+  struct AreaRelease {  // (the area and the in-flight entry go back on every exit; under dc.mu)
+    DeviceCtx &dc;
+    DeviceCtx::ResArea &area;
+    std::unique_lock<std::mutex> &lk;
+    uint32_t seq = 0;
+    bool posted = false;
+    ~AreaRelease() {
+      if (!lk.owns_lock()) lk.lock();
+      if (posted) dc.res_inflight.erase(seq);
+      area.busy = false;
+    }
+  } rel{dc, area, lk};
+  // the live launch must serve this shape from the next sequence number: another shape, new
+  // block memory, or a launch that left, and no query of another caller still in flight ->
+  // quit / launch; queries in flight are served first (a quit is posted behind them)
+  for (;;) {
+    const bool dead = dc.res_alive && aql_done(dc.aql);
+    if (dc.res_alive && !dead && dc.res_kernel == sym && dc.res_groups == W && dc.res_epoch == dc.mem_epoch) break;
+    if (dc.res_inflight.empty()) {
+      resident_quit(dc);
+      if (!resident_launch(dc, sym, threads, W, dc.res_seq + 1)) return -1;
+      break;
+    }
+    res_wait_unlocked(dc, lk, [&] { return dc.res_inflight.empty(); }, "resident search: queries in flight never completed (5 s)");
+  }
   const uint32_t nsegs = PA.nsegs, nbms = PA.nbms;
   // the argument words this query uses (res_word_used)
   thread_local std::vector<std::pair<uint32_t, uint32_t>> parts;
@@ -1251,32 +1670,39 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
   parts.push_back({uint32_t(offsetof(PoolArgs, nsegs)), uint32_t(sizeof(PoolArgs) - offsetof(PoolArgs, nsegs))});
   hipEvent_t e0, e1;
   const bool timed = (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
-  // counts a cache line apart (TSG_RES_CSTRIDE, u32 units: 16 = one line per workgroup; 1 = packed)
-  static const uint32_t cs = DeviceCtx::env_u32("TSG_RES_CSTRIDE", 16, 1, 64);
-  const size_t hdr = 256, cntb = align_up(size_t(W) * 4 * cs, 256);
-  auto *qst = reinterpret_cast<unsigned long long *>(static_cast<uint8_t *>(dc.res_host.p) + 64);
+  const size_t tslot = timed ? dc.tring_used - 1 : 0;
+  // workgroup stamps: timed queries, and every 16th query for the XCD split (the first 8 all)
+  const bool stamp = timed || (debug_xsplit() && (dc.res_xsamples < 8 || dc.res_qn % 16 == 0));
+  dc.res_qn++;
+  const uint32_t cs = kResCountStride;
+  const size_t hdr = 256, cntb = align_up(size_t(W) * 4 * cs, 256), stb = align_up(size_t(W) * 16, 256);
   uint32_t *counts = nullptr;
+  unsigned long long *qst = nullptr;
   const uint8_t *recs = nullptr;
   auto post = [&] {
     PA.seg_cap = dc.pool_seg;
-    dc.hres.ensure(hdr + cntb + size_t(W) * PA.seg_cap * sizeof(MatchRec));
-    uint8_t *base = static_cast<uint8_t *>(dc.hres.p);
+    area.buf.ensure(res_area_bytes(W, PA.seg_cap));
+    uint8_t *base = static_cast<uint8_t *>(area.buf.p);
     counts = reinterpret_cast<uint32_t *>(base + hdr);
-    recs = base + hdr + cntb;
+    qst = reinterpret_cast<unsigned long long *>(base + hdr + cntb);
+    recs = base + hdr + cntb + stb;
     PA.counts = counts;
-    PA.recs = base + hdr + cntb;
+    PA.recs = base + hdr + cntb + stb;
     PA.err = reinterpret_cast<uint32_t *>(base);
-    PA.qstamps = timed ? qst : nullptr;
+    PA.qstamps = stamp ? qst : nullptr;
     PA.cstride = cs;
     for (uint32_t w = 0; w < W; w++) counts[size_t(w) * cs] = kCountPending;
-    res_post(dc, ++dc.res_seq, kResSearch, &PA, &parts);
+    if (rel.posted) dc.res_inflight.erase(rel.seq);
+    rel.seq = ++dc.res_seq;
+    rel.posted = true;
+    dc.res_inflight[rel.seq] = uint32_t(ai);
+    res_post(dc, rel.seq, kResSearch, &PA, &parts);
     dc.res_queries++;
   };
-  // every workgroup's count (stored after its records); a launch that ends first (it left on
-  // an idle timeout just as this query was posted) is launched again: it serves the posted
-  // query from its slot
+  // every workgroup's count (stored after its records), with dc.mu released; a launch that ended
+  // first (it left on an idle timeout just as this query was posted) is launched again from the
+  // oldest query not served (res_relaunch_inflight)
   auto wait = [&] {
-    const uint32_t seq = dc.res_seq;
     const auto t0 = std::chrono::steady_clock::now();
     const bool prof = prof_on();
     thread_local std::vector<uint8_t> seen;
@@ -1284,7 +1710,8 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
     uint32_t lo = 0, nseen = 0;
     const uint32_t seg = PA.seg_cap;
     static const bool prefetch = DeviceCtx::env_u32("TSG_RES_PREFETCH", 1, 0, 1) != 0;
-    for (uint32_t it = 1, relaunches = 0;; it++) {
+    lk.unlock();
+    for (uint32_t it = 1;; it++) {
       // counts not seen yet; a finished workgroup's records are pulled into this core's
       // caches while the others still run (the copy after the wait then hits them)
       for (uint32_t w = lo; w < W; w++) {
@@ -1307,33 +1734,23 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
       if (lo == W) {
         if (prof)
           prof_add("res.last_count", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        lk.lock();
         return;
       }
-      if ((it & 0xfffffu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+      if ((it & 0xfffffu) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        lk.lock();
         fail(TSG_E_DEVICE, "resident search: no answer in 5 s");
-      if ((it & 255u) == 0 && aql_done(dc.aql)) {
-        bool all = true;
-        for (uint32_t w = 0; w < W && all; w++) all = __atomic_load_n(counts + size_t(w) * cs, __ATOMIC_ACQUIRE) != kCountPending;
-        if (all) return;
+      }
+      if ((it & 255u) == 0) {
+        lk.lock();
         if (__atomic_load_n(static_cast<uint32_t *>(dc.res_host.p), __ATOMIC_ACQUIRE))
           fail(TSG_E_DEVICE, "resident search: a mailbox slot never verified");
-        if (++relaunches > 2) fail(TSG_E_DEVICE, "resident search kernel ended without serving the query");
-        for (uint32_t w2 = 0; w2 < W; w2++) counts[size_t(w2) * cs] = kCountPending;
-        seen.assign(W, 0);
-        lo = 0;
-        dc.res_seq = seq - 1;  // (the launch's first query is the posted one)
-        if (!resident_launch(dc, dc.res_kernel, threads, W)) fail(TSG_E_DEVICE, "resident search relaunch failed");
-        dc.res_seq = seq;
-        dc.res_relaunches++;
+        res_relaunch_inflight(dc);
+        lk.unlock();
       }
       __builtin_ia32_pause();
     }
   };
-  tr.mark("plan");
-  post();
-  tr.mark("search");
-  wait();
-  tr.mark("sync");
   auto scan = [&](uint64_t &total, uint32_t &maxc) {
     total = 0;
     maxc = 0;
@@ -1343,25 +1760,48 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
     }
   };
   uint64_t total = 0;
-  uint32_t maxc = 0;
-  scan(total, maxc);
-  uint32_t reruns = 0;
-  // a workgroup's records exceed its host segment: a larger segment and the query again; more
-  // than its LDS regions hold: the other paths
-  while (maxc > std::min(PA.seg_cap, rec_cap)) {
-    if (maxc > rec_cap) {
-      dc.pool_skip = 16;
-      return 0;
-    }
-    uint32_t want = 2 * PA.seg_cap;
-    while (want < maxc) want <<= 1;
-    dc.pool_seg = std::min(want, rec_cap);
+  uint32_t maxc = 0, reruns = 0;
+  try {
+    tr.mark("plan");
     post();
+    tr.mark("search");
     wait();
-    reruns++;
+    tr.mark("sync");
     scan(total, maxc);
+    // a workgroup's records exceed its host segment: a larger segment and the query again; more
+    // than its LDS regions hold: the other paths
+    while (maxc > std::min(PA.seg_cap, rec_cap)) {
+      if (maxc > rec_cap) {
+        dc.pool_skip = 16;
+        return 0;
+      }
+      uint32_t want = 2 * PA.seg_cap;
+      while (want < maxc) want <<= 1;
+      dc.pool_seg = std::min(want, rec_cap);
+      post();
+      wait();
+      reruns++;
+      scan(total, maxc);
+    }
+  } catch (...) {
+    //  the launch may still write into this area: it is set aside until shutdown, the
+    // launch is ended (bounded) and the next query starts a new one
+    if (!lk.owns_lock()) lk.lock();
+    dc.res_quarantine.push_back(area.buf);
+    area.buf = DeviceCtx::ResArea().buf;
+    try {
+      resident_quit(dc);
+    } catch (...) {
+    }
+    dc.res_alive = false;
+    throw;
   }
+  if (const uint32_t rj = __atomic_exchange_n(static_cast<uint32_t *>(dc.res_host.p) + kResRejectWord, 0u, __ATOMIC_ACQ_REL))
+    dc.res_rejects += rj;
   if (dc.pool_seg > 32 && uint64_t(maxc) * 8 < dc.pool_seg) dc.pool_seg >>= 1;
+  if (stamp) {
+    if (debug_xsplit()) res_calibrate(dc, qst, PA, U, W);
+  }
   if (timed) {  // the query's span on the device: first workgroup to see it .. last to finish
     unsigned long long lo = ~0ull, hi = 0;
     for (uint32_t w = 0; w < W; w++) {
@@ -1389,11 +1829,12 @@ static int resident_search(DeviceCtx &dc, PoolArgs &PA, const std::vector<ScanSe
                    sn[W / 2], sn[W * 9 / 10], sn[W - 1], en[0], en[W / 10], en[W / 2], en[W * 9 / 10], en[W - 1]);
     }
     if (dc.tring_res.size() < dc.tring_used) dc.tring_res.resize(dc.tring_used);
-    dc.tring_aql[dc.tring_used - 1] = -3;
-    dc.tring_res[dc.tring_used - 1] = hi > lo ? (hi - lo) * 10ull : 0ull;  // (100 MHz ticks)
+    dc.tring_aql[tslot] = -3;
+    dc.tring_res[tslot] = hi > lo ? (hi - lo) * 10ull : 0ull;  // (100 MHz ticks)
   }
   out.kernel_ns = out.scan_ns = 0;
   out.reruns = reruns;
+  out.resident = true;
   tr.mark("events");
   // records: the segments in workgroup order are the reference order (static runs, each
   // wave's matches in scan order); a limit keeps each block part's first L
@@ -1444,7 +1885,8 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
                  uint32_t limit, uint32_t flags, const std::vector<ScanSeg> &segs, const std::vector<NarrowSeg> &nsegv,
                  const std::vector<std::array<uint32_t, 8>> &nbms,
                  const std::vector<std::array<uint8_t, kArgTerms>> &nbmi,
-                 const std::vector<const DevBlockDesc *> &seg_desc, bool has_dur, Tracer &tr, SearchOut &out) {
+                 const std::vector<const DevBlockDesc *> &seg_desc, bool has_dur, Tracer &tr, SearchOut &out,
+                 std::unique_lock<std::mutex> &lk) {
   hipStream_t s = dc.stream;
   const uint32_t nsegs = uint32_t(segs.size()), W = uint32_t(dc.num_cu);
   PoolArgs PA;
@@ -1546,12 +1988,19 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   const bool time_all = flags & TSG_SEARCH_TIME_ALL, time_scan = flags & (TSG_SEARCH_TIME_SCAN | TSG_SEARCH_TIME_ALL);
   // the resident kernel serves the query when it can (the only context on the device, no
   // per-call HIP events or stamps asked for); otherwise the queue and the CUs are freed first
+  // (and no other process has a context on the GPU: cotenant_others)
   if (dc.res_on && dc.aql && !want_stamps && !time_scan && (U + W - 1) / W <= kResMaxUnits &&
       contexts_on(dc.ordinal) == 1) {
-    const int r = resident_search(dc, PA, segs, blocks, q, limit, flags, has_dur, kResThreads, W, rec_cap, tr, out);
-    if (r >= 0) return r == 1;
+    if (cotenant_others(dc) == 0) {
+      const int r = resident_search(dc, lk, PA, segs, blocks, q, limit, flags, has_dur, kResThreads, W, rec_cap, tr, out);
+      if (r >= 0) return r == 1;
+    } else {
+      dc.res_cotenant_queries++;
+      out.path |= TSG_PATH_COTENANT;
+    }
   }
   resident_quit(dc);
+  dc.res_plain_queries++;
   hipEvent_t e0 = dc.es0, e1 = dc.es1;
   const bool defer = !time_scan && (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
   uint32_t *counts = nullptr;

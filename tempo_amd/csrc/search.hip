@@ -1752,14 +1752,18 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   Tracer tr;
   out.compact = false;
   out.pos.clear();
-  std::lock_guard<std::mutex> lk(dc.mu);
+  out.resident = false;
+  out.path = 0;
+  // (a resident-kernel query releases dc.mu while it runs: other callers post theirs meanwhile)
+  std::unique_lock<std::mutex> lk(dc.mu);
   HIP_OK(hipSetDevice(dc.ordinal));
   hipStream_t s = dc.stream;
-  if (dc.num_cu == 0) {
+  if (dc.dev_cu == 0) {
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dc.ordinal));
-    dc.num_cu = prop.multiProcessorCount;
+    dc.dev_cu = prop.multiProcessorCount;
   }
+  dc.num_cu = debug_groups() ? int(debug_groups()) : dc.dev_cu;
 
   // ---- plan (scratch vectors kept per thread: no allocation per query once warm)
   struct PlanScratch {
@@ -2065,13 +2069,15 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   const bool ds16 = (!q.has_min || q.min_ns <= kDs16MaxMs * 1000000ull) && (!q.has_max || q.max_ns <= kDs16MaxMs * 1000000ull);
   if (fast && narrow && ds16 && !dc.seg_off && !dc.pool_off) {
     if (dc.pool_skip) dc.pool_skip--;
-    else if (pool_search(dc, blocks, q, limit, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out)) {
+    else if (pool_search(dc, blocks, q, limit, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out, lk)) {
       if (ranges) drop_before_ranges(blocks, *ranges, out);
       out.pool = true;
+      out.path |= out.resident ? TSG_PATH_RESIDENT : TSG_PATH_PLAIN;
       return;
     }
   }
   resident_quit(dc);  // (the other paths' kernels need the CUs the resident search launch holds)
+  out.path |= TSG_PATH_OTHER;
   const FastFn fast_seg = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, true) : nullptr;
   const FastFn fast_lb = fast ? pick_fast(q.nterms, has_dur, q.has_range, all_w1, false) : nullptr;
   const void *kfn = fast ? reinterpret_cast<const void *>(seg ? fast_seg : fast_lb)

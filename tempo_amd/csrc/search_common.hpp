@@ -143,6 +143,7 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
                  uint32_t limit, uint32_t flags, const std::vector<ScanSeg> &segs, const std::vector<NarrowSeg> &nsegv,
                  const std::vector<std::array<uint32_t, 8>> &nbms,
                  const std::vector<std::array<uint8_t, kArgTerms>> &nbmi,
-                 const std::vector<const DevBlockDesc *> &seg_desc, bool has_dur, Tracer &tr, SearchOut &out);
+                 const std::vector<const DevBlockDesc *> &seg_desc, bool has_dur, Tracer &tr, SearchOut &out,
+                 std::unique_lock<std::mutex> &lk);
 
 }  // namespace tsg

@@ -43,6 +43,11 @@ SEARCH_TIME_SCAN = 1  # tsg_search_opts.flags: HIP events around the scan kernel
 SEARCH_TIME_ALL = 2   # ... and around the whole device sequence
 SEARCH_TIME_DEFER = 4  # events around the search kernel, read later by Engine.kernel_times()
 
+PATH_RESIDENT = 1  # tsg_metrics.path (ABI 7): search_resident_kernel served (part of) the search
+PATH_PLAIN = 2     # search_pool_kernel / search_static_kernel as plain launches
+PATH_OTHER = 4     # search_fast_kernel, the dictionary pass, the general path
+PATH_COTENANT = 8  # the resident kernel declined: another process has a context on the GPU
+
 
 class TsgError(RuntimeError):
     def __init__(self, code, msg):
@@ -75,7 +80,8 @@ class _Metrics(C.Structure):
     _fields_ = [("traces_inspected", C.c_uint32), ("blocks_inspected", C.c_uint32),
                 ("blocks_skipped", C.c_uint32), ("reruns", C.c_uint32), ("bytes_inspected", C.c_uint64),
                 ("device_bytes_read", C.c_uint64), ("kernel_ns", C.c_uint64),
-                ("scan_kernel_ns", C.c_uint64), ("scan_bytes", C.c_uint64)]
+                ("scan_kernel_ns", C.c_uint64), ("scan_bytes", C.c_uint64),
+                ("path", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class _Result(C.Structure):
@@ -93,6 +99,10 @@ class _Result(C.Structure):
 class _SearchOpts(C.Structure):
     _fields_ = [("limit", C.c_uint32), ("flags", C.c_uint32), ("query_id", C.c_uint64),
                 ("seen_ids", C.c_void_p), ("nseen", C.c_uint64)]
+
+
+class _SearchItem(C.Structure):
+    _fields_ = [("blocks", C.c_void_p), ("nblocks", C.c_size_t), ("query", C.c_void_p), ("opts", _SearchOpts)]
 
 
 class _BlockInfo(C.Structure):
@@ -150,7 +160,7 @@ EXPORTED = [
     "tsg_proto_search", "tsg_proto_result_free", "tsg_go_parse", "tsg_write_v2_block",
     "tsg_write_search_block", "tsg_write_wal_search", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
     "tsg_synth_v2_block", "tsg_live_block_open_mem", "tsg_search_tags", "tsg_search_tag_values",
-    "tsg_result_pack", "tsg_wire_merge",
+    "tsg_result_pack", "tsg_wire_merge", "tsg_search_batch", "tsg_debug_set",
 ]
 
 _lib = None
@@ -199,6 +209,9 @@ def lib():
         L.tsg_search.argtypes = [vp, C.POINTER(vp), C.c_size_t, C.POINTER(_Query), C.POINTER(_SearchOpts),
                                  C.POINTER(C.POINTER(_Result))]
         L.tsg_result_free.argtypes = [C.POINTER(_Result)]
+        L.tsg_search_batch.argtypes = [vp, C.POINTER(_SearchItem), C.c_size_t, C.c_uint32,
+                                       C.POINTER(C.POINTER(_Result)), C.POINTER(C.c_uint64)]
+        L.tsg_debug_set.argtypes = [C.c_char_p, C.c_int64]
         L.tsg_kernel_times.argtypes = [vp, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_size_t)]
         L.tsg_results_combine.argtypes = [C.POINTER(_Result), C.c_uint32, C.POINTER(C.POINTER(_Result))]
         L.tsg_v2block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]
@@ -357,6 +370,7 @@ class SearchMetrics:
     block_errors: List[Optional[str]] = field(default_factory=list)
     skipped_traces: int = 0  # SearchMetrics.SkippedTraces (the proto path's MaxBytes skips; 0 here)
     reruns: int = 0  # extra launches after a record overflow (tsg_metrics.reruns)
+    path: int = 0  # PATH_* bits of the kernels that served the search (tsg_metrics.path, ABI 7)
 
 
 def _unpack(rp) -> (List[TraceSearchMetadata], SearchMetrics):
@@ -377,7 +391,7 @@ def _unpack(rp) -> (List[TraceSearchMetadata], SearchMetrics):
     errs = [r.block_error[i].decode(errors="replace") if st[i] else None for i in range(r.nblocks)]
     return out, SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,
                               m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes, st, errs,
-                              reruns=m.reruns)
+                              reruns=m.reruns, path=m.path)
 
 
 # ---------------------------------------------------------------------------
@@ -446,6 +460,46 @@ class Engine:
         finally:
             lib().tsg_result_free(rp)
 
+    def search_batch(self, items, depth: int = 0, unpack: bool = True):
+        """tsg_search_batch: items = [(blocks, pipeline[, limit]), ...], served back to back (the
+        resident kernel takes the next query while earlier ones run). Returns (results, device_ns):
+        results[i] = (matches, SearchMetrics) as Engine.search returns them (unpack=False: (match
+        count, SearchMetrics)); device_ns = the batch's resident launch's dispatch duration (0 when
+        the batch did not run on one resident launch per device)."""
+        n = len(items)
+        keep = []
+        arr = (_SearchItem * max(n, 1))()
+        for i, it in enumerate(items):
+            blocks, pipeline = it[0], it[1]
+            limit = it[2] if len(it) > 2 else 0
+            ba = (C.c_void_p * max(len(blocks), 1))(*[b.h.value for b in blocks])
+            keep.append(ba)
+            arr[i].blocks = C.cast(ba, C.c_void_p).value
+            arr[i].nblocks = len(blocks)
+            arr[i].query = pipeline.query_addr
+            arr[i].opts = _SearchOpts(limit=limit)
+        outs = (C.POINTER(_Result) * max(n, 1))()
+        dns = C.c_uint64()
+        rc = lib().tsg_search_batch(self.h, arr, n, depth, outs, C.byref(dns))
+        res = []
+        try:
+            if rc:
+                _check(rc)
+            for i in range(n):
+                if unpack:
+                    res.append(_unpack(outs[i]))
+                else:
+                    r = outs[i].contents
+                    m = r.metrics
+                    res.append((r.n, SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected,
+                                                   m.blocks_skipped, m.device_bytes_read, m.kernel_ns,
+                                                   m.scan_kernel_ns, m.scan_bytes, reruns=m.reruns, path=m.path)))
+        finally:
+            for i in range(n):
+                if outs[i]:
+                    lib().tsg_result_free(outs[i])
+        return res, dns.value
+
     def search_raw(self, blocks: Sequence["BackendSearchBlock"], pipeline: Pipeline, limit: int = 0,
                    flags: int = 0, metrics: bool = True):
         """tsg_search without unpacking the matches into Python objects: returns
@@ -480,7 +534,8 @@ class Engine:
         r = rp.contents
         n, m = r.n, r.metrics
         met = SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,
-                            m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
+                            m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes,
+                            reruns=m.reruns, path=m.path)
         free(rp)
         return n, met
 
@@ -545,7 +600,8 @@ class Engine:
             cols["names"] = names
             m = r.metrics
             met = SearchMetrics(m.traces_inspected, m.bytes_inspected, m.blocks_inspected, m.blocks_skipped,
-                                m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes)
+                                m.device_bytes_read, m.kernel_ns, m.scan_kernel_ns, m.scan_bytes,
+                                reruns=m.reruns, path=m.path)
             return cols, met
         finally:
             lib().tsg_result_free(rp)
@@ -608,10 +664,14 @@ class Engine:
 
     def resident_counters(self, dev: int = 0) -> dict:
         """tsg_device_counters: the resident search kernel's launches, queries served, relaunches
-        (a launch that left on its idle timeout as a query was posted) and quits."""
-        buf = (C.c_uint64 * 4)()
-        _check(lib().tsg_device_counters(self.h, dev, buf, 4))
-        return dict(zip(("launches", "queries", "relaunches", "quits"), list(buf)))
+        (a launch that left on its idle timeout as a query was posted), quits, slot reads the
+        kernel rejected (check mismatch), narrow queries launched plainly because another process
+        has a context on the GPU, narrow queries launched plainly (any reason), XCD-split samples."""
+        keys = ("launches", "queries", "relaunches", "quits", "rejects", "cotenant_queries", "plain_queries",
+                "xsplit_samples")
+        buf = (C.c_uint64 * len(keys))()
+        _check(lib().tsg_device_counters(self.h, dev, buf, len(keys)))
+        return dict(zip(keys, list(buf)))
 
     def kernel_times(self, cap: int = 65536) -> List[int]:
         """Durations (ns) of the searches run with SEARCH_TIME_DEFER since the last
@@ -758,6 +818,12 @@ class Engine:
 
 
 _block_closes = [0]  # BackendSearchBlock closes so far
+
+
+def debug_set(name: str, value: int) -> None:
+    """tsg_debug_set: process-wide test hooks ("res_torn": the next `value` resident posts are
+    written torn, then repaired)."""
+    _check(lib().tsg_debug_set(name.encode(), value))
 
 
 def _seen(opts, seen):

@@ -47,7 +47,30 @@ def test_no_device_fails_loudly():
 
 
 def test_abi_version():
-    assert T.lib().tsg_abi_version() == 6
+    assert T.lib().tsg_abi_version() == 7
+
+
+def test_struct_layouts_match_header(tmp_path):
+    # the ctypes mirrors of the ABI-7 structs against the compiled header (gcc, no GPU)
+    import ctypes as C
+    import subprocess
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "tsg.h"\nint main(void){printf("%zu %zu %zu %zu %zu\\n",'
+                   ' sizeof(tsg_metrics), sizeof(tsg_result), offsetof(tsg_result, nblocks), sizeof(tsg_search_item),'
+                   ' offsetof(tsg_metrics, path));return 0;}\n')
+    exe = tmp_path / "sz"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.check_call(["gcc", "-I", inc, str(src), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got == [C.sizeof(tsg._Metrics), C.sizeof(tsg._Result), tsg._Result.nblocks.offset, C.sizeof(tsg._SearchItem),
+                   tsg._Metrics.path.offset]
+
+
+def test_debug_set_rejects_unknown_hooks():
+    with pytest.raises(T.TsgError) as e:
+        T.debug_set("no_such_hook", 1)
+    assert e.value.code == tsg.TSG_E_INVALID
+    T.debug_set("res_torn", 0)  # (a known hook: accepted without a device)
 
 
 @pytest.mark.parametrize("req,terms", [
