@@ -10,7 +10,7 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+LIB_PATH = os.environ.get("ORACLE_LIB_PATH") or os.path.join(HERE, "build", "liboracle.so")  # (override: the ASan build, tests/sanitize)
 
 
 def build():

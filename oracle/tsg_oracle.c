@@ -1607,7 +1607,7 @@ static uint32_t gob_off(const gob *f) { return (uint32_t)(f->cap - f->head); } /
 static void gob_grow(gob *f) {                                                  /* growByteBuffer */
   size_t nc = f->cap ? f->cap * 2 : 1;
   uint8_t *nb = (uint8_t *)calloc(nc, 1);
-  memcpy(nb + (nc - f->cap), f->b, f->cap);
+  if (f->cap) memcpy(nb + (nc - f->cap), f->b, f->cap);
   free(f->b);
   f->head += nc - f->cap;
   f->b = nb;

@@ -104,8 +104,8 @@ SearchMeta parse_search_meta(const uint8_t *p, size_t n) {
   SearchMeta m;
   if (json_field(js, "version", v)) m.version = std::string(v);
   if (json_field(js, "encoding", v)) m.encoding = parse_encoding(v);
-  if (json_field(js, "indexPageSize", v)) m.index_page_size = uint32_t(std::stoull(std::string(v)));
-  if (json_field(js, "indexRecords", v)) m.index_records = uint32_t(std::stoull(std::string(v)));
+  if (json_field(js, "indexPageSize", v)) m.index_page_size = json_u32(v, "indexPageSize");
+  if (json_field(js, "indexRecords", v)) m.index_records = json_u32(v, "indexRecords");
   return m;
 }
 

@@ -18,6 +18,19 @@
 
 namespace tsg {
 
+uint32_t json_u32(std::string_view v, const char *field) {
+  while (!v.empty() && (v.front() == ' ' || v.front() == '\t' || v.front() == '\n' || v.front() == '\r')) v.remove_prefix(1);
+  while (!v.empty() && (v.back() == ' ' || v.back() == '\t' || v.back() == '\n' || v.back() == '\r')) v.remove_suffix(1);
+  if (v.empty() || v.size() > 10) fail(TSG_E_CORRUPT, std::string("meta.json: bad ") + field);
+  uint64_t x = 0;
+  for (char c : v) {
+    if (c < '0' || c > '9') fail(TSG_E_CORRUPT, std::string("meta.json: bad ") + field);
+    x = x * 10 + uint64_t(c - '0');
+  }
+  if (x > 0xffffffffull) fail(TSG_E_CORRUPT, std::string("meta.json: ") + field + " out of range");
+  return uint32_t(x);
+}
+
 // ---- xxhash64 (github.com/cespare/xxhash v1.1.0) -------------------------------
 static constexpr uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL,
                           P3 = 1609587929392839161ULL, P4 = 9650029242287828579ULL,

@@ -69,6 +69,8 @@ inline int bytes_compare(const uint8_t *a, size_t al, const uint8_t *b, size_t b
 
 // ---- hashes -----------------------------------------------------------------
 uint64_t xxhash64(const uint8_t *p, size_t n);  // cespare/xxhash Sum64 (seed 0)
+// A meta.json number field as uint32 (decimal digits only, <= 2^32-1); anything else -> TSG_E_CORRUPT
+uint32_t json_u32(std::string_view v, const char *field);
 uint32_t fnv1_32(const uint8_t *p, size_t n);   // hash/fnv New32 (pkg/util/hash.go:15-20)
 void murmur3_128(const uint8_t *p, size_t n, uint64_t &h1, uint64_t &h2);  // spaolacci/murmur3 Sum128
 uint32_t crc32c(const uint8_t *p, size_t n);

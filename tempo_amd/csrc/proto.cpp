@@ -674,8 +674,8 @@ void proto_load_host(ProtoBlock &b, const std::string &dir) {
   else if (denc == "v2") b.v2 = true;
   else fail(TSG_E_UNSUPPORTED, "unknown dataEncoding '" + denc + "' (model.NewObjectDecoder)");
   const std::string ips = json_get(js, "indexPageSize"), tr = json_get(js, "totalRecords");
-  const uint32_t page_size = ips.empty() ? 0 : uint32_t(std::stoul(ips));
-  b.total_records = tr.empty() ? 0 : uint32_t(std::stoul(tr));
+  const uint32_t page_size = ips.empty() ? 0 : json_u32(ips, "indexPageSize");
+  b.total_records = tr.empty() ? 0 : json_u32(tr, "totalRecords");
   std::vector<uint8_t> idx, data;
   if (!read_file(dir + "/index", idx)) fail(TSG_E_IO, "index missing");
   if (!read_file(dir + "/data", data)) fail(TSG_E_IO, "data missing");

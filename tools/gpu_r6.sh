@@ -1,0 +1,64 @@
+#!/bin/bash
+# Round-6 GPU session script. Stages by $1 (comma list); each GPU step under its own timeout,
+# the script stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STAGES="${1:-new,quick}"
+has() { [[ ",$STAGES," == *",$1,"* ]]; }
+T="python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider"
+B="--cfg3 0 --cfg4 0 --cfg5 0 --shim-steps 0 --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --parity 0 --cfg1 0"
+summ() {  # one-line summary of a bench JSON line
+  python3 - "$1" "$2" <<'EOF'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+l = d.get("latency_us", {})
+out = [sys.argv[2], "value %.1fG" % (d["value"] / 1e9), "frac %s" % (round(d["roofline"]["frac"], 3) if d["roofline"]["frac"] else None),
+       "step mean %.1f p50 %.1f" % (l["step"]["mean"], l["step"]["p50"]) if l.get("step") else "",
+       "kernel mean %.2f" % l["kernel"]["mean"] if l.get("kernel") else ""]
+if "batched" in d:
+    b = d["batched"]
+    out.append("batched dev/q %s wall/q %.1f frac %s ok %s" % (b["device_us_per_query"] and round(b["device_us_per_query"], 2),
+                                                            b["wall_us_per_query"], b["frac"] and round(b["frac"], 3),
+                                                            b["counts_match_and_resident"]))
+if "limit20" in d:
+    out.append("lim20 step mean %.1f" % d["limit20"]["step_us"]["mean"])
+if "shim" in d:
+    s = d["shim"]
+    out.append("shim p50 %.1f p99 %.1f | lim20 p50 %.1f p99 %.1f max %.1f" % (
+        s["query_us"]["p50"], s["query_us"]["p99"], s["limit20"]["query_us"]["p50"], s["limit20"]["query_us"]["p99"],
+        s["limit20"]["query_us"]["max"]))
+print(" ".join(out))
+EOF
+}
+if has new; then
+  timeout -k 10 600 $T -m gpu tests/test_gpu_resident2.py tests/test_gpu_multidevice.py tests/test_gpu_resident.py > gpurun_out/pt_new.log 2>&1
+  rc=$?; echo "new rc=$rc"; grep -E "PASS|FAIL|Error|error" gpurun_out/pt_new.log | tail -30; tail -4 gpurun_out/pt_new.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has tests; then
+  timeout -k 10 600 $T -m gpu ${TESTS:-tests/test_gpu_coalesce.py tests/test_gpu_pool.py tests/test_gpu_search.py} > gpurun_out/pt.log 2>&1
+  rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has alltests; then
+  timeout -k 10 900 $T -m gpu tests > gpurun_out/pt_all.log 2>&1
+  rc=$?; echo "alltests rc=$rc"; tail -4 gpurun_out/pt_all.log; [ $rc -eq 0 ] || exit $rc
+fi
+if has quick; then
+  timeout -k 10 400 python3 bench.py --steps 200 --warmup 5 --limit-steps 0 $B > gpurun_out/quick.json 2> gpurun_out/quick.err
+  rc=$?; echo "quick rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/quick.err; exit $rc; }
+  summ gpurun_out/quick.json quick
+  TSG_RES_XSPLIT=0 timeout -k 10 400 python3 bench.py --steps 200 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/quick_nox.json 2> gpurun_out/quick_nox.err
+  rc=$?; echo "quick_nox rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/quick_nox.err; exit $rc; }
+  summ gpurun_out/quick_nox.json quick_noxsplit
+fi
+if has prof; then  # host phases of the main line
+  TSG_PROF=1 timeout -k 10 400 python3 bench.py --steps 400 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/prof.json 2> gpurun_out/prof.err
+  rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/prof.err; exit $rc; }
+  summ gpurun_out/prof.json prof; grep -E "^\[tsg\] prof|tsg_search|res\.|launch|sync|post" gpurun_out/prof.err | tail -40
+fi
+if has driver; then
+  timeout -k 10 900 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/driver.json 2> gpurun_out/driver.err
+  rc=$?; echo "driver rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/driver.err; exit $rc; }
+  summ gpurun_out/driver.json driver
+fi
+echo "all stages done"
