@@ -18,7 +18,9 @@
 #include <unordered_map>
 #include <unordered_set>
 
+#include <execinfo.h>
 #include <fcntl.h>
+#include <csignal>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -636,8 +638,27 @@ const char *tsg_last_error(void) { return g_last_error.c_str(); }
 int tsg_abi_version(void) { return TSG_ABI_VERSION; }
 void tsg_free(void *p) { std::free(p); }
 
+// TSG_SEGV_TRACE=1 (diagnostics): a fault in the process prints the native stack (libtsg's
+// frames as module + offset: addr2line on the same libtsg.so resolves them), then dies as before
+static void segv_trace(int sig) {
+  void *frames[64];
+  const int n = backtrace(frames, 64);
+  static const char msg[] = "[tsg] fatal signal, native stack:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int tsg_init(const tsg_options *opts, tsg_ctx **out) {
   if (!out) return TSG_E_INVALID;
+  static const bool segv = [] {
+    if (!std::getenv("TSG_SEGV_TRACE")) return false;
+    signal(SIGSEGV, segv_trace);
+    signal(SIGBUS, segv_trace);
+    return true;
+  }();
+  (void)segv;
   return guard([&] {
     auto *c = new tsg_ctx();
     try {
@@ -2202,11 +2223,14 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
           }
         }
         while (wouts.size() < devs.size()) wouts.emplace_back();
+        // (the parts run on the devices' worker threads: a thread_local named inside the lambda
+        // would be the worker's own; this reference is the caller's)
+        std::deque<SearchOut> &wo = wouts;
         std::vector<uint8_t> used_pool(devs.size(), 0);
         if (!devs.empty())
         ctx->fan_out(devs.size(), [&](size_t i) { return devs[i]; },
                      [&](size_t i) {
-                       SearchOut &o = wouts[i];
+                       SearchOut &o = wo[i];
                        o.recs.clear();
                        o.term_any.clear();
                        o.path = 0;

@@ -251,7 +251,7 @@ uint64_t resident_batch_begin(DeviceCtx &dc);
 uint64_t resident_batch_end(DeviceCtx &dc, uint64_t launches_before);
 // test hooks (tsg_debug_set): "res_torn", "groups" (search launches plan for this many CUs:
 // e.g. 8 makes a resident query of 6 M entries run > 1536 units per workgroup), "xsplit"
-// (0/1: the resident kernel's XCD-weighted split; default TSG_RES_XSPLIT, 1)
+// (0/1: the resident kernel's XCD-weighted split; default TSG_RES_XSPLIT, 0)
 int debug_set(const char *name, int64_t value);
 uint32_t debug_groups();
 bool debug_xsplit();

@@ -1478,7 +1478,9 @@ uint64_t resident_batch_end(DeviceCtx &dc, uint64_t launches_before) {
   return ns;
 }
 static std::atomic<uint32_t> g_groups{0};
-static std::atomic<bool> g_xsplit{DeviceCtx::env_u32("TSG_RES_XSPLIT", 1, 0, 1) != 0};
+// (off by default: equalising the XCDs' mean ends raised every XCD's time per unit, span 24.9 vs
+// 24.2 us in paired runs, profiles/r06_xsplit; TSG_RES_XSPLIT=1 turns it on)
+static std::atomic<bool> g_xsplit{DeviceCtx::env_u32("TSG_RES_XSPLIT", 0, 0, 1) != 0};
 uint32_t debug_groups() { return g_groups.load(std::memory_order_relaxed); }
 bool debug_xsplit() { return g_xsplit.load(std::memory_order_relaxed); }
 int debug_set(const char *name, int64_t value) {
@@ -1817,7 +1819,14 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
       }
       static const bool raw = std::getenv("TSG_RES_DUMP")[0] == '2';
       if (raw) {  // every workgroup's end (0.01 us after the first seen), workgroup order
-        std::string line = "[tsg] resident ends:";
+        std::string line = "[tsg] resident xsplit:";
+        for (int x = 0; x < 8; x++) line += " " + std::to_string(PA.xsplit ? dc.res_xf[x] : 0.125);
+        line += "\n[tsg] resident runs:";
+        for (uint32_t w = 0; w < W; w++)
+          line += " " + std::to_string(PA.xsplit ? PA.xn[w & 7] + ((w >> 3) < PA.xr[w & 7] ? 1u : 0u) : PA.wq + (w < PA.wr ? 1u : 0u));
+        line += "\n[tsg] resident seen:";
+        for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(qst[2 * w] - lo);
+        line += "\n[tsg] resident ends:";
         for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(qst[2 * w + 1] - lo);
         line += "\n[tsg] resident counts:";
         for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(counts[size_t(w) * cs]);

@@ -76,7 +76,8 @@ def test_runs_longer_than_two_units_per_thread(engine, paths):
     try:
         n = sum(b.info()["entries"] for b in blocks)
         assert n // 512 // 8 > 1536, n
-        for q in (QA, QC):
+        qa2 = dict(QA, tags={"service.name": "svc-21", "http.method": "post", "status.code": "error"})
+        for q in (QA, qa2):
             res = engine.search(blocks, T.Pipeline(request(q)))
             assert got(res) == expected(paths, q)
             assert res[1].path & T.PATH_RESIDENT, res[1].path
@@ -176,6 +177,7 @@ def test_xsplit_matches_even_runs(engine, paths):
     """The XCD-weighted split (after its calibration samples) and even runs give the same
     records and metrics."""
     blocks = [engine.open_block(p) for p in paths[:6]]
+    T.debug_set("xsplit", 1)
     try:
         pa = T.Pipeline(request(QA))
         e = expected(paths[:6], QA)
@@ -189,7 +191,7 @@ def test_xsplit_matches_even_runs(engine, paths):
             assert got(engine.search(blocks, pa)) == e
         assert engine.resident_counters()["xsplit_samples"] == s1
     finally:
-        T.debug_set("xsplit", 1)
+        T.debug_set("xsplit", 0)
         for b in blocks:
             b.close()
 

@@ -35,6 +35,10 @@ if has new; then
   timeout -k 10 600 $T -m gpu tests/test_gpu_resident2.py tests/test_gpu_multidevice.py tests/test_gpu_resident.py > gpurun_out/pt_new.log 2>&1
   rc=$?; echo "new rc=$rc"; grep -E "PASS|FAIL|Error|error" gpurun_out/pt_new.log | tail -30; tail -4 gpurun_out/pt_new.log; [ $rc -eq 0 ] || exit $rc
 fi
+if has mdev; then  # (non-fatal: the stages after it still run)
+  TSG_SEGV_TRACE=1 timeout -k 10 400 $T -m gpu tests/test_gpu_multidevice.py > gpurun_out/pt_mdev.log 2>&1
+  echo "mdev rc=$?"; grep -E "PASS|FAIL|Error|error|tsg\]|libtsg" gpurun_out/pt_mdev.log | head -60; tail -4 gpurun_out/pt_mdev.log
+fi
 if has tests; then
   timeout -k 10 600 $T -m gpu ${TESTS:-tests/test_gpu_coalesce.py tests/test_gpu_pool.py tests/test_gpu_search.py} > gpurun_out/pt.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
@@ -50,6 +54,12 @@ if has quick; then
   TSG_RES_XSPLIT=0 timeout -k 10 400 python3 bench.py --steps 200 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/quick_nox.json 2> gpurun_out/quick_nox.err
   rc=$?; echo "quick_nox rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/quick_nox.err; exit $rc; }
   summ gpurun_out/quick_nox.json quick_noxsplit
+fi
+if has dump; then  # per-workgroup seen / end stamps of the timed main-line queries, XCD split on and off
+  TSG_RES_DUMP=2 timeout -k 10 400 python3 bench.py --steps 200 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/dump_x.json 2> gpurun_out/dump_x.err
+  echo "dump_x rc=$?"; summ gpurun_out/dump_x.json dump_x
+  TSG_RES_XSPLIT=0 TSG_RES_DUMP=2 timeout -k 10 400 python3 bench.py --steps 200 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/dump_n.json 2> gpurun_out/dump_n.err
+  echo "dump_n rc=$?"; summ gpurun_out/dump_n.json dump_n
 fi
 if has prof; then  # host phases of the main line
   TSG_PROF=1 timeout -k 10 400 python3 bench.py --steps 400 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/prof.json 2> gpurun_out/prof.err
