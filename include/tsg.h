@@ -354,8 +354,11 @@ int tsg_search_batch(tsg_ctx *ctx, const tsg_search_item *items, size_t n, uint3
 /* ABI 7, test hooks (process-wide): "res_torn" = k: the next k resident-kernel posts write the
  * mailbox slot as a read that caught the host's writes half landed would see it (two argument
  * words moved by +-d: the plain sum unchanged) and repair it 200 us later; the kernel must
- * re-read the slot (tsg_device_counters[4] counts the rejected reads). TSG_E_INVALID for an
- * unknown name. */
+ * re-read the slot (tsg_device_counters[4] counts the rejected reads). "groups" = n (0 = the
+ * device's CUs): search launches plan for n CUs. "xsplit" = 0/1: the resident kernel's
+ * XCD-weighted split (default TSG_RES_XSPLIT, off). "lb_bitmap" = 0/1/2: full scans on the
+ * dictionary-pass path return one bit per entry never / always / after a dense one (default
+ * TSG_LB_BITMAP, 2). TSG_E_INVALID for an unknown name. */
 int tsg_debug_set(const char *name, int64_t value);
 
 /* Durations (ns) of the search kernels launched with TSG_SEARCH_TIME_DEFER since

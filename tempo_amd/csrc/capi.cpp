@@ -2003,6 +2003,11 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
         }
       }
       if (list.size() < 2 || list.size() > kChunk || dict < kPipeDict) return false;
+      // (a sparse result has nothing for the host to fill while the device works: one launch
+      // — six launches of an absent needle had cost 93 us of scan kernels; TSG_PIPE_SPARSE=1
+      // pipelines whatever the last full scan's density)
+      const char *e3 = std::getenv("TSG_PIPE_SPARSE");
+      if (!(e3 && std::atoi(e3)) && !device_last_dense(*pdev)) return false;
       // one block in the last launch (its result fill is the part nothing overlaps) and in the
       // first (the host starts filling sooner); kPipeBlocks per launch between them
       const size_t nl = list.size();

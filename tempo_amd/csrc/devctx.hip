@@ -131,6 +131,7 @@ void ctx_shutdown(Ctx &c) {
       if (e) (void)hipEventDestroy(e);
     dc->hres.release();
     dc->hany.release();
+    dc->hbits.release();
     (void)hipEventDestroy(dc->ev0);
     (void)hipEventDestroy(dc->ev1);
     (void)hipEventDestroy(dc->es0);

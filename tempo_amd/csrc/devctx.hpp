@@ -112,6 +112,10 @@ struct DeviceCtx {
   // dict_sets kernels set danyf in device memory; one copy here; read after the sync)
   HostBuf hany{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};
   DevBuf danyf;  // (the device-side flags hany is copied from)
+  // look-back bitmap mode (search.hip): one bit per scanned entry, written by the scan kernel;
+  // lb_dense: the last full scan on the general path had more than one match per 64 entries
+  HostBuf hbits{nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};
+  bool lb_dense = false;
   unsigned long long epoch = 0, ticket_base = 0;  // lookup launches
   uint32_t search_epoch = 0;
   bool fast_off = std::getenv("TSG_NO_FAST") != nullptr;  // force the general (prep + search) path

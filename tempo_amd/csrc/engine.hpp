@@ -242,6 +242,9 @@ void device_find(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block *>
 int device_ordinal(const DeviceCtx &dc);
 // resident search counters: launches, queries served, relaunches after an idle-exit race, quits
 void device_counters(DeviceCtx &dc, uint64_t out[8]);
+// The last full scan on the device's dictionary-pass path had more than one match per 64
+// entries (search.hip: its next full scans there return bitmaps; tsg_search pipelines them)
+bool device_last_dense(DeviceCtx &dc);
 // Durations of the TSG_SEARCH_TIME_DEFER launches since the last call (waits for the stream).
 void device_kernel_times(DeviceCtx &dc, std::vector<uint64_t> &ns);
 // tsg_search_batch (pool.hip): begin ends the device's resident launch and gives the next one
@@ -254,6 +257,7 @@ uint64_t resident_batch_end(DeviceCtx &dc, uint64_t launches_before);
 // (0/1: the resident kernel's XCD-weighted split; default TSG_RES_XSPLIT, 0)
 int debug_set(const char *name, int64_t value);
 uint32_t debug_groups();
+uint32_t debug_lb_bitmap();  // "lb_bitmap": 0 never / 1 always / 2 auto (TSG_LB_BITMAP, default 2)
 bool debug_xsplit();
 
 }  // namespace tsg

@@ -1481,7 +1481,9 @@ static std::atomic<uint32_t> g_groups{0};
 // (off by default: equalising the XCDs' mean ends raised every XCD's time per unit, span 24.9 vs
 // 24.2 us in paired runs, profiles/r06_xsplit; TSG_RES_XSPLIT=1 turns it on)
 static std::atomic<bool> g_xsplit{DeviceCtx::env_u32("TSG_RES_XSPLIT", 0, 0, 1) != 0};
+static std::atomic<uint32_t> g_lb_bitmap{DeviceCtx::env_u32("TSG_LB_BITMAP", 2, 0, 2)};
 uint32_t debug_groups() { return g_groups.load(std::memory_order_relaxed); }
+uint32_t debug_lb_bitmap() { return g_lb_bitmap.load(std::memory_order_relaxed); }
 bool debug_xsplit() { return g_xsplit.load(std::memory_order_relaxed); }
 int debug_set(const char *name, int64_t value) {
   if (!name) return TSG_E_INVALID;
@@ -1495,6 +1497,10 @@ int debug_set(const char *name, int64_t value) {
   }
   if (!std::strcmp(name, "xsplit")) {
     g_xsplit.store(value != 0);
+    return TSG_OK;
+  }
+  if (!std::strcmp(name, "lb_bitmap")) {
+    g_lb_bitmap.store(uint32_t(std::min<int64_t>(2, std::max<int64_t>(0, value))));
     return TSG_OK;
   }
   return TSG_E_INVALID;

@@ -29,6 +29,7 @@ struct ScanSeg {
   uint32_t block_idx, steal_base;  // claim counter value at launch start (tail tiles)
   uint64_t cap;  // limit mode: records kept from this block
   uint64_t e0;   // first scan position searched (a multiple of the pool unit; 0 = the whole block up to n)
+  uint64_t bm_word0;  // bitmap mode: the block's first word in ScanParams::bitmap (nunits x 16 words)
 };
 
 struct MatchRec {  // == SearchOut::Rec

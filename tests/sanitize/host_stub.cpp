@@ -118,10 +118,12 @@ void device_counters(DeviceCtx &dc, uint64_t out[8]) {
   for (int i = 0; i < 8; i++) out[i] = 0;
 }
 void device_kernel_times(DeviceCtx &, std::vector<uint64_t> &ns) { ns.clear(); }
+bool device_last_dense(DeviceCtx &) { return true; }
 uint64_t resident_batch_begin(DeviceCtx &) { return 0; }
 uint64_t resident_batch_end(DeviceCtx &, uint64_t) { return 0; }
 int debug_set(const char *name, int64_t) {
-  return name && (!std::strcmp(name, "res_torn") || !std::strcmp(name, "groups") || !std::strcmp(name, "xsplit"))
+  return name && (!std::strcmp(name, "res_torn") || !std::strcmp(name, "groups") || !std::strcmp(name, "xsplit") ||
+                  !std::strcmp(name, "lb_bitmap"))
              ? TSG_OK
              : TSG_E_INVALID;
 }

@@ -129,3 +129,29 @@ def test_stream_every_start_a_candidate(engine, tmp_path):
             assert check(engine, [blk], [path], {"db.statement": nd})
     finally:
         blk.close()
+
+
+@pytest.mark.parametrize("mode", [1, 0, 2])
+def test_bitmap_mode_and_dead_terms(engine, dict_blocks, mode):
+    """Full scans on the dictionary-pass path return one bit per entry (bitmap mode, 1 / auto 2
+    after a dense query) or 8-byte positions (0): the same records and metrics as the oracle;
+    limit queries keep positions. A term no dictionary value matches skips its block's scan on
+    the device (needle absent in one block, in both, and a second term absent)."""
+    paths, long_vals = dict_blocks
+    blocks = [engine.open_block(p) for p in paths]
+    T.debug_set("lb_bitmap", mode)
+    try:
+        for tags in ({"db.statement": "a"}, {"db.statement": "e"}, {"multi": "ab"}, {"db.statement": "cab e"},
+                     {"db.statement": long_vals[0][:40]}, {"db.statement": "no-such-needle"},
+                     {"db.statement": "a", "multi": "no-such-needle"}, {"db.statement": "d ", "multi": "c"}):
+            check(engine, blocks, paths, tags)
+        got, met = engine.search(blocks, T.Pipeline(T.SearchRequest(tags={"db.statement": "a"})), limit=7)
+        exp, omet, st = O.search([O.Block(p) for p in paths], tags={"db.statement": "a"}, limit=7)
+        assert [tsg_key(m) for m in got] == [match_key(m) for m in exp]
+        # the needle in one block only: the other block's scan is skipped, its metrics still count
+        only = long_vals[0][100:140]
+        check(engine, blocks, paths, {"db.statement": only})
+    finally:
+        T.debug_set("lb_bitmap", 2)
+        for b in blocks:
+            b.close()

@@ -69,6 +69,7 @@ def test_pipelined_equals_oracle_and_one_launch(engine, paths, monkeypatch, qi, 
     monkeypatch.setenv("TSG_PIPE_DICT_MB", "0")
     assert run(engine, order, q) == exp  # one launch
     monkeypatch.setenv("TSG_PIPE_DICT_MB", "1")
+    monkeypatch.setenv("TSG_PIPE_SPARSE", "1")
     monkeypatch.setenv("TSG_PIPE_BLOCKS", per_launch)
     assert run(engine, order, q) == exp  # pipelined
     # a limit query is never pipelined; its result is the oracle's consumer
@@ -77,6 +78,7 @@ def test_pipelined_equals_oracle_and_one_launch(engine, paths, monkeypatch, qi, 
 
 def test_pipelined_repeat_and_one_block(engine, paths, monkeypatch):
     monkeypatch.setenv("TSG_PIPE_DICT_MB", "1")
+    monkeypatch.setenv("TSG_PIPE_SPARSE", "1")
     monkeypatch.setenv("TSG_PIPE_BLOCKS", "1")
     q = QUERIES[0]
     order = [paths["hc2"], paths["hc0"], paths["hc1"]]

@@ -39,6 +39,27 @@ if has mdev; then  # (non-fatal: the stages after it still run)
   TSG_SEGV_TRACE=1 timeout -k 10 400 $T -m gpu tests/test_gpu_multidevice.py > gpurun_out/pt_mdev.log 2>&1
   echo "mdev rc=$?"; grep -E "PASS|FAIL|Error|error|tsg\]|libtsg" gpurun_out/pt_mdev.log | head -60; tail -4 gpurun_out/pt_mdev.log
 fi
+if has cfg4; then
+  timeout -k 10 600 $T -m gpu tests/test_gpu_dict_stream.py tests/test_gpu_block_filter.py tests/test_gpu_pipelined.py > gpurun_out/pt_cfg4.log 2>&1
+  rc=$?; echo "cfg4 tests rc=$rc"; grep -E "FAIL|Error" gpurun_out/pt_cfg4.log | head -20; tail -3 gpurun_out/pt_cfg4.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 --limit-steps 0 --batch-queries 0 --cfg3 0 --cfg5 0 --shim-steps 0 --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --cfg1 0 --cfg4 1 --parity 1 > gpurun_out/cfg4.json 2> gpurun_out/cfg4.err
+  rc=$?; echo "cfg4 bench rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/cfg4.err; exit $rc; }
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/cfg4.json').read().strip().splitlines()[-1]); c=d['cfg4']
+print('parity', c.get('parity',{}).get('ok'))
+for k,v in c['queries'].items(): print(k, 'matches', v['matches'], 'scan_us', v['scan_us'], 'step_us p50/p99', v['step_us']['p50'], v['step_us']['p99'], 'dev p50', v['device_us']['p50'], 'sod', round(v['step_over_device'] or 0,2))
+"
+fi
+if has cfg4ab; then  # pipelined chunk size A/B (TSG_PIPE_BLOCKS)
+  for pb in 2 4; do
+    TSG_PIPE_BLOCKS=$pb timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 --limit-steps 0 --batch-queries 0 --cfg3 0 --cfg5 0 --shim-steps 0 --concurrent-steps 0 --mall-steps 0 --cpu-baseline 0 --cfg1 0 --cfg4 1 --cfg4-steps 20 --parity 0 > gpurun_out/cfg4_pb$pb.json 2> gpurun_out/cfg4_pb$pb.err
+    rc=$?; echo "cfg4 pb=$pb rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/cfg4_pb$pb.err; exit $rc; }
+    python3 -c "
+import json; d=json.loads(open('gpurun_out/cfg4_pb$pb.json').read().strip().splitlines()[-1]); c=d['cfg4']
+for k,v in c['queries'].items(): print(' ', k, 'scan p50', v['scan_us']['p50'], 'step p50/p99 %.0f %.0f' % (v['step_us']['p50'], v['step_us']['p99']), 'dev p50 %.0f' % v['device_us']['p50'], 'sod %.2f' % (v['step_over_device'] or 0))
+"
+  done
+fi
 if has tests; then
   timeout -k 10 600 $T -m gpu ${TESTS:-tests/test_gpu_coalesce.py tests/test_gpu_pool.py tests/test_gpu_search.py} > gpurun_out/pt.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
