@@ -111,7 +111,8 @@ def summary(out):
          "load_gb_per_s": g("load_gb_per_s"), "cfg4_load_gb_per_s": g("cfg4", "load_gb_per_s"),
          "cfg1_kernel_us_p50": g("cfg1", "gpu", "kernel_us", "p50"),
          "batched_device_us_per_query": g("batched", "device_us_per_query"), "batched_frac": g("batched", "frac"),
-         "batched_wall_us_per_query": g("batched", "wall_us_per_query")}
+         "batched_wall_us_per_query": g("batched", "wall_us_per_query"),
+         "merged_shm_step_us_p50": g("merge", "shm", "step_us", "p50"), "merged_gloo_step_us_p50": g("merge", "step_us", "p50")}
     for name, q in (g("cfg4", "queries") or {}).items():
         s["cfg4_" + name] = {"step_over_device": round(q["step_over_device"], 3) if q.get("step_over_device") else None,
                              "scan_us_p50": round(q["scan_us"]["p50"], 1), "dict_frac": round(q["dict_frac"], 3)
@@ -1041,6 +1042,32 @@ def merge_leg(args, eng, base, pipe, rank, world, dist):
             res["merged_traces"] = len(merged)
             res["inspected_traces"] = merged.metrics.inspected_traces
             res["block_errors"] = sum(1 for x in merged.block_status if x)
+        # the merged query through shared memory (the node's ranks: tsg_shm_put / tsg_shm_merge):
+        # each timed step = this rank's full scan + its response into its slot; rank 0's step also
+        # waits for every rank and merges (queries back to back: no barrier between them)
+        try:
+            shm = shard.ShmGather("tsg_bench_%s" % os.environ.get("MASTER_PORT", "0"), world, rank, group=g)
+            try:
+                for _ in range(3):
+                    m3 = shm.query(local(), everything, nb)
+                dist.barrier(group=g)
+                ts3 = []
+                for _ in range(args.merge_steps):
+                    t0 = time.perf_counter()
+                    m3 = shm.query(local(), everything, nb)
+                    ts3.append(time.perf_counter() - t0)
+                dist.barrier(group=g)
+                tt3 = torch.tensor([sum(ts3)], dtype=torch.float64)
+                dist.all_reduce(tt3, op=dist.ReduceOp.MAX, group=g)
+                res["shm"] = {"step_us": pct([x * 1e6 for x in ts3]),
+                              "entries_per_s": len(base) * args.entries * world * args.merge_steps / float(tt3.item()),
+                              "transport": "shared memory (/dev/shm) slots per rank, merged in place on rank 0"}
+                if rank == 0:
+                    res["shm"]["same_as_gloo"] = bool(len(m3) == len(merged) and (m3.recs == merged.recs).all())
+            finally:
+                shm.close()
+        except Exception as e:  # noqa: BLE001
+            res["shm"] = {"error": repr(e)}
         if SHARED_GPU:
             res["rccl"] = "skipped: shared device (--ranks-share-gpu: RCCL needs one GPU per rank)"
             return res

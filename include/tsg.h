@@ -410,6 +410,21 @@ int tsg_result_pack(const tsg_result *r, uint8_t **out, size_t *out_len);
 int tsg_wire_merge(const uint8_t *const *wires, const size_t *lens, size_t n, uint64_t limit, uint64_t total_blocks,
                    uint8_t *out, size_t cap, size_t *out_len);
 
+/* ABI 7: the same merge for the ranks of one node through shared memory (/dev/shm/<name>): each
+ * rank puts its wire for query `seq` (1, 2, ... in every rank's call order) into its slot;
+ * rank 0's tsg_shm_merge waits for every rank's response to `seq` and merges them in place (as
+ * tsg_wire_merge, ranks in order). Slots are double buffered: a rank may put query seq + 1
+ * while rank 0 merges seq. Waits are bounded by timeout_s (TSG_E_DEVICE: a rank did not
+ * answer). Rank 0 opens with reset = 1 before the others open (tempo_amd/shard.py ShmGather:
+ * a barrier between); rank 0's close removes the file. A response above slot_bytes ->
+ * TSG_E_INVALID (the caller gathers it another way). */
+typedef struct tsg_shm tsg_shm;
+int tsg_shm_open(const char *name, uint32_t world, uint32_t rank, uint64_t slot_bytes, int reset, tsg_shm **out);
+void tsg_shm_close(tsg_shm *s);
+int tsg_shm_put(tsg_shm *s, uint32_t seq, const uint8_t *wire, size_t len, double timeout_s);
+int tsg_shm_merge(tsg_shm *s, uint32_t seq, uint64_t limit, uint64_t total_blocks, uint8_t *out, size_t cap,
+                  size_t *out_len, double timeout_s);
+
 /* ---- v2 trace blocks: batched trace-ID lookup --------------------------------- */
 /* Reads <block_dir>/{meta.json,bloom-N...,index}; verifies index page checksums. */
 int tsg_v2block_open(tsg_ctx *ctx, const char *block_dir, int device_hint, tsg_v2block **out);

@@ -397,6 +397,48 @@ def distributed_search_packed(search_local: Callable[[], WireSource], limit: int
     return merged if columns else (merged.traces(), merged.metrics)
 
 
+class ShmGather:
+    """The frontend merge for the ranks of one node through shared memory (tsg_shm_*, DESIGN.md
+    §5): each rank puts its wire response for a query into its slot of /dev/shm/<name>, rank 0
+    merges every rank's slot in place when all have answered (no collective, no copy into a
+    tensor). Queries are numbered 1, 2, ... in call order on every rank; a rank may put query
+    s + 1 while rank 0 merges s (double-buffered slots). Rank 0 creates the file (reset) before
+    the others open it: `group` (a torch.distributed group of the node's ranks) orders that.
+    A response larger than `slot_bytes` fails its put (TSG_E_INVALID): gather it another way."""
+
+    def __init__(self, name: str, world: int, rank: int, group=None, slot_bytes: int = 16 << 20):
+        import torch.distributed as dist
+        self.world, self.rank, self.slot_bytes, self.seq = world, rank, slot_bytes, 0
+        self.h = C.c_void_p()
+        self._out = None
+        if rank == 0:
+            _check(lib().tsg_shm_open(name.encode(), world, rank, slot_bytes, 1, C.byref(self.h)))
+        dist.barrier(group=group)
+        if rank != 0:
+            _check(lib().tsg_shm_open(name.encode(), world, rank, slot_bytes, 0, C.byref(self.h)))
+        dist.barrier(group=group)
+
+    def query(self, wire, limit: int, total_blocks: int, timeout_s: float = 60.0) -> Optional["Response"]:
+        """Put this rank's wire for the next query; on rank 0 return the merged Response."""
+        self.seq = self.seq + 1 if self.seq < 0xFFFFFFFF else 1
+        w = _wire_of(wire)
+        _check(lib().tsg_shm_put(self.h, self.seq, w.ctypes.data, w.size, timeout_s))
+        if self.rank != 0:
+            return None
+        if self._out is None:
+            self._out = np.empty(self.world * self.slot_bytes + 4096, np.uint8)
+        ln = C.c_size_t()
+        lim = min(int(limit), 2**64 - 1)
+        _check(lib().tsg_shm_merge(self.h, self.seq, lim, total_blocks, self._out.ctypes.data, self._out.size,
+                                   C.byref(ln), timeout_s))
+        return from_wire(self._out[:ln.value])
+
+    def close(self):
+        if self.h:
+            lib().tsg_shm_close(self.h)
+            self.h = C.c_void_p()
+
+
 def shard_ids(n_ids: int, world: int, rank: int) -> range:
     """Contiguous probe-id slice owned by `rank` (config 5: 10 M ids over the GPUs)."""
     return shard_range(n_ids, world, rank)

@@ -161,6 +161,7 @@ EXPORTED = [
     "tsg_write_search_block", "tsg_write_wal_search", "tsg_fb_search_entry", "tsg_fb_search_header", "tsg_synth_search_block",
     "tsg_synth_v2_block", "tsg_live_block_open_mem", "tsg_search_tags", "tsg_search_tag_values",
     "tsg_result_pack", "tsg_wire_merge", "tsg_search_batch", "tsg_debug_set",
+    "tsg_shm_open", "tsg_shm_close", "tsg_shm_put", "tsg_shm_merge",
 ]
 
 _lib = None
@@ -212,6 +213,11 @@ def lib():
         L.tsg_search_batch.argtypes = [vp, C.POINTER(_SearchItem), C.c_size_t, C.c_uint32,
                                        C.POINTER(C.POINTER(_Result)), C.POINTER(C.c_uint64)]
         L.tsg_debug_set.argtypes = [C.c_char_p, C.c_int64]
+        L.tsg_shm_open.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.POINTER(vp)]
+        L.tsg_shm_close.argtypes = [vp]
+        L.tsg_shm_put.argtypes = [vp, C.c_uint32, vp, C.c_size_t, C.c_double]
+        L.tsg_shm_merge.argtypes = [vp, C.c_uint32, C.c_uint64, C.c_uint64, vp, C.c_size_t, C.POINTER(C.c_size_t),
+                                    C.c_double]
         L.tsg_kernel_times.argtypes = [vp, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_size_t)]
         L.tsg_results_combine.argtypes = [C.POINTER(_Result), C.c_uint32, C.POINTER(C.POINTER(_Result))]
         L.tsg_v2block_open.argtypes = [vp, C.c_char_p, C.c_int, C.POINTER(vp)]

@@ -5,6 +5,7 @@ querier response comes from the oracle (test-side stand-in for
 `Engine.search_request`); what is under test is the sharding, the gather and the
 frontend merge (modules/frontend/searchsharding.go:32-125) in `tempo_amd.shard`.
 """
+import ctypes as C
 import os
 import random
 import socket
@@ -309,3 +310,56 @@ def test_gloo_id_sharded_lookup(world):
         rc, exp = O.lookup([O.V2Block(p) for p in paths], ids, nthreads=1)
         np.testing.assert_array_equal(got, np.array(exp, dtype=np.int64).reshape(-1, 5))
         assert len(np.unique(got[:, 0])) >= 600
+
+
+def _shm_worker(rank, world, port, paths, limit, outdir, rounds):
+    import json
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = None
+    try:
+        g = shard.ShmGather("tsg_test_shm_%d" % port, world, rank, slot_bytes=1 << 20)
+        mine = [paths[i] for i in shard.shard_range(len(paths), world, rank)]
+        out = []
+        for r in range(rounds):  # (queries back to back: the double-buffered slots, no barrier between)
+            lim = limit if r % 2 == 0 else 3
+            merged = g.query(shard.to_wire(shard.response_from_traces(*_rank_response(mine, lim))), lim, len(paths))
+            if rank == 0:
+                out.append(_key((merged.traces(), merged.metrics)))
+            else:
+                assert merged is None
+        if rank == 0:
+            with open(os.path.join(outdir, "shm.json"), "w") as f:
+                json.dump(out, f)
+        dist.barrier()
+    finally:
+        if g is not None:
+            g.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shm_gather_matches_frontend_merge(world):
+    """The shared-memory gather (tsg_shm_put / tsg_shm_merge) gives the frontend merge of the
+    ranks' responses in rank order, query after query (alternating limits)."""
+    import json
+    with tempfile.TemporaryDirectory() as td:
+        paths = _make_blocks(td)
+        rounds = 7
+        mp.spawn(_shm_worker, args=(world, _free_port(), paths, 1000, td, rounds), nprocs=world, join=True)
+        with open(os.path.join(td, "shm.json")) as f:
+            got = json.load(f)
+        assert len(got) == rounds
+        for r in range(rounds):
+            lim = 1000 if r % 2 == 0 else 3
+            resp = [_rank_response([paths[i] for i in shard.shard_range(len(paths), world, k)], lim)
+                    for k in range(world)]
+            exp = _key(shard.merge_responses(resp, lim, len(paths)))
+            assert got[r] == [list(map(list, exp[0])), list(exp[1])], r
+        assert not [f for f in os.listdir("/dev/shm") if f.startswith("tsg_test_shm_")]  # (rank 0 removed it)
+
+
+def test_shm_rejects_bad_arguments():
+    h = C.c_void_p()
+    assert T.lib().tsg_shm_open(b"tsg_test_bad", 2, 2, 1024, 1, C.byref(h)) == T.TSG_E_INVALID
+    assert T.lib().tsg_shm_open(b"tsg_test_bad", 0, 0, 1024, 1, C.byref(h)) == T.TSG_E_INVALID

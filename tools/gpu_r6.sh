@@ -60,6 +60,15 @@ for k,v in c['queries'].items(): print(' ', k, 'scan p50', v['scan_us']['p50'], 
 "
   done
 fi
+if has share2; then  # the N=2 path with both ranks on the one GPU (merged query: gloo and shared memory)
+  timeout -k 10 600 python3 bench.py --gpus 2 --ranks-share-gpu --steps 100 --warmup 5 --merge-steps 50 $B --batch-queries 0 --limit-steps 0 > gpurun_out/share2.json 2> gpurun_out/share2.err
+  rc=$?; echo "share2 rc=$rc"; [ $rc -eq 0 ] || { tail -30 gpurun_out/share2.err; exit $rc; }
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/share2.json').read().strip().splitlines()[-1]); m=d.get('merge',{})
+print('value %.1fG step mean %.1f' % (d['value']/1e9, d['latency_us']['step']['mean']))
+print('gloo merged step', m.get('step_us')); print('shm', m.get('shm'))
+"
+fi
 if has tests; then
   timeout -k 10 600 $T -m gpu ${TESTS:-tests/test_gpu_coalesce.py tests/test_gpu_pool.py tests/test_gpu_search.py} > gpurun_out/pt.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
