@@ -160,10 +160,12 @@ def _ref_merge(responses, limit, total_blocks):
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_native_merge_matches_restatement(seed):
+@pytest.mark.parametrize("presorted", [False, True])
+def test_native_merge_matches_restatement(seed, presorted):
     """tsg_wire_merge vs the per-record restatement: duplicate ids across and inside
     responses (first wins), equal start times (first position wins), ids that differ only in
-    leading zeros (one hex TraceID), the quit rule at several limits."""
+    leading zeros (one hex TraceID), the quit rule at several limits. presorted: every response
+    start-descending (as a rank's result is), the merge's k-way path instead of its sort."""
     rng = random.Random(seed)
     pool = [bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(300)]
     pool += [bytes(12) + bytes(rng.getrandbits(8) for _ in range(4)) for _ in range(20)]
@@ -177,6 +179,8 @@ def test_native_merge_matches_restatement(seed):
                                             root_trace_name=rng.choice(["", "x", "yy"]),
                                             start_time_unix_nano=rng.choice([5, 7, 10 ** 18 + rng.randrange(1000)]),
                                             duration_ms=rng.randrange(100)))
+        if presorted:
+            ts.sort(key=lambda t: -t.start_time_unix_nano)
         nb = rng.randrange(0, 4)
         st = [rng.choice([0, 0, 2]) for _ in range(nb)]
         met = T.SearchMetrics(rng.randrange(1000), rng.randrange(10 ** 6), nb, rng.randrange(3), block_status=st,
