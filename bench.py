@@ -1048,6 +1048,15 @@ def merge_leg(args, eng, base, pipe, rank, world, dist):
         try:
             shm = shard.ShmGather("tsg_bench_%s" % os.environ.get("MASTER_PORT", "0"), world, rank, group=g)
             try:
+                # this rank's part alone (search + pack, no gather): what the merged step adds is
+                # the step minus this (both ranks on one GPU under --ranks-share-gpu: their scans
+                # share it, so this is measured with the other rank scanning too)
+                dist.barrier(group=g)
+                tl = []
+                for _ in range(args.merge_steps):
+                    t0 = time.perf_counter()
+                    local()
+                    tl.append(time.perf_counter() - t0)
                 for _ in range(3):
                     m3 = shm.query(local(), everything, nb)
                 dist.barrier(group=g)
@@ -1059,7 +1068,7 @@ def merge_leg(args, eng, base, pipe, rank, world, dist):
                 dist.barrier(group=g)
                 tt3 = torch.tensor([sum(ts3)], dtype=torch.float64)
                 dist.all_reduce(tt3, op=dist.ReduceOp.MAX, group=g)
-                res["shm"] = {"step_us": pct([x * 1e6 for x in ts3]),
+                res["shm"] = {"step_us": pct([x * 1e6 for x in ts3]), "local_search_wire_us": pct([x * 1e6 for x in tl]),
                               "entries_per_s": len(base) * args.entries * world * args.merge_steps / float(tt3.item()),
                               "transport": "shared memory (/dev/shm) slots per rank, merged in place on rank 0"}
                 if rank == 0:

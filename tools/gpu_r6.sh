@@ -69,6 +69,18 @@ print('value %.1fG step mean %.1f' % (d['value']/1e9, d['latency_us']['step']['m
 print('gloo merged step', m.get('step_us')); print('shm', m.get('shm'))
 "
 fi
+if has rprof; then  # rocprofv3 over resident launches that each serve 64 batched queries
+  RB="python3 bench.py --steps 8 --warmup 2 --limit-steps 0 --batch-queries 64 --batch-reps 6 $B"
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rp_res -o res -- $RB > gpurun_out/rp_res.json 2> gpurun_out/rp_res.err
+  rc=$?; echo "rprof trace rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/rp_res.err; exit $rc; }
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 240 rocprofv3 --pmc $c -d gpurun_out/rp_$c -o p -- $RB > gpurun_out/rp_$c.json 2> gpurun_out/rp_$c.err
+    rc=$?; echo "rprof $c rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/rp_$c.err; exit $rc; }
+  done
+  find gpurun_out/rp_res gpurun_out/rp_FETCH_SIZE gpurun_out/rp_WRITE_SIZE -name "*.csv" | head -20
+  summ gpurun_out/rp_res.json rp_res
+fi
 if has tests; then
   timeout -k 10 600 $T -m gpu ${TESTS:-tests/test_gpu_coalesce.py tests/test_gpu_pool.py tests/test_gpu_search.py} > gpurun_out/pt.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
