@@ -60,7 +60,9 @@ static std::string lib_dir() {
 Aql *aql_open(int hip_ordinal) {
   const char *e = std::getenv("TSG_AQL");
   if (e && std::atoi(e) == 0) return nullptr;
-  std::ifstream in(lib_dir() + "/libtsg_pool.co", std::ios::binary);
+  // (TSG_POOL_CO: another build of the same kernels, for A/B measurements)
+  const char *alt = std::getenv("TSG_POOL_CO");
+  std::ifstream in(alt && *alt ? std::string(alt) : lib_dir() + "/libtsg_pool.co", std::ios::binary);
   if (!in) {
     note("no libtsg_pool.co beside libtsg.so");
     return nullptr;

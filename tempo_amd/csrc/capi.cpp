@@ -19,6 +19,7 @@
 #include <unordered_set>
 
 #include <execinfo.h>
+#include <sys/syscall.h>
 #include <fcntl.h>
 #include <csignal>
 #include <sys/mman.h>
@@ -430,9 +431,23 @@ struct ResultHolder {
     }
     const std::string_view v = h.dict_value(key, vid);
     len[i] = uint32_t(v.size());
-    off[i] = v.empty() ? 0 : intern_lookup(v.data(), v.size());
+    if (v.empty()) {
+      off[i] = 0;
+    } else if (small_names) {  // (appended: the per-block cache above is the only dedupe)
+      if (arena_size + v.size() > arena_cap) arena_grow(arena_size + v.size());
+      std::memcpy(arena + arena_size, v.data(), v.size());
+      off[i] = arena_size;
+      arena_size += v.size();
+    } else {
+      off[i] = intern_lookup(v.data(), v.size());
+    }
     if (slot) *slot = VcSlot{vc_gen, uint32_t(v.size()), off[i]};
   }
+  // A result of few records skips the intern table: its names go to the arena as the records
+  // meet them (deduped per block by the value-id cache). The table's probe was ~1/3 of the host
+  // time of a 500-record search (tools/host_prof.py); what it saves — a dense result's arena
+  // holding each distinct name once — does not arise below a few thousand records.
+  bool small_names = false;
   size_t size() const { return start.size(); }
   void resize(size_t n) {
     ids.resize(16 * n);
@@ -476,6 +491,7 @@ struct ResultHolder {
     svc_p.clear();
     name_p.clear();
     ptrs_ready = false;
+    small_names = false;
     bstatus.clear();
     berr_s.clear();
     berr.clear();
@@ -650,12 +666,26 @@ static void segv_trace(int sig) {
   raise(sig);
 }
 
+// ... and SIGUSR2 sent to one thread (pthread_kill: a test's hung caller) prints that thread's
+// native stack and lets it go on
+static void stack_dump(int) {
+  void *frames[64];
+  const int n = backtrace(frames, 64);
+  char msg[64];
+  const int l = std::snprintf(msg, sizeof msg, "[tsg] thread %ld native stack:\n", long(syscall(SYS_gettid)));
+  (void)!write(2, msg, size_t(l));
+  backtrace_symbols_fd(frames, n, 2);
+}
+
 int tsg_init(const tsg_options *opts, tsg_ctx **out) {
   if (!out) return TSG_E_INVALID;
   static const bool segv = [] {
     if (!std::getenv("TSG_SEGV_TRACE")) return false;
+    void *f[2];
+    (void)backtrace(f, 2);  // (loads the unwinder now, not inside a handler)
     signal(SIGSEGV, segv_trace);
     signal(SIGBUS, segv_trace);
+    signal(SIGUSR2, stack_dump);
     return true;
   }();
   (void)segv;
@@ -2320,6 +2350,7 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     const clk::time_point t_dev = trace ? clk::now() : clk::time_point();
     if (!pipelined) {
       res->reserve(nrec);
+      res->small_names = nrec <= 4096;
       res->resize(nrec);
     }
     const clk::time_point t_res = trace ? clk::now() : clk::time_point();

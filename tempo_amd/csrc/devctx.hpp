@@ -141,7 +141,8 @@ struct DeviceCtx {
   // TSG_POOL_CHUNK = log2 units per dynamic claim (4), TSG_POOL_LOOK = claims of lookahead (8),
   // TSG_POOL_WAVES = waves per workgroup (16)
   bool pool_off = std::getenv("TSG_NO_POOL") != nullptr;
-  uint32_t pool_skip = 0;  // queries left to skip the pool after a record-buffer overflow
+  uint32_t pool_skip = 0;  // searches of query pool_skip_key left to skip the pool after a record-buffer overflow
+  uint64_t pool_skip_key = 0;
   static uint32_t env_u32(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi) {
     const char *e = std::getenv(name);
     if (!e) return dflt;

@@ -901,23 +901,31 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
       }
     };
     // the unit's matches into the LDS buffer in scan order (k-step, lane, j), in two halves:
-    // eval_a finds them, ranks them and issues the gathers of each lane's first match; the
-    // caller then issues the wave's next unit loads; eval_b stores the gathered records (its
-    // wait covers the gathers alone: they were issued first) and any further match of a lane
-    // (rare: gathered one at a time). A gather is a full memory latency under the scan's load:
-    // taken before the next unit's loads, it had left the wave one unit in flight meanwhile,
-    // and the workgroups holding matches ended ≈ 0.8 us after those without
+    // eval_a finds them, ranks them and issues the gathers of each lane's first match into a
+    // Pend (registers); eval_b stores them to LDS one unit of the same stream later (the loop
+    // below). A lane's further matches (rare) are gathered and stored at once. A gather is a
+    // full memory latency under the scan's load: waited for before the next unit's loads it had
+    // left the wave one unit in flight meanwhile (workgroups holding matches ended ≈ 0.8 us
+    // after those without); waited for right after them, ≈ 0.17 us per record (r06 stamps,
+    // profiles/r06_xsplit/analysis.txt); one unit later, nothing: the wave waits there for the
+    // loads issued after the gathers anyway.
     struct Pend {
-      uint32_t mask, e0, rank0[kSteps], bidx, r, ei, il;
-      bool any, has;
       u32x4 id;
       uint64_t st, en, nm;
-      const uint8_t *ids, *id_len;
-      const uint64_t *st_ns, *en_ns;
-      const uint32_t *names;
+      uint32_t ei, r_il, bidx;  // r_il: LDS rank | id length << 16
+      bool has;
+    };
+    auto put = [&](uint32_t r, const u32x4 &id, uint64_t st, uint64_t en, uint32_t ei, uint32_t bidx, uint32_t il,
+                   uint64_t nm) {
+      unsigned long long *d = s_rec + uint64_t(r) * 6;
+      d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
+      d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
+      d[2] = st;
+      d[3] = en;
+      d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
+      d[5] = nm;
     };
     auto eval_a = [&](const Regs &Rg, Pend &Pd) {
-      Pd.any = false;
       Pd.has = false;
       // the unit's block: lanes test the block boundaries, the ballot counts those passed
       const uint32_t u = ua + Rg.k;
@@ -945,15 +953,14 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
       base = uint32_t(__builtin_amdgcn_readfirstlane(base));
       const DevBlockDesc *D = uniform_ptr(A.desc[blk]);
       const auto *Dc = K4(D);
-      Pd.ids = Dc->ids;
-      Pd.st_ns = Dc->start_ns;
-      Pd.en_ns = Dc->end_ns;
-      Pd.names = Dc->names;
-      Pd.id_len = Dc->id_len;
-      Pd.bidx = uint32_t(__builtin_amdgcn_readfirstlane(P.block_idx));
+      const uint8_t *ids = Dc->ids, *id_len = Dc->id_len;
+      const uint64_t *st_ns = Dc->start_ns, *en_ns = Dc->end_ns;
+      const uint64_t *names = reinterpret_cast<const uint64_t *>(Dc->names);
+      const uint32_t bidx = uint32_t(__builtin_amdgcn_readfirstlane(P.block_idx));
+      Pd.bidx = bidx;
       const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
       // each step's first rank for this lane (ballots: every lane takes part)
-      uint32_t before = 0;
+      uint32_t rank0[kSteps], before = 0;
 #pragma unroll
       for (int kk = 0; kk < kSteps; kk++) {
         const uint32_t nib = (mask >> (4 * kk)) & 0xfu;
@@ -964,52 +971,38 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
           lower += uint32_t(__popcll(bb & below));
           tot += uint32_t(__popcll(bb));
         }
-        Pd.rank0[kk] = base + before + lower;
+        rank0[kk] = base + before + lower;
         before += tot;
       }
-      Pd.any = true;
-      Pd.mask = mask;
-      Pd.e0 = Rg.e0;
-      if (mask) {
+      if (!mask) return;
+      {
         const uint32_t bit = uint32_t(__builtin_ctz(mask)), kk = bit >> 2, j = bit & 3u;
-        Pd.r = (kk ? Pd.rank0[1] : Pd.rank0[0]) + uint32_t(__popc((mask >> (4 * kk)) & ((1u << j) - 1u)));
-        Pd.ei = Rg.e0 + kk * 256 + uint32_t(lane) * 4 + j;
-        if (Pd.r < rec_cap) {
+        const uint32_t r = (kk ? rank0[1] : rank0[0]) + uint32_t(__popc((mask >> (4 * kk)) & ((1u << j) - 1u)));
+        const uint32_t ei = Rg.e0 + kk * 256 + uint32_t(lane) * 4 + j;
+        if (r < rec_cap) {
           Pd.has = true;
-          Pd.id = *G<u32x4>(Pd.ids + uint64_t(Pd.ei) * 16);
-          Pd.st = G(Pd.st_ns)[Pd.ei];
-          Pd.en = G(Pd.en_ns)[Pd.ei];
-          Pd.nm = G(reinterpret_cast<const uint64_t *>(Pd.names))[Pd.ei];
-          Pd.il = G(Pd.id_len)[Pd.ei];
+          Pd.ei = ei;
+          Pd.id = *G<u32x4>(ids + uint64_t(ei) * 16);
+          Pd.st = G(st_ns)[ei];
+          Pd.en = G(en_ns)[ei];
+          Pd.nm = G(names)[ei];
+          Pd.r_il = r | uint32_t(G(id_len)[ei]) << 16;
         }
       }
-    };
-    auto put = [&](uint32_t r, const u32x4 &id, uint64_t st, uint64_t en, uint32_t ei, uint32_t bidx, uint32_t il,
-                   uint64_t nm) {
-      unsigned long long *d = s_rec + uint64_t(r) * 6;
-      d[0] = (unsigned long long)id.x | (unsigned long long)id.y << 32;
-      d[1] = (unsigned long long)id.z | (unsigned long long)id.w << 32;
-      d[2] = st;
-      d[3] = en;
-      d[4] = (unsigned long long)ei | (unsigned long long)(bidx | (il << 24)) << 32;
-      d[5] = nm;
-    };
-    auto eval_b = [&](const Pend &Pd) {
-      if (!Pd.any) return;
-      if (Pd.has) put(Pd.r, Pd.id, Pd.st, Pd.en, Pd.ei, Pd.bidx, Pd.il, Pd.nm);
       // a lane's further matches, one at a time (a loop kept rolled: the gathers of 8 records
-      // at once had pushed the kernel past its 128 registers)
-      const uint32_t mask = Pd.mask;
+      // at once had pushed the kernel past its registers)
 #pragma unroll 1
       for (uint32_t m = mask & (mask - 1u); m; m &= m - 1) {
         const uint32_t bit = uint32_t(__builtin_ctz(m)), kk = bit >> 2, j = bit & 3u;
-        const uint32_t r = (kk ? Pd.rank0[1] : Pd.rank0[0]) + uint32_t(__popc((mask >> (4 * kk)) & ((1u << j) - 1u)));
+        const uint32_t r = (kk ? rank0[1] : rank0[0]) + uint32_t(__popc((mask >> (4 * kk)) & ((1u << j) - 1u)));
         if (r >= rec_cap) continue;
-        const uint32_t ei = Pd.e0 + kk * 256 + uint32_t(lane) * 4 + j;
-        const u32x4 id = *G<u32x4>(Pd.ids + uint64_t(ei) * 16);
-        put(r, id, G(Pd.st_ns)[ei], G(Pd.en_ns)[ei], ei, Pd.bidx, G(Pd.id_len)[ei],
-            G(reinterpret_cast<const uint64_t *>(Pd.names))[ei]);
+        const uint32_t ei = Rg.e0 + kk * 256 + uint32_t(lane) * 4 + j;
+        const u32x4 id = *G<u32x4>(ids + uint64_t(ei) * 16);
+        put(r, id, G(st_ns)[ei], G(en_ns)[ei], ei, bidx, G(id_len)[ei], G(names)[ei]);
       }
+    };
+    auto eval_b = [&](const Pend &Pd) {
+      if (Pd.has) put(Pd.r_il & 0xffffu, Pd.id, Pd.st, Pd.en, Pd.ei, Pd.bidx, Pd.r_il >> 16, Pd.nm);
     };
     const bool interleave = (R.mode & 1u) != 0;
     auto claim = [&](uint32_t prev) -> uint32_t {
@@ -1022,21 +1015,27 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     uint32_t ka = wave, kb = wave + nwv;
     if (ka < nk) load(ra, ka);
     if (kb < nk) load(rb, kb);
-    Pend pd;
+    // a unit's gathers are stored one unit later (eval_b of unit n of a stream runs before
+    // eval_a of unit n+1 of the same stream): by then the loads issued after them are being
+    // waited for anyway (vector loads complete in order), so a match costs the wave no stall
+    Pend pa, pb;
+    pa.has = pb.has = false;
     while (ka < nk || kb < nk) {
       if (ka < nk) {
-        eval_a(ra, pd);
+        eval_b(pa);
+        eval_a(ra, pa);
         ka = claim(ka);
         if (ka < nk) load(ra, ka);
-        eval_b(pd);
       }
       if (kb < nk) {
-        eval_a(rb, pd);
+        eval_b(pb);
+        eval_a(rb, pb);
         kb = claim(kb);
         if (kb < nk) load(rb, kb);
-        eval_b(pd);
       }
     }
+    eval_b(pa);
+    eval_b(pb);
     __syncthreads();
     // ---- units' counts -> exclusive offsets (s_uc in place), then each unit's records to the
     // host segment at its offset, then the count
@@ -1781,6 +1780,7 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
     while (maxc > std::min(PA.seg_cap, rec_cap)) {
       if (maxc > rec_cap) {
         dc.pool_skip = 16;
+        dc.pool_skip_key = pool_query_key(q);
         return 0;
       }
       uint32_t want = 2 * PA.seg_cap;
@@ -2135,8 +2135,9 @@ bool pool_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> 
   // smaller one, TSG_POOL_REC)
   if (maxc > std::min(PA.seg_cap, rec_cap)) {
     for (;;) {
-      if (maxc > rec_cap) {  // dense: this query (and the next few) take the other paths
+      if (maxc > rec_cap) {  // dense: this query (and its next few searches) take the other paths
         dc.pool_skip = 16;
+        dc.pool_skip_key = pool_query_key(q);
         return false;
       }
       if (maxc <= PA.seg_cap) break;

@@ -2157,7 +2157,7 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // segment / look-back paths below when a workgroup's matches overflow its LDS buffer
   const bool ds16 = (!q.has_min || q.min_ns <= kDs16MaxMs * 1000000ull) && (!q.has_max || q.max_ns <= kDs16MaxMs * 1000000ull);
   if (fast && narrow && ds16 && !dc.seg_off && !dc.pool_off) {
-    if (dc.pool_skip) dc.pool_skip--;
+    if (dc.pool_skip && dc.pool_skip_key == pool_query_key(q)) dc.pool_skip--;
     else if (pool_search(dc, blocks, q, limit, flags, segs, nsegv, nbms, nbmi, seg_desc, has_dur, tr, out, lk)) {
       if (ranges) drop_before_ranges(blocks, *ranges, out);
       out.pool = true;

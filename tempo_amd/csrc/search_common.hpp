@@ -43,6 +43,20 @@ static_assert(sizeof(MatchRec) == 48, "record layout");
 static_assert(sizeof(MatchRec) == sizeof(SearchOut::Rec), "record layout");
 
 constexpr int kThreads = 256;
+// A query's shape for the pool kernels' overflow memory (DeviceCtx::pool_skip): its terms,
+// duration bounds and time range. A record-buffer overflow skips the pool for the next few
+// searches of the SAME query only: other queries interleaved with a dense one (concurrent
+// callers) keep the resident kernel.
+inline uint64_t pool_query_key(const tsg_query &q) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t(q.nterms) << 40) ^ (uint64_t(q.has_min) << 33) ^
+               (uint64_t(q.has_max) << 34) ^ (uint64_t(q.has_range) << 35);
+  h ^= q.min_ns * 0xBF58476D1CE4E5B9ull ^ q.max_ns * 0x94D049BB133111EBull ^
+       (uint64_t(q.start_s) << 32 | q.end_s) * 0xD6E8FEB86659FD93ull;
+  for (uint32_t t = 0; t < q.nterms; t++)
+    h = (h ^ xxhash64(q.keys[t], q.key_lens[t]) ^ (xxhash64(q.values[t], q.value_lens[t]) * 31)) *
+        0x9E3779B97F4A7C15ull;
+  return h;
+}
 constexpr int kSteps = 2;                     // 8 entries per thread per tile
 constexpr int kTile = kThreads * 4 * kSteps;  // 2048 entries
 constexpr uint32_t kMaskAll = (1u << (4 * kSteps)) - 1;

@@ -9,7 +9,10 @@
 // a hash of (e, the query) falls below 1/32 (capped, ranged and ordered as the real path hands
 // them over), so that concurrent callers with different queries get different, checkable
 // records. tsg_init fails with TSG_E_DEVICE (as without a GPU) unless TSG_STUB_DEVICES=n is set.
+#include <algorithm>
 #include <chrono>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -57,12 +60,19 @@ static uint64_t query_hash(const tsg_query &q) {
   }
   return h;
 }
+// TSG_STUB_ONE_IN: one entry in n matches (default 32); TSG_STUB_SLEEP_US: the stand-in device
+// time (default 20 + 0..63 us by query); both for tools/host_prof.py's host-cost runs
+static uint64_t stub_env(const char *name, uint64_t dflt) {
+  const char *e = std::getenv(name);
+  return e ? std::strtoull(e, nullptr, 10) : dflt;
+}
 bool stub_match(const tsg_query &q, uint64_t e) {  // (also called by the stress driver)
+  static const uint64_t one_in = std::max<uint64_t>(1, stub_env("TSG_STUB_ONE_IN", 32));
   uint64_t x = (e + 1) * 0xD6E8FEB86659FD93ull ^ query_hash(q);
   x ^= x >> 32;
   x *= 0xD6E8FEB86659FD93ull;
   x ^= x >> 29;
-  return (x & 31u) == 0;
+  return x % one_in == 0;
 }
 
 void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>> &blocks, const tsg_query &q,
@@ -88,8 +98,31 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
       e0 = std::min<uint64_t>((*ranges)[i].first, e1) / 512 * 512;
     }
     uint64_t kept = 0;
+    // (TSG_STUB_CACHE=1, tools/host_prof.py: a block's matches are found once per query, so that
+    // the stand-in device costs nothing per search; the host's share is what is measured)
+    static const bool cache = stub_env("TSG_STUB_CACHE", 0) != 0;
+    const std::vector<uint32_t> *hit = nullptr;
+    if (cache) {
+      static std::mutex mu;
+      static std::map<std::pair<const HostBlock *, uint64_t>, std::vector<uint32_t>> memo;
+      std::lock_guard<std::mutex> g(mu);
+      auto &v = memo[{&h, query_hash(q)}];
+      if (v.empty()) {
+        for (uint64_t e = 0; e < h.n; e++)
+          if (stub_match(q, e)) v.push_back(uint32_t(e));
+        v.push_back(UINT32_MAX);
+      }
+      hit = &v;
+    }
+    size_t hi = 0;
     for (uint64_t e = e0; e < e1 && (!limit || kept < limit); e++) {
-      if (!stub_match(q, e)) continue;
+      if (hit) {
+        while ((*hit)[hi] < e) hi++;
+        if ((*hit)[hi] >= e1) break;
+        e = (*hit)[hi];
+      } else if (!stub_match(q, e)) {
+        continue;
+      }
       SearchOut::Rec r;
       std::memcpy(r.id, h.ids.data() + e * 16, 16);
       r.start = h.start[e];
@@ -108,7 +141,9 @@ void device_search(DeviceCtx &dc, const std::vector<std::pair<uint32_t, Block *>
   // the device's time, with dc.mu released as the resident path releases it: other callers
   // plan meanwhile (the interleavings ThreadSanitizer sees)
   lk.unlock();
-  std::this_thread::sleep_for(std::chrono::microseconds(20 + (query_hash(q) & 63)));
+  static const uint64_t sleep_us = stub_env("TSG_STUB_SLEEP_US", ~0ull);
+  const uint64_t us = sleep_us == ~0ull ? 20 + (query_hash(q) & 63) : sleep_us;
+  if (us) std::this_thread::sleep_for(std::chrono::microseconds(us));
 }
 
 int device_numa_node(const DeviceCtx &) { return -1; }

