@@ -81,6 +81,18 @@ if has rprof; then  # rocprofv3 over resident launches that each serve 64 batche
   find gpurun_out/rp_res gpurun_out/rp_FETCH_SIZE gpurun_out/rp_WRITE_SIZE -name "*.csv" | head -20
   summ gpurun_out/rp_res.json rp_res
 fi
+if has ab; then  # library builds side by side (AB="w8 w12": tools/_bin/<v>/libtsg.so + its code object)
+  for v in ${AB:-w8 w12}; do
+    L=$PWD/tools/_bin/$v/libtsg.so
+    TSG_LIB_PATH=$L timeout -k 10 500 $T -m gpu ${ABTESTS:-tests/test_gpu_resident.py tests/test_gpu_pool.py} > gpurun_out/pt_ab_$v.log 2>&1
+    rc=$?; echo "ab $v tests rc=$rc"; tail -n 2 gpurun_out/pt_ab_$v.log; [ $rc -eq 0 ] || exit $rc
+    TSG_LIB_PATH=$L timeout -k 10 400 python3 bench.py --steps 200 --warmup 5 --limit-steps 0 $B > gpurun_out/quick_$v.json 2> gpurun_out/quick_$v.err
+    rc=$?; echo "ab $v quick rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/quick_$v.err; exit $rc; }
+    summ gpurun_out/quick_$v.json quick_$v
+    TSG_LIB_PATH=$L TSG_RES_DUMP=1 timeout -k 10 400 python3 bench.py --steps 100 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/dump_$v.json 2> gpurun_out/dump_$v.err
+    echo "ab $v dump rc=$?"; grep "resident stamps" gpurun_out/dump_$v.err | tail -3
+  done
+fi
 if has tests; then
   timeout -k 10 600 $T -m gpu ${TESTS:-tests/test_gpu_coalesce.py tests/test_gpu_pool.py tests/test_gpu_search.py} > gpurun_out/pt.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
