@@ -687,6 +687,7 @@ struct ResidentArgs {
   uint32_t idle_ticks;   // s_memrealtime ticks without a post before a workgroup leaves
   uint32_t nthreads, ngroups;
   uint32_t mode, pad;  // TSG_RES_MODE (experiments): bit 0 = units interleaved over the waves (no LDS claims),
+                       // bit 3 = no gathers (zero records), bit 4 = no records stored (counts only),
                        // bit 2 = poll the slot header alone, load the arguments once it shows the query,
                        // bit 1 = longer sleeps between doorbell polls
 };
@@ -912,7 +913,7 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     struct Pend {
       u32x4 id;
       uint64_t st, en, nm;
-      uint32_t ei, r_il, bidx;  // r_il: LDS rank | id length << 16
+      uint32_t ei, r, ilw, bidx;  // ilw: the aligned word holding the id length byte
       bool has;
     };
     auto put = [&](uint32_t r, const u32x4 &id, uint64_t st, uint64_t en, uint32_t ei, uint32_t bidx, uint32_t il,
@@ -979,14 +980,24 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
         const uint32_t bit = uint32_t(__builtin_ctz(mask)), kk = bit >> 2, j = bit & 3u;
         const uint32_t r = (kk ? rank0[1] : rank0[0]) + uint32_t(__popc((mask >> (4 * kk)) & ((1u << j) - 1u)));
         const uint32_t ei = Rg.e0 + kk * 256 + uint32_t(lane) * 4 + j;
-        if (r < rec_cap) {
+        if (r < rec_cap && (R.mode & 8u)) {  // (experiment: no gathers, zero records)
+          Pd.has = true;
+          Pd.ei = ei;
+          Pd.r = r;
+          Pd.id = u32x4{0, 0, 0, 0};
+          Pd.st = Pd.en = Pd.nm = 0;
+          Pd.ilw = 0;
+        } else if (r < rec_cap) {
           Pd.has = true;
           Pd.ei = ei;
           Pd.id = *G<u32x4>(ids + uint64_t(ei) * 16);
           Pd.st = G(st_ns)[ei];
           Pd.en = G(en_ns)[ei];
           Pd.nm = G(names)[ei];
-          Pd.r_il = r | uint32_t(G(id_len)[ei]) << 16;
+          // (the id length's aligned word, untouched until the store: no arithmetic on a
+          // gathered value here, or the wave waits for the gathers at once)
+          Pd.r = r;
+          Pd.ilw = *G<uint32_t>(id_len + (ei & ~3u));
         }
       }
       // a lane's further matches, one at a time (a loop kept rolled: the gathers of 8 records
@@ -1002,7 +1013,7 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
       }
     };
     auto eval_b = [&](const Pend &Pd) {
-      if (Pd.has) put(Pd.r_il & 0xffffu, Pd.id, Pd.st, Pd.en, Pd.ei, Pd.bidx, Pd.r_il >> 16, Pd.nm);
+      if (Pd.has) put(Pd.r, Pd.id, Pd.st, Pd.en, Pd.ei, Pd.bidx, (Pd.ilw >> (8 * (Pd.ei & 3u))) & 0xffu, Pd.nm);
     };
     const bool interleave = (R.mode & 1u) != 0;
     auto claim = [&](uint32_t prev) -> uint32_t {
@@ -1068,7 +1079,7 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     }
     const uint32_t seg_cap = uint32_t(__builtin_amdgcn_readfirstlane(A.seg_cap));
     const bool over = total > rec_cap;
-    if (!over && total <= seg_cap && total) {
+    if (!over && total <= seg_cap && total && !(R.mode & 16u)) {  // (mode 16: experiment, no records out)
       // output record p -> its LDS record: each unit with matches writes its range of the map
       // (a binary search of the offsets per output word had been ~7 dependent LDS reads)
       for (uint32_t k = uint32_t(tid); k < nk; k += nthreads) {

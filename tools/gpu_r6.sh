@@ -115,6 +115,12 @@ if has dump; then  # per-workgroup seen / end stamps of the timed main-line quer
   TSG_RES_XSPLIT=0 TSG_RES_DUMP=2 timeout -k 10 400 python3 bench.py --steps 200 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/dump_n.json 2> gpurun_out/dump_n.err
   echo "dump_n rc=$?"; summ gpurun_out/dump_n.json dump_n
 fi
+if has modes; then  # per-workgroup stamps under TSG_RES_MODE experiments (MODES="0 8 16")
+  for m in ${MODES:-0 8 16}; do
+    TSG_RES_MODE=$m TSG_RES_DUMP=2 timeout -k 10 400 python3 bench.py --steps 200 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/mode_$m.json 2> gpurun_out/mode_$m.err
+    echo "mode $m rc=$?"; summ gpurun_out/mode_$m.json mode_$m
+  done
+fi
 if has prof; then  # host phases of the main line
   TSG_PROF=1 timeout -k 10 400 python3 bench.py --steps 400 --warmup 5 --limit-steps 0 --batch-queries 0 $B > gpurun_out/prof.json 2> gpurun_out/prof.err
   rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/prof.err; exit $rc; }
