@@ -75,7 +75,7 @@ else:
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def pmc_traffic(workload_key):
+def pmc_traffic(workload_key, kernel=None):
     try:
         with open(PMC_FILE) as f:
             d = json.load(f)
@@ -83,7 +83,7 @@ def pmc_traffic(workload_key):
         return None, None
     w = d.get(workload_key, {})
     for name, ent in w.items():
-        if KERNEL.replace(" ", "") in name.replace(" ", ""):  # rocprof: "void tsg::search_fast_kernel<...>(tsg::QArgs)"
+        if (kernel or KERNEL).replace(" ", "") in name.replace(" ", ""):  # rocprof: "void tsg::search_fast_kernel<...>(tsg::QArgs)"
             return ent.get("traffic_bytes_per_launch"), ent.get("source", w.get("_source"))
     return None, None
 
@@ -1253,7 +1253,8 @@ def main():
     achieved = scan_bytes / scan_avg_ns if scan_avg_ns else None  # bytes/ns == GB/s
     regime = "hbm" if len(sets) * scan_bytes > 256 * 2**20 * 1.5 else "mall"
     # (the PMC figure of this layout: the pool kernels' 11 B/entry columns, round 4 on)
-    traffic, traffic_src = pmc_traffic(f"blocks={args.blocks},entries={args.entries},sets={len(sets)},layout=ds")
+    traffic, traffic_src = pmc_traffic(f"blocks={args.blocks},entries={args.entries},sets={len(sets)},layout=ds",
+                                       kernel_name)
     out = {
         "metric": METRIC,
         "value": value,
