@@ -2011,33 +2011,39 @@ int tsg_search(tsg_ctx *ctx, tsg_block *const *blocks, size_t nblocks, const tsg
     std::vector<std::vector<std::pair<uint32_t, Block *>>> pchunks;
     DeviceCtx *pdev = nullptr;
     auto pipelined_plan = [&]() -> bool {
-      // (read per query: a test turns it on for small blocks; two getenv calls per full scan)
-      const char *e1 = std::getenv("TSG_PIPE_DICT_MB"), *e2 = std::getenv("TSG_PIPE_BLOCKS");
-      const uint64_t kPipeDict = uint64_t(e1 ? std::atoll(e1) : 2048) << 20;  // wide-term dictionary bytes, all blocks
-      const size_t kPipeBlocks = size_t(std::max(1, e2 ? std::atoi(e2) : 2));
-      if (!kPipeDict || nseen) return false;
-      std::vector<std::pair<uint32_t, Block *>> list;
-      uint64_t dict = 0;
+      if (nseen) return false;
+      // the blocks, one device (the plain fan-out otherwise), before anything costlier
+      thread_local std::vector<std::pair<uint32_t, Block *>> list;
+      list.clear();
       for (size_t i = 0; i < nblocks; i++) {
         if (state[i] != 2 || !blocks[i]->b.dc) continue;
         Block &b = blocks[i]->b;
-        if (pdev && b.dc != pdev) return false;  // (one device: the plain fan-out otherwise)
+        if (pdev && b.dc != pdev) return false;
         pdev = b.dc;
         list.push_back({uint32_t(i), &b});
-        for (uint32_t t = 0; t < q->nterms; t++) {
-          const auto it = b.host->key_index.find(
-              std::string(reinterpret_cast<const char *>(q->keys[t]), q->key_lens[t]));
-          if (it == b.host->key_index.end() || size_t(it->second) >= b.dev.keys.size()) continue;
-          const DevKey &k = b.dev.keys[size_t(it->second)];
-          if (k.width != 1) dict += k.dict_nbytes;
-        }
       }
-      if (list.size() < 2 || list.size() > kChunk || dict < kPipeDict) return false;
+      if (list.size() < 2 || list.size() > kChunk) return false;
       // (a sparse result has nothing for the host to fill while the device works: one launch
       // — six launches of an absent needle had cost 93 us of scan kernels; TSG_PIPE_SPARSE=1
-      // pipelines whatever the last full scan's density)
+      // pipelines whatever the last full scan's density. Checked before the dictionary sizes:
+      // their per-block key lookups had cost every sparse full scan ~1 us of host time)
       const char *e3 = std::getenv("TSG_PIPE_SPARSE");
       if (!(e3 && std::atoi(e3)) && !device_last_dense(*pdev)) return false;
+      // (read per query: a test turns it on for small blocks)
+      const char *e1 = std::getenv("TSG_PIPE_DICT_MB"), *e2 = std::getenv("TSG_PIPE_BLOCKS");
+      const uint64_t kPipeDict = uint64_t(e1 ? std::atoll(e1) : 2048) << 20;  // wide-term dictionary bytes, all blocks
+      const size_t kPipeBlocks = size_t(std::max(1, e2 ? std::atoi(e2) : 2));
+      if (!kPipeDict) return false;
+      uint64_t dict = 0;
+      for (const auto &bp : list)
+        for (uint32_t t = 0; t < q->nterms; t++) {
+          const auto it = bp.second->host->key_index.find(
+              std::string(reinterpret_cast<const char *>(q->keys[t]), q->key_lens[t]));
+          if (it == bp.second->host->key_index.end() || size_t(it->second) >= bp.second->dev.keys.size()) continue;
+          const DevKey &k = bp.second->dev.keys[size_t(it->second)];
+          if (k.width != 1) dict += k.dict_nbytes;
+        }
+      if (dict < kPipeDict) return false;
       // one block in the last launch (its result fill is the part nothing overlaps) and in the
       // first (the host starts filling sooner); kPipeBlocks per launch between them
       const size_t nl = list.size();
