@@ -830,7 +830,10 @@ def cfg4_leg(args, eng, workdir, rank, gen_thread=None):
     kept = {}
     for name, q in CFG4_QUERIES:
         pipe = T.Pipeline(T.SearchRequest(**q))
+        # (the warmup with the timed steps' flags: a first TIME_ALL search of the dense query had
+        # been one step in 20 at 5-6x the median, its first-use allocations inside the timing)
         n0, _ = eng.search_raw(blocks, pipe)
+        eng.search_raw(blocks, pipe, flags=T.SEARCH_TIME_ALL)
         ts_all, dict_ns, scan_ns, steps = [], [], [], []
         met = None
         for i in range(args.cfg4_steps):
