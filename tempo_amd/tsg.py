@@ -618,6 +618,23 @@ class Engine:
         consumer) packed by tsg_result_pack into a wire buffer (numpy uint8): what a rank
         ships to the merging rank (tempo_amd.shard). No per-record Python."""
         import numpy as np
+        if combine is None and seen is None and not query_id:
+            # (the search_raw call cache: prebuilt ctypes arguments, no per-call array building)
+            fn, free, args, rp = self._raw_call(blocks, pipeline, limit, flags)[:4]
+            rc = fn(*args)
+            if rc:
+                _check(rc)
+            try:
+                out, ln = C.POINTER(C.c_uint8)(), C.c_size_t()
+                _check(lib().tsg_result_pack(rp, C.byref(out), C.byref(ln)))
+                try:
+                    buf = np.empty(ln.value, np.uint8)
+                    C.memmove(buf.ctypes.data, out, ln.value)
+                    return buf
+                finally:
+                    lib().tsg_free(out)
+            finally:
+                free(rp)
         arr = (C.c_void_p * max(len(blocks), 1))(*[b.h for b in blocks])
         opts = _SearchOpts(limit=limit, flags=flags, query_id=query_id)
         seen_arr = _seen(opts, seen)  # noqa: F841
