@@ -659,6 +659,10 @@ constexpr uint32_t kResSlots = 64, kResSlotBytes = 8192, kResHdrBytes = 64;
 constexpr uint32_t kResSearch = 1, kResQuit = 2;
 constexpr uint32_t kResMaxUnits = 2048;  // units per workgroup (the LDS tables); larger queries launch plainly
 constexpr uint32_t kResRejectWord = 8;   // ResidentArgs::err word counting rejected slot reads
+// a timed query's {seen, end} stamps, one 64-byte line per workgroup: four workgroups' 16-byte
+// stamps in one line had been partial-line writes to a shared line from four CUs, which land one
+// after another (the count lines' lesson, round 5): ~5 us more per timed query
+constexpr uint32_t kResStampStride = 8;
 struct ResHeader {  // the first 16 B of a mailbox slot; PoolArgs at +kResHdrBytes
   uint32_t seq, cmd, h0, h1;  // h0, h1: res_hash of (seq, cmd, the used argument words)
 };
@@ -688,6 +692,7 @@ struct ResidentArgs {
   uint32_t nthreads, ngroups;
   uint32_t mode, pad;  // TSG_RES_MODE (experiments): bit 0 = units interleaved over the waves (no LDS claims),
                        // bit 3 = no gathers (zero records), bit 4 = no records stored (counts only),
+                       // bit 6 = (host) timed queries without workgroup stamps (no span),
                        // bit 2 = poll the slot header alone, load the arguments once it shows the query,
                        // bit 1 = longer sleeps between doorbell polls
 };
@@ -1096,11 +1101,7 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
         host_store(dst0 + i, s_rec[uint64_t(s_map[p]) * 6 + j]);
       }
     }
-    if (tid == 0 && A.qstamps) {
-      unsigned long long *qs = uniform_ptr(A.qstamps);
-      host_store(qs + 2ull * w, t_seen);
-      host_store(qs + 2ull * w + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    }
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // the count last (more matches than the LDS buffer holds: the host reruns the query on the
@@ -1108,6 +1109,14 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     if (tid == 0)
       host_store(uniform_ptr(A.counts) + uint64_t(w) * max(1u, uint32_t(__builtin_amdgcn_readfirstlane(A.cstride))),
                  over ? max(total, rec_cap + 1) : total);
+    // a timed query's stamps after the count, not before it: the count's wait for its stores
+    // had included their round trip on every workgroup (~6 us more per timed query; the host
+    // waits for the stamps themselves, which it cleared at the post)
+    if (tid == 0 && A.qstamps) {  // (a 64-byte line per workgroup: kResStampStride)
+      unsigned long long *qs = uniform_ptr(A.qstamps) + uint64_t(w) * kResStampStride;
+      host_store(qs, t_seen);
+      host_store(qs + 1, t_end);
+    }
     __syncthreads();  // (the LDS tables are reused by the next query)
   }
 }
@@ -1522,7 +1531,7 @@ int debug_set(const char *name, int64_t value) {
 // query's records were read.
 static constexpr uint32_t kResCountStride = 16;  // one 64-byte line per workgroup's count
 static size_t res_area_bytes(uint32_t W, uint32_t seg) {
-  return 256 + align_up(size_t(W) * 4 * kResCountStride, 256) + align_up(size_t(W) * 16, 256) +
+  return 256 + align_up(size_t(W) * 4 * kResCountStride, 256) + align_up(size_t(W) * 8 * kResStampStride, 256) +
          size_t(W) * seg * sizeof(MatchRec);
 }
 
@@ -1596,12 +1605,12 @@ static uint32_t res_max_run(const PoolArgs &PA, uint32_t U, uint32_t W) {
 static void res_calibrate(DeviceCtx &dc, const unsigned long long *qst, const PoolArgs &PA, uint32_t U, uint32_t W) {
   if (W % 8 || U < 32u * W) return;
   unsigned long long lo = ~0ull;
-  for (uint32_t w = 0; w < W; w++) lo = std::min(lo, qst[2 * w]);
+  for (uint32_t w = 0; w < W; w++) lo = std::min(lo, qst[size_t(w) * kResStampStride]);
   double E[8] = {}, n[8] = {};
   uint32_t cnt[8] = {};
   for (uint32_t w = 0; w < W; w++) {
     const uint32_t x = w & 7u, i = w >> 3;
-    const unsigned long long e = qst[2 * w + 1];
+    const unsigned long long e = qst[size_t(w) * kResStampStride + 1];
     if (e < lo || e - lo > 100000000ull) return;  // (a stamp not written: skip the sample)
     E[x] += double(e - lo);
     n[x] += PA.xsplit ? double(PA.xn[x] + (i < PA.xr[x] ? 1u : 0u)) : double(PA.wq + (w < PA.wr ? 1u : 0u));
@@ -1690,10 +1699,11 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
   const bool timed = (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
   const size_t tslot = timed ? dc.tring_used - 1 : 0;
   // workgroup stamps: timed queries, and every 16th query for the XCD split (the first 8 all)
-  const bool stamp = timed || (debug_xsplit() && (dc.res_xsamples < 8 || dc.res_qn % 16 == 0));
+  static const bool no_stamps = (DeviceCtx::env_u32("TSG_RES_MODE", 0, 0, 255) & 64u) != 0;  // (experiment)
+  const bool stamp = !no_stamps && (timed || (debug_xsplit() && (dc.res_xsamples < 8 || dc.res_qn % 16 == 0)));
   dc.res_qn++;
   const uint32_t cs = kResCountStride;
-  const size_t hdr = 256, cntb = align_up(size_t(W) * 4 * cs, 256), stb = align_up(size_t(W) * 16, 256);
+  const size_t hdr = 256, cntb = align_up(size_t(W) * 4 * cs, 256), stb = align_up(size_t(W) * 8 * kResStampStride, 256);
   uint32_t *counts = nullptr;
   unsigned long long *qst = nullptr;
   const uint8_t *recs = nullptr;
@@ -1710,6 +1720,8 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
     PA.qstamps = stamp ? qst : nullptr;
     PA.cstride = cs;
     for (uint32_t w = 0; w < W; w++) counts[size_t(w) * cs] = kCountPending;
+    if (stamp)  // (the stamps land after the counts: 0 = not yet)
+      for (uint32_t x = 0; x < W; x++) qst[size_t(x) * kResStampStride] = qst[size_t(x) * kResStampStride + 1] = 0;
     if (rel.posted) dc.res_inflight.erase(rel.seq);
     rel.seq = ++dc.res_seq;
     rel.posted = true;
@@ -1747,11 +1759,20 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
         if (prefetch) {
           const uint8_t *p0 = recs + uint64_t(w) * seg * sizeof(MatchRec);
           for (uint64_t o = 0; o < uint64_t(std::min(c, seg)) * sizeof(MatchRec); o += 64) __builtin_prefetch(p0 + o);
+          if (stamp) __builtin_prefetch(qst + uint64_t(w) * kResStampStride);  // (a timed query's stamps)
         }
       }
       if (lo == W) {
         if (prof)
           prof_add("res.last_count", std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        if (stamp) {  // a timed query's stamps, stored after each workgroup's count (bounded: a missing one reads 0)
+          const auto ts = std::chrono::steady_clock::now();
+          for (uint32_t x = 0; x < W; x++)
+            while ((__atomic_load_n(qst + size_t(x) * kResStampStride, __ATOMIC_ACQUIRE) == 0 ||
+                    __atomic_load_n(qst + size_t(x) * kResStampStride + 1, __ATOMIC_ACQUIRE) == 0) &&
+                   std::chrono::steady_clock::now() - ts < std::chrono::milliseconds(2))
+              __builtin_ia32_pause();
+        }
         lk.lock();
         return;
       }
@@ -1824,15 +1845,15 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
   if (timed) {  // the query's span on the device: first workgroup to see it .. last to finish
     unsigned long long lo = ~0ull, hi = 0;
     for (uint32_t w = 0; w < W; w++) {
-      lo = std::min(lo, __atomic_load_n(qst + 2 * w, __ATOMIC_ACQUIRE));
-      hi = std::max(hi, __atomic_load_n(qst + 2 * w + 1, __ATOMIC_ACQUIRE));
+      lo = std::min(lo, __atomic_load_n(qst + size_t(w) * kResStampStride, __ATOMIC_ACQUIRE));
+      hi = std::max(hi, __atomic_load_n(qst + size_t(w) * kResStampStride + 1, __ATOMIC_ACQUIRE));
     }
     static const bool dump = std::getenv("TSG_RES_DUMP") != nullptr;
     if (dump) {  // spread of the workgroups' {seen, end} stamps (us after the first seen)
       std::vector<double> sn(W), en(W);
       for (uint32_t w = 0; w < W; w++) {
-        sn[w] = double(qst[2 * w] - lo) / 100.0;
-        en[w] = double(qst[2 * w + 1] - lo) / 100.0;
+        sn[w] = double(qst[size_t(w) * kResStampStride] - lo) / 100.0;
+        en[w] = double(qst[size_t(w) * kResStampStride + 1] - lo) / 100.0;
       }
       static const bool raw = std::getenv("TSG_RES_DUMP")[0] == '2';
       if (raw) {  // every workgroup's end (0.01 us after the first seen), workgroup order
@@ -1842,9 +1863,9 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
         for (uint32_t w = 0; w < W; w++)
           line += " " + std::to_string(PA.xsplit ? PA.xn[w & 7] + ((w >> 3) < PA.xr[w & 7] ? 1u : 0u) : PA.wq + (w < PA.wr ? 1u : 0u));
         line += "\n[tsg] resident seen:";
-        for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(qst[2 * w] - lo);
+        for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(qst[size_t(w) * kResStampStride] - lo);
         line += "\n[tsg] resident ends:";
-        for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(qst[2 * w + 1] - lo);
+        for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(qst[size_t(w) * kResStampStride + 1] - lo);
         line += "\n[tsg] resident counts:";
         for (uint32_t w = 0; w < W; w++) line += " " + std::to_string(counts[size_t(w) * cs]);
         std::fprintf(stderr, "%s\n", line.c_str());
