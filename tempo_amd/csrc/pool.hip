@@ -1106,12 +1106,16 @@ __global__ void __launch_bounds__(kResThreads, 1) search_resident_kernel(Residen
     __syncthreads();
     // the count last (more matches than the LDS buffer holds: the host reruns the query on the
     // segment / look-back path)
-    if (tid == 0)
-      host_store(uniform_ptr(A.counts) + uint64_t(w) * max(1u, uint32_t(__builtin_amdgcn_readfirstlane(A.cstride))),
-                 over ? max(total, rec_cap + 1) : total);
-    // a timed query's stamps after the count, not before it: the count's wait for its stores
-    // had included their round trip on every workgroup (~6 us more per timed query; the host
-    // waits for the stamps themselves, which it cleared at the post)
+    // with the low 32 bits of the seen / end stamps in the same 16-byte store: a timed query's
+    // span costs no store of its own (separate stamp stores had cost ~4-6 us per timed query:
+    // before the count, the count waited for their round trip; after it, the next query's first
+    // waits did)
+    if (tid == 0) {
+      uint32_t *cl = uniform_ptr(A.counts) + uint64_t(w) * max(1u, uint32_t(__builtin_amdgcn_readfirstlane(A.cstride)));
+      const u32x4 v = {over ? max(total, rec_cap + 1) : total, uint32_t(t_seen), uint32_t(t_end), 0u};
+      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(cl), "v"(v) : "memory");
+    }
+    // the full stamps (diagnostics: TSG_RES_DUMP, the XCD calibration) after the count
     if (tid == 0 && A.qstamps) {  // (a 64-byte line per workgroup: kResStampStride)
       unsigned long long *qs = uniform_ptr(A.qstamps) + uint64_t(w) * kResStampStride;
       host_store(qs, t_seen);
@@ -1699,8 +1703,10 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
   const bool timed = (flags & TSG_SEARCH_TIME_DEFER) && dc.defer_slot(e0, e1);
   const size_t tslot = timed ? dc.tring_used - 1 : 0;
   // workgroup stamps: timed queries, and every 16th query for the XCD split (the first 8 all)
-  static const bool no_stamps = (DeviceCtx::env_u32("TSG_RES_MODE", 0, 0, 255) & 64u) != 0;  // (experiment)
-  const bool stamp = !no_stamps && (timed || (debug_xsplit() && (dc.res_xsamples < 8 || dc.res_qn % 16 == 0)));
+  // full workgroup stamps only for the diagnostics that read them per workgroup (a timed query's
+  // span comes from the count lines: each carries its workgroup's seen / end stamps' low 32 bits)
+  static const bool dump_stamps = std::getenv("TSG_RES_DUMP") != nullptr;
+  const bool stamp = (timed && dump_stamps) || (debug_xsplit() && (dc.res_xsamples < 8 || dc.res_qn % 16 == 0));
   dc.res_qn++;
   const uint32_t cs = kResCountStride;
   const size_t hdr = 256, cntb = align_up(size_t(W) * 4 * cs, 256), stb = align_up(size_t(W) * 8 * kResStampStride, 256);
@@ -1843,13 +1849,18 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
     if (debug_xsplit()) res_calibrate(dc, qst, PA, U, W);
   }
   if (timed) {  // the query's span on the device: first workgroup to see it .. last to finish
-    unsigned long long lo = ~0ull, hi = 0;
+    // (from the count lines: the stamps' low 32 bits, 100 MHz: relative to workgroup 0's seen)
+    const uint32_t ref = counts[1];
+    int64_t dlo = INT64_MAX, dhi = INT64_MIN;
     for (uint32_t w = 0; w < W; w++) {
-      lo = std::min(lo, __atomic_load_n(qst + size_t(w) * kResStampStride, __ATOMIC_ACQUIRE));
-      hi = std::max(hi, __atomic_load_n(qst + size_t(w) * kResStampStride + 1, __ATOMIC_ACQUIRE));
+      dlo = std::min<int64_t>(dlo, int32_t(counts[size_t(w) * cs + 1] - ref));
+      dhi = std::max<int64_t>(dhi, int32_t(counts[size_t(w) * cs + 2] - ref));
     }
+    const unsigned long long span = dhi > dlo ? uint64_t(dhi - dlo) : 0;
     static const bool dump = std::getenv("TSG_RES_DUMP") != nullptr;
     if (dump) {  // spread of the workgroups' {seen, end} stamps (us after the first seen)
+      unsigned long long lo = ~0ull;  // (the full stamps' first seen)
+      for (uint32_t w = 0; w < W; w++) lo = std::min(lo, qst[size_t(w) * kResStampStride]);
       std::vector<double> sn(W), en(W);
       for (uint32_t w = 0; w < W; w++) {
         sn[w] = double(qst[size_t(w) * kResStampStride] - lo) / 100.0;
@@ -1877,7 +1888,7 @@ static int resident_search(DeviceCtx &dc, std::unique_lock<std::mutex> &lk, Pool
     }
     if (dc.tring_res.size() < dc.tring_used) dc.tring_res.resize(dc.tring_used);
     dc.tring_aql[tslot] = -3;
-    dc.tring_res[tslot] = hi > lo ? (hi - lo) * 10ull : 0ull;  // (100 MHz ticks)
+    dc.tring_res[tslot] = span * 10ull;  // (100 MHz ticks)
   }
   out.kernel_ns = out.scan_ns = 0;
   out.reruns = reruns;
