@@ -36,8 +36,11 @@
  *                         tempodb/encoding/v2/index_reader.go:85-114) and the
  *                         tempodb.Find block prefilter (tempodb/tempodb.go:492-511)
  *
- * Threading: a tsg_ctx is thread-safe. Searches on one device are serialised on
- * that device's stream; blocks on different devices are searched in parallel.
+ * Threading: a tsg_ctx is thread-safe. Blocks on different devices are searched in
+ * parallel. On one device, narrow searches from concurrent callers (and the items of
+ * tsg_search_batch) are in flight together: each is posted to the device's resident search
+ * kernel while earlier ones run, and the kernel serves them back to back (up to
+ * TSG_RES_DEPTH at once); other searches on the device are serialised on its stream.
  *
  * Errors: every int-returning call returns a TSG_* status; tsg_last_error()
  * returns the thread-local message of the last failure on this thread.
