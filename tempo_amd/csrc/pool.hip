@@ -692,7 +692,6 @@ struct ResidentArgs {
   uint32_t nthreads, ngroups;
   uint32_t mode, pad;  // TSG_RES_MODE (experiments): bit 0 = units interleaved over the waves (no LDS claims),
                        // bit 3 = no gathers (zero records), bit 4 = no records stored (counts only),
-                       // bit 6 = (host) timed queries without workgroup stamps (no span),
                        // bit 2 = poll the slot header alone, load the arguments once it shows the query,
                        // bit 1 = longer sleeps between doorbell polls
 };
