@@ -330,7 +330,7 @@ __device__ __forceinline__ void d_id_hash(const uint8_t *id, uint32_t &fnv, uint
   d_hashes(a, b, h);
 }
 
-extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_count_kernel(LkParams P) {
+__device__ __forceinline__ void lookup_count_body(const LkParams &P) {
   __shared__ uint32_t s_tile;
   __shared__ unsigned long long s_w[kLkThreads / 64], s_excl;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -415,6 +415,18 @@ extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_count_kernel(LkP
   }
   __syncthreads();
   if (i < P.nids) P.offsets[i] = s_excl + before + v - cnt;
+}
+extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_count_kernel(LkParams P) { lookup_count_body(P); }
+// the same pass at more waves per SIMD: 72 VGPRs and 7 waves, no spills (the default; config 5
+// 2.07 vs 2.12-2.13 ms per call at 6 waves, 2.13 at 8 waves with 48 B of spills per lane —
+// profiles/r06_lookup; TSG_LK_OCC=6 / 8 select the others)
+extern "C" __global__ void __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(7)))
+lookup_count_kernel_w7(LkParams P) {
+  lookup_count_body(P);
+}
+extern "C" __global__ void __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(8)))
+lookup_count_kernel_w8(LkParams P) {
+  lookup_count_body(P);
 }
 
 extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_write_kernel(LkParams P) {
@@ -873,7 +885,13 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
     lookup_transpose_kernel<<<uint32_t((threads + 255) / 256), 256, 0, s>>>(tp);
     HIP_OK(hipGetLastError());
   }
-  lookup_count_kernel<<<tiles, kLkThreads, 0, s>>>(P);
+  static const int occ = [] {
+    const char *e = std::getenv("TSG_LK_OCC");
+    return e ? std::atoi(e) : 7;
+  }();
+  if (occ == 8) lookup_count_kernel_w8<<<tiles, kLkThreads, 0, s>>>(P);
+  else if (occ == 6) lookup_count_kernel<<<tiles, kLkThreads, 0, s>>>(P);
+  else lookup_count_kernel_w7<<<tiles, kLkThreads, 0, s>>>(P);
   HIP_OK(hipGetLastError());
   dc.ticket_base += tiles;
   uint64_t total = 0;
