@@ -330,6 +330,7 @@ __device__ __forceinline__ void d_id_hash(const uint8_t *id, uint32_t &fnv, uint
   d_hashes(a, b, h);
 }
 
+template <bool NT>
 __device__ __forceinline__ void lookup_count_body(const LkParams &P) {
   __shared__ uint32_t s_tile;
   __shared__ unsigned long long s_w[kLkThreads / 64], s_excl;
@@ -341,7 +342,14 @@ __device__ __forceinline__ void lookup_count_body(const LkParams &P) {
   uint32_t cnt = 0;
   if (i < P.nids) {
     uint8_t id[16];
-    memcpy(id, P.ids + i * 16, 16);
+    if (NT) {  // (streamed once: kept out of L2, which holds what it can of the slab table)
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+      const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(P.ids) + i);
+#pragma unroll
+      for (int q = 0; q < 16; q++) id[q] = uint8_t(w[q / 4] >> (8 * (q % 4)));
+    } else {
+      memcpy(id, P.ids + i * 16, 16);
+    }
     uint32_t fnv;
     uint64_t h[4];
     d_id_hash(id, fnv, h);
@@ -352,7 +360,8 @@ __device__ __forceinline__ void lookup_count_body(const LkParams &P) {
       }
       cnt++;
     });
-    P.hit_cnt[i] = cnt;
+    if (NT) __builtin_nontemporal_store(cnt, P.hit_cnt + i);
+    else P.hit_cnt[i] = cnt;
   }
   // block scan of counts
   unsigned long long v = cnt;
@@ -414,19 +423,27 @@ __device__ __forceinline__ void lookup_count_body(const LkParams &P) {
     }
   }
   __syncthreads();
-  if (i < P.nids) P.offsets[i] = s_excl + before + v - cnt;
+  if (i < P.nids) {
+    if (NT) __builtin_nontemporal_store(uint64_t(s_excl + before + v - cnt), P.offsets + i);
+    else P.offsets[i] = s_excl + before + v - cnt;
+  }
 }
-extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_count_kernel(LkParams P) { lookup_count_body(P); }
+extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_count_kernel(LkParams P) { lookup_count_body<false>(P); }
 // the same pass at more waves per SIMD: 72 VGPRs and 7 waves, no spills (the default; config 5
 // 2.07 vs 2.12-2.13 ms per call at 6 waves, 2.13 at 8 waves with 48 B of spills per lane —
 // profiles/r06_lookup; TSG_LK_OCC=6 / 8 select the others)
 extern "C" __global__ void __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(7)))
 lookup_count_kernel_w7(LkParams P) {
-  lookup_count_body(P);
+  lookup_count_body<false>(P);
+}
+// ids loaded and counts / offsets stored non-temporally (experiment, TSG_LK_OCC=17)
+extern "C" __global__ void __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(7)))
+lookup_count_kernel_w7nt(LkParams P) {
+  lookup_count_body<true>(P);
 }
 extern "C" __global__ void __launch_bounds__(kLkThreads) __attribute__((amdgpu_waves_per_eu(8)))
 lookup_count_kernel_w8(LkParams P) {
-  lookup_count_body(P);
+  lookup_count_body<false>(P);
 }
 
 extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_write_kernel(LkParams P) {
@@ -891,6 +908,7 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
   }();
   if (occ == 8) lookup_count_kernel_w8<<<tiles, kLkThreads, 0, s>>>(P);
   else if (occ == 6) lookup_count_kernel<<<tiles, kLkThreads, 0, s>>>(P);
+  else if (occ == 17) lookup_count_kernel_w7nt<<<tiles, kLkThreads, 0, s>>>(P);
   else lookup_count_kernel_w7<<<tiles, kLkThreads, 0, s>>>(P);
   HIP_OK(hipGetLastError());
   dc.ticket_base += tiles;
