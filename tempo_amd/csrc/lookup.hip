@@ -60,7 +60,10 @@ struct LkParams {
   const uint32_t *direct;    // block ordinals probed one by one (ascending)
   const uint8_t *ids;
   uint64_t nids;
-  uint32_t pair, pad0;  // slab probes two at a time (TSG_LK_PAIR=1; default one at a time)
+  uint32_t pair;  // slab probes two at a time (TSG_LK_PAIR=1; default one at a time)
+  uint32_t smaj;  // kept hits slot-major, (block, record) pairs at hit_b as uint2 (hit j of id i at
+                  // j * nids + i: a wave's stores of its ids' first hits land in adjacent words), or
+                  // id-major in hit_b / hit_r (i * kHitK + j, TSG_LK_SLOTMAJOR=0)
   unsigned long long epoch, ticket_base;
   unsigned long long *ticket, *gran;
   uint64_t *offsets;  // per id: first output slot
@@ -355,8 +358,12 @@ __device__ __forceinline__ void lookup_count_body(const LkParams &P) {
     d_id_hash(id, fnv, h);
     for_each_hit(P, id, fnv, h, [&](uint32_t b, int32_t r) {
       if (cnt < kHitK) {
-        P.hit_b[i * kHitK + cnt] = b;
-        P.hit_r[i * kHitK + cnt] = r;
+        if (P.smaj) {  // (block and record in one 8-byte store)
+          reinterpret_cast<uint2 *>(P.hit_b)[uint64_t(cnt) * P.nids + i] = make_uint2(b, uint32_t(r));
+        } else {
+          P.hit_b[i * kHitK + cnt] = b;
+          P.hit_r[i * kHitK + cnt] = r;
+        }
       }
       cnt++;
     });
@@ -455,8 +462,14 @@ extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_write_kernel(LkP
     uint32_t hb[kHitK];
     int32_t hr[kHitK];
     for (uint32_t j = 0; j < cnt; j++) {
-      hb[j] = P.hit_b[i * kHitK + j];
-      hr[j] = P.hit_r[i * kHitK + j];
+      if (P.smaj) {
+        const uint2 br = reinterpret_cast<const uint2 *>(P.hit_b)[uint64_t(j) * P.nids + i];
+        hb[j] = br.x;
+        hr[j] = int32_t(br.y);
+      } else {
+        hb[j] = P.hit_b[i * kHitK + j];
+        hr[j] = P.hit_r[i * kHitK + j];
+      }
       for (uint32_t q = j; q > 0 && hb[q - 1] > hb[q]; q--) {
         uint32_t tb = hb[q]; hb[q] = hb[q - 1]; hb[q - 1] = tb;
         int32_t tr = hr[q]; hr[q] = hr[q - 1]; hr[q - 1] = tr;
@@ -876,6 +889,11 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
     return e ? uint32_t(std::atoi(e) != 0) : 0u;  // (pairs: 2.18 vs 2.15 ms per config-5 step, profiles/r03_lookup)
   }();
   P.pair = pair;
+  static const uint32_t smaj = [] {
+    const char *e = std::getenv("TSG_LK_SLOTMAJOR");
+    return e ? uint32_t(std::atoi(e) != 0) : 1u;
+  }();
+  P.smaj = smaj;
   P.epoch = dc.epoch;
   P.ticket_base = dc.ticket_base;
   P.ticket = static_cast<unsigned long long *>(dc.ticket.p);
@@ -883,9 +901,9 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
   P.offsets = static_cast<uint64_t *>(dc.vmatch.p);
   P.total = static_cast<uint64_t *>(dc.hdr.p);
   P.err = static_cast<uint32_t *>(dc.err.p);
-  dc.lkhits.ensure(std::max<uint64_t>(nids, 1) * (4 + kHitK * 8));
+  dc.lkhits.ensure((std::max<uint64_t>(nids, 1) + 1) * (4 + kHitK * 8));
   P.hit_cnt = static_cast<uint32_t *>(dc.lkhits.p);
-  P.hit_b = P.hit_cnt + nids;
+  P.hit_b = P.hit_cnt + ((nids + 1) & ~uint64_t(1));  // (8-byte aligned: the slot-major uint2 pairs)
   P.hit_r = reinterpret_cast<int32_t *>(P.hit_b + nids * kHitK);
   HIP_OK(hipEventRecord(dc.ev0, s));
   for (size_t i = 0; i < slabs.size(); i++) {  // (inside the timed region: built per call)
