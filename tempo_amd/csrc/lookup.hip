@@ -78,6 +78,11 @@ struct LkParams {
   int32_t *o_rec;
   uint64_t *o_start;
   uint32_t *o_len;
+  // the write pass places its columns itself (o_* = obase + total x column offsets, total read
+  // from the count pass's *total), so the host need not read the total between the passes; a
+  // total above ocap (or a count pass that failed) writes nothing and the host relaunches
+  uint8_t *obase;
+  uint64_t ocap;
 };
 
 __device__ __forceinline__ uint64_t d_rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
@@ -456,6 +461,16 @@ lookup_count_kernel_w8(LkParams P) {
 extern "C" __global__ void __launch_bounds__(kLkThreads) lookup_write_kernel(LkParams P) {
   const uint64_t i = uint64_t(blockIdx.x) * kLkThreads + threadIdx.x;
   if (i >= P.nids) return;
+  if (P.obase) {
+    const uint64_t total = __builtin_amdgcn_readfirstlane(uint32_t(*P.total)) |
+                           uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(*P.total >> 32))) << 32;
+    if (total > P.ocap || *P.err) return;
+    P.o_start = reinterpret_cast<uint64_t *>(P.obase);
+    P.o_id = reinterpret_cast<uint32_t *>(P.obase + total * 8);
+    P.o_block = reinterpret_cast<uint32_t *>(P.obase + total * 12);
+    P.o_rec = reinterpret_cast<int32_t *>(P.obase + total * 16);
+    P.o_len = reinterpret_cast<uint32_t *>(P.obase + total * 20);
+  }
   const uint32_t cnt = P.hit_cnt[i];
   const uint64_t o0 = P.offsets[i];
   if (cnt <= kHitK) {  // every hit was kept by the count pass: sort by block, copy
@@ -930,6 +945,31 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
   else lookup_count_kernel_w7<<<tiles, kLkThreads, 0, s>>>(P);
   HIP_OK(hipGetLastError());
   dc.ticket_base += tiles;
+  // The write pass follows at once, its columns sized on the device for up to ocap hits (one
+  // per id, or what the output buffer already holds): no host round trip between the passes.
+  const size_t per = 4 + 4 + 4 + 8 + 4;
+  static const bool host_sized = [] {  // (TSG_LK_HOSTSIZE=1: the round-5 order, the total read first)
+    const char *e = std::getenv("TSG_LK_HOSTSIZE");
+    return e && std::atoi(e) != 0;
+  }();
+  uint64_t want = std::max<uint64_t>(nids, 1);
+  if (host_sized) {
+    uint64_t t0 = 0;
+    HIP_OK(hipMemcpyAsync(&t0, dc.hdr.p, 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    want = std::max<uint64_t>(want, t0);
+  }
+  dc.out.ensure(want * per + 64);
+  P.obase = static_cast<uint8_t *>(dc.out.p);
+  P.ocap = (dc.out.cap - 64) / per;
+  static const uint64_t cap_test = [] {  // (test hook: TSG_LK_OCAP=n caps the first write pass's
+    const char *e = std::getenv("TSG_LK_OCAP");  // columns at n hits, so the relaunch runs)
+    return e ? uint64_t(std::strtoull(e, nullptr, 10)) : ~0ULL;
+  }();
+  P.ocap = std::min<uint64_t>(P.ocap, cap_test);
+  lookup_write_kernel<<<tiles, kLkThreads, 0, s>>>(P);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(dc.ev1, s));
   uint64_t total = 0;
   uint32_t errf = 0;
   HIP_OK(hipMemcpyAsync(&total, dc.hdr.p, 8, hipMemcpyDeviceToHost, s));
@@ -939,17 +979,20 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
     HIP_OK(hipMemset(dc.err.p, 0, 4));
     fail(TSG_E_DEVICE, "lookup look-back timed out");
   }
-  size_t per = 4 + 4 + 4 + 8 + 4;
-  dc.out.ensure(std::max<uint64_t>(total, 1) * per + 64);
+  if (total > P.ocap) {  // more hits than the columns held: grow them and write again
+    dc.out.ensure(total * per + 64);
+    P.obase = static_cast<uint8_t *>(dc.out.p);
+    P.ocap = (dc.out.cap - 64) / per;
+    lookup_write_kernel<<<tiles, kLkThreads, 0, s>>>(P);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(dc.ev1, s));
+  }
   auto *ob = static_cast<uint8_t *>(dc.out.p);
   P.o_start = reinterpret_cast<uint64_t *>(ob);
   P.o_id = reinterpret_cast<uint32_t *>(ob + total * 8);
   P.o_block = reinterpret_cast<uint32_t *>(ob + total * 12);
   P.o_rec = reinterpret_cast<int32_t *>(ob + total * 16);
   P.o_len = reinterpret_cast<uint32_t *>(ob + total * 20);
-  lookup_write_kernel<<<tiles, kLkThreads, 0, s>>>(P);
-  HIP_OK(hipGetLastError());
-  HIP_OK(hipEventRecord(dc.ev1, s));
   out.id_idx.resize(total);
   out.block_idx.resize(total);
   out.rec.resize(total);
