@@ -208,3 +208,51 @@ def test_lookup_and_find_across_devices(tmp_path):
     for i, b, st, obj in fgot:
         assert obj == exp[(i, b)]
     assert sum(g[2] == T.TSG_OK for g in fgot) >= 1500
+
+
+_LK_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import tempo_amd as T
+ids = np.load(sys.argv[2])
+eng = T.Engine(devices=[0])
+blocks = [eng.open_v2block(p) for p in sys.argv[4:]]
+got, _ = eng.lookup(blocks, ids)
+np.save(sys.argv[3], got)
+for b in blocks:
+    b.close()
+eng.close()
+"""
+
+
+@pytest.mark.parametrize("env", [{"TSG_LK_OCAP": "1"}, {"TSG_LK_SLOTMAJOR": "0", "TSG_LK_HOSTSIZE": "1"},
+                                 {"TSG_LK_OCC": "6"}])
+def test_lookup_pass_variants(tmp_path, env):
+    """The count / write passes' alternatives, each read once per process (so a child process):
+    the write pass's relaunch when the hits outnumber its first columns (TSG_LK_OCAP=1 caps them
+    at one hit), the round-5 id-major kept hits with the host reading the total between the
+    passes, and the 6-wave count pass — every one returns the oracle's hits."""
+    import subprocess
+    import sys
+    paths, stored = [], []
+    for b in range(3):
+        p = os.path.join(str(tmp_path), "v%d" % b)
+        stored.append(T.synth_v2_block(p, 8000 + 2000 * b, seed=40 + b))
+        paths.append(p)
+    rng = np.random.default_rng(4)
+    ids = np.concatenate([s[rng.integers(0, len(s), 1500)] for s in stored] +
+                         [rng.integers(0, 256, size=(3000, 16), dtype=np.uint8)])
+    rng.shuffle(ids)
+    ip, op = os.path.join(str(tmp_path), "ids.npy"), os.path.join(str(tmp_path), "got.npy")
+    np.save(ip, ids)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    e.update(env)
+    r = subprocess.run([sys.executable, "-c", _LK_CHILD, root, ip, op, *paths], env=e, timeout=100,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = np.load(op)
+    exp = oracle_hits(paths, ids)
+    assert len(exp) > 1
+    np.testing.assert_array_equal(got, exp)
