@@ -324,6 +324,49 @@ extern "C" __global__ void __launch_bounds__(256) lookup_transpose_kernel(TrPara
   }
 }
 
+// The same table, the 32 x 64 bit block of a thread transposed as two 32 x 32 bit matrices with
+// log2(32) = 5 rounds of masked swaps (each round swaps the off-diagonal j x j blocks of every
+// 2j x 2j block), ~400 ALU ops per 1024 bits instead of one shift-and-or per bit.
+__device__ __forceinline__ void d_tr32(uint32_t (&A)[32]) {
+  uint32_t m = 0x0000FFFFu;
+#pragma unroll
+  for (int j = 16; j; j >>= 1, m ^= (m << j)) {
+#pragma unroll
+    for (int k0 = 0; k0 < 32; k0 += 2 * j)
+#pragma unroll
+      for (int k = k0; k < k0 + j; k++) {
+        const uint32_t t = ((A[k] >> j) ^ A[k + j]) & m;
+        A[k + j] ^= t;
+        A[k] ^= t << j;
+      }
+  }
+}
+extern "C" __global__ void __launch_bounds__(256) lookup_transpose2_kernel(TrParams P) {
+  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint32_t jc = uint32_t(g % P.W);
+  const uint64_t rest = g / P.W;
+  const uint64_t w = rest % P.words, s = rest / P.words;
+  if (s >= P.shards) return;
+  uint32_t lo[32], hi[32];
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    const uint32_t mj = jc * 32 + uint32_t(j);
+    const uint64_t x = mj < P.J ? P.bloom[mj][s * P.words + w] : 0ULL;
+    lo[j] = uint32_t(x);
+    hi[j] = uint32_t(x >> 32);
+  }
+  d_tr32(lo);
+  d_tr32(hi);
+  uint32_t *out = P.T + (s * P.bitlen + w * 64) * P.W + jc;
+  const uint32_t nq = uint32_t(min<uint64_t>(64, P.bitlen - w * 64));
+#pragma unroll
+  for (int q = 0; q < 32; q++)
+    if (uint32_t(q) < nq) out[uint64_t(q) * P.W] = lo[q];
+#pragma unroll
+  for (int q = 0; q < 32; q++)
+    if (uint32_t(q) + 32 < nq) out[uint64_t(q + 32) * P.W] = hi[q];
+}
+
 constexpr int kLkThreads = 256;
 constexpr uint32_t kHitK = 4;
 constexpr unsigned long long kGAgg = 1, kGInc = 2;
@@ -932,7 +975,12 @@ void device_lookup(DeviceCtx &dc, const std::vector<std::pair<uint32_t, V2Block 
     tp.J = slabs[i].J;
     if (tp.words * 64 < tp.bitlen) fail(TSG_E_CORRUPT, "bloom shorter than its bit length");
     const uint64_t threads = uint64_t(tp.shards) * tp.words * tp.W;
-    lookup_transpose_kernel<<<uint32_t((threads + 255) / 256), 256, 0, s>>>(tp);
+    static const bool tr_bits = [] {  // (TSG_LK_TR=1: the bit-at-a-time transpose)
+      const char *e = std::getenv("TSG_LK_TR");
+      return e && std::atoi(e) == 1;
+    }();
+    if (tr_bits) lookup_transpose_kernel<<<uint32_t((threads + 255) / 256), 256, 0, s>>>(tp);
+    else lookup_transpose2_kernel<<<uint32_t((threads + 255) / 256), 256, 0, s>>>(tp);
     HIP_OK(hipGetLastError());
   }
   static const int occ = [] {

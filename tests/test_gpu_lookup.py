@@ -226,13 +226,13 @@ eng.close()
 """
 
 
-@pytest.mark.parametrize("env", [{"TSG_LK_OCAP": "1"}, {"TSG_LK_SLOTMAJOR": "0", "TSG_LK_HOSTSIZE": "1"},
+@pytest.mark.parametrize("env", [{"TSG_LK_OCAP": "1"}, {"TSG_LK_SLOTMAJOR": "0", "TSG_LK_HOSTSIZE": "1", "TSG_LK_TR": "1"},
                                  {"TSG_LK_OCC": "6"}])
 def test_lookup_pass_variants(tmp_path, env):
     """The count / write passes' alternatives, each read once per process (so a child process):
     the write pass's relaunch when the hits outnumber its first columns (TSG_LK_OCAP=1 caps them
     at one hit), the round-5 id-major kept hits with the host reading the total between the
-    passes, and the 6-wave count pass — every one returns the oracle's hits."""
+    passes and the bit-at-a-time slab transpose, and the 6-wave count pass — every one returns the oracle's hits."""
     import subprocess
     import sys
     paths, stored = [], []
